@@ -1,0 +1,40 @@
+# Makefile — builds the MI355X product (build/libsid.so, build/sid) and the
+# test-only oracle (oracle/_build, oracle/_ref).  `make -j8`.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+BUILD := build
+SRC := sid_amd/csrc
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude
+HOSTFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Iinclude
+
+KERNELS := local synth lynch
+HOSTSRC := capi lynch_host parse emit
+OBJS := $(KERNELS:%=$(BUILD)/%.o) $(HOSTSRC:%=$(BUILD)/%.o)
+HDRS := include/sid.h $(wildcard $(SRC)/*.h)
+
+all: $(BUILD)/libsid.so $(BUILD)/sid oracle
+
+$(BUILD)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# host-only translation units: compiled by hipcc as HIP (they include the HIP
+# runtime headers); parse/emit use no HIP at all
+$(BUILD)/%.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/libsid.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -lpthread
+
+$(BUILD)/sid: $(SRC)/main.cpp $(BUILD)/libsid.so include/sid.h
+	$(HIPCC) $(HOSTFLAGS) -o $@ $(SRC)/main.cpp -L$(BUILD) -lsid -Wl,-rpath,'$$ORIGIN' -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BUILD)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

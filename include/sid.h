@@ -1,0 +1,183 @@
+/*
+ * sid.h — C ABI of libsid.so, the MI355X-native per-site genotype caller.
+ *
+ * Drop-in boundary.  EvolBioInf/sid has no plugin/FFI API; its internal seam
+ * is the four method functions declared at call.hpp:40-43,
+ *     std::vector<OutputRecord> callX(std::istream&, ...)
+ * called only from sid.cpp:92-100.  This header replaces that seam with plain
+ * pointers and sizes (no C++ or torch types), split where the data crosses the
+ * host/device boundary:
+ *
+ *   host text --(sid_parse_*: pileup.cpp:13-153)--> SoA counts (u16 x 4 per site)
+ *   counts --(sid_call_local / sid_profile_* + sid_lynch_* + sid_lookup_sites:
+ *             call.cpp:62-289, lynch.hpp/.cpp, stats.cpp)--> code + 2 x f64 per site
+ *   code + confs --(sid_format_csv: call.hpp:29-38, sid.cpp:102-105)--> CSV text
+ *
+ * Conventions
+ *   - Caller owns every buffer.  "device" pointers are HIP device memory
+ *     (hipMalloc / torch); "host" pointers are ordinary or pinned host memory.
+ *   - No exception crosses the ABI: every function returns SID_OK (0) or a
+ *     SID_E* status; sid_strerror() names it.
+ *   - Device work is asynchronous on the caller's stream (hipStream_t passed as
+ *     void*, NULL = default stream) unless the function says it synchronises.
+ *   - One sid_ctx per device and host thread (thread-compatible, not
+ *     thread-safe).
+ *   - Per-site result code: bits 0-1 = gt[0] base (0..3 = A,C,G,T), bits 2-3 =
+ *     gt[1] base, bit 7 = het label, bit 6 = site dropped (its profile was
+ *     filtered, coverage < 4, and the reference prints no record for it:
+ *     call.cpp:131-140).
+ *   - Counts layout: profile_t (pileup.hpp:7) = 4 x uint16 {A,C,G,T} per site,
+ *     array of structures, 8 bytes per site.
+ */
+#ifndef SID_H
+#define SID_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- status -- */
+enum {
+    SID_OK = 0,
+    SID_EINVAL = 1,      /* bad argument (null pointer, misuse)                     */
+    SID_EHIP = 2,        /* HIP runtime error (sid_last_hip_error() has the code)   */
+    SID_ENOMEM = 3,      /* host or device allocation failed                        */
+    SID_EMALFORMED = 4,  /* "Malformed pileup line"                pileup.cpp:9       */
+    SID_EMISSING_MQ = 5, /* "Malformed pileup line or missing mapping qualities" :10 */
+    SID_ENULLCHROM = 6,  /* no first token: the reference assigns a NULL char* to a
+                            std::string (pileup.cpp:18) and dies with SIGSEGV       */
+    SID_ESTATE = 7,      /* call order violated (e.g. lookup before lynch_prepare)  */
+    SID_EBADFUNC = 8,    /* non-finite objective at the simplex start: GSL would
+                            abort (nmsimplex2 set; optimization.hpp:55)            */
+    SID_EEMPTY = 9,      /* no profile with coverage >= 4: the reference indexes an
+                            empty vector in adjustBenjaminiHochberg (stats.cpp:73) */
+};
+const char* sid_strerror(int status);
+int sid_last_hip_error(void);
+/* Library version string, e.g. "sid-mi355x 0.1.0 (gfx950)". */
+const char* sid_version(void);
+
+/* --------------------------------------------------------------- options -- */
+enum { SID_METHOD_LOCAL = 0, SID_METHOD_LIKELIHOOD_RATIO = 1, SID_METHOD_BAYES = 2 };
+
+/* GlobalOptions, sid.cpp:11-17 */
+typedef struct {
+    int method;                  /* -m   (default SID_METHOD_LOCAL)                */
+    int estimate_prior;          /* -R   (default 0)                               */
+    double snp_prior;            /* -r   (default -1 = no prior)                   */
+    double significance_level;   /* -p   (default 0.05)                            */
+    double site_error_threshold; /* -E   (default 0.1)                             */
+} sid_opts;
+void sid_opts_default(sid_opts* o);
+
+/* ------------------------------------------------------------- contexts -- */
+typedef struct sid_ctx sid_ctx;
+int sid_device_count(int* n);
+/* Binds `device` (hipSetDevice) for the calling thread and builds the
+ * per-context constant tables (log table, chi-square constants). */
+int sid_create(int device, const sid_opts* opts, sid_ctx** out);
+int sid_destroy(sid_ctx* ctx);
+/* Replaces snp_prior after the -R estimate (call.cpp:223-234). */
+int sid_set_prior(sid_ctx* ctx, double snp_prior);
+
+/* ------------------------------------------------------- -m local (a5-a8) --
+ * Per-site replacement of callSiteMLError's per-profile loop + per-site gather
+ * (call.cpp:213-289; likelihoods lynch.hpp:48-55,76-80,92-96; LRT
+ * stats.cpp:29-37).  counts/code/hom_conf/het_conf are device pointers. */
+int sid_call_local(sid_ctx* ctx, const uint16_t* counts, size_t n, uint8_t* code,
+                   double* hom_conf, double* het_conf, void* stream);
+
+/* ---------------------------------------------- Lynch path (a11-a17) -------
+ * 1. sid_profile_reset + sid_profile_accumulate (any number of batches):
+ *    device hash histogram of the site profiles (countUniqueProfiles,
+ *    pileup.cpp:169-196).
+ * 2. optional multi-device / multi-rank merge: sid_profile_table exports the
+ *    sorted unique profiles, sid_profile_load replaces the context's table by
+ *    a merged one (counts are summed by the caller).
+ * 3. sid_lynch_prepare: coverage >= 4 filter (call.cpp:66-70), nucleotide
+ *    distribution (pileup.cpp:198-217), Nelder-Mead estimate of (pi, eps)
+ *    with the objective evaluated on the GPU (lynch.cpp:17-61,
+ *    optimization.hpp:50-89), per-profile 10-genotype likelihoods at eps-hat
+ *    (lynch.hpp:57-74,82-90), then the per-method class table:
+ *    likelihood_ratio: LRT + Benjamini-Hochberg (call.cpp:85-127,
+ *    stats.cpp:58-80); bayes: posteriors (call.cpp:170-194); local -R: only
+ *    the prior (use sid_set_prior + sid_call_local afterwards).
+ * 4. sid_lookup_sites: per-site gather of the class table (call.cpp:129-140). */
+typedef struct {
+    double heterozygosity;   /* pi-hat   ("# heterozygosity: %e", call.cpp:79)   */
+    double error_rate;       /* eps-hat  ("# error: %e", call.cpp:80)            */
+    double fval;             /* objective at the returned vertex                */
+    double dist[4];          /* nucleotide distribution                         */
+    int iterations;          /* NM iterations (optimization.hpp:70)             */
+    int converged;           /* 0: "did not converge in 1000 iterations"        */
+    uint64_t evaluations;    /* objective evaluations                           */
+    uint64_t n_unique;       /* profiles after the coverage filter ("# unique profiles") */
+} sid_estimate;
+
+int sid_profile_reset(sid_ctx* ctx, void* stream);
+int sid_profile_accumulate(sid_ctx* ctx, const uint16_t* counts, size_t n, void* stream);
+/* Synchronises.  keys[i] = A<<48 | C<<32 | G<<16 | T (numeric order ==
+ * lexicographic profile_t order); counts64[i] = sites with that profile.
+ * With keys == NULL only *u is returned. */
+int sid_profile_table(sid_ctx* ctx, uint64_t* keys, uint64_t* counts64, size_t cap, size_t* u);
+int sid_profile_load(sid_ctx* ctx, const uint64_t* keys, const uint64_t* counts64, size_t u);
+/* Objective -sum count*log((1-pi)Lhom+pi*Lhet) over the filtered table at
+ * (pi, eps), lynch.cpp:37-61.  Valid after sid_lynch_prepare (or
+ * sid_lynch_setup).  Synchronises. */
+int sid_lynch_setup(sid_ctx* ctx, sid_estimate* est /* dist, n_unique filled */);
+int sid_lynch_objective(sid_ctx* ctx, double pi, double eps, double* out);
+/* verbose != 0 prints the reference's "# ..." stderr lines. Synchronises. */
+int sid_lynch_prepare(sid_ctx* ctx, int verbose, sid_estimate* est);
+int sid_lookup_sites(sid_ctx* ctx, const uint16_t* counts, size_t n, uint8_t* code,
+                     double* hom_conf, double* het_conf, void* stream);
+
+/* ----------------------------------------------------- synthetic input -----
+ * Counter-based generator (BASELINE.md "Synthetic generator"): site i of a
+ * run is a pure function of (seed, first_site + i), identical on host and
+ * device.  sites_per_chrom splits the run into chromosomes chr1, chr2, ...
+ * (positions restart at 1; keeps positions < 2^31). */
+int sid_synth_counts(sid_ctx* ctx, uint64_t seed, double mean_depth, uint64_t first_site,
+                     size_t n, uint16_t* counts /* device */, void* stream);
+/* Host text of sites [first_site, first_site+n).  Returns the bytes needed in
+ * *len; writes at most cap bytes (call with buf == NULL to size). */
+int sid_synth_text(uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
+                   uint64_t sites_per_chrom, char* buf, size_t cap, size_t* len);
+/* Host counts of the same sites (for tests; no GPU needed). */
+int sid_synth_counts_host(uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
+                          uint16_t* counts);
+
+/* ------------------------------------------------------ host parser --------
+ * parsePileupLine / parseReadBases semantics (pileup.cpp:13-153) over a text
+ * buffer, multi-threaded.  Empty lines are skipped (call.cpp:14).  On a
+ * malformed line the status is SID_EMALFORMED / SID_ENULLCHROM and
+ * *err_line is the 0-based line number of the first bad line. */
+typedef struct sid_sites sid_sites;
+int sid_parse_text(const char* text, size_t len, int nthreads, sid_sites** out,
+                   uint64_t* err_line);
+void sid_sites_free(sid_sites* s);
+size_t sid_sites_count(const sid_sites* s);
+const uint16_t* sid_sites_counts(const sid_sites* s);   /* host, n x 4          */
+const int32_t* sid_sites_positions(const sid_sites* s); /* host, n              */
+/* Chromosome runs: segment k covers sites [start_k, start_{k+1}). */
+size_t sid_sites_chrom_segments(const sid_sites* s);
+const char* sid_sites_chrom_name(const sid_sites* s, size_t k, uint64_t* start);
+
+/* ------------------------------------------------------ CSV emitter --------
+ * Formats records [begin, end) exactly like operator<<(OutputRecord)
+ * (call.hpp:29-38: chrom,pos,label,gt,%g,%g,conf_type) into buf; sites with
+ * code bit 6 set are skipped.  conf_type: "p_value" or "probability".
+ * Returns bytes written in *len, or SID_ENOMEM if cap is too small (then *len
+ * is a sufficient size). */
+int sid_format_csv(const sid_sites* s, size_t begin, size_t end, const uint8_t* code,
+                   const double* hom_conf, const double* het_conf, const char* conf_type,
+                   char* buf, size_t cap, size_t* len);
+/* %g formatting of one double exactly as std::ostream does (precision 6). */
+int sid_format_double(double v, char* buf, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SID_H */

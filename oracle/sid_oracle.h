@@ -35,7 +35,7 @@ enum {
     ORACLE_OK = 0,
     ORACLE_EMALFORMED = 1,        /* "Malformed pileup line"                 pileup.cpp:9   */
     ORACLE_EMISSING_MQ = 2,       /* "... or missing mapping qualities"      pileup.cpp:10  */
-    ORACLE_ENULLCHROM = 3,        /* std::string(nullptr) -> std::logic_error pileup.cpp:18 */
+    ORACLE_ENULLCHROM = 3,        /* std::string = (char*)NULL: SIGSEGV      pileup.cpp:18 */
 };
 
 enum { ORACLE_LOCAL = 0, ORACLE_LIKELIHOOD_RATIO = 1, ORACLE_BAYES = 2 };

@@ -82,8 +82,11 @@ static void read_file(FILE* in, sites_t* s)
             if (rc == ORACLE_EMALFORMED) die_terminate("std::invalid_argument", "Malformed pileup line");
             if (rc == ORACLE_EMISSING_MQ)
                 die_terminate("std::invalid_argument", "Malformed pileup line or missing mapping qualities");
-            if (rc == ORACLE_ENULLCHROM)
-                die_terminate("std::logic_error", "basic_string::_M_construct null not valid");
+            if (rc == ORACLE_ENULLCHROM) { /* std::string = (char*)NULL: strlen(NULL) */
+                fflush(stdout);
+                signal(SIGSEGV, SIG_DFL);
+                raise(SIGSEGV);
+            }
             push_site(s, &l);
         }
     }

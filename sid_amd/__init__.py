@@ -1,0 +1,300 @@
+"""sid_amd — Python bindings of libsid.so, the MI355X-native sid hot path.
+
+The product is the C ABI in ``include/sid.h`` (``build/libsid.so``) and the
+``build/sid`` command line that mirrors the reference's ``sid`` binary
+(sid.cpp:1-110).  This module is a thin ctypes layer over that ABI for the
+tests and ``bench.py``; it adds no computation of its own.
+
+Device memory and streams come from PyTorch (plumbing only): when torch is
+importable it is imported *before* libsid.so is loaded, so the process holds a
+single HIP runtime.  There is no CPU fallback: if ``build/libsid.so`` is
+missing, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "build", "libsid.so")
+CLI_PATH = os.path.join(ROOT, "build", "sid")
+
+METHOD_LOCAL, METHOD_LIKELIHOOD_RATIO, METHOD_BAYES = 0, 1, 2
+METHODS = {"local": METHOD_LOCAL, "likelihood_ratio": METHOD_LIKELIHOOD_RATIO,
+           "bayes": METHOD_BAYES}
+
+SID_OK = 0
+STATUS = {0: "SID_OK", 1: "SID_EINVAL", 2: "SID_EHIP", 3: "SID_ENOMEM", 4: "SID_EMALFORMED",
+          5: "SID_EMISSING_MQ", 6: "SID_ENULLCHROM", 7: "SID_ESTATE", 8: "SID_EBADFUNC",
+          9: "SID_EEMPTY"}
+
+CODE_HET = 0x80
+CODE_DROPPED = 0x40
+
+
+class SidError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = f"{what}: {STATUS.get(status, status)}" if what else STATUS.get(status, str(status))
+        if status == 2 and _LIB is not None:
+            msg += f" (hip error {_LIB.sid_last_hip_error()})"
+        super().__init__(msg)
+
+
+class Opts(C.Structure):
+    """sid_opts = GlobalOptions (sid.cpp:11-17)."""
+    _fields_ = [("method", C.c_int), ("estimate_prior", C.c_int), ("snp_prior", C.c_double),
+                ("significance_level", C.c_double), ("site_error_threshold", C.c_double)]
+
+
+class Estimate(C.Structure):
+    _fields_ = [("heterozygosity", C.c_double), ("error_rate", C.c_double), ("fval", C.c_double),
+                ("dist", C.c_double * 4), ("iterations", C.c_int), ("converged", C.c_int),
+                ("evaluations", C.c_uint64), ("n_unique", C.c_uint64)]
+
+
+_LIB = None
+
+# (name, restype, argtypes) for every entry point of include/sid.h
+_P, _SZ, _U64, _I, _D = C.c_void_p, C.c_size_t, C.c_uint64, C.c_int, C.c_double
+SIGNATURES = [
+    ("sid_strerror", C.c_char_p, [_I]),
+    ("sid_last_hip_error", _I, []),
+    ("sid_version", C.c_char_p, []),
+    ("sid_opts_default", None, [C.POINTER(Opts)]),
+    ("sid_device_count", _I, [C.POINTER(C.c_int)]),
+    ("sid_create", _I, [_I, C.POINTER(Opts), C.POINTER(_P)]),
+    ("sid_destroy", _I, [_P]),
+    ("sid_set_prior", _I, [_P, _D]),
+    ("sid_call_local", _I, [_P, _P, _SZ, _P, _P, _P, _P]),
+    ("sid_profile_reset", _I, [_P, _P]),
+    ("sid_profile_accumulate", _I, [_P, _P, _SZ, _P]),
+    ("sid_profile_table", _I, [_P, _P, _P, _SZ, C.POINTER(C.c_size_t)]),
+    ("sid_profile_load", _I, [_P, _P, _P, _SZ]),
+    ("sid_lynch_setup", _I, [_P, C.POINTER(Estimate)]),
+    ("sid_lynch_objective", _I, [_P, _D, _D, C.POINTER(C.c_double)]),
+    ("sid_lynch_prepare", _I, [_P, _I, C.POINTER(Estimate)]),
+    ("sid_lookup_sites", _I, [_P, _P, _SZ, _P, _P, _P, _P]),
+    ("sid_synth_counts", _I, [_P, _U64, _D, _U64, _SZ, _P, _P]),
+    ("sid_synth_text", _I, [_U64, _D, _U64, _SZ, _U64, _P, _SZ, C.POINTER(C.c_size_t)]),
+    ("sid_synth_counts_host", _I, [_U64, _D, _U64, _SZ, _P]),
+    ("sid_parse_text", _I, [C.c_char_p, _SZ, _I, C.POINTER(_P), C.POINTER(C.c_uint64)]),
+    ("sid_sites_free", None, [_P]),
+    ("sid_sites_count", _SZ, [_P]),
+    ("sid_sites_counts", _P, [_P]),
+    ("sid_sites_positions", _P, [_P]),
+    ("sid_sites_chrom_segments", _SZ, [_P]),
+    ("sid_sites_chrom_name", C.c_char_p, [_P, _SZ, C.POINTER(C.c_uint64)]),
+    ("sid_format_csv", _I, [_P, _SZ, _SZ, _P, _P, _P, C.c_char_p, _P, _SZ, C.POINTER(C.c_size_t)]),
+    ("sid_format_double", _I, [_D, C.c_char_p, _SZ]),
+]
+
+
+def lib():
+    """Load build/libsid.so (torch first, if importable: one HIP runtime)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run `make` (or __graft_entry__.build()); "
+                           "sid_amd has no CPU fallback")
+    try:  # plumbing: device memory / streams / distributed come from torch
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    for name, res, args in SIGNATURES:
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def check(status: int, what: str = ""):
+    if status != SID_OK:
+        raise SidError(status, what)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def make_opts(method="local", estimate_prior=False, snp_prior=-1.0, significance_level=0.05,
+              site_error_threshold=0.1) -> Opts:
+    o = Opts()
+    lib().sid_opts_default(C.byref(o))
+    o.method = METHODS[method] if isinstance(method, str) else int(method)
+    o.estimate_prior = int(bool(estimate_prior))
+    o.snp_prior = float(snp_prior)
+    o.significance_level = float(significance_level)
+    o.site_error_threshold = float(site_error_threshold)
+    return o
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    st = lib().sid_device_count(C.byref(n))
+    return n.value if st == SID_OK else 0
+
+
+# --------------------------------------------------------------- host side --
+@dataclass
+class Sites:
+    counts: np.ndarray          # (n, 4) uint16, A C G T
+    positions: np.ndarray       # (n,) int32
+    chroms: list                # [(start_site, name)]
+    handle: object = None       # sid_sites* kept for format_csv
+
+    def __len__(self):
+        return len(self.positions)
+
+    def __del__(self):
+        if self.handle is not None and _LIB is not None:
+            _LIB.sid_sites_free(self.handle)
+            self.handle = None
+
+
+def parse_text(text: bytes, threads: int = 0) -> Sites:
+    """sid_parse_text: pileup text -> SoA (pileup.cpp:13-153 semantics)."""
+    L = lib()
+    h = C.c_void_p()
+    bad = C.c_uint64(0)
+    st = L.sid_parse_text(text, len(text), threads, C.byref(h), C.byref(bad))
+    if st != SID_OK:
+        err = SidError(st, "parse")
+        err.line = bad.value
+        raise err
+    n = L.sid_sites_count(h)
+    counts = np.ctypeslib.as_array(C.cast(L.sid_sites_counts(h), C.POINTER(C.c_uint16)),
+                                   shape=(n * 4,)).reshape(n, 4).copy() if n else np.zeros((0, 4), np.uint16)
+    pos = np.ctypeslib.as_array(C.cast(L.sid_sites_positions(h), C.POINTER(C.c_int32)),
+                                shape=(n,)).copy() if n else np.zeros(0, np.int32)
+    chroms = []
+    for k in range(L.sid_sites_chrom_segments(h)):
+        start = C.c_uint64(0)
+        name = L.sid_sites_chrom_name(h, k, C.byref(start))
+        chroms.append((start.value, name))
+    return Sites(counts, pos, chroms, h)
+
+
+def format_csv(sites: Sites, code: np.ndarray, hom: np.ndarray, het: np.ndarray,
+               conf_type: str = "p_value") -> bytes:
+    L = lib()
+    code = np.ascontiguousarray(code, np.uint8)
+    hom = np.ascontiguousarray(hom, np.float64)
+    het = np.ascontiguousarray(het, np.float64)
+    need = C.c_size_t(0)
+    n = len(sites)
+    L.sid_format_csv(sites.handle, 0, n, _ptr(code), _ptr(hom), _ptr(het), conf_type.encode(),
+                     None, 0, C.byref(need))
+    buf = C.create_string_buffer(max(need.value, 1))
+    ln = C.c_size_t(0)
+    check(L.sid_format_csv(sites.handle, 0, n, _ptr(code), _ptr(hom), _ptr(het), conf_type.encode(),
+                           buf, need.value, C.byref(ln)), "format")
+    return buf.raw[: ln.value]
+
+
+def format_double(v: float) -> str:
+    buf = C.create_string_buffer(48)
+    k = lib().sid_format_double(float(v), buf, 48)
+    return buf.value.decode()
+
+
+def synth_text(seed: int, n: int, depth: float = 30.0, first: int = 0,
+               sites_per_chrom: int = 0) -> bytes:
+    L = lib()
+    ln = C.c_size_t(0)
+    check(L.sid_synth_text(seed, depth, first, n, sites_per_chrom, None, 0, C.byref(ln)), "synth")
+    buf = C.create_string_buffer(max(ln.value, 1))
+    check(L.sid_synth_text(seed, depth, first, n, sites_per_chrom, buf, ln.value, C.byref(ln)), "synth")
+    return buf.raw[: ln.value]
+
+
+def synth_counts_host(seed: int, n: int, depth: float = 30.0, first: int = 0) -> np.ndarray:
+    out = np.zeros((n, 4), np.uint16)
+    check(lib().sid_synth_counts_host(seed, depth, first, n, _ptr(out)), "synth")
+    return out
+
+
+# ------------------------------------------------------------- device side --
+class Context:
+    """One sid_ctx (one device, one host thread)."""
+
+    def __init__(self, device: int = 0, **opts):
+        self.opts = make_opts(**opts)
+        self.device = device
+        h = C.c_void_p()
+        check(lib().sid_create(device, C.byref(self.opts), C.byref(h)), "sid_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sid_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_prior(self, prior: float):
+        check(lib().sid_set_prior(self.h, float(prior)), "sid_set_prior")
+
+    # raw device-pointer entry points -------------------------------------
+    def call_local(self, counts_ptr, n, code_ptr, hom_ptr, het_ptr, stream=None):
+        check(lib().sid_call_local(self.h, counts_ptr, n, code_ptr, hom_ptr, het_ptr, stream),
+              "sid_call_local")
+
+    def lookup_sites(self, counts_ptr, n, code_ptr, hom_ptr, het_ptr, stream=None):
+        check(lib().sid_lookup_sites(self.h, counts_ptr, n, code_ptr, hom_ptr, het_ptr, stream),
+              "sid_lookup_sites")
+
+    def profile_reset(self, stream=None):
+        check(lib().sid_profile_reset(self.h, stream), "sid_profile_reset")
+
+    def profile_accumulate(self, counts_ptr, n, stream=None):
+        check(lib().sid_profile_accumulate(self.h, counts_ptr, n, stream), "sid_profile_accumulate")
+
+    def profile_table(self):
+        u = C.c_size_t(0)
+        check(lib().sid_profile_table(self.h, None, None, 0, C.byref(u)), "sid_profile_table")
+        keys = np.zeros(u.value, np.uint64)
+        cnts = np.zeros(u.value, np.uint64)
+        if u.value:
+            check(lib().sid_profile_table(self.h, _ptr(keys), _ptr(cnts), u.value, C.byref(u)),
+                  "sid_profile_table")
+        return keys, cnts
+
+    def profile_load(self, keys: np.ndarray, cnts: np.ndarray):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        cnts = np.ascontiguousarray(cnts, np.uint64)
+        check(lib().sid_profile_load(self.h, _ptr(keys), _ptr(cnts), len(keys)), "sid_profile_load")
+
+    def lynch_setup(self) -> Estimate:
+        e = Estimate()
+        check(lib().sid_lynch_setup(self.h, C.byref(e)), "sid_lynch_setup")
+        return e
+
+    def lynch_objective(self, pi: float, eps: float) -> float:
+        out = C.c_double(0)
+        check(lib().sid_lynch_objective(self.h, pi, eps, C.byref(out)), "sid_lynch_objective")
+        return out.value
+
+    def lynch_prepare(self, verbose: bool = False) -> Estimate:
+        e = Estimate()
+        check(lib().sid_lynch_prepare(self.h, int(verbose), C.byref(e)), "sid_lynch_prepare")
+        return e
+
+    def synth_counts(self, seed, depth, first, n, counts_ptr, stream=None):
+        check(lib().sid_synth_counts(self.h, seed, depth, first, n, counts_ptr, stream),
+              "sid_synth_counts")
+
+
+def profile_key(counts: np.ndarray) -> np.ndarray:
+    c = counts.astype(np.uint64)
+    return (c[:, 0] << np.uint64(48)) | (c[:, 1] << np.uint64(32)) | (c[:, 2] << np.uint64(16)) | c[:, 3]

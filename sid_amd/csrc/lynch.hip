@@ -1,0 +1,458 @@
+// lynch.hip — Lynch ML path kernels.
+//
+//   sid_hist_kernel      countUniqueProfiles (pileup.cpp:169-196) as a hash
+//                        histogram: per-block LDS pre-aggregation, then one
+//                        global atomic per (block, distinct profile).
+//   sid_objective_kernel compoundLikelihood (lynch.cpp:37-61) over the
+//                        filtered unique profiles: one lane per profile,
+//                        10-genotype mixture in the log domain
+//                        (lynch.hpp:57-74,82-90), count*ln L reduced per
+//                        block in double-double.
+//   sid_profile_lik_kernel  per-profile (L_hom, L_het) at eps-hat
+//                        (lynch.cpp:28-33) as emulated long doubles.
+//   sid_classify_kernel  LRT (call.cpp:93-104) or bayes posteriors
+//                        (call.cpp:170-194) per profile.
+//   sid_lookup_kernel    per-site gather of the class table
+//                        (call.cpp:129-140) through a compact,
+//                        L2/MALL-resident hash of the U profiles.
+#include <hip/hip_runtime.h>
+
+#include "sid_math.h"
+
+#define SID_EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
+#define SID_LN_LDBL_TRUE_MIN (-SID_LDBL_DENORM_SHIFT)
+
+__device__ __forceinline__ uint64_t sid_hash64(uint64_t k)
+{
+    k ^= k >> 33;
+    k *= 0xFF51AFD7ED558CCDull;
+    k ^= k >> 33;
+    k *= 0xC4CEB9FE1A85EC53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+// profile_t (A,C,G,T little-endian u16) -> key with lexicographic numeric order
+__device__ __forceinline__ uint64_t sid_profile_key(uint64_t w)
+{
+    return ((w & 0xffffull) << 48) | (((w >> 16) & 0xffffull) << 32) | (((w >> 32) & 0xffffull) << 16) |
+           (w >> 48);
+}
+
+__device__ __forceinline__ void sid_global_insert(unsigned long long* gkeys, unsigned long long* gcnt,
+                                                  uint64_t gmask, unsigned long long* distinct,
+                                                  uint64_t key, unsigned long long add)
+{
+    uint64_t h = sid_hash64(key) & gmask;
+    for (uint64_t probe = 0; probe <= gmask; ++probe) {
+        unsigned long long prev = atomicCAS(&gkeys[h], SID_EMPTY_KEY, (unsigned long long)key);
+        if (prev == SID_EMPTY_KEY || prev == key) {
+            atomicAdd(&gcnt[h], add);
+            if (prev == SID_EMPTY_KEY) atomicAdd(distinct, 1ull);
+            return;
+        }
+        h = (h + 1) & gmask;
+    }
+}
+
+#define SID_HIST_LCAP 4096
+#define SID_HIST_PROBES 32
+
+// counts: n sites; keys of value SID_EMPTY_KEY (all four counts 65535) go to
+// special[0].  stats[0] = distinct keys inserted in the global table.
+__global__ __launch_bounds__(256) void sid_hist_kernel(const uint64_t* __restrict__ counts, size_t n,
+                                                       size_t per_block, unsigned long long* gkeys,
+                                                       unsigned long long* gcnt, uint64_t gmask,
+                                                       unsigned long long* stats)
+{
+    __shared__ unsigned long long lkeys[SID_HIST_LCAP];
+    __shared__ unsigned int lcnt[SID_HIST_LCAP];
+    for (int i = threadIdx.x; i < SID_HIST_LCAP; i += blockDim.x) {
+        lkeys[i] = SID_EMPTY_KEY;
+        lcnt[i] = 0;
+    }
+    __syncthreads();
+    const size_t begin = (size_t)blockIdx.x * per_block;
+    const size_t end = begin + per_block < n ? begin + per_block : n;
+    for (size_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
+        const uint64_t key = sid_profile_key(counts[i]);
+        if (key == SID_EMPTY_KEY) {
+            atomicAdd(&stats[1], 1ull);
+            continue;
+        }
+        uint32_t h = (uint32_t)(sid_hash64(key) & (SID_HIST_LCAP - 1));
+        bool done = false;
+        for (int p = 0; p < SID_HIST_PROBES; ++p) {
+            unsigned long long prev = atomicCAS(&lkeys[h], SID_EMPTY_KEY, (unsigned long long)key);
+            if (prev == SID_EMPTY_KEY || prev == key) {
+                atomicAdd(&lcnt[h], 1u);
+                done = true;
+                break;
+            }
+            h = (h + 1) & (SID_HIST_LCAP - 1);
+        }
+        if (!done) sid_global_insert(gkeys, gcnt, gmask, &stats[0], key, 1ull);
+    }
+    __syncthreads();
+    for (int s = threadIdx.x; s < SID_HIST_LCAP; s += blockDim.x) {
+        if (lkeys[s] != SID_EMPTY_KEY)
+            sid_global_insert(gkeys, gcnt, gmask, &stats[0], lkeys[s], lcnt[s]);
+    }
+}
+
+__global__ void sid_hist_rehash_kernel(const unsigned long long* okeys, const unsigned long long* ocnt,
+                                       uint64_t ocap, unsigned long long* gkeys,
+                                       unsigned long long* gcnt, uint64_t gmask,
+                                       unsigned long long* distinct)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ocap;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        if (okeys[i] != SID_EMPTY_KEY) sid_global_insert(gkeys, gcnt, gmask, distinct, okeys[i], ocnt[i]);
+}
+
+__global__ void sid_hist_compact_kernel(const unsigned long long* gkeys, const unsigned long long* gcnt,
+                                        uint64_t cap, unsigned long long* okeys,
+                                        unsigned long long* ocnt, unsigned long long* nout)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (gkeys[i] != SID_EMPTY_KEY) {
+            unsigned long long k = atomicAdd(nout, 1ull);
+            okeys[k] = gkeys[i];
+            ocnt[k] = gcnt[i];
+        }
+    }
+}
+
+// ------------------------------------------------ 10-genotype mixture -----
+// sid_lynch_eval: sid_math.h
+
+__device__ __forceinline__ double sid_lse2(double a, double b)
+{
+    double m = fmax(a, b);
+    if (m == -__builtin_inf()) return m;
+    return m + log1p(exp(fmin(a, b) - m));
+}
+
+// one powl factor n*ln(base); 0 when n == 0; underflow of the long double -> 0
+__device__ __forceinline__ double sid_pow_ln(double lbase, uint32_t n)
+{
+    if (n == 0) return 0.0;
+    double v = (double)n * lbase;
+    return v < SID_LN_LDBL_TRUE_MIN ? -__builtin_inf() : v;
+}
+
+// ln of d * powl(x, a) * powl(y, b) with the reference's underflow points
+__device__ __forceinline__ double sid_term(double ld, double pa, double pb)
+{
+    double t = ld + pa;
+    if (t < SID_LN_LDBL_TRUE_MIN) return -__builtin_inf();
+    t += pb;
+    return t < SID_LN_LDBL_TRUE_MIN ? -__builtin_inf() : t;
+}
+
+// ln of the pre-M sums of lynch.hpp:82-90 (hom) and :57-74 (het)
+__device__ __forceinline__ void sid_mixture(uint64_t key, const sid_lynch_eval& E, double& s_hom,
+                                            double& s_het)
+{
+    uint32_t n[4] = {(uint32_t)(key >> 48), (uint32_t)((key >> 32) & 0xffff),
+                     (uint32_t)((key >> 16) & 0xffff), (uint32_t)(key & 0xffff)};
+    const uint32_t c = n[0] + n[1] + n[2] + n[3];
+    double m = -__builtin_inf();
+    double t[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        t[i] = sid_term(E.ld[i], sid_pow_ln(E.la, n[i]), sid_pow_ln(E.lb, c - n[i]));
+        m = fmax(m, t[i]);
+    }
+    double acc = 0.0;
+    if (m != -__builtin_inf()) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc += exp(t[i] - m);
+        s_hom = m + log(acc);
+    } else {
+        s_hom = m;
+    }
+    double u[6];
+    double mu = -__builtin_inf();
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = i + 1; j < 4; ++j) {
+            u[k] = sid_term(E.ldd[k], sid_pow_ln(E.lh, n[i] + n[j]), sid_pow_ln(E.lb, c - n[i] - n[j]));
+            mu = fmax(mu, u[k]);
+            ++k;
+        }
+    if (mu != -__builtin_inf()) {
+        double a2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) a2 += exp(u[q] - mu);
+        s_het = mu + log(a2) + E.lnorm;
+    } else {
+        s_het = mu;
+    }
+}
+
+__device__ __forceinline__ void sid_two_sum(double a, double b, double& s, double& e)
+{
+    s = a + b;
+    double bb = s - a;
+    e = (a - (s - bb)) + (b - bb);
+}
+
+// partial[2*block] = hi, partial[2*block+1] = lo of sum count*ln L
+__global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __restrict__ keys,
+                                                            const uint32_t* __restrict__ cnt,
+                                                            const double* __restrict__ lnM, size_t u,
+                                                            sid_lynch_eval E, double* partial)
+{
+    double hi = 0.0, lo = 0.0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < u;
+         i += (size_t)gridDim.x * blockDim.x) {
+        double sh, st;
+        sid_mixture(keys[i], E, sh, st);
+        // L = (1-pi) M S_hom + pi M S_het  (lynch.cpp:46-47); M multiplies last
+        double lhom = sh == -__builtin_inf() ? sh : lnM[i] + sh;
+        double lhet = st == -__builtin_inf() ? st : lnM[i] + st;
+        double lL = sid_lse2(E.l1p + lhom, E.lp + lhet);
+        if (lL > -__builtin_inf() && !isnan(lL)) {   // if (L > 0)
+            double v = lL * (double)cnt[i];          // logl(L) * p.count
+            double p = fma(lL, (double)cnt[i], -v);  // exact product error
+            double s, e;
+            sid_two_sum(hi, v, s, e);
+            hi = s;
+            lo += e + p;
+        }
+    }
+    // wave64 then block reduction, double-double
+    __shared__ double sh_hi[4], sh_lo[4];
+    for (int off = 32; off > 0; off >>= 1) {
+        double ohi = __shfl_down(hi, off, 64);
+        double olo = __shfl_down(lo, off, 64);
+        double s, e;
+        sid_two_sum(hi, ohi, s, e);
+        hi = s;
+        lo += olo + e;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        sh_hi[wid] = hi;
+        sh_lo[wid] = lo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double H = 0.0, Lo = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+            double s, e;
+            sid_two_sum(H, sh_hi[w], s, e);
+            H = s;
+            Lo += sh_lo[w] + e;
+        }
+        partial[2 * blockIdx.x] = H;
+        partial[2 * blockIdx.x + 1] = Lo;
+    }
+}
+
+// Per-profile L_hom, L_het at eps-hat as emulated long doubles (ln, sign=+).
+__global__ __launch_bounds__(256) void sid_profile_lik_kernel(const uint64_t* __restrict__ keys,
+                                                              const double* __restrict__ lnM,
+                                                              size_t u, sid_lynch_eval E,
+                                                              double* __restrict__ lhom,
+                                                              double* __restrict__ lhet)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < u;
+         i += (size_t)gridDim.x * blockDim.x) {
+        double sh, st;
+        sid_mixture(keys[i], E, sh, st);
+        sid_ld M;
+        M.ln = lnM[i];
+        M.neg = 0;
+        M = ld_round(M);
+        sid_ld H, T;
+        H.ln = sh;
+        H.neg = 0;
+        T.ln = st;
+        T.neg = 0;
+        lhom[i] = ld_mul(M, ld_round(H)).ln;
+        lhet[i] = ld_mul(M, ld_round(T)).ln;
+    }
+}
+
+// x86 prints NaNs made by invalid operations as "-nan" (default NaN has the
+// sign bit set); give every NaN the same sign.
+__device__ __forceinline__ double sid_x86_nan(double v) { return isnan(v) ? -__builtin_nan("") : v; }
+
+// mode 0: likelihood_ratio p-values (before BH); mode 1: bayes posteriors.
+__global__ __launch_bounds__(256) void sid_classify_kernel(const uint64_t* __restrict__ keys,
+                                                           const double* __restrict__ lhom,
+                                                           const double* __restrict__ lhet, size_t u,
+                                                           int mode, int use_prior, double pi,
+                                                           double lg15, double* __restrict__ c1,
+                                                           double* __restrict__ c2,
+                                                           uint8_t* __restrict__ code)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < u;
+         i += (size_t)gridDim.x * blockDim.x) {
+        sid_ld H, T;
+        H.ln = lhom[i];
+        H.neg = 0;
+        T.ln = lhet[i];
+        T.neg = 0;
+        // profile_t from the key, then majors (call.cpp:52-60)
+        const uint64_t k = keys[i];
+        const uint64_t w = (k >> 48) | (((k >> 32) & 0xffff) << 16) | (((k >> 16) & 0xffff) << 32) |
+                           ((k & 0xffff) << 48);
+        uint32_t f, s, nf, ns, cov;
+        sid_major(w, f, s, nf, ns, cov);
+        if (mode == 0) {
+            if (use_prior) {                                  // call.cpp:94-97
+                T = ld_mul(T, ld_from_double(pi));
+                H = ld_mul(H, ld_from_double(1 - pi));
+            }
+            c1[i] = sid_x86_nan(ld_lrt(T, H, lg15));          // p_hom
+            c2[i] = sid_x86_nan(ld_lrt(H, T, lg15));          // p_het
+            code[i] = (uint8_t)(f | (s << 2));                // label decided after BH (host)
+        } else {
+            sid_ld aH = ld_mul(H, ld_from_double(1 - pi));    // call.cpp:177-178
+            sid_ld aT = ld_mul(T, ld_from_double(pi));
+            sid_ld sum;
+            sum.ln = sid_lse2(aH.ln, aT.ln);
+            sum.neg = 0;
+            sum = ld_round(sum);
+            double ph, pt;
+            if (ld_is_zero(sum) || isnan(sum.ln) || isinf(sum.ln)) {
+                ph = (ld_is_zero(aH) && !ld_is_zero(sum)) ? 0.0 : -__builtin_nan("");
+                pt = (ld_is_zero(aT) && !ld_is_zero(sum)) ? 0.0 : -__builtin_nan("");
+            } else {
+                ph = exp(aH.ln - sum.ln);
+                pt = exp(aT.ln - sum.ln);
+            }
+            c1[i] = sid_x86_nan(ph);
+            c2[i] = sid_x86_nan(pt);
+            const bool het = ld_gt(aT, aH) && !isnan(ph) && !isnan(pt);   // P_het > P_hom
+            code[i] = (uint8_t)(f | ((het ? s : f) << 2) | (het ? 0x80u : 0u));
+        }
+    }
+}
+
+// Compact class hash: slot -> profile index (or ~0u); open addressing.
+__global__ __launch_bounds__(256) void sid_lookup_kernel(const uint64_t* __restrict__ counts, size_t n,
+                                                         const unsigned long long* __restrict__ ckeys,
+                                                         const uint32_t* __restrict__ cidx,
+                                                         uint64_t cmask, uint32_t special_idx,
+                                                         const uint8_t* __restrict__ pcode,
+                                                         const double* __restrict__ p1,
+                                                         const double* __restrict__ p2,
+                                                         uint8_t* __restrict__ code,
+                                                         double* __restrict__ hom,
+                                                         double* __restrict__ het)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t key = sid_profile_key(counts[i]);
+        uint64_t h = sid_hash64(key) & cmask;
+        uint32_t idx = 0xFFFFFFFFu;
+        if (key == SID_EMPTY_KEY) {        // the all-65535 profile is kept out of the table
+            idx = special_idx;
+        } else {
+            for (uint64_t probe = 0; probe <= cmask; ++probe) {
+                const unsigned long long k = ckeys[h];
+                if (k == key) {
+                    idx = cidx[h];
+                    break;
+                }
+                if (k == SID_EMPTY_KEY) break;
+                h = (h + 1) & cmask;
+            }
+        }
+        if (idx == 0xFFFFFFFFu) {          // profile filtered (coverage < 4): no record
+            code[i] = 0x40;
+            hom[i] = 0.0;
+            het[i] = 0.0;
+        } else {
+            code[i] = pcode[idx];
+            hom[i] = p1[idx];
+            het[i] = p2[idx];
+        }
+    }
+}
+
+// ------------------------------------------------------------ launchers --
+extern "C" {
+
+hipError_t sid_launch_hist(const uint16_t* counts, size_t n, unsigned long long* gkeys,
+                           unsigned long long* gcnt, uint64_t gmask, unsigned long long* stats,
+                           hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const size_t per_block = 16384;
+    const size_t grid = (n + per_block - 1) / per_block;
+    sid_hist_kernel<<<(unsigned)grid, 256, 0, st>>>((const uint64_t*)counts, n, per_block, gkeys, gcnt,
+                                                    gmask, stats);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_rehash(const unsigned long long* okeys, const unsigned long long* ocnt,
+                             uint64_t ocap, unsigned long long* gkeys, unsigned long long* gcnt,
+                             uint64_t gmask, unsigned long long* distinct, hipStream_t st)
+{
+    uint64_t g = (ocap + 255) / 256;
+    sid_hist_rehash_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(okeys, ocnt, ocap, gkeys,
+                                                                            gcnt, gmask, distinct);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_compact(const unsigned long long* gkeys, const unsigned long long* gcnt,
+                              uint64_t cap, unsigned long long* okeys, unsigned long long* ocnt,
+                              unsigned long long* nout, hipStream_t st)
+{
+    uint64_t g = (cap + 255) / 256;
+    sid_hist_compact_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(gkeys, gcnt, cap, okeys,
+                                                                             ocnt, nout);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_objective(const uint64_t* keys, const uint32_t* cnt, const double* lnM, size_t u,
+                                const sid_lynch_eval* E, double* partial, int grid, hipStream_t st)
+{
+    sid_objective_kernel<<<grid, 256, 0, st>>>(keys, cnt, lnM, u, *E, partial);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_profile_lik(const uint64_t* keys, const double* lnM, size_t u,
+                                  const sid_lynch_eval* E, double* lhom, double* lhet, hipStream_t st)
+{
+    if (u == 0) return hipSuccess;
+    uint64_t g = (u + 255) / 256;
+    sid_profile_lik_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(keys, lnM, u, *E, lhom, lhet);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_classify(const uint64_t* keys, const double* lhom, const double* lhet, size_t u,
+                               int mode, int use_prior, double pi, double lg15, double* c1, double* c2,
+                               uint8_t* code, hipStream_t st)
+{
+    if (u == 0) return hipSuccess;
+    uint64_t g = (u + 255) / 256;
+    sid_classify_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(keys, lhom, lhet, u, mode,
+                                                                         use_prior, pi, lg15, c1, c2, code);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned long long* ckeys,
+                             const uint32_t* cidx, uint64_t cmask, uint32_t special_idx,
+                             const uint8_t* pcode,
+                             const double* p1, const double* p2, uint8_t* code, double* hom,
+                             double* het, int grid_cap, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    uint64_t g = (n + 255) / 256;
+    unsigned grid = (unsigned)(g < (uint64_t)grid_cap ? g : (uint64_t)grid_cap);
+    sid_lookup_kernel<<<grid, 256, 0, st>>>((const uint64_t*)counts, n, ckeys, cidx, cmask, special_idx,
+                                            pcode, p1, p2,
+                                            code, hom, het);
+    return hipGetLastError();
+}
+
+}  // extern "C"

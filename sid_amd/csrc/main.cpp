@@ -1,0 +1,415 @@
+// main.cpp — the `sid` command line on MI355X.
+//
+// Same surface as sid.cpp:1-110: getopt flags -h -m -r -R -p -E with the
+// reference's defaults, help text, error messages and exit codes; CSV on
+// stdout, "# ..." diagnostics on stderr.  Behind it:
+//
+//   mmap(file) -> sid_parse_text (N host threads) -> counts resident in HBM
+//   (one shard per GPU) -> sid_call_local | sid_profile_* + sid_lynch_prepare
+//   + sid_lookup_sites -> code/confs back to pinned host memory ->
+//   sid_format_csv (N host threads) -> stdout in input order.
+//
+// Extra long options (no short letter, so they cannot collide with the
+// reference's flags): --devices N, --threads N, --stats.
+//
+// As in the reference, the whole input is parsed before anything is written
+// to stdout, so a malformed line aborts with no CSV output (call.cpp:11-20
+// reads the file before sid.cpp:102 prints the header).
+#include <fcntl.h>
+#include <getopt.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <csignal>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/sid.h"
+
+namespace {
+
+struct Options {
+    std::string method = "local";
+    sid_opts o;
+    int devices = 1;
+    int threads = 0;
+    bool stats = false;
+};
+
+// sid.cpp:26-58; std::map<char,...> iterates E R h m p r
+const struct {
+    char flag;
+    const char* name;
+    int has_arg;
+    const char* description;
+} OPTIONS[] = {
+    {'E', "ERROR", 1, "Maximum allowed site error rate for 'local' method. Default: 0.1"},
+    {'R', "", 0, "Estimate SNP prior from data, applicable for methods 'likelihood_ratio', 'local', 'quality'. Conflicts -r."},
+    {'h', "help", 0, "Print this help message"},
+    {'m', "METHOD", 1, "Select the method to use for SNP calling: 'likelihood_ratio' , 'bayes', 'local' or 'quality', default: local"},
+    {'p', "LEVEL", 1, "Significance level for statistical tests, only applicable for methods 'likelihood_ratio', 'local'. Default: 0.05"},
+    {'r', "PRIOR", 1, "Use the given prior for SNPs, applicable for methods 'local', 'quality'. Conflicts -R. Default: no prior"},
+};
+
+[[noreturn]] void terminate_like(const char* type, const char* what)
+{
+    std::fflush(stdout);
+    std::fprintf(stderr, "terminate called after throwing an instance of '%s'\n  what():  %s\n", type, what);
+    std::abort();
+}
+
+[[noreturn]] void fail(const char* what, int rc)
+{
+    std::fflush(stdout);
+    if (rc == SID_EHIP)
+        std::fprintf(stderr, "sid: %s: %s (hip error %d)\n", what, sid_strerror(rc), sid_last_hip_error());
+    else
+        std::fprintf(stderr, "sid: %s: %s\n", what, sid_strerror(rc));
+    std::exit(EXIT_FAILURE);
+}
+
+#define CHECK(call, what)                 \
+    do {                                  \
+        int rc_ = (call);                 \
+        if (rc_ != SID_OK) fail(what, rc_); \
+    } while (0)
+
+#define HCHECK(call, what)                                                              \
+    do {                                                                                \
+        hipError_t e_ = (call);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            std::fprintf(stderr, "sid: %s: %s\n", what, hipGetErrorString(e_));         \
+            std::exit(EXIT_FAILURE);                                                    \
+        }                                                                               \
+    } while (0)
+
+double now()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Input {
+    const char* data = nullptr;
+    size_t len = 0;
+    void* map = nullptr;
+    std::string owned;
+};
+
+// std::ifstream semantics: open failure -> "Could not open file" (sid.cpp:86-89)
+bool open_input(const char* path, Input& in)
+{
+    int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return false;
+    struct stat st;
+    if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+        in.len = (size_t)st.st_size;
+        if (in.len) {
+            in.map = mmap(nullptr, in.len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            if (in.map == MAP_FAILED) {
+                in.map = nullptr;
+            } else {
+                madvise(in.map, in.len, MADV_SEQUENTIAL);
+                in.data = (const char*)in.map;
+            }
+        }
+        if (in.len && !in.map) {   // fall back to read()
+            in.owned.resize(in.len);
+            size_t off = 0;
+            while (off < in.len) {
+                ssize_t r = ::read(fd, &in.owned[off], in.len - off);
+                if (r <= 0) break;
+                off += (size_t)r;
+            }
+            in.owned.resize(off);
+            in.data = in.owned.data();
+            in.len = off;
+        }
+    } else if (fstat(fd, &st) == 0 && S_ISDIR(st.st_mode)) {
+        // std::ifstream opens a directory, getline then fails: no records
+        in.len = 0;
+    } else {   // pipe / character device
+        char buf[1 << 16];
+        ssize_t r;
+        while ((r = ::read(fd, buf, sizeof buf)) > 0) in.owned.append(buf, (size_t)r);
+        in.data = in.owned.data();
+        in.len = in.owned.size();
+    }
+    ::close(fd);
+    return true;
+}
+
+struct Shard {
+    size_t begin = 0, end = 0;
+    sid_ctx* ctx = nullptr;
+    uint16_t* d_counts = nullptr;
+    uint8_t* d_code = nullptr;
+    double* d_hom = nullptr;
+    double* d_het = nullptr;
+    hipStream_t stream = nullptr;
+};
+
+}  // namespace
+
+int main(int argc, char** argv)
+{
+    Options opt;
+    sid_opts_default(&opt.o);
+    static const struct option LONG[] = {{"devices", required_argument, nullptr, 1},
+                                         {"threads", required_argument, nullptr, 2},
+                                         {"stats", no_argument, nullptr, 3},
+                                         {nullptr, 0, nullptr, 0}};
+    int flag;
+    while ((flag = getopt_long(argc, argv, "E:Rhm:p:r:", LONG, nullptr)) != -1) {
+        switch (flag) {
+        case 'E': opt.o.site_error_threshold = std::atof(optarg); break;
+        case 'R': opt.o.estimate_prior = 1; break;
+        case 'm': opt.method = optarg; break;
+        case 'p': opt.o.significance_level = std::atof(optarg); break;
+        case 'r': opt.o.snp_prior = std::atof(optarg); break;
+        case 'h':
+            std::fputs("sid [flags] input_file\n", stdout);
+            for (const auto& o : OPTIONS) {
+                std::printf("\t-%c", o.flag);
+                if (o.has_arg > 0) std::printf(" %s", o.name);
+                std::printf("\t%s\n", o.description);
+            }
+            break;
+        case 1: opt.devices = std::max(1, std::atoi(optarg)); break;
+        case 2: opt.threads = std::max(1, std::atoi(optarg)); break;
+        case 3: opt.stats = true; break;
+        default: std::exit(EXIT_FAILURE);
+        }
+    }
+    if (optind >= argc) {
+        std::fflush(stdout);
+        std::fputs("No file name given!\n", stderr);
+        std::exit(EXIT_FAILURE);
+    }
+    const char* path = argv[optind];
+    Input in;
+    if (!open_input(path, in)) {
+        std::fflush(stdout);
+        std::fprintf(stderr, "Could not open file: %s\n", path);
+        std::exit(EXIT_FAILURE);
+    }
+    int method = -1;
+    if (opt.method == "local") method = SID_METHOD_LOCAL;
+    else if (opt.method == "bayes") method = SID_METHOD_BAYES;
+    else if (opt.method == "likelihood_ratio") method = SID_METHOD_LIKELIHOOD_RATIO;
+    else if (opt.method == "quality") {
+        std::fflush(stdout);
+        std::fputs("sid: -m quality is not implemented in this build (SURVEY.md §8(f) rank 3)\n", stderr);
+        std::exit(EXIT_FAILURE);
+    }
+    if (method < 0) {   // sid.cpp:92-102: unknown method -> header only
+        std::printf("chrom,pos,label,gt,hom_conf,het_conf,conf_type\n");
+        return 0;
+    }
+    opt.o.method = method;
+    if (method == SID_METHOD_BAYES) opt.o.estimate_prior = 0;   // callBayes(in) ignores -R/-r/-p
+    const int T = opt.threads > 0 ? opt.threads
+                                  : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+
+    // ---------------------------------------------------------------- parse --
+    double t0 = now();
+    sid_sites* sites = nullptr;
+    uint64_t bad = 0;
+    int prc = sid_parse_text(in.data, in.len, T, &sites, &bad);
+    if (prc == SID_EMALFORMED) terminate_like("std::invalid_argument", "Malformed pileup line");
+    if (prc == SID_ENULLCHROM) {
+        // pileup.cpp:18 assigns a NULL char* to std::string: the reference
+        // dies in strlen() with SIGSEGV, printing nothing
+        std::fflush(stdout);
+        std::signal(SIGSEGV, SIG_DFL);
+        std::raise(SIGSEGV);
+    }
+    CHECK(prc, "parse");
+    if (in.map) munmap(in.map, in.len);
+    in.map = nullptr;
+    const size_t n = sid_sites_count(sites);
+    const uint16_t* h_counts = sid_sites_counts(sites);
+    double t1 = now();
+
+    // -------------------------------------------------------------- compute --
+    uint8_t* h_code = nullptr;
+    double *h_hom = nullptr, *h_het = nullptr;
+    int ndev = 0;
+    CHECK(sid_device_count(&ndev), "device query");
+    if (ndev <= 0) {
+        std::fflush(stdout);
+        std::fputs("sid: no HIP device available\n", stderr);
+        std::exit(EXIT_FAILURE);
+    }
+    const int D = std::max(1, std::min(opt.devices, ndev));
+    const size_t nn = std::max<size_t>(n, 1);
+    if (hipHostMalloc((void**)&h_code, nn, hipHostMallocDefault) != hipSuccess) h_code = (uint8_t*)std::malloc(nn);
+    if (hipHostMalloc((void**)&h_hom, nn * 8, hipHostMallocDefault) != hipSuccess) h_hom = (double*)std::malloc(nn * 8);
+    if (hipHostMalloc((void**)&h_het, nn * 8, hipHostMallocDefault) != hipSuccess) h_het = (double*)std::malloc(nn * 8);
+
+    std::vector<Shard> sh(D);
+    for (int d = 0; d < D; ++d) {
+        sh[d].begin = n * d / D;
+        sh[d].end = n * (d + 1) / D;
+    }
+    const bool lynch = method != SID_METHOD_LOCAL || opt.o.estimate_prior;
+    auto upload = [&](int d) {
+        Shard& s = sh[d];
+        CHECK(sid_create(d, &opt.o, &s.ctx), "context");
+        HCHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "stream");
+        const size_t m = std::max<size_t>(s.end - s.begin, 1);
+        HCHECK(hipMalloc(&s.d_counts, m * 8), "device counts");
+        HCHECK(hipMalloc(&s.d_code, m), "device code");
+        HCHECK(hipMalloc(&s.d_hom, m * 8), "device hom_conf");
+        HCHECK(hipMalloc(&s.d_het, m * 8), "device het_conf");
+        if (s.end > s.begin)
+            HCHECK(hipMemcpyAsync(s.d_counts, h_counts + 4 * s.begin, (s.end - s.begin) * 8,
+                                  hipMemcpyHostToDevice, s.stream),
+                   "H2D");
+        if (lynch) {
+            CHECK(sid_profile_reset(s.ctx, s.stream), "histogram");
+            CHECK(sid_profile_accumulate(s.ctx, s.d_counts, s.end - s.begin, s.stream), "histogram");
+        }
+        HCHECK(hipStreamSynchronize(s.stream), "H2D");
+    };
+    auto finish = [&](int d) {
+        Shard& s = sh[d];
+        (void)hipSetDevice(d);
+        const size_t m = s.end - s.begin;
+        if (method == SID_METHOD_LOCAL)
+            CHECK(sid_call_local(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "local");
+        else
+            CHECK(sid_lookup_sites(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "lookup");
+        if (m) {
+            HCHECK(hipMemcpyAsync(h_code + s.begin, s.d_code, m, hipMemcpyDeviceToHost, s.stream), "D2H");
+            HCHECK(hipMemcpyAsync(h_hom + s.begin, s.d_hom, m * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
+            HCHECK(hipMemcpyAsync(h_het + s.begin, s.d_het, m * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
+        }
+        HCHECK(hipStreamSynchronize(s.stream), "D2H");
+    };
+    {
+        std::vector<std::thread> th;
+        for (int d = 1; d < D; ++d) th.emplace_back(upload, d);
+        upload(0);
+        for (auto& x : th) x.join();
+    }
+    if (lynch) {
+        // merge the per-device histograms (the single exchange of the path)
+        std::vector<uint64_t> keys, cnts;
+        for (int d = 0; d < D; ++d) {
+            (void)hipSetDevice(d);
+            size_t u = 0;
+            CHECK(sid_profile_table(sh[d].ctx, nullptr, nullptr, 0, &u), "profile table");
+            size_t at = keys.size();
+            keys.resize(at + u);
+            cnts.resize(at + u);
+            CHECK(sid_profile_table(sh[d].ctx, keys.data() + at, cnts.data() + at, u, &u), "profile table");
+        }
+        std::vector<int> rcs(D, SID_OK);
+        std::vector<sid_estimate> est(D);
+        auto prep = [&](int d) {
+            (void)hipSetDevice(d);
+            if (D > 1) {
+                int rc = sid_profile_load(sh[d].ctx, keys.data(), cnts.data(), keys.size());
+                if (rc) { rcs[d] = rc; return; }
+            }
+            rcs[d] = sid_lynch_prepare(sh[d].ctx, d == 0, &est[d]);
+            if (rcs[d] == SID_OK && method == SID_METHOD_LOCAL)
+                rcs[d] = sid_set_prior(sh[d].ctx, est[d].heterozygosity);   // call.cpp:233
+        };
+        // device 0 prints the reference's diagnostics; the others run the same
+        // deterministic estimate silently
+        prep(0);
+        if (rcs[0] == SID_EEMPTY) {
+            std::fflush(stdout);
+            std::fputs("sid: no profile with coverage >= 4 (the reference crashes here)\n", stderr);
+            std::exit(139);
+        }
+        if (rcs[0] == SID_EBADFUNC) {
+            std::fflush(stdout);
+            std::fputs("gsl: nmsimplex2.c: ERROR: non-finite function value encountered\n"
+                       "Default GSL error handler invoked.\n", stderr);
+            std::abort();
+        }
+        CHECK(rcs[0], "estimate");
+        std::vector<std::thread> th;
+        for (int d = 1; d < D; ++d) th.emplace_back(prep, d);
+        for (auto& x : th) x.join();
+        for (int d = 1; d < D; ++d) CHECK(rcs[d], "estimate");
+    }
+    {
+        std::vector<std::thread> th;
+        for (int d = 1; d < D; ++d) th.emplace_back(finish, d);
+        finish(0);
+        for (auto& x : th) x.join();
+    }
+    double t2 = now();
+
+    // ----------------------------------------------------------------- emit --
+    std::fputs("chrom,pos,label,gt,hom_conf,het_conf,conf_type\n", stdout);
+    std::fflush(stdout);
+    const char* conf_type = method == SID_METHOD_BAYES ? "probability" : "p_value";
+    const size_t BLOCK = 1u << 18;
+    const size_t nblocks = (n + BLOCK - 1) / BLOCK;
+    std::vector<std::vector<char>> bufs(nblocks);
+    std::vector<size_t> lens(nblocks, 0);
+    std::vector<std::atomic<int>> ready(nblocks);
+    for (auto& r : ready) r.store(0);
+    std::atomic<size_t> next{0};
+    auto worker = [&] {
+        for (;;) {
+            size_t b = next.fetch_add(1);
+            if (b >= nblocks) return;
+            size_t lo = b * BLOCK, hi = std::min(n, lo + BLOCK);
+            size_t need = 0;
+            sid_format_csv(sites, lo, hi, h_code, h_hom, h_het, conf_type, nullptr, 0, &need);
+            bufs[b].resize(need);
+            size_t len = 0;
+            int rc = sid_format_csv(sites, lo, hi, h_code, h_hom, h_het, conf_type, bufs[b].data(), need, &len);
+            lens[b] = rc == SID_OK ? len : 0;
+            ready[b].store(1, std::memory_order_release);
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t) th.emplace_back(worker);
+        for (size_t b = 0; b < nblocks; ++b) {
+            while (!ready[b].load(std::memory_order_acquire)) std::this_thread::yield();
+            size_t off = 0;
+            while (off < lens[b]) {
+                ssize_t w = ::write(1, bufs[b].data() + off, lens[b] - off);
+                if (w <= 0) break;
+                off += (size_t)w;
+            }
+            std::vector<char>().swap(bufs[b]);
+        }
+        for (auto& x : th) x.join();
+    }
+    double t3 = now();
+    if (opt.stats) {
+        std::fprintf(stderr,
+                     "{\"sites\": %zu, \"devices\": %d, \"threads\": %d, \"parse_s\": %.6f, "
+                     "\"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, \"sites_per_s\": %.1f}\n",
+                     n, D, T, t1 - t0, t2 - t1, t3 - t2, t3 - t0, n / std::max(1e-9, t3 - t0));
+    }
+    for (auto& s : sh) {
+        (void)hipSetDevice((int)(&s - sh.data()));
+        (void)hipFree(s.d_counts);
+        (void)hipFree(s.d_code);
+        (void)hipFree(s.d_hom);
+        (void)hipFree(s.d_het);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+        sid_destroy(s.ctx);
+    }
+    sid_sites_free(sites);
+    return 0;
+}

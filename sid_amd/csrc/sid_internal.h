@@ -1,0 +1,44 @@
+// sid_internal.h — libsid.so internals shared by the C-ABI translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/sid.h"
+#include "sid_math.h"
+
+// kernels (local.hip, synth.hip, lynch.hip)
+extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t* code,
+                                       double* hom, double* het, const sid_local_k* K,
+                                       const double* d_lnt, int grid_cap, hipStream_t stream);
+extern "C" hipError_t sid_launch_synth(uint64_t seed, uint64_t first, size_t n,
+                                       const uint64_t* d_cdf, uint32_t kmax, uint16_t* counts,
+                                       hipStream_t stream);
+
+// Lynch-path device state (lynch.hip)
+struct sid_lynch_dev;
+sid_lynch_dev* sid_lynch_dev_create(int* err);
+void sid_lynch_dev_destroy(sid_lynch_dev* L);
+
+struct sid_ctx {
+    int device = 0;
+    sid_opts opts{};
+    sid_local_k K{};
+    double* d_lnt = nullptr;     // ln(k), k < SID_LUTN
+    int grid_cap = 2048;
+    // synthetic generator: Poisson CDF thresholds for the last mean depth
+    uint64_t* d_cdf = nullptr;
+    uint32_t cdf_k = 0;
+    double cdf_mean = -1.0;
+    // Lynch path
+    sid_lynch_dev* lynch = nullptr;
+};
+
+// host helpers (capi.cpp)
+int sid_set_hip_error(hipError_t e);
+double sid_gsl_lngamma(double x);   // GSL 2.7.1 gsl_sf_lngamma restated (x >= 0.5)
+void sid_build_local_k(const sid_opts& o, sid_local_k* K);
+// Poisson(mean) CDF as 64-bit thresholds (synth.h); returns kmax
+uint32_t sid_poisson_cdf(double mean, std::vector<uint64_t>& cdf);

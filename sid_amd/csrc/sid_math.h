@@ -1,0 +1,196 @@
+// sid_math.h — device arithmetic shared by the sid kernels (gfx950).
+//
+// The reference computes likelihoods in x87 80-bit long double, linear domain
+// (lynch.hpp:48-96, call.cpp:247-262); gfx950 has no 80-bit type, so the
+// kernels work in the log domain in f64:
+//
+//   * fast path (every site of the 30x/200x configs): ln l = sum n*ln(base)
+//     from an LDS table of ln(k); the multinomial coefficient M cancels in
+//     every likelihood ratio, so it is not evaluated.  Valid while every
+//     long-double intermediate of the reference stays a normal number; the
+//     caller checks the bound and otherwise takes
+//   * the emulated path: each long-double value is carried as (ln|v|, sign)
+//     and every multiplication is rounded through ld_round(), which applies
+//     the x87 format's overflow (-> inf), denormal quantisation (2^-16445
+//     steps) and underflow (-> 0), so 0, inf, NaN and the denormal region
+//     come out where the reference's long doubles put them.
+//
+// The chi-square tail (gsl_cdf_chisq_Q(x, 1), stats.cpp:33-35) is
+// erfc(sqrt(x/2)) in the normal range; in the denormal range it follows
+// GSL 2.7.1's gamma_inc_Q_CF (D * (a/x) * F) so the result rounds like GSL's.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SID_LUTN 1024               // ln(k) table, k < SID_LUTN  (coverage < 1024 fast path)
+#define SID_LN2 0.69314718055994530942
+#define SID_LN3 1.09861228866810969140
+#define SID_LN_LDBL_MAX 11356.523406294143949      // ln(LDBL_MAX), x87 80-bit
+#define SID_LN_LDBL_MIN (-11355.137111933024058)   // ln(LDBL_MIN) = -16382 ln 2
+#define SID_LDBL_DENORM_SHIFT 11398.805021138601254 // 16445 ln 2: ln(LDBL_TRUE_MIN) = -shift
+#define SID_FAST_FLOOR (-11000.0)                   // fast path while every ln >= this
+
+struct sid_local_k {
+    double E;          // site_error_threshold
+    double sig;        // significance_level
+    double cA1, cB1;   // ln(1-E), ln(E/3.)            capped hom bases
+    double cA2, cB2;   // ln((1-2./3.*E)/2.), ln(E/3.) capped het bases
+    double lp1, lp2;   // ln|1-prior|, ln(prior)        (prior_on)
+    double prior;      // snp_prior
+    double lg15;       // GSL lngamma(1.5) (gamma_inc_D)
+    int prior_on;      // snp_prior > 0                 call.cpp:256
+    int general;       // E < 0 or prior > 1: every site takes the emulated path
+};
+
+// Per-(pi, eps) constants of the 10-genotype mixture (lynch.hpp:57-90),
+// computed on the host for each objective evaluation.
+struct sid_lynch_eval {
+    double la;        // ln(1 - e)
+    double lb;        // ln(e / 3.)
+    double lh;        // ln((1 - 2./3. * e) / 2.)
+    double ld[4];     // ln d_i
+    double ldd[6];    // ln(d_i * d_j), i < j (double product, lynch.hpp:65)
+    double lnorm;     // -ln(1 - sum d_i^2)          (lynch.hpp:70-72)
+    double l1p, lp;   // ln(1 - pi), ln(pi)
+};
+
+// ---------------------------------------------------------------- chi^2_1 --
+// GSL 2.7.1 gamma_inc_F_CF (modified Lentz), a = 0.5.
+__device__ __forceinline__ double sid_gamma_F_CF(double x)
+{
+    const double eps = 2.2204460492503131e-16;
+    const double small = eps * eps * eps;
+    double hn = 1.0, Cn = 1.0 / small, Dn = 1.0;
+    for (int n = 2; n < 5000; n++) {
+        double an = (n & 1) ? 0.5 * (n - 1) / x : (0.5 * n - 0.5) / x;
+        Dn = 1.0 + an * Dn;
+        if (fabs(Dn) < small) Dn = small;
+        Cn = 1.0 + an / Cn;
+        if (fabs(Cn) < small) Cn = small;
+        Dn = 1.0 / Dn;
+        double delta = Cn * Dn;
+        hn *= delta;
+        if (fabs(delta - 1.0) < eps) break;
+    }
+    return hn;
+}
+
+// gsl_cdf_chisq_Q(x, 1) (cdf/chisq.c -> cdf/gamma.c gsl_cdf_gamma_Q(x, 0.5, 2))
+__device__ __noinline__ double sid_chisq_Q_tail(double y, double lg15)
+{
+    if (isinf(y)) return __builtin_nan("");           // D = exp(inf - inf)
+    if (y > 1.0e6) return 0.0;                          // gamma_inc_Q_large_x: D == 0
+    double D = exp(0.5 * log(y) - y - lg15);            // gamma_inc_D, a < 10
+    return D * (0.5 / y) * sid_gamma_F_CF(y);
+}
+
+__device__ __forceinline__ double sid_chisq_Q(double x, double lg15)
+{
+    if (!(x > 0.0)) return (x <= 0.0) ? 1.0 : x;        // x <= 0 -> 1; NaN -> NaN
+    double y = x / 2.0;
+    if (y <= 700.0) return erfc(sqrt(y));               // Q(1/2, y) = erfc(sqrt(y)), normal range
+    return sid_chisq_Q_tail(y, lg15);
+}
+
+// ------------------------------------------------------ major alleles a5 --
+// call.cpp:52-60: stable ascending sort of {0,1,2,3} by count -> first =
+// idx[3], second = idx[2].  Equivalent key 4*count+idx (ties -> higher index).
+__device__ __forceinline__ void sid_major(uint64_t w, uint32_t& f, uint32_t& s, uint32_t& nf,
+                                          uint32_t& ns, uint32_t& cov)
+{
+    uint32_t n0 = (uint32_t)(w & 0xffffu), n1 = (uint32_t)((w >> 16) & 0xffffu);
+    uint32_t n2 = (uint32_t)((w >> 32) & 0xffffu), n3 = (uint32_t)(w >> 48);
+    uint32_t k0 = n0 << 2, k1 = (n1 << 2) | 1u, k2 = (n2 << 2) | 2u, k3 = (n3 << 2) | 3u;
+    uint32_t a = max(k0, k1), b = min(k0, k1), c = max(k2, k3), d = min(k2, k3);
+    uint32_t kf = max(a, c);
+    uint32_t ks = max(min(a, c), max(b, d));
+    f = kf & 3u;
+    s = ks & 3u;
+    nf = kf >> 2;
+    ns = ks >> 2;
+    cov = n0 + n1 + n2 + n3;
+}
+
+// ------------------------------------------ emulated x87 long double ------
+struct sid_ld {
+    double ln;   // ln|v|: -inf = 0, +inf = inf, NaN = NaN
+    int neg;
+};
+
+__device__ __forceinline__ sid_ld ld_round(sid_ld v)
+{
+    if (v.ln > SID_LN_LDBL_MAX) {
+        v.ln = __builtin_inf();
+    } else if (v.ln < SID_LN_LDBL_MIN && v.ln != -__builtin_inf()) {
+        double q = rint(exp(v.ln + SID_LDBL_DENORM_SHIFT));   // multiples of LDBL_TRUE_MIN
+        v.ln = (q == 0.0) ? -__builtin_inf() : log(q) - SID_LDBL_DENORM_SHIFT;
+    }
+    return v;
+}
+
+__device__ __forceinline__ sid_ld ld_mul(sid_ld a, sid_ld b)
+{
+    sid_ld r;
+    r.ln = a.ln + b.ln;   // 0 * inf -> (-inf) + inf = NaN, as in IEEE
+    r.neg = a.neg ^ b.neg;
+    return ld_round(r);
+}
+
+__device__ __forceinline__ sid_ld ld_from_double(double x)
+{
+    sid_ld r;
+    r.ln = (x == 0.0) ? -__builtin_inf() : log(fabs(x));
+    r.neg = x < 0.0;
+    return r;
+}
+
+// powl(b, n) for an integer exponent n >= 0
+__device__ __forceinline__ sid_ld ld_pow(double b, uint32_t n)
+{
+    sid_ld r;
+    if (n == 0) {
+        r.ln = 0.0;   // powl(x, 0) == 1 for every x, NaN included
+        r.neg = 0;
+        return r;
+    }
+    r.ln = (b == 0.0) ? -__builtin_inf() : (double)n * log(fabs(b));
+    r.neg = (b < 0.0) && (n & 1u);
+    return ld_round(r);
+}
+
+__device__ __forceinline__ bool ld_is_zero(sid_ld a) { return a.ln == -__builtin_inf(); }
+
+// a > b on the represented long doubles (false if either is NaN)
+__device__ __forceinline__ bool ld_gt(sid_ld a, sid_ld b)
+{
+    if (isnan(a.ln) || isnan(b.ln)) return false;
+    int sa = ld_is_zero(a) ? 0 : (a.neg ? -1 : 1);
+    int sb = ld_is_zero(b) ? 0 : (b.neg ? -1 : 1);
+    if (sa != sb) return sa > sb;
+    if (sa > 0) return a.ln > b.ln;
+    if (sa < 0) return a.ln < b.ln;
+    return false;
+}
+
+// stats.cpp:29-37 likelihoodRatioTest(l_H0, l_H1) on emulated long doubles
+__device__ __noinline__ double ld_lrt(sid_ld l0, sid_ld l1, double lg15)
+{
+    if (ld_is_zero(l0)) return 0.0;                           // gsl_cdf_chisq_Q(DBL_MAX, 1)
+    if (isnan(l0.ln) || l0.neg) return __builtin_nan("");     // logl(NaN / negative)
+    bool take1 = !isnan(l1.ln) && ld_gt(l1, l0);              // fmaxl(l0, l1)
+    double mx = take1 ? l1.ln : l0.ln;
+    double chisq = -2.0 * (l0.ln - mx);
+    return sid_chisq_Q(chisq, lg15);
+}
+
+// multinomialCoefficient, lynch.hpp:48-55: expl of the double lnGamma sum
+__device__ __forceinline__ double sid_ln_multinomial(uint64_t w, uint32_t cov)
+{
+    double v = lgamma((double)cov + 1.0);
+    v -= lgamma((double)(w & 0xffffu) + 1.0);
+    v -= lgamma((double)((w >> 16) & 0xffffu) + 1.0);
+    v -= lgamma((double)((w >> 32) & 0xffffu) + 1.0);
+    v -= lgamma((double)(w >> 48) + 1.0);
+    return v;
+}

@@ -1,0 +1,84 @@
+"""Device-side conveniences over the C ABI (tests, bench, smoke).
+
+Buffers are torch CUDA(=HIP) tensors used purely as device allocations; every
+computation runs in libsid.so kernels.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import Context, Estimate, lib  # noqa: F401
+
+
+def _torch():
+    lib()  # torch is imported before libsid.so
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("no HIP device visible: sid_amd.gpu needs an MI355X")
+    return torch
+
+
+def device_buffers(n: int, device: int = 0):
+    """counts (n,4) int16, code (n) uint8, hom/het (n) float64 on `device`."""
+    torch = _torch()
+    dev = torch.device("cuda", device)
+    counts = torch.empty((max(n, 1), 4), dtype=torch.int16, device=dev)
+    code = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    hom = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+    het = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+    return counts, code, hom, het
+
+
+def stream_handle(device: int = 0):
+    torch = _torch()
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def to_device(counts_np: np.ndarray, device: int = 0):
+    torch = _torch()
+    a = np.ascontiguousarray(counts_np, np.uint16).view(np.int16)
+    return torch.from_numpy(a.copy()).to(torch.device("cuda", device))
+
+
+def run_local(counts_np: np.ndarray, device: int = 0, **opts):
+    """-m local over host counts; returns (code, hom_conf, het_conf) numpy."""
+    torch = _torch()
+    n = len(counts_np)
+    ctx = Context(device, method="local", **opts)
+    d_counts = to_device(counts_np.reshape(-1, 4), device) if n else None
+    _, code, hom, het = device_buffers(n, device)
+    st = stream_handle(device)
+    if n:
+        ctx.call_local(d_counts.data_ptr(), n, code.data_ptr(), hom.data_ptr(), het.data_ptr(), st)
+    torch.cuda.synchronize(device)
+    ctx.close()
+    return code[:n].cpu().numpy(), hom[:n].cpu().numpy(), het[:n].cpu().numpy()
+
+
+def run_method(counts_np: np.ndarray, method: str = "local", device: int = 0, verbose=False, **opts):
+    """Full method on host counts, as the CLI runs it on one device.
+
+    Returns (code, hom_conf, het_conf, estimate-or-None)."""
+    torch = _torch()
+    n = len(counts_np)
+    estimate_prior = bool(opts.get("estimate_prior", False))
+    ctx = Context(device, method=method, **opts)
+    d_counts = to_device(counts_np.reshape(-1, 4), device) if n else None
+    _, code, hom, het = device_buffers(n, device)
+    st = stream_handle(device)
+    cptr = d_counts.data_ptr() if n else None
+    est = None
+    if method != "local" or estimate_prior:
+        ctx.profile_reset(st)
+        ctx.profile_accumulate(cptr, n, st)
+        est = ctx.lynch_prepare(verbose)
+        if method == "local":
+            ctx.set_prior(est.heterozygosity)
+    if n:
+        if method == "local":
+            ctx.call_local(cptr, n, code.data_ptr(), hom.data_ptr(), het.data_ptr(), st)
+        else:
+            ctx.lookup_sites(cptr, n, code.data_ptr(), hom.data_ptr(), het.data_ptr(), st)
+    torch.cuda.synchronize(device)
+    ctx.close()
+    return code[:n].cpu().numpy(), hom[:n].cpu().numpy(), het[:n].cpu().numpy(), est

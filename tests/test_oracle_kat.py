@@ -1,0 +1,143 @@
+"""Pin the CPU oracle (and the product's host parser) to the reference's own
+known answers: the Catch KATs of test/*.cpp (tests/golden/kat.json) and, when
+oracle/_ref is built, the reference's pileup.cpp itself.  CPU only."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KAT = json.load(open(os.path.join(HERE, "golden", "kat.json")))
+
+
+def line_for(bases, ref):
+    # a minimal pileup line whose read-bases field is `bases`
+    return b"c\t1\t" + ref.encode() + b"\t0\t" + (bases.encode() if bases else b"*") + b"\t*"
+
+
+@pytest.mark.parametrize("k", KAT["read_bases"], ids=lambda k: k["cite"])
+def test_read_bases_oracle(oracle, k):
+    assert oracle.read_bases(k["bases"].encode(), k["ref"].encode()).tolist() == k["counts"]
+
+
+@pytest.mark.parametrize("k", KAT["read_bases"], ids=lambda k: k["cite"])
+def test_read_bases_product(sid, k):
+    if k["bases"] == "":
+        pytest.skip("an empty read-bases field is not representable inside a tab-separated line")
+    s = sid.parse_text(line_for(k["bases"], k["ref"]))
+    assert s.counts[0].tolist() == k["counts"]
+
+
+@pytest.mark.parametrize("k", KAT["read_bases"], ids=lambda k: k["cite"])
+def test_read_bases_reference_build(oracle, k):
+    if not oracle.ref_pileup_available():
+        pytest.skip("oracle/_ref not built (reference sources absent)")
+    if k["bases"] == "":
+        pytest.skip("empty field")
+    out = oracle.ref_pileup("lines", line_for(k["bases"], k["ref"]) + b"\n").decode().split("\t")
+    assert out[0] == "OK" and [int(x) for x in out[3:7]] == k["counts"]
+
+
+def test_qualities_oracle(oracle):
+    import ctypes as C
+    for k in KAT["qualities"]:
+        buf = (C.c_uint8 * 16)()
+        n = oracle.lib().oracle_parse_qualities(k["text"].encode(), buf, 16)
+        assert list(buf[:n]) == k["values"], k["cite"]
+
+
+def test_full_line(oracle, sid):
+    k = KAT["line"]
+    s = sid.parse_text(k["text"].encode())
+    assert s.chroms == [(0, k["chrom"].encode())]
+    assert s.positions.tolist() == [k["position"]]
+    assert s.counts[0].tolist() == k["counts"]
+    if oracle.ref_pileup_available():
+        out = oracle.ref_pileup("lines", k["text"].encode() + b"\n").decode().split()
+        assert out[:3] == ["OK", k["chrom"], str(k["position"])]
+        assert [int(x) for x in out[3:7]] == k["counts"]
+        q = oracle.ref_pileup("quals", b"++5D5\nDD55D\n").decode().splitlines()
+        assert [int(x) for x in q[0].split()] == k["base_qualities"]
+        assert [int(x) for x in q[1].split()] == k["mapping_qualities"]
+
+
+@pytest.mark.parametrize("k", KAT["unique_profiles"], ids=lambda k: k["cite"])
+def test_unique_profiles(oracle, k):
+    sites = np.array(k["sites"], np.uint16).reshape(-1, 4)
+    rows, _, _ = oracle.unique_profiles(sites)
+    assert [[list(p), c] for p, c, _ in rows] == k["unique"]
+
+
+@pytest.mark.parametrize("k", KAT["distribution"], ids=lambda k: k["cite"])
+def test_distribution(oracle, k):
+    sites = [p for p, c in k["profiles"] for _ in range(c)]
+    d = oracle.distribution(np.array(sites, np.uint16).reshape(-1, 4), min_coverage4=False)
+    assert np.allclose(d, k["dist"], rtol=0, atol=1e-15)
+
+
+def test_distribution_reference_build(oracle):
+    if not oracle.ref_pileup_available():
+        pytest.skip("oracle/_ref not built")
+    rng = np.random.default_rng(7)
+    sites = rng.integers(0, 40, size=(5000, 4)).astype(np.uint16)
+    sites[::7] = sites[3]  # repeats
+    data = "\n".join(" ".join(map(str, r)) for r in sites).encode() + b"\n"
+    ref = oracle.ref_pileup("profiles", data).decode().splitlines()
+    rows, ptr, u = oracle.unique_profiles(sites)
+    assert len(ref) == u + 1
+    for line, (p, c, cov) in zip(ref[:-1], rows):
+        assert [int(x) for x in line.split()] == list(p) + [c, cov]
+    dref = [float(x) for x in ref[-1].split()[1:]]
+    d = oracle.distribution(sites, min_coverage4=False)
+    assert d.tolist() == dref   # bit-exact
+
+
+# ---- GSL restatement: chi-square tail and lnGamma against scipy / mpmath ----
+def test_chisq_Q_against_scipy_mpmath(oracle):
+    import mpmath as mp
+    import scipy.special as sp
+    mp.mp.dps = 50
+    xs = np.concatenate([np.geomspace(1e-12, 1e3, 400), np.linspace(1000, 1400, 50)])
+    for x in xs:
+        q = oracle.chisq_Q(x)
+        t = float(mp.erfc(mp.sqrt(mp.mpf(float(x)) / 2)))
+        assert abs(q - t) <= 1e-12 * t, (x, q, t)      # GSL's own accuracy: ~5e-14
+        s = sp.chdtrc(1, x)
+        assert abs(q - s) <= 1e-12 * s
+    assert oracle.chisq_Q(0.0) == 1.0 and oracle.chisq_Q(-1.0) == 1.0
+    assert oracle.chisq_Q(1.7976931348623157e308) == 0.0
+    assert math.isnan(oracle.chisq_Q(float("nan")))
+
+
+def test_lngamma_against_scipy(oracle):
+    import scipy.special as sp
+    for x in [1.5, 3, 4, 10, 31, 100, 1000, 12345, 262141]:
+        assert abs(oracle.lngamma(x) - sp.gammaln(x)) <= 1e-13 * max(1, abs(sp.gammaln(x)))
+    assert oracle.lngamma(1.0) == 0.0 and oracle.lngamma(2.0) == 0.0
+
+
+# ---- outputs the survey observed from the reference build ----
+EDGE = (b"c1\t1\tA\t0\t*\t*\n"
+        b"c1\t2\tA\t4\tAACC\tIIII\n"
+        b"c1\t3\tA\t4\tCCAA\tIIII\n"
+        b"c1\t4\tN\t6\t..,,GG\tIIIIII\n"
+        b"c1\t5\tA\t4\t.*,N,\tIIII\n"
+        b"\n"
+        b"c1\t6\tA\t4\t.+2AC,-1T.\tIIII\n"
+        b"c1\t7\tG\t12\tGGGGGGCCCCCC\tIIIIIIIIIIII\n"
+        b"c1\t8\tC\t41\t" + b"C" * 41 + b"\tIIII\n"
+        b"c1\t9\tA\t3\t^I.$.a\tIII\n")
+
+
+def test_survey_observed_outputs(oracle, tmp_path):
+    p = tmp_path / "edge.plp"
+    p.write_bytes(EDGE)
+    out = oracle.run_cli([str(p)]).stdout.decode().splitlines()
+    want = {"1": "hom,TT,1,1", "2": "het,CA,1,0.00358864", "3": "het,CA,1,0.00358864",
+            "4": "hom,GG,0.095891,1", "5": "hom,AA,0.0414167,1", "6": "hom,AA,0.0414167,1",
+            "7": "het,GC,1,4.5561e-07", "8": "hom,CC,4.73216e-14,1", "9": "hom,AA,0.0414167,1"}
+    assert out[0] == "chrom,pos,label,gt,hom_conf,het_conf,conf_type"
+    got = {l.split(",")[1]: ",".join(l.split(",")[2:6]) for l in out[1:]}
+    assert got == want
