@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""bench.py — genome sites/s of the sid hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): 50,000,000 synthetic 30x diploid
+sites per GPU, `-m local`.  A step is one pass of the hot path
+(sid_call_local: counts -> code + hom_conf + het_conf) over one batch of 50M
+sites already resident in HBM.  N GPUs = N ranks (torchrun), each with its own
+50M-site range of the counter-based generator (weak scaling, no data-path
+collective; gloo only for the barrier and the max over ranks).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+  roofline      25 algorithmic bytes/site (8 B counts in, 1 B code + 2 x 8 B
+                confs out) / average kernel duration from HIP events on the
+                launch stream, against 8 TB/s HBM3E;
+  cpu_baseline  the oracle's end-to-end CLI (reference sid.cpp/call.cpp
+                restated in C, single thread, text -> CSV) on a bounded sample
+                of the same workload, rank 0 at N=1 only;
+  e2e           the product CLI (build/sid) on the same sample text
+                (parse + GPU + CSV emit), informational.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BYTES_PER_SITE = 25          # 8 in + 17 out
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--sites", type=int, default=50_000_000, help="sites per GPU")
+    p.add_argument("--depth", type=float, default=30.0)
+    p.add_argument("--seed", type=int, default=2)
+    p.add_argument("--cpu-sample", type=int, default=2_000_000,
+                   help="sites in the CPU-baseline / e2e sample (0 = skip)")
+    p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_local_r01.json"),
+                   help="per-launch HBM traffic from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
+    return p.parse_args()
+
+
+def main():
+    a = parse_args()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    import torch  # plumbing: device memory, streams, events, process group
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sid_amd
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    n = a.sites
+    ctx = sid_amd.Context(local_rank)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    counts = torch.empty((n, 4), dtype=torch.int16, device=dev)
+    code = torch.empty(n, dtype=torch.uint8, device=dev)
+    hom = torch.empty(n, dtype=torch.float64, device=dev)
+    het = torch.empty(n, dtype=torch.float64, device=dev)
+    # inputs resident in HBM before the timed region: this rank's site range
+    ctx.synth_counts(a.seed, a.depth, rank * n, n, counts.data_ptr(), sh)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        ctx.call_local(counts.data_ptr(), n, code.data_ptr(), hom.data_ptr(), het.data_ptr(), sh)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        step()
+        e.record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / a.steps
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    # a cheap on-device sanity check of this rank's last step (host oracle
+    # parity is covered by tests/ and smoke())
+    nhet = int((code >= 0x80).sum().item())
+
+    if rank == 0:
+        value = world * n * a.steps / elapsed
+        achieved = BYTES_PER_SITE * n / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if a.pmc_json and os.path.exists(a.pmc_json):
+            try:
+                pm = json.load(open(a.pmc_json))
+                if int(pm.get("sites", -1)) == n:
+                    traffic = pm.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "genome sites/sec (whole node) on 30x synthetic pileup; 1/2/4/8 GPU scaling",
+            "value": value,
+            "unit": "sites/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (counter-based 30x diploid pileup generator, BASELINE.md), counts resident in HBM",
+            "config": {"workload": "C2: -m local, 50M-site 30x synthetic pileup per GPU",
+                       "sites_per_gpu": n, "depth": a.depth, "seed": a.seed, "method": "local",
+                       "parallelism": f"site-range shards x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel_ms": kern_ms, "bytes_per_site": BYTES_PER_SITE},
+            "het_sites_last_step": nhet,
+        }
+        if world == 1 and a.cpu_sample > 0:
+            out["cpu_baseline"], e2e = cpu_and_e2e(a)
+            if e2e is not None:
+                out["e2e"] = e2e
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_and_e2e(a):
+    """Oracle CLI (reference path restated, 1 thread) and product CLI on the same
+    bounded sample text of the C2 workload."""
+    import sid_amd
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    m = a.cpu_sample
+    text = sid_amd.synth_text(a.seed, m, a.depth)
+    base = None
+    e2e = None
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "c2_sample.plp")
+        with open(path, "wb") as f:
+            f.write(text)
+        del text
+        if not os.path.exists(oracle.CLI):
+            oracle.build()
+        t0 = time.perf_counter()
+        with open(os.devnull, "wb") as dn:
+            r = subprocess.run([oracle.CLI, path], stdout=dn, stderr=subprocess.PIPE)
+        dt = time.perf_counter() - t0
+        base = {"value": m / dt if r.returncode == 0 else None, "unit": "sites/s", "cores": 1,
+                "kind": "port",
+                "sample": f"{m:,} sites of the C2 generator (seed {a.seed}, {a.depth:g}x), "
+                          f"pileup text -> CSV to /dev/null, oracle/_build/sid_oracle "
+                          f"(call.cpp/lynch.hpp/stats.cpp restated, single thread), {dt:.2f} s"}
+        if not a.no_e2e and os.path.exists(sid_amd.CLI_PATH):
+            with open(os.devnull, "wb") as dn:
+                t0 = time.perf_counter()
+                r = subprocess.run([sid_amd.CLI_PATH, "--stats", path], stdout=dn, stderr=subprocess.PIPE)
+                dt = time.perf_counter() - t0
+            if r.returncode == 0:
+                try:
+                    st = json.loads(r.stderr.decode().strip().splitlines()[-1])
+                except Exception:
+                    st = {}
+                e2e = {"value": m / dt, "unit": "sites/s", "wall_s": dt, "cli_stats": st,
+                       "note": "build/sid on the same sample text: mmap + parse + H2D + kernel + D2H + "
+                               "CSV emit to /dev/null (includes process start-up and HIP init)"}
+    return base, e2e
+
+
+if __name__ == "__main__":
+    main()

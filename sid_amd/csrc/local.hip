@@ -41,8 +41,8 @@ __device__ __noinline__ uint32_t local_site_general(uint64_t w, const sid_local_
         l1 = ld_mul(l1, ld_from_double(1 - K.prior));
         l2 = ld_mul(l2, ld_from_double(K.prior));
     }
-    p1 = ld_lrt(l2, l1, K.lg15);
-    p2 = ld_lrt(l1, l2, K.lg15);
+    p1 = sid_x86_nan(ld_lrt(l2, l1, K.lg15));
+    p2 = sid_x86_nan(ld_lrt(l1, l2, K.lg15));
     const bool het = ld_gt(l2, l1) && p2 < K.sig;   // call.cpp:266
     return f | ((het ? s : f) << 2) | (het ? 0x80u : 0u);
 }

@@ -279,10 +279,6 @@ __global__ __launch_bounds__(256) void sid_profile_lik_kernel(const uint64_t* __
     }
 }
 
-// x86 prints NaNs made by invalid operations as "-nan" (default NaN has the
-// sign bit set); give every NaN the same sign.
-__device__ __forceinline__ double sid_x86_nan(double v) { return isnan(v) ? -__builtin_nan("") : v; }
-
 // mode 0: likelihood_ratio p-values (before BH); mode 1: bayes posteriors.
 __global__ __launch_bounds__(256) void sid_classify_kernel(const uint64_t* __restrict__ keys,
                                                            const double* __restrict__ lhom,

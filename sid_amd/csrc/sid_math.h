@@ -55,6 +55,10 @@ struct sid_lynch_eval {
     double l1p, lp;   // ln(1 - pi), ln(pi)
 };
 
+// x86 prints NaNs made by invalid operations as "-nan" (default NaN has the
+// sign bit set); give every NaN the same sign.
+__device__ __forceinline__ double sid_x86_nan(double v) { return isnan(v) ? -__builtin_nan("") : v; }
+
 // ---------------------------------------------------------------- chi^2_1 --
 // GSL 2.7.1 gamma_inc_F_CF (modified Lentz), a = 0.5.
 __device__ __forceinline__ double sid_gamma_F_CF(double x)
