@@ -1,0 +1,126 @@
+"""Lynch ML path parity: device histogram, GPU
+objective + host Nelder-Mead, per-profile classification and per-site lookup
+against the oracle (lynch.cpp/optimization.hpp/stats.cpp/call.cpp restated,
+long double).  (pi-hat, eps-hat) must come out bit-identical (same simplex
+trajectory), labels/gt bit-exact, confidences within 1e-10."""
+import numpy as np
+import pytest
+
+from helpers import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def table_via_gpu(gpu, sid, counts, chunks=1):
+    import torch
+    ctx = sid.Context(0, method="likelihood_ratio")
+    d = gpu.to_device(counts)
+    ctx.profile_reset(None)
+    n = len(counts)
+    bounds = np.linspace(0, n, chunks + 1).astype(int)
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        ctx.profile_accumulate(d.data_ptr() + 8 * int(lo), int(hi - lo), None)
+    torch.cuda.synchronize()
+    k, c = ctx.profile_table()
+    ctx.close()
+    return k, c
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_histogram_matches_countUniqueProfiles(gpu, sid, oracle, chunks):
+    counts = sid.synth_counts_host(3, 300_000, 30.0)
+    k, c = table_via_gpu(gpu, sid, counts, chunks)
+    rows, _, u = oracle.unique_profiles(counts)
+    assert len(k) == u
+    assert k.tolist() == [int(sid.profile_key(np.array([p], np.uint16))[0]) for p, _, _ in rows]
+    assert c.tolist() == [cnt for _, cnt, _ in rows]
+
+
+def test_histogram_many_distinct_grows_table(gpu, sid, oracle):
+    rng = np.random.default_rng(1)
+    counts = rng.integers(0, 200, size=(400_000, 4)).astype(np.uint16)   # ~all distinct
+    counts[::5] = counts[1]
+    counts[7] = [65535, 65535, 65535, 65535]                              # sentinel-valued key
+    k, c = table_via_gpu(gpu, sid, counts, chunks=2)
+    kk, cc = np.unique(sid.profile_key(counts), return_counts=True)
+    assert k.tolist() == kk.tolist() and c.tolist() == cc.tolist()
+
+
+def test_objective_matches_compoundLikelihood(gpu, sid, oracle):
+    counts = sid.synth_counts_host(3, 200_000, 30.0)
+    ctx = sid.Context(0, method="likelihood_ratio")
+    d = gpu.to_device(counts)
+    ctx.profile_reset(None)
+    ctx.profile_accumulate(d.data_ptr(), len(counts), None)
+    est = ctx.lynch_setup()
+    assert np.allclose(list(est.dist), oracle.distribution(counts), rtol=0, atol=0)
+    worst = 0.0
+    for pi, eps in [(1e-3, 1e-3), (1.1e-3, 1e-3), (1e-3, 1.1e-3), (5e-4, 8e-3), (0.2, 0.05),
+                    (0.0, 0.01), (1e-3, 0.0), (1.0, 0.5), (-1e-9, 0.1), (0.5, 1.5)]:
+        g = ctx.lynch_objective(pi, eps)
+        r = oracle.compound_likelihood(counts, pi, eps)
+        if r == g:
+            continue
+        rel = abs(g - r) / abs(r)
+        worst = max(worst, rel)
+        assert rel < 1e-13, (pi, eps, g, r)
+    ctx.close()
+
+
+CASES = [
+    ("likelihood_ratio", dict(estimate_prior=True)),
+    ("likelihood_ratio", dict()),
+    ("likelihood_ratio", dict(significance_level=0.2)),
+    ("bayes", dict()),
+    ("local", dict(estimate_prior=True)),
+]
+
+
+@pytest.mark.parametrize("depth,n,seed", [(30.0, 100_000, 3), (200.0, 20_000, 5), (8.0, 50_000, 7)])
+@pytest.mark.parametrize("method,o", CASES, ids=lambda x: str(x))
+def test_method_parity(gpu, sid, oracle, depth, n, seed, method, o):
+    counts = sid.synth_counts_host(seed, n, depth)
+    code, hom, het, est = gpu.run_method(counts, method, **o)
+    rc, rcode, rhom, rhet, rest, u = oracle.call_method(counts, method, **o)
+    assert rc == 0
+    assert (est.heterozygosity, est.error_rate, est.iterations, est.converged) == \
+        (rest.heterozygosity, rest.error_rate, rest.iterations, rest.converged)
+    if method != "local":
+        assert est.n_unique == u
+    assert_parity(code, hom, het, rcode, rhom, rhet, what=f"{method} {o} {depth}x")
+
+
+def test_merged_tables_equal_single_context(gpu, sid, oracle):
+    import torch
+    counts = sid.synth_counts_host(9, 120_000, 30.0)
+    parts = [counts[:50_000], counts[50_000:]]
+    tables = [table_via_gpu(gpu, sid, p) for p in parts]
+    from sid_amd.dist import merge_profile_tables
+    k, c = merge_profile_tables(tables)
+    outs = []
+    for p in parts:
+        ctx = sid.Context(0, method="likelihood_ratio", estimate_prior=True)
+        d = gpu.to_device(p)
+        ctx.profile_reset(None)
+        ctx.profile_accumulate(d.data_ptr(), len(p), None)
+        ctx.profile_load(k, c)
+        ctx.lynch_prepare()
+        _, code, hom, het = gpu.device_buffers(len(p))
+        ctx.lookup_sites(d.data_ptr(), len(p), code.data_ptr(), hom.data_ptr(), het.data_ptr(), None)
+        torch.cuda.synchronize()
+        outs.append((code[:len(p)].cpu().numpy(), hom[:len(p)].cpu().numpy(), het[:len(p)].cpu().numpy()))
+        ctx.close()
+    code = np.concatenate([o[0] for o in outs])
+    hom = np.concatenate([o[1] for o in outs])
+    het = np.concatenate([o[2] for o in outs])
+    rc, rcode, rhom, rhet, rest, u = oracle.call_method(counts, "likelihood_ratio", estimate_prior=True)
+    assert_parity(code, hom, het, rcode, rhom, rhet, what="merged tables")
+
+
+def test_no_profile_with_coverage_4(gpu, sid):
+    counts = np.array([[1, 0, 0, 0], [0, 2, 1, 0], [0, 0, 0, 0]], np.uint16)
+    with pytest.raises(sid.SidError) as e:
+        gpu.run_method(counts, "likelihood_ratio")
+    assert e.value.status == 9
+    code, hom, het, est = gpu.run_method(counts, "local", estimate_prior=True)  # -R local still runs
+    assert len(code) == 3

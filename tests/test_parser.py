@@ -161,3 +161,21 @@ def test_edge_semantics(sid):
     assert s.positions[0] == np.int32(np.int64(99999999999).astype(np.int32))
     assert s.counts[0].tolist() == [2, 0, 0, 0]
     assert len(sid.parse_text(b"")) == 0 and len(sid.parse_text(b"\n\n\n")) == 0
+
+
+def test_fuzz_against_committed_reference_vectors(sid):
+    """Same corpus as above, against the reference's outputs committed in
+    tests/golden/ref_pileup_fuzz.tsv.gz (works where /root/reference is absent)."""
+    import gzip
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_pileup_fuzz.tsv.gz")
+    ref = []
+    for o in gzip.open(path).read().split(b"\n")[:-1]:
+        f = o.split(b"\t")
+        if f[0] == b"OK":
+            ref.append(("OK", f[1].decode("latin-1"), int(f[2])) + tuple(int(x) for x in f[3:7]))
+        else:
+            ref.append(("ERR", f[1].decode()))
+    lines = [l for s in (1, 2, 3) for l in fuzz_lines(s, 1500) if l and not blank(l)]
+    mine = [product_line(sid, l) for l in lines]
+    assert mine == ref

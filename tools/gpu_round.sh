@@ -11,9 +11,10 @@ for s in $STEPS; do
   case $s in
     cli)
       python3 -c "import sys; sys.path.insert(0,'.'); import sid_amd; open('$O/c1.plp','wb').write(sid_amd.synth_text(1, 10000, 30.0))" &&
-      timeout -k 10 120 ./build/sid $O/c1.plp > $O/c1_local.csv 2> $O/cli.err &&
-      ./oracle/_build/sid_oracle $O/c1.plp > $O/c1_local_oracle.csv &&
-      cmp $O/c1_local.csv $O/c1_local_oracle.csv > $O/cli.cmp 2>&1; echo "cli rc=$?" | tee -a $O/steps.log ;;
+      timeout -k 10 120 ./build/sid $O/c1.plp > $O/c1_local.csv 2> $O/cli.err
+      rc=$?; echo "cli rc=$rc" | tee -a $O/steps.log; [ $rc -eq 0 ] || exit $rc
+      ./oracle/_build/sid_oracle $O/c1.plp > $O/c1_local_oracle.csv
+      cmp $O/c1_local.csv $O/c1_local_oracle.csv > $O/cli.cmp 2>&1; echo "cli cmp=$?" | tee -a $O/steps.log ;;
     smoke)
       timeout -k 10 600 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
       rc=$?; echo "smoke rc=$rc" | tee -a $O/steps.log; [ $rc -eq 0 ] || exit $rc ;;
