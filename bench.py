@@ -44,6 +44,8 @@ def parse_args():
     p.add_argument("--cpu-sample", type=int, default=2_000_000,
                    help="sites in the CPU-baseline / e2e sample (0 = skip)")
     p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--direct", action="store_true",
+                   help="A/B: bypass the class-table kernel (SID_LOCAL_DIRECT=1)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_local_r01.json"),
                    help="per-launch HBM traffic from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
     return p.parse_args()
@@ -51,6 +53,8 @@ def parse_args():
 
 def main():
     a = parse_args()
+    if a.direct:
+        os.environ["SID_LOCAL_DIRECT"] = "1"
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
@@ -136,6 +140,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kern_ms, "bytes_per_site": BYTES_PER_SITE},
             "het_sites_last_step": nhet,
+            "kernel_path": "direct" if a.direct else "class-table + fix-up",
         }
         if world == 1 and a.cpu_sample > 0:
             out["cpu_baseline"], e2e = cpu_and_e2e(a)

@@ -105,6 +105,15 @@ extern "C" int sid_device_count(int* n)
     return SID_OK;
 }
 
+// class table of the -m local fast path for the context's options
+static hipError_t sid_build_table(sid_ctx* c)
+{
+    if (c->K.general) return hipSuccess;
+    hipError_t e = sid_launch_local_table_build(&c->K, c->d_lnt, c->ws.table, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return e;
+}
+
 extern "C" int sid_create(int device, const sid_opts* opts, sid_ctx** out)
 {
     if (!out) return SID_EINVAL;
@@ -117,11 +126,21 @@ extern "C" int sid_create(int device, const sid_opts* opts, sid_ctx** out)
     sid_build_local_k(c->opts, &c->K);
     if (const char* g = std::getenv("SID_GRID_CAP")) c->grid_cap = std::max(1, std::atoi(g));
 
+    if (const char* g = std::getenv("SID_TABLE_GRID")) c->ws.table_grid = std::max(1, std::atoi(g));
+    if (const char* g = std::getenv("SID_LOCAL_DIRECT")) c->ws.direct = std::atoi(g) != 0;
+
     std::vector<double> lnt(SID_LUTN);
     lnt[0] = -INFINITY;
     for (int k = 1; k < SID_LUTN; ++k) lnt[k] = std::log((double)k);
+    const size_t tab = 8192;   // SID_TAB_N (local.hip)
+    c->ws.cap = 4u << 20;
     e = hipMalloc(&c->d_lnt, SID_LUTN * sizeof(double));
     if (e == hipSuccess) e = hipMemcpy(c->d_lnt, lnt.data(), SID_LUTN * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&c->ws.table, tab * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&c->ws.miss, (size_t)c->ws.cap * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&c->ws.ctr, 2 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(c->ws.ctr, 0, 2 * sizeof(uint32_t));
+    if (e == hipSuccess) e = sid_build_table(c);
     if (e != hipSuccess) {
         int rc = sid_set_hip_error(e);
         sid_destroy(c);
@@ -137,6 +156,9 @@ extern "C" int sid_destroy(sid_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->d_lnt) (void)hipFree(c->d_lnt);
     if (c->d_cdf) (void)hipFree(c->d_cdf);
+    if (c->ws.table) (void)hipFree(c->ws.table);
+    if (c->ws.miss) (void)hipFree(c->ws.miss);
+    if (c->ws.ctr) (void)hipFree(c->ws.ctr);
     if (c->lynch) sid_lynch_dev_destroy(c->lynch);
     delete c;
     return SID_OK;
@@ -147,7 +169,9 @@ extern "C" int sid_set_prior(sid_ctx* c, double snp_prior)
     if (!c) return SID_EINVAL;
     c->opts.snp_prior = snp_prior;
     sid_build_local_k(c->opts, &c->K);
-    return SID_OK;
+    (void)hipSetDevice(c->device);
+    hipError_t e = sid_build_table(c);
+    return e == hipSuccess ? SID_OK : sid_set_hip_error(e);
 }
 
 extern "C" int sid_call_local(sid_ctx* c, const uint16_t* counts, size_t n, uint8_t* code,
@@ -158,8 +182,9 @@ extern "C" int sid_call_local(sid_ctx* c, const uint16_t* counts, size_t n, uint
     if (!counts || !code || !hom_conf || !het_conf) return SID_EINVAL;
     if (((uintptr_t)counts & 7u) || ((uintptr_t)hom_conf & 7u) || ((uintptr_t)het_conf & 7u))
         return SID_EINVAL;
-    hipError_t e = sid_launch_local(counts, n, code, hom_conf, het_conf, &c->K, c->d_lnt,
+    hipError_t e = sid_launch_local(counts, n, code, hom_conf, het_conf, &c->K, c->d_lnt, &c->ws,
                                     c->grid_cap, (hipStream_t)stream);
+    c->ws.parity ^= 1;   // the fix-up kernel zeroed the other counter
     return e == hipSuccess ? SID_OK : sid_set_hip_error(e);
 }
 

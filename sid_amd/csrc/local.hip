@@ -12,7 +12,7 @@
 // Each thread owns 4 consecutive sites: two 16-B loads, one 4-B code store,
 // two 16-B stores per confidence column, so every wave instruction moves
 // whole 64-B segments.  The ln(k) table lives in LDS (8 KiB per block).
-#include "sid_math.h"
+#include "sid_internal.h"
 
 namespace {
 
@@ -41,28 +41,35 @@ __device__ __noinline__ uint32_t local_site_general(uint64_t w, const sid_local_
         l1 = ld_mul(l1, ld_from_double(1 - K.prior));
         l2 = ld_mul(l2, ld_from_double(K.prior));
     }
-    p1 = sid_x86_nan(ld_lrt(l2, l1, K.lg15));
-    p2 = sid_x86_nan(ld_lrt(l1, l2, K.lg15));
+    // near-tie refinement while both are positive normal long doubles
+    if (!l1.neg && !l2.neg && l1.ln > SID_LN_LDBL_MIN && l2.ln > SID_LN_LDBL_MIN &&
+        l1.ln < SID_LN_LDBL_MAX && l2.ln < SID_LN_LDBL_MAX && fabs(l1.ln - l2.ln) < SID_TIE_BAND &&
+        e1 > 0 && e2 >= 0 && !(K.prior_on && K.prior >= 1)) {
+        const double d = sid_local_refine_d(nf, ns, r2, K.E, K.prior_on, K.prior);
+        l1.ln = l2.ln + d;
+    }
+    p1 = ld_lrt(l2, l1, K.lg15);
+    p2 = ld_lrt(l1, l2, K.lg15);
     const bool het = ld_gt(l2, l1) && p2 < K.sig;   // call.cpp:266
     return f | ((het ? s : f) << 2) | (het ? 0x80u : 0u);
 }
 
-template <bool GENERAL>
-__device__ __forceinline__ uint32_t local_site(uint64_t w, const sid_local_k& K,
-                                               const double* __restrict__ lnt, double& p1,
-                                               double& p2)
+// Fast path of call.cpp:238-273 for a site with major counts nf >= ns and
+// r2 = coverage - nf - ns other reads.  Depends only on (nf, ns, r2) and the
+// options, which is what makes the class table below possible.  Returns
+// false when a long double of the reference would leave the normal range
+// (then the emulated path must be used).
+__device__ __forceinline__ bool local_fast_p(uint32_t nf, uint32_t ns, uint32_t r2,
+                                             const sid_local_k& K, const double* __restrict__ lnt,
+                                             double& p1, double& p2, bool& l2_gt_l1)
 {
-    if (GENERAL) return local_site_general(w, K, p1, p2);
-    uint32_t f, s, nf, ns, cov;
-    sid_major(w, f, s, nf, ns, cov);
-    if (cov >= SID_LUTN) return local_site_general(w, K, p1, p2);
-    const uint32_t r1 = cov - nf, r2 = r1 - ns, m2 = nf + ns;
-
+    const uint32_t cov = nf + ns + r2;
+    if (cov >= SID_LUTN) return false;
+    const uint32_t r1 = cov - nf, m2 = nf + ns;
     // capping decisions on exactly the reference's doubles (call.cpp:243-253)
     const double dc = (double)cov;
     const bool cap1 = (double)r1 / dc > K.E;
     const bool cap2 = 1.5 * (double)r2 / dc > K.E;
-
     // uncapped bases: 1-e1 = nf/c, e1/3 = r1/(3c), (1-2e2/3)/2 = m2/(2c), e2/3 = r2/(2c)
     const double Lc = lnt[cov];
     const double lA1 = cap1 ? K.cA1 : lnt[nf] - Lc;
@@ -78,10 +85,9 @@ __device__ __forceinline__ uint32_t local_site(uint64_t w, const sid_local_k& K,
     const double ninf = -__builtin_inf();
     const bool z1 = ln1 == ninf, z2 = ln2 == ninf;
     // every long double of the reference is a normal number (or an exact 0)?
-    if (!((ln1 >= SID_FAST_FLOOR || z1) && (ln2 >= SID_FAST_FLOOR || z2)))
-        return local_site_general(w, K, p1, p2);
-
-    const double d = ln1 - ln2;
+    if (!((ln1 >= SID_FAST_FLOOR || z1) && (ln2 >= SID_FAST_FLOOR || z2))) return false;
+    double d = ln1 - ln2;
+    if (!z1 && !z2 && fabs(d) < SID_TIE_BAND) d = sid_local_refine_d(nf, ns, r2, K.E, K.prior_on, K.prior);
     // p1 = LRT(l2, l1), p2 = LRT(l1, l2); at most one chi^2 is non-zero
     const double chi1 = z2 ? 1.7976931348623157e308 : ((!z1 && d > 0.0) ? 2.0 * d : 0.0);
     const double chi2 = z1 ? 1.7976931348623157e308 : ((!z2 && d < 0.0) ? -2.0 * d : 0.0);
@@ -89,7 +95,21 @@ __device__ __forceinline__ uint32_t local_site(uint64_t w, const sid_local_k& K,
     const double q = sid_chisq_Q(chi, K.lg15);
     p1 = (chi1 == chi) ? q : 1.0;
     p2 = (chi2 == chi) ? q : 1.0;
-    const bool het = !z2 && (z1 || d < 0.0) && p2 < K.sig;
+    l2_gt_l1 = !z2 && (z1 || d < 0.0);
+    return true;
+}
+
+template <bool GENERAL>
+__device__ __forceinline__ uint32_t local_site(uint64_t w, const sid_local_k& K,
+                                               const double* __restrict__ lnt, double& p1,
+                                               double& p2)
+{
+    if (GENERAL) return local_site_general(w, K, p1, p2);
+    uint32_t f, s, nf, ns, cov;
+    sid_major(w, f, s, nf, ns, cov);
+    bool gt;
+    if (!local_fast_p(nf, ns, cov - nf - ns, K, lnt, p1, p2, gt)) return local_site_general(w, K, p1, p2);
+    const bool het = gt && p2 < K.sig;   // call.cpp:266
     return f | ((het ? s : f) << 2) | (het ? 0x80u : 0u);
 }
 
@@ -146,20 +166,238 @@ __global__ __launch_bounds__(256) void sid_local_kernel_x1(const uint64_t* __res
     }
 }
 
+// ------------------------------------------------------ class table ------
+// Every fast-path result is a function of (nf, ns, r2) only, so the hot
+// kernel reads it from a table built once per option set (the reference's
+// per-unique-profile memoisation, call.cpp:217-221, as a dense LDS table):
+//   entry (nf < 256, ns < 8, r2 < 4) = one double v
+//     v >= +0       p1 = v, p2 = 1            (l2 <= l1)
+//     v <= -0       p1 = 1, p2 = -v           (l2 >  l1; het iff p2 < sig)
+//     NaN           p1 = p2 = 0               (l1 == l2 == 0)
+//     +inf          not tabulated: the fix-up kernel computes the site
+// 64 KiB in LDS; sites outside the table (het sites, coverage >= 256 ...)
+// are appended to a miss list (one atomic per wave) for the fix-up kernel.
+#define SID_TAB_NF 256
+#define SID_TAB_NS 8
+#define SID_TAB_NR 4
+#define SID_TAB_N (SID_TAB_NF * SID_TAB_NS * SID_TAB_NR)
+
+__global__ __launch_bounds__(256) void sid_local_table_build(sid_local_k K, const double* __restrict__ lnt,
+                                                            double* __restrict__ table)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= SID_TAB_N) return;
+    const uint32_t r2 = i % SID_TAB_NR, ns = (i / SID_TAB_NR) % SID_TAB_NS, nf = i / (SID_TAB_NR * SID_TAB_NS);
+    double v = __builtin_inf();
+    double p1, p2;
+    bool gt;
+    // a profile with these majors exists iff nf >= ns and both minor counts <= ns
+    if (nf >= ns && r2 <= 2 * ns && local_fast_p(nf, ns, r2, K, lnt, p1, p2, gt)) {
+        if (p1 == 0.0 && p2 == 0.0) v = __builtin_nan("");
+        else if (gt) v = -p2;       // p1 == 1
+        else v = p1;                // p2 == 1
+    }
+    table[i] = v;
+}
+
+__device__ __forceinline__ uint32_t table_site(uint64_t w, const double* __restrict__ T, double sig,
+                                               double& p1, double& p2)
+{
+    uint32_t f, s, nf, ns, cov;
+    sid_major(w, f, s, nf, ns, cov);
+    const uint32_t r2 = cov - nf - ns;
+    double v = __builtin_inf();
+    if (nf < SID_TAB_NF && ns < SID_TAB_NS && r2 < SID_TAB_NR) v = T[(nf * SID_TAB_NS + ns) * SID_TAB_NR + r2];
+    bool het = false;
+    if (isinf(v)) {
+        p1 = p2 = 0.0;
+        return 0xFFu;   // miss marker (not a valid code: bits 4-5 are never set)
+    }
+    if (isnan(v)) {
+        p1 = p2 = 0.0;
+    } else if (signbit(v)) {
+        p1 = 1.0;
+        p2 = -v;
+        het = p2 < sig;
+    } else {
+        p1 = v;
+        p2 = 1.0;
+    }
+    return f | ((het ? s : f) << 2) | (het ? 0x80u : 0u);
+}
+
+// wave-aggregated append of the lanes' missed site indices
+__device__ __forceinline__ void append_misses(uint32_t nmiss, const uint32_t* idx, uint32_t* miss,
+                                              uint32_t cap, uint32_t* ctr)
+{
+    const unsigned long long any = __ballot(nmiss != 0);
+    if (!any) return;
+    // exclusive prefix of nmiss over the wave
+    uint32_t incl = nmiss;
+    const int lane = threadIdx.x & 63;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(ctr, total);
+    base = __shfl(base, 0, 64);
+    uint32_t o = base + incl - nmiss;
+    for (uint32_t j = 0; j < nmiss; ++j, ++o)
+        if (o < cap) miss[o] = idx[j];
+}
+
+__global__ __launch_bounds__(1024) void sid_local_table_x4(const ulonglong2* __restrict__ counts, size_t ngroups,
+                                                           uint32_t* __restrict__ code4, double2* __restrict__ hom,
+                                                           double2* __restrict__ het,
+                                                           const double* __restrict__ g_table, double sig,
+                                                           uint32_t* __restrict__ miss, uint32_t cap,
+                                                           uint32_t* __restrict__ ctr)
+{
+    __shared__ double T[SID_TAB_N];
+    {
+        const double2* src = (const double2*)g_table;
+        double2* dst = (double2*)T;
+        for (int i = threadIdx.x; i < SID_TAB_N / 2; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t g0 = (size_t)blockIdx.x * blockDim.x; g0 < ngroups; g0 += stride) {
+        const size_t g = g0 + threadIdx.x;
+        uint32_t nmiss = 0, idx[4];
+        if (g < ngroups) {
+            const ulonglong2 a = counts[2 * g];
+            const ulonglong2 b = counts[2 * g + 1];
+            double h0, h1, h2, h3, t0, t1, t2, t3;
+            const uint32_t c0 = table_site(a.x, T, sig, h0, t0);
+            const uint32_t c1 = table_site(a.y, T, sig, h1, t1);
+            const uint32_t c2 = table_site(b.x, T, sig, h2, t2);
+            const uint32_t c3 = table_site(b.y, T, sig, h3, t3);
+            code4[g] = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+            hom[2 * g] = make_double2(h0, h1);
+            hom[2 * g + 1] = make_double2(h2, h3);
+            het[2 * g] = make_double2(t0, t1);
+            het[2 * g + 1] = make_double2(t2, t3);
+            const uint32_t s0 = (uint32_t)(4 * g);
+            if (c0 == 0xFFu) idx[nmiss++] = s0;
+            if (c1 == 0xFFu) idx[nmiss++] = s0 + 1;
+            if (c2 == 0xFFu) idx[nmiss++] = s0 + 2;
+            if (c3 == 0xFFu) idx[nmiss++] = s0 + 3;
+        }
+        append_misses(nmiss, idx, miss, cap, ctr);
+    }
+}
+
+__global__ __launch_bounds__(1024) void sid_local_table_x1(const uint64_t* __restrict__ counts, size_t n,
+                                                           uint8_t* __restrict__ code, double* __restrict__ hom,
+                                                           double* __restrict__ het,
+                                                           const double* __restrict__ g_table, double sig,
+                                                           uint32_t* __restrict__ miss, uint32_t cap,
+                                                           uint32_t* __restrict__ ctr, size_t base)
+{
+    __shared__ double T[SID_TAB_N];
+    for (int i = threadIdx.x; i < SID_TAB_N; i += blockDim.x) T[i] = g_table[i];
+    __syncthreads();
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i0 = (size_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+        const size_t i = i0 + threadIdx.x;
+        uint32_t nmiss = 0, idx[1];
+        if (i < n) {
+            double h, t;
+            const uint32_t c = table_site(counts[i], T, sig, h, t);
+            code[i] = (uint8_t)c;
+            hom[i] = h;
+            het[i] = t;
+            if (c == 0xFFu) idx[nmiss++] = (uint32_t)(base + i);
+        }
+        append_misses(nmiss, idx, miss, cap, ctr);
+    }
+}
+
+// Sites the table does not cover: the miss list (or, if it overflowed, a
+// scan for the 0xFF marker).  Resets the other parity's counter for the next
+// call on this stream.
+__global__ __launch_bounds__(256) void sid_local_fixup(const uint64_t* __restrict__ counts, size_t n,
+                                                       uint8_t* __restrict__ code, double* __restrict__ hom,
+                                                       double* __restrict__ het, sid_local_k K,
+                                                       const double* __restrict__ lnt,
+                                                       const uint32_t* __restrict__ miss, uint32_t cap,
+                                                       uint32_t* __restrict__ ctr, int parity)
+{
+    const uint32_t m = ctr[parity];
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr[parity ^ 1] = 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m <= cap) {
+        for (size_t j = t0; j < m; j += stride) {
+            const uint32_t i = miss[j];
+            double h, t;
+            code[i] = (uint8_t)local_site<false>(counts[i], K, lnt, h, t);
+            hom[i] = h;
+            het[i] = t;
+        }
+    } else {
+        for (size_t i = t0; i < n; i += stride) {
+            if (code[i] != 0xFFu) continue;
+            double h, t;
+            code[i] = (uint8_t)local_site<false>(counts[i], K, lnt, h, t);
+            hom[i] = h;
+            het[i] = t;
+        }
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------- launcher --
 // Called by the C ABI (capi.cpp).  counts must be at least 8-byte aligned
-// (profile_t is 8 bytes); the x4 kernel is used when the arrays allow 16-B
-// accesses, the x1 kernel for the rest.
+// (profile_t is 8 bytes).  Non-general option sets: table kernel (x4 when the
+// arrays allow 16-B accesses, x1 otherwise) + fix-up kernel.  General option
+// sets (E < 0, prior > 1): the direct kernels with the emulated path.
+extern "C" hipError_t sid_launch_local_table_build(const sid_local_k* K, const double* d_lnt, double* d_table,
+                                                   hipStream_t stream)
+{
+    sid_local_table_build<<<SID_TAB_N / 256, 256, 0, stream>>>(*K, d_lnt, d_table);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t* code,
                                        double* hom, double* het, const sid_local_k* K,
-                                       const double* d_lnt, int grid_cap, hipStream_t stream)
+                                       const double* d_lnt, const sid_local_ws* ws, int grid_cap,
+                                       hipStream_t stream)
 {
     if (n == 0) return hipSuccess;
-    const int block = 256;
     const bool aligned = (((uintptr_t)counts | (uintptr_t)hom | (uintptr_t)het) & 15u) == 0 &&
                          (((uintptr_t)code) & 3u) == 0;
+    if (!K->general && ws && ws->table && !ws->direct) {
+        const uint32_t cap = n < 0xFFFFFFFFull ? ws->cap : 0u;   // u32 site indices
+        uint32_t* ctr = ws->ctr + ws->parity;
+        const int tb = 1024;
+        size_t done = 0;
+        if (aligned && n >= 4) {
+            const size_t ngroups = n / 4;
+            size_t want = (ngroups + tb - 1) / tb;
+            int grid = (int)(want < (size_t)ws->table_grid ? want : (size_t)ws->table_grid);
+            sid_local_table_x4<<<grid, tb, 0, stream>>>((const ulonglong2*)counts, ngroups, (uint32_t*)code,
+                                                        (double2*)hom, (double2*)het, ws->table, K->sig,
+                                                        ws->miss, cap, ctr);
+            done = ngroups * 4;
+        }
+        if (done < n) {
+            const size_t rest = n - done;
+            size_t want = (rest + tb - 1) / tb;
+            int grid = (int)(want < (size_t)ws->table_grid ? want : (size_t)ws->table_grid);
+            // miss indices are recorded relative to `counts` (base = done)
+            sid_local_table_x1<<<grid, tb, 0, stream>>>((const uint64_t*)counts + done, rest, code + done,
+                                                        hom + done, het + done, ws->table, K->sig,
+                                                        ws->miss, cap, ctr, done);
+        }
+        sid_local_fixup<<<256, 256, 0, stream>>>((const uint64_t*)counts, n, code, hom, het, *K, d_lnt,
+                                                 ws->miss, cap, ws->ctr, ws->parity);
+        return hipGetLastError();
+    }
+    const int block = 256;
     size_t done = 0;
     if (aligned && n >= 4) {
         const size_t ngroups = n / 4;

@@ -306,8 +306,8 @@ __global__ __launch_bounds__(256) void sid_classify_kernel(const uint64_t* __res
                 T = ld_mul(T, ld_from_double(pi));
                 H = ld_mul(H, ld_from_double(1 - pi));
             }
-            c1[i] = sid_x86_nan(ld_lrt(T, H, lg15));          // p_hom
-            c2[i] = sid_x86_nan(ld_lrt(H, T, lg15));          // p_het
+            c1[i] = ld_lrt(T, H, lg15);                       // p_hom
+            c2[i] = ld_lrt(H, T, lg15);                       // p_het
             code[i] = (uint8_t)(f | (s << 2));                // label decided after BH (host)
         } else {
             sid_ld aH = ld_mul(H, ld_from_double(1 - pi));    // call.cpp:177-178

@@ -9,10 +9,24 @@
 #include "../../include/sid.h"
 #include "sid_math.h"
 
+// -m local workspace (class table + miss list), one per context
+struct sid_local_ws {
+    double* table = nullptr;     // SID_TAB_N entries (local.hip)
+    uint32_t* miss = nullptr;    // miss list
+    uint32_t cap = 0;            // miss list capacity
+    uint32_t* ctr = nullptr;     // [2] miss counters, alternating per call
+    int parity = 0;
+    int table_grid = 512;        // blocks of the table kernel (2 per CU)
+    int direct = 0;              // SID_LOCAL_DIRECT=1: bypass the table (A/B)
+};
+
 // kernels (local.hip, synth.hip, lynch.hip)
 extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t* code,
                                        double* hom, double* het, const sid_local_k* K,
-                                       const double* d_lnt, int grid_cap, hipStream_t stream);
+                                       const double* d_lnt, const sid_local_ws* ws, int grid_cap,
+                                       hipStream_t stream);
+extern "C" hipError_t sid_launch_local_table_build(const sid_local_k* K, const double* d_lnt,
+                                                   double* d_table, hipStream_t stream);
 extern "C" hipError_t sid_launch_synth(uint64_t seed, uint64_t first, size_t n,
                                        const uint64_t* d_cdf, uint32_t kmax, uint16_t* counts,
                                        hipStream_t stream);
@@ -32,6 +46,7 @@ struct sid_ctx {
     uint64_t* d_cdf = nullptr;
     uint32_t cdf_k = 0;
     double cdf_mean = -1.0;
+    sid_local_ws ws;
     // Lynch path
     sid_lynch_dev* lynch = nullptr;
 };

@@ -83,7 +83,7 @@ __device__ __forceinline__ double sid_gamma_F_CF(double x)
 // gsl_cdf_chisq_Q(x, 1) (cdf/chisq.c -> cdf/gamma.c gsl_cdf_gamma_Q(x, 0.5, 2))
 __device__ __noinline__ double sid_chisq_Q_tail(double y, double lg15)
 {
-    if (isinf(y)) return __builtin_nan("");           // D = exp(inf - inf)
+    if (isinf(y)) return -__builtin_nan("");          // D = exp(inf - inf): default NaN
     if (y > 1.0e6) return 0.0;                          // gamma_inc_Q_large_x: D == 0
     double D = exp(0.5 * log(y) - y - lg15);            // gamma_inc_D, a < 10
     return D * (0.5 / y) * sid_gamma_F_CF(y);
@@ -96,6 +96,148 @@ __device__ __forceinline__ double sid_chisq_Q(double x, double lg15)
     if (y <= 700.0) return erfc(sqrt(y));               // Q(1/2, y) = erfc(sqrt(y)), normal range
     return sid_chisq_Q_tail(y, lg15);
 }
+
+// ------------------------------------------------------- double-double --
+// Near-ties l1 ~ l2 put p = Q(chi^2) on its sqrt(chi^2) branch near 1, where
+// a 1e-14 error in ln l becomes a 1e-7 error in p.  There the kernels
+// recompute ln l1 - ln l2 from the reference's own double bases with ~1e-30
+// accuracy (QD-style double-double exp/log), so exact ties of the reference
+// come out as exact ties and near-ties agree to ~1e-16.
+struct sid_dd {
+    double hi, lo;
+};
+
+__host__ __device__ __forceinline__ sid_dd dd_two_sum(double a, double b)
+{
+    double s = a + b;
+    double bb = s - a;
+    sid_dd r;
+    r.hi = s;
+    r.lo = (a - (s - bb)) + (b - bb);
+    return r;
+}
+
+__host__ __device__ __forceinline__ sid_dd dd_norm(double hi, double lo)
+{
+    double s = hi + lo;
+    sid_dd r;
+    r.hi = s;
+    r.lo = lo - (s - hi);
+    return r;
+}
+
+__host__ __device__ __forceinline__ sid_dd dd_add(sid_dd a, sid_dd b)
+{
+    sid_dd s = dd_two_sum(a.hi, b.hi);
+    sid_dd t = dd_two_sum(a.lo, b.lo);
+    s.lo += t.hi;
+    s = dd_norm(s.hi, s.lo);
+    s.lo += t.lo;
+    return dd_norm(s.hi, s.lo);
+}
+
+__host__ __device__ __forceinline__ sid_dd dd_neg(sid_dd a)
+{
+    a.hi = -a.hi;
+    a.lo = -a.lo;
+    return a;
+}
+
+__host__ __device__ __forceinline__ sid_dd dd_mul(sid_dd a, sid_dd b)
+{
+    double p = a.hi * b.hi;
+    double e = fma(a.hi, b.hi, -p);
+    e += a.hi * b.lo + a.lo * b.hi;
+    return dd_norm(p, e);
+}
+
+__host__ __device__ __forceinline__ sid_dd dd_mul_d(sid_dd a, double b)
+{
+    double p = a.hi * b;
+    double e = fma(a.hi, b, -p);
+    e += a.lo * b;
+    return dd_norm(p, e);
+}
+
+__host__ __device__ __forceinline__ sid_dd dd_div_d(sid_dd a, double b)
+{
+    const double q1 = a.hi / b;
+    const double r = fma(-q1, b, a.hi) + a.lo;   // exact remainder of the hi part
+    return dd_norm(q1, r / b);
+}
+
+__host__ __device__ __forceinline__ sid_dd dd_ldexp(sid_dd a, int k)
+{
+    a.hi = ldexp(a.hi, k);
+    a.lo = ldexp(a.lo, k);
+    return a;
+}
+
+// exp of a double-double, |x| < 700
+__host__ __device__ __noinline__ sid_dd dd_exp(sid_dd x)
+{
+    const sid_dd ln2 = {0.6931471805599452862, 2.319046813846299558e-17};
+    const double k = rint(x.hi / ln2.hi);
+    sid_dd r = dd_add(x, dd_neg(dd_mul_d(ln2, k)));
+    r = dd_ldexp(r, -10);                       // |r| < 3.4e-4
+    // e^r - 1 by Taylor to r^9 (error < 1e-36)
+    sid_dd term = r, em1 = r;
+    for (int i = 2; i <= 9; ++i) {
+        term = dd_div_d(dd_mul(term, r), (double)i);
+        em1 = dd_add(em1, term);
+    }
+    // (1 + em1)^(2^10): em1 <- 2 em1 + em1^2
+    for (int i = 0; i < 10; ++i) em1 = dd_add(dd_mul_d(em1, 2.0), dd_mul(em1, em1));
+    sid_dd one = {1.0, 0.0};
+    return dd_ldexp(dd_add(one, em1), (int)k);
+}
+
+// ln(b) for a finite double b > 0 (denormals included), as a double-double:
+// b = m 2^e, m in [0.5, 1); ln m by one Newton step on a double-double exp.
+__host__ __device__ __noinline__ sid_dd dd_log(double b)
+{
+    int e;
+    const double m = frexp(b, &e);
+    const double y = log(m);
+    sid_dd E = dd_exp(sid_dd{-y, 0.0});        // ~ 1/m
+    sid_dd t = dd_mul_d(E, m);                  // ~ 1
+    t = dd_add(t, sid_dd{-1.0, 0.0});           // tiny
+    sid_dd t2 = dd_mul(t, t);
+    t = dd_add(t, sid_dd{-0.5 * t2.hi, -0.5 * t2.lo});
+    const sid_dd ln2 = {0.6931471805599452862, 2.319046813846299558e-17};
+    return dd_add(dd_add(sid_dd{y, 0.0}, t), dd_mul_d(ln2, (double)e));
+}
+
+// n * ln(b) with powl(b, 0) == 1
+__host__ __device__ __forceinline__ sid_dd dd_nlog(double b, uint32_t n)
+{
+    if (n == 0) return sid_dd{0.0, 0.0};
+    return dd_mul_d(dd_log(b), (double)n);
+}
+
+// ---------------------------------------------------- near-tie refinement --
+// ln l1 - ln l2 of call.cpp:238-262 from the reference's double bases,
+// double-double accurate.  Only called when both likelihoods are non-zero.
+__host__ __device__ __noinline__ double sid_local_refine_d(uint32_t nf, uint32_t ns, uint32_t r2, double E,
+                                                  int prior_on, double prior)
+{
+    const uint32_t cov = nf + ns + r2, r1 = cov - nf, m2 = nf + ns;
+    double e1 = (double)r1 / (double)cov;
+    if (e1 > E) e1 = E;
+    double e2 = 1.5 * (double)r2 / (double)cov;
+    if (e2 > E) e2 = E;
+    sid_dd l1 = dd_add(dd_nlog(1 - e1, nf), dd_nlog(e1 / 3., r1));
+    sid_dd l2 = dd_add(dd_nlog((1 - 2. / 3. * e2) / 2., m2), dd_nlog(e2 / 3., r2));
+    if (prior_on) {
+        l1 = dd_add(l1, dd_log(1 - prior));
+        l2 = dd_add(l2, dd_log(prior));
+    }
+    sid_dd d = dd_add(l1, dd_neg(l2));
+    // below the resolution of any evaluation of the reference: an exact tie
+    if (fabs(d.hi) <= 1e-28 * (fabs(l1.hi) + fabs(l2.hi))) return 0.0;
+    return d.hi + d.lo;
+}
+#define SID_TIE_BAND 5e-7   // |ln l1 - ln l2| below this is refined
 
 // ------------------------------------------------------ major alleles a5 --
 // call.cpp:52-60: stable ascending sort of {0,1,2,3} by count -> first =
@@ -177,14 +319,19 @@ __device__ __forceinline__ bool ld_gt(sid_ld a, sid_ld b)
     return false;
 }
 
-// stats.cpp:29-37 likelihoodRatioTest(l_H0, l_H1) on emulated long doubles
+// stats.cpp:29-37 likelihoodRatioTest(l_H0, l_H1) on emulated long doubles.
+// NaN signs follow the x86-64 reference build: glibc logl() of a negative
+// number returns +NaN; an invalid x87/SSE operation (0*inf, inf-inf) gives
+// the default NaN, which has the sign bit set; NaN operands propagate.
 __device__ __noinline__ double ld_lrt(sid_ld l0, sid_ld l1, double lg15)
 {
     if (ld_is_zero(l0)) return 0.0;                           // gsl_cdf_chisq_Q(DBL_MAX, 1)
-    if (isnan(l0.ln) || l0.neg) return __builtin_nan("");     // logl(NaN / negative)
+    if (isnan(l0.ln)) return -__builtin_nan("");              // l0 came from 0*inf
+    if (l0.neg) return __builtin_nan("");                     // logl(negative)
     bool take1 = !isnan(l1.ln) && ld_gt(l1, l0);              // fmaxl(l0, l1)
     double mx = take1 ? l1.ln : l0.ln;
     double chisq = -2.0 * (l0.ln - mx);
+    if (isnan(chisq)) return -__builtin_nan("");              // inf - inf
     return sid_chisq_Q(chisq, lg15);
 }
 
