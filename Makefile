@@ -4,7 +4,9 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 BUILD := build
 SRC := sid_amd/csrc
-HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude
+# -ffp-contract=off: device doubles round like the reference's x86-64 SSE2 build (no
+# FMA contraction), and the double-double error-free transforms stay exact
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-function -Iinclude
 HOSTFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Iinclude
 
 KERNELS := local synth lynch

@@ -59,7 +59,7 @@ __device__ __noinline__ uint32_t local_site_general(uint64_t w, const sid_local_
 // options, which is what makes the class table below possible.  Returns
 // false when a long double of the reference would leave the normal range
 // (then the emulated path must be used).
-__device__ __forceinline__ bool local_fast_p(uint32_t nf, uint32_t ns, uint32_t r2,
+__host__ __device__ __forceinline__ bool local_fast_p(uint32_t nf, uint32_t ns, uint32_t r2,
                                              const sid_local_k& K, const double* __restrict__ lnt,
                                              double& p1, double& p2, bool& l2_gt_l1)
 {

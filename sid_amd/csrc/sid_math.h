@@ -61,7 +61,7 @@ __device__ __forceinline__ double sid_x86_nan(double v) { return isnan(v) ? -__b
 
 // ---------------------------------------------------------------- chi^2_1 --
 // GSL 2.7.1 gamma_inc_F_CF (modified Lentz), a = 0.5.
-__device__ __forceinline__ double sid_gamma_F_CF(double x)
+__host__ __device__ __forceinline__ double sid_gamma_F_CF(double x)
 {
     const double eps = 2.2204460492503131e-16;
     const double small = eps * eps * eps;
@@ -81,15 +81,15 @@ __device__ __forceinline__ double sid_gamma_F_CF(double x)
 }
 
 // gsl_cdf_chisq_Q(x, 1) (cdf/chisq.c -> cdf/gamma.c gsl_cdf_gamma_Q(x, 0.5, 2))
-__device__ __noinline__ double sid_chisq_Q_tail(double y, double lg15)
+static __host__ __device__ __noinline__ double sid_chisq_Q_tail(double y, double lg15)
 {
-    if (isinf(y)) return -__builtin_nan("");          // D = exp(inf - inf): default NaN
+    if (__builtin_isinf(y)) return -__builtin_nan("");   // D = exp(inf - inf): default NaN
     if (y > 1.0e6) return 0.0;                          // gamma_inc_Q_large_x: D == 0
     double D = exp(0.5 * log(y) - y - lg15);            // gamma_inc_D, a < 10
     return D * (0.5 / y) * sid_gamma_F_CF(y);
 }
 
-__device__ __forceinline__ double sid_chisq_Q(double x, double lg15)
+__host__ __device__ __forceinline__ double sid_chisq_Q(double x, double lg15)
 {
     if (!(x > 0.0)) return (x <= 0.0) ? 1.0 : x;        // x <= 0 -> 1; NaN -> NaN
     double y = x / 2.0;
@@ -174,7 +174,7 @@ __host__ __device__ __forceinline__ sid_dd dd_ldexp(sid_dd a, int k)
 }
 
 // exp of a double-double, |x| < 700
-__host__ __device__ __noinline__ sid_dd dd_exp(sid_dd x)
+static __host__ __device__ __noinline__ sid_dd dd_exp(sid_dd x)
 {
     const sid_dd ln2 = {0.6931471805599452862, 2.319046813846299558e-17};
     const double k = rint(x.hi / ln2.hi);
@@ -194,7 +194,7 @@ __host__ __device__ __noinline__ sid_dd dd_exp(sid_dd x)
 
 // ln(b) for a finite double b > 0 (denormals included), as a double-double:
 // b = m 2^e, m in [0.5, 1); ln m by one Newton step on a double-double exp.
-__host__ __device__ __noinline__ sid_dd dd_log(double b)
+static __host__ __device__ __noinline__ sid_dd dd_log(double b)
 {
     int e;
     const double m = frexp(b, &e);
@@ -218,7 +218,7 @@ __host__ __device__ __forceinline__ sid_dd dd_nlog(double b, uint32_t n)
 // ---------------------------------------------------- near-tie refinement --
 // ln l1 - ln l2 of call.cpp:238-262 from the reference's double bases,
 // double-double accurate.  Only called when both likelihoods are non-zero.
-__host__ __device__ __noinline__ double sid_local_refine_d(uint32_t nf, uint32_t ns, uint32_t r2, double E,
+static __host__ __device__ __noinline__ double sid_local_refine_d(uint32_t nf, uint32_t ns, uint32_t r2, double E,
                                                   int prior_on, double prior)
 {
     const uint32_t cov = nf + ns + r2, r1 = cov - nf, m2 = nf + ns;
@@ -242,7 +242,7 @@ __host__ __device__ __noinline__ double sid_local_refine_d(uint32_t nf, uint32_t
 // ------------------------------------------------------ major alleles a5 --
 // call.cpp:52-60: stable ascending sort of {0,1,2,3} by count -> first =
 // idx[3], second = idx[2].  Equivalent key 4*count+idx (ties -> higher index).
-__device__ __forceinline__ void sid_major(uint64_t w, uint32_t& f, uint32_t& s, uint32_t& nf,
+__host__ __device__ __forceinline__ void sid_major(uint64_t w, uint32_t& f, uint32_t& s, uint32_t& nf,
                                           uint32_t& ns, uint32_t& cov)
 {
     uint32_t n0 = (uint32_t)(w & 0xffffu), n1 = (uint32_t)((w >> 16) & 0xffffu);
