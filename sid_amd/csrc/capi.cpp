@@ -128,6 +128,8 @@ extern "C" int sid_create(int device, const sid_opts* opts, sid_ctx** out)
 
     if (const char* g = std::getenv("SID_TABLE_GRID")) c->ws.table_grid = std::max(1, std::atoi(g));
     if (const char* g = std::getenv("SID_LOCAL_DIRECT")) c->ws.direct = std::atoi(g) != 0;
+    if (const char* g = std::getenv("SID_TABLE_UNROLL")) c->ws.unroll = std::atoi(g);
+    if (const char* g = std::getenv("SID_TABLE_NT")) c->ws.nt = std::atoi(g) != 0;
 
     std::vector<double> lnt(SID_LUTN);
     lnt[0] = -INFINITY;

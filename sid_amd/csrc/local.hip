@@ -226,67 +226,81 @@ __device__ __forceinline__ uint32_t table_site(uint64_t w, const double* __restr
     return f | ((het ? s : f) << 2) | (het ? 0x80u : 0u);
 }
 
-// wave-aggregated append of the lanes' missed site indices
-__device__ __forceinline__ void append_misses(uint32_t nmiss, const uint32_t* idx, uint32_t* miss,
-                                              uint32_t cap, uint32_t* ctr)
+// Sites are processed in pairs (one 16-B profile_t load per lane), U pairs
+// per thread per tile, lanes contiguous in every wave instruction: loads and
+// the 16-B conf stores move 1 KiB per instruction, the 2-B code stores 128 B
+// (one full L2 line).  Misses go to an LDS list (one LDS atomic per missed
+// site), flushed with one global atomic per block.
+#define SID_LMISS 2048
+
+typedef double sid_dvec2 __attribute__((ext_vector_type(2)));
+
+template <typename T>
+__device__ __forceinline__ void st_stream(T* p, T v, bool nt)
 {
-    const unsigned long long any = __ballot(nmiss != 0);
-    if (!any) return;
-    // exclusive prefix of nmiss over the wave
-    uint32_t incl = nmiss;
-    const int lane = threadIdx.x & 63;
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    const uint32_t total = __shfl(incl, 63, 64);
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(ctr, total);
-    base = __shfl(base, 0, 64);
-    uint32_t o = base + incl - nmiss;
-    for (uint32_t j = 0; j < nmiss; ++j, ++o)
-        if (o < cap) miss[o] = idx[j];
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
 }
 
-__global__ __launch_bounds__(1024) void sid_local_table_x4(const ulonglong2* __restrict__ counts, size_t ngroups,
-                                                           uint32_t* __restrict__ code4, double2* __restrict__ hom,
-                                                           double2* __restrict__ het,
+template <int U, bool NT>
+__global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __restrict__ pairs, size_t npairs,
+                                                           uint16_t* __restrict__ code2, sid_dvec2* __restrict__ hom,
+                                                           sid_dvec2* __restrict__ het,
                                                            const double* __restrict__ g_table, double sig,
                                                            uint32_t* __restrict__ miss, uint32_t cap,
                                                            uint32_t* __restrict__ ctr)
 {
     __shared__ double T[SID_TAB_N];
+    __shared__ uint32_t lmiss[SID_LMISS];
+    __shared__ uint32_t lcnt, gbase;
     {
         const double2* src = (const double2*)g_table;
         double2* dst = (double2*)T;
         for (int i = threadIdx.x; i < SID_TAB_N / 2; i += blockDim.x) dst[i] = src[i];
     }
+    if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t g0 = (size_t)blockIdx.x * blockDim.x; g0 < ngroups; g0 += stride) {
-        const size_t g = g0 + threadIdx.x;
-        uint32_t nmiss = 0, idx[4];
-        if (g < ngroups) {
-            const ulonglong2 a = counts[2 * g];
-            const ulonglong2 b = counts[2 * g + 1];
-            double h0, h1, h2, h3, t0, t1, t2, t3;
-            const uint32_t c0 = table_site(a.x, T, sig, h0, t0);
-            const uint32_t c1 = table_site(a.y, T, sig, h1, t1);
-            const uint32_t c2 = table_site(b.x, T, sig, h2, t2);
-            const uint32_t c3 = table_site(b.y, T, sig, h3, t3);
-            code4[g] = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
-            hom[2 * g] = make_double2(h0, h1);
-            hom[2 * g + 1] = make_double2(h2, h3);
-            het[2 * g] = make_double2(t0, t1);
-            het[2 * g + 1] = make_double2(t2, t3);
-            const uint32_t s0 = (uint32_t)(4 * g);
-            if (c0 == 0xFFu) idx[nmiss++] = s0;
-            if (c1 == 0xFFu) idx[nmiss++] = s0 + 1;
-            if (c2 == 0xFFu) idx[nmiss++] = s0 + 2;
-            if (c3 == 0xFFu) idx[nmiss++] = s0 + 3;
+    const size_t tile = (size_t)blockDim.x * U;
+    for (size_t base = (size_t)blockIdx.x * tile; base < npairs; base += (size_t)gridDim.x * tile) {
+        ulonglong2 c[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const size_t p = base + (size_t)j * blockDim.x + threadIdx.x;
+            if (p < npairs) c[j] = pairs[p];
         }
-        append_misses(nmiss, idx, miss, cap, ctr);
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const size_t p = base + (size_t)j * blockDim.x + threadIdx.x;
+            if (p < npairs) {
+                double h0, h1, t0, t1;
+                const uint32_t a = table_site(c[j].x, T, sig, h0, t0);
+                const uint32_t b = table_site(c[j].y, T, sig, h1, t1);
+                st_stream(code2 + p, (uint16_t)(a | (b << 8)), NT);
+                st_stream(hom + p, sid_dvec2{h0, h1}, NT);
+                st_stream(het + p, sid_dvec2{t0, t1}, NT);
+                if (a == 0xFFu || b == 0xFFu) {
+                    for (int k = 0; k < 2; ++k) {
+                        if ((k ? b : a) != 0xFFu) continue;
+                        const uint32_t idx = (uint32_t)(2 * p + k);
+                        const uint32_t slot = atomicAdd(&lcnt, 1u);
+                        if (slot < SID_LMISS) {
+                            lmiss[slot] = idx;
+                        } else {
+                            const uint32_t g = atomicAdd(ctr, 1u);
+                            if (g < cap) miss[g] = idx;
+                        }
+                    }
+                }
+            }
+        }
     }
+    __syncthreads();
+    const uint32_t nl = lcnt < SID_LMISS ? lcnt : SID_LMISS;
+    if (nl == 0) return;
+    if (threadIdx.x == 0) gbase = atomicAdd(ctr, nl);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
+        if (gbase + i < cap) miss[gbase + i] = lmiss[i];
 }
 
 __global__ __launch_bounds__(1024) void sid_local_table_x1(const uint64_t* __restrict__ counts, size_t n,
@@ -300,18 +314,16 @@ __global__ __launch_bounds__(1024) void sid_local_table_x1(const uint64_t* __res
     for (int i = threadIdx.x; i < SID_TAB_N; i += blockDim.x) T[i] = g_table[i];
     __syncthreads();
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i0 = (size_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
-        const size_t i = i0 + threadIdx.x;
-        uint32_t nmiss = 0, idx[1];
-        if (i < n) {
-            double h, t;
-            const uint32_t c = table_site(counts[i], T, sig, h, t);
-            code[i] = (uint8_t)c;
-            hom[i] = h;
-            het[i] = t;
-            if (c == 0xFFu) idx[nmiss++] = (uint32_t)(base + i);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        double h, t;
+        const uint32_t c = table_site(counts[i], T, sig, h, t);
+        code[i] = (uint8_t)c;
+        hom[i] = h;
+        het[i] = t;
+        if (c == 0xFFu) {   // ragged / unaligned remainder only: plain global append
+            const uint32_t g = atomicAdd(ctr, 1u);
+            if (g < cap) miss[g] = (uint32_t)(base + i);
         }
-        append_misses(nmiss, idx, miss, cap, ctr);
     }
 }
 
@@ -375,14 +387,24 @@ extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t
         uint32_t* ctr = ws->ctr + ws->parity;
         const int tb = 1024;
         size_t done = 0;
-        if (aligned && n >= 4) {
-            const size_t ngroups = n / 4;
-            size_t want = (ngroups + tb - 1) / tb;
+        const bool aligned2 = (((uintptr_t)counts | (uintptr_t)hom | (uintptr_t)het) & 15u) == 0 &&
+                              (((uintptr_t)code) & 1u) == 0;
+        if (aligned2 && n >= 2) {
+            const size_t npairs = n / 2;
+            const int U = ws->unroll;
+            size_t want = (npairs + (size_t)tb * U - 1) / ((size_t)tb * U);
             int grid = (int)(want < (size_t)ws->table_grid ? want : (size_t)ws->table_grid);
-            sid_local_table_x4<<<grid, tb, 0, stream>>>((const ulonglong2*)counts, ngroups, (uint32_t*)code,
-                                                        (double2*)hom, (double2*)het, ws->table, K->sig,
-                                                        ws->miss, cap, ctr);
-            done = ngroups * 4;
+            auto* P = (const ulonglong2*)counts;
+            auto* C2 = (uint16_t*)code;
+            auto* H = (sid_dvec2*)hom;
+            auto* Q = (sid_dvec2*)het;
+            if (U == 1 && !ws->nt) sid_local_table_p2<1, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
+            else if (U == 1) sid_local_table_p2<1, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
+            else if (U == 4 && !ws->nt) sid_local_table_p2<4, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
+            else if (U == 4) sid_local_table_p2<4, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
+            else if (!ws->nt) sid_local_table_p2<2, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
+            else sid_local_table_p2<2, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
+            done = npairs * 2;
         }
         if (done < n) {
             const size_t rest = n - done;

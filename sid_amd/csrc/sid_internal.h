@@ -16,8 +16,10 @@ struct sid_local_ws {
     uint32_t cap = 0;            // miss list capacity
     uint32_t* ctr = nullptr;     // [2] miss counters, alternating per call
     int parity = 0;
-    int table_grid = 512;        // blocks of the table kernel (2 per CU)
+    int table_grid = 1024;       // blocks of the table kernel (2 resident per CU)
     int direct = 0;              // SID_LOCAL_DIRECT=1: bypass the table (A/B)
+    int unroll = 2;              // SID_TABLE_UNROLL: pairs per thread per tile (1, 2, 4)
+    int nt = 0;                  // SID_TABLE_NT=1: non-temporal output stores
 };
 
 // kernels (local.hip, synth.hip, lynch.hip)
