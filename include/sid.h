@@ -90,6 +90,13 @@ int sid_set_prior(sid_ctx* ctx, double snp_prior);
 int sid_call_local(sid_ctx* ctx, const uint16_t* counts, size_t n, uint8_t* code,
                    double* hom_conf, double* het_conf, void* stream);
 
+/* Measurement (bench.py): while enabled, sid_call_local records HIP events on
+ * its stream around its main (class-table) kernel and its fix-up kernel.
+ * sid_timing_read synchronises on them, returns the per-call averages of
+ * the calls since the previous read, and resets. */
+int sid_timing_enable(sid_ctx* ctx, int enable);
+int sid_timing_read(sid_ctx* ctx, uint64_t* calls, double* main_ms, double* fixup_ms);
+
 /* ---------------------------------------------- Lynch path (a11-a17) -------
  * 1. sid_profile_reset + sid_profile_accumulate (any number of batches):
  *    device hash histogram of the site profiles (countUniqueProfiles,

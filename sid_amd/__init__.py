@@ -70,6 +70,8 @@ SIGNATURES = [
     ("sid_destroy", _I, [_P]),
     ("sid_set_prior", _I, [_P, _D]),
     ("sid_call_local", _I, [_P, _P, _SZ, _P, _P, _P, _P]),
+    ("sid_timing_enable", _I, [_P, _I]),
+    ("sid_timing_read", _I, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     ("sid_profile_reset", _I, [_P, _P]),
     ("sid_profile_accumulate", _I, [_P, _P, _SZ, _P]),
     ("sid_profile_table", _I, [_P, _P, _P, _SZ, C.POINTER(C.c_size_t)]),
@@ -249,6 +251,15 @@ class Context:
     def call_local(self, counts_ptr, n, code_ptr, hom_ptr, het_ptr, stream=None):
         check(lib().sid_call_local(self.h, counts_ptr, n, code_ptr, hom_ptr, het_ptr, stream),
               "sid_call_local")
+
+    def timing_enable(self, on=True):
+        check(lib().sid_timing_enable(self.h, int(bool(on))), "sid_timing_enable")
+
+    def timing_read(self):
+        """(calls, main kernel ms, fix-up kernel ms) averaged since the last read."""
+        k, m, f = C.c_uint64(0), C.c_double(0), C.c_double(0)
+        check(lib().sid_timing_read(self.h, C.byref(k), C.byref(m), C.byref(f)), "sid_timing_read")
+        return k.value, m.value, f.value
 
     def lookup_sites(self, counts_ptr, n, code_ptr, hom_ptr, het_ptr, stream=None):
         check(lib().sid_lookup_sites(self.h, counts_ptr, n, code_ptr, hom_ptr, het_ptr, stream),

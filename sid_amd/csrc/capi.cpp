@@ -162,6 +162,12 @@ extern "C" int sid_destroy(sid_ctx* c)
     if (c->ws.miss) (void)hipFree(c->ws.miss);
     if (c->ws.ctr) (void)hipFree(c->ws.ctr);
     if (c->lynch) sid_lynch_dev_destroy(c->lynch);
+    for (auto& v : {c->ev_pool, c->ev_pending})
+        for (auto& ev : v) {
+            (void)hipEventDestroy(ev.start);
+            (void)hipEventDestroy(ev.mid);
+            (void)hipEventDestroy(ev.end);
+        }
     delete c;
     return SID_OK;
 }
@@ -184,10 +190,65 @@ extern "C" int sid_call_local(sid_ctx* c, const uint16_t* counts, size_t n, uint
     if (!counts || !code || !hom_conf || !het_conf) return SID_EINVAL;
     if (((uintptr_t)counts & 7u) || ((uintptr_t)hom_conf & 7u) || ((uintptr_t)het_conf & 7u))
         return SID_EINVAL;
+    sid_timing_ev ev{nullptr, nullptr, nullptr};
+    if (c->timing) {
+        if (c->ev_pool.empty()) {
+            sid_timing_ev x;
+            if (hipEventCreate(&x.start) != hipSuccess || hipEventCreate(&x.mid) != hipSuccess ||
+                hipEventCreate(&x.end) != hipSuccess)
+                return SID_EHIP;
+            c->ev_pool.push_back(x);
+        }
+        ev = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        (void)hipEventRecord(ev.start, (hipStream_t)stream);
+        c->ws.ev_mid = ev.mid;
+    }
     hipError_t e = sid_launch_local(counts, n, code, hom_conf, het_conf, &c->K, c->d_lnt, &c->ws,
                                     c->grid_cap, (hipStream_t)stream);
     c->ws.parity ^= 1;   // the fix-up kernel zeroed the other counter
+    if (c->timing) {
+        c->ws.ev_mid = nullptr;
+        (void)hipEventRecord(ev.end, (hipStream_t)stream);
+        c->ev_pending.push_back(ev);
+    }
     return e == hipSuccess ? SID_OK : sid_set_hip_error(e);
+}
+
+// ----------------------------------------------------------- measurement --
+extern "C" int sid_timing_enable(sid_ctx* c, int enable)
+{
+    if (!c) return SID_EINVAL;
+    c->timing = enable != 0;
+    return SID_OK;
+}
+
+extern "C" int sid_timing_read(sid_ctx* c, uint64_t* calls, double* main_ms, double* fixup_ms)
+{
+    if (!c) return SID_EINVAL;
+    double m = 0, f = 0;
+    uint64_t k = 0;
+    for (auto& ev : c->ev_pending) {
+        hipError_t e = hipEventSynchronize(ev.end);
+        if (e != hipSuccess) return sid_set_hip_error(e);
+        float a = 0, b = 0;
+        // the general-option path records no mid event: all time is "main"
+        if (hipEventElapsedTime(&a, ev.start, ev.mid) == hipSuccess &&
+            hipEventElapsedTime(&b, ev.mid, ev.end) == hipSuccess) {
+            m += a;
+            f += b;
+        } else {
+            (void)hipEventElapsedTime(&a, ev.start, ev.end);
+            m += a;
+        }
+        ++k;
+        c->ev_pool.push_back(ev);
+    }
+    c->ev_pending.clear();
+    if (calls) *calls = k;
+    if (main_ms) *main_ms = k ? m / k : 0.0;
+    if (fixup_ms) *fixup_ms = k ? f / k : 0.0;
+    return SID_OK;
 }
 
 // ------------------------------------------------------------- synthetic --

@@ -415,6 +415,7 @@ extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t
                                                         hom + done, het + done, ws->table, K->sig,
                                                         ws->miss, cap, ctr, done);
         }
+        if (ws->ev_mid) (void)hipEventRecord(ws->ev_mid, stream);   // measurement: main | fix-up
         sid_local_fixup<<<256, 256, 0, stream>>>((const uint64_t*)counts, n, code, hom, het, *K, d_lnt,
                                                  ws->miss, cap, ws->ctr, ws->parity);
         return hipGetLastError();

@@ -20,6 +20,11 @@ struct sid_local_ws {
     int direct = 0;              // SID_LOCAL_DIRECT=1: bypass the table (A/B)
     int unroll = 2;              // SID_TABLE_UNROLL: pairs per thread per tile (1, 2, 4)
     int nt = 0;                  // SID_TABLE_NT=1: non-temporal output stores
+    hipEvent_t ev_mid = nullptr; // set only while timing: recorded between main and fix-up
+};
+
+struct sid_timing_ev {
+    hipEvent_t start, mid, end;
 };
 
 // kernels (local.hip, synth.hip, lynch.hip)
@@ -49,6 +54,9 @@ struct sid_ctx {
     uint32_t cdf_k = 0;
     double cdf_mean = -1.0;
     sid_local_ws ws;
+    // measurement (sid_timing_enable / sid_timing_read)
+    int timing = 0;
+    std::vector<sid_timing_ev> ev_pool, ev_pending;
     // Lynch path
     sid_lynch_dev* lynch = nullptr;
 };
