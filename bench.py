@@ -8,6 +8,13 @@ sites already resident in HBM.  N GPUs = N ranks (torchrun), each with its own
 50M-site range of the counter-based generator (weak scaling, no data-path
 collective; gloo only for the barrier and the max over ranks).
 
+With --method likelihood_ratio (BASELINE configs[2], "C3": the reference has
+no `-m lynch`; SURVEY.md §8(d) runs C3 as `-R -m likelihood_ratio`), a step is
+the whole Lynch path over the resident 50M sites: profile histogram (device
+hash), [N>1: one all-gather of the histograms], Nelder-Mead on the GPU
+objective, classification + Benjamini-Hochberg, and the per-site lookup.
+`--method bayes` runs the same with the posterior classification.
+
 Prints ONE JSON line on rank 0 (contract in the task statement), including
   roofline      25 algorithmic bytes/site (8 B counts in, 1 B code + 2 x 8 B
                 confs out) / average kernel duration from HIP events on the
@@ -40,10 +47,13 @@ def parse_args():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--sites", type=int, default=50_000_000, help="sites per GPU")
     p.add_argument("--depth", type=float, default=30.0)
-    p.add_argument("--seed", type=int, default=2)
+    p.add_argument("--seed", type=int, default=None, help="default: 2 (C2) / 3 (C3)")
     p.add_argument("--cpu-sample", type=int, default=2_000_000,
                    help="sites in the CPU-baseline / e2e sample (0 = skip)")
     p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--method", default="local", choices=["local", "likelihood_ratio", "bayes"],
+                   help="local = C2 (default); likelihood_ratio = C3 (with -R, as SURVEY.md §8(d)); bayes")
+    p.add_argument("--no-R", action="store_true", help="C3 without -R (estimate_prior off)")
     p.add_argument("--direct", action="store_true",
                    help="A/B: bypass the class-table kernel (SID_LOCAL_DIRECT=1)")
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_local_r01.json"),
@@ -53,6 +63,8 @@ def parse_args():
 
 def main():
     a = parse_args()
+    if a.seed is None:
+        a.seed = 2 if a.method == "local" else 3
     if a.direct:
         os.environ["SID_LOCAL_DIRECT"] = "1"
     rank = int(os.environ.get("RANK", 0))
@@ -77,6 +89,9 @@ def main():
     # inputs resident in HBM before the timed region: this rank's site range
     ctx.synth_counts(a.seed, a.depth, rank * n, n, counts.data_ptr(), sh)
     torch.cuda.synchronize(dev)
+    if a.method != "local":
+        ctx.close()
+        return bench_lynch(a, torch, dist, rank, world, dev, counts, code, hom, het)
 
     def step():
         ctx.call_local(counts.data_ptr(), n, code.data_ptr(), hom.data_ptr(), het.data_ptr(), sh)
@@ -171,9 +186,121 @@ def main():
         dist.destroy_process_group()
 
 
+LYNCH_HIST_BYTES = 8         # histogram pass reads the counts
+LYNCH_LOOKUP_BYTES = 25      # lookup pass: 8 in + 17 out
+
+
+def bench_lynch(a, torch, dist, rank, world, dev, counts, code, hom, het):
+    """C3: the whole -R -m likelihood_ratio (or bayes) path per step."""
+    import sid_amd
+    from sid_amd import dist as sdist
+    n = a.sites
+    R = not a.no_R
+    ctx = sid_amd.Context(dev.index, method=a.method, estimate_prior=R)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    cp = counts.data_ptr()
+    ev = []
+
+    def step(record):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        t0 = time.perf_counter()
+        if e:
+            e[0].record(stream)
+        ctx.profile_reset(sh)
+        ctx.profile_accumulate(cp, n, sh)
+        if e:
+            e[1].record(stream)
+        if world > 1:   # the one exchange of the Lynch path: O(U) histogram
+            keys, cnts = ctx.profile_table()
+            keys, cnts = sdist.allgather_profile_table(keys, cnts)
+            ctx.profile_load(keys, cnts)
+        t1 = time.perf_counter()
+        est = ctx.lynch_prepare(False)
+        t2 = time.perf_counter()
+        if e:
+            e[2].record(stream)
+        ctx.lookup_sites(cp, n, code.data_ptr(), hom.data_ptr(), het.data_ptr(), sh)
+        if e:
+            e[3].record(stream)
+            ev.append((e, t1 - t0, t2 - t1))
+        return est
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        est = step(True)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    hist_ms = sum(e[0].elapsed_time(e[1]) for e, _, _ in ev) / a.steps
+    look_ms = sum(e[2].elapsed_time(e[3]) for e, _, _ in ev) / a.steps
+    prep_ms = sum(p for _, _, p in ev) / a.steps * 1e3
+    if dist:
+        t = torch.tensor([elapsed, hist_ms, look_ms, prep_ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, hist_ms, look_ms, prep_ms = (float(x) for x in t)
+    nhet = int((code >= 0x80).sum().item())
+    u = len(ctx.profile_table()[0])
+    if rank == 0:
+        hist_gbs = LYNCH_HIST_BYTES * n / (hist_ms * 1e-3) / 1e9
+        look_gbs = LYNCH_LOOKUP_BYTES * n / (look_ms * 1e-3) / 1e9
+        dom = ("sid_lookup_sites", look_gbs, look_ms) if look_ms >= hist_ms else \
+              ("sid_profile_accumulate", hist_gbs, hist_ms)
+        out = {
+            "metric": "genome sites/sec (whole node) on 30x synthetic pileup; 1/2/4/8 GPU scaling",
+            "value": world * n * a.steps / elapsed,
+            "unit": "sites/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (counter-based 30x diploid pileup generator, BASELINE.md), counts resident in HBM",
+            "config": {"workload": f"C3: {'-R ' if R else ''}-m {a.method}, 50M-site 30x synthetic pileup per GPU",
+                       "sites_per_gpu": n, "depth": a.depth, "seed": a.seed, "method": a.method,
+                       "estimate_prior": R, "parallelism": f"site-range shards x{world} + histogram all-gather"},
+            "roofline": {"bound": "hbm", "achieved": dom[1], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": dom[1] / HBM_PEAK_GBS, "traffic": None, "kernel": dom[0], "kernel_ms": dom[2],
+                         "kernels": {"sid_profile_accumulate": {"ms": hist_ms, "bytes_per_site": LYNCH_HIST_BYTES,
+                                                                "GBps": hist_gbs},
+                                     "sid_lookup_sites": {"ms": look_ms, "bytes_per_site": LYNCH_LOOKUP_BYTES,
+                                                          "GBps": look_gbs}}},
+            "phases_ms": {"histogram": hist_ms, "estimate_classify_host": prep_ms, "lookup": look_ms},
+            "estimate": {"pi": est.heterozygosity, "eps": est.error_rate, "iterations": est.iterations,
+                         "evaluations": est.evaluations, "unique_profiles": u},
+            "het_sites_last_step": nhet,
+        }
+        if world == 1 and a.cpu_sample > 0:
+            out["cpu_baseline"], e2e = cpu_and_e2e(a)
+            if e2e is not None:
+                out["e2e"] = e2e
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def method_flags(a):
+    if a.method == "local":
+        return []
+    return (["-R"] if not a.no_R else []) + ["-m", a.method]
+
+
 def cpu_and_e2e(a):
     """Oracle CLI (reference path restated, 1 thread) and product CLI on the same
-    bounded sample text of the C2 workload."""
+    bounded sample text of the workload."""
     import sid_amd
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -190,17 +317,17 @@ def cpu_and_e2e(a):
             oracle.build()
         t0 = time.perf_counter()
         with open(os.devnull, "wb") as dn:
-            r = subprocess.run([oracle.CLI, path], stdout=dn, stderr=subprocess.PIPE)
+            r = subprocess.run([oracle.CLI] + method_flags(a) + [path], stdout=dn, stderr=subprocess.PIPE)
         dt = time.perf_counter() - t0
         base = {"value": m / dt if r.returncode == 0 else None, "unit": "sites/s", "cores": 1,
                 "kind": "port",
-                "sample": f"{m:,} sites of the C2 generator (seed {a.seed}, {a.depth:g}x), "
+                "sample": f"{m:,} sites of the {'C2' if a.method == 'local' else 'C3'} generator {' '.join(method_flags(a))} (seed {a.seed}, {a.depth:g}x), "
                           f"pileup text -> CSV to /dev/null, oracle/_build/sid_oracle "
                           f"(call.cpp/lynch.hpp/stats.cpp restated, single thread), {dt:.2f} s"}
         if not a.no_e2e and os.path.exists(sid_amd.CLI_PATH):
             with open(os.devnull, "wb") as dn:
                 t0 = time.perf_counter()
-                r = subprocess.run([sid_amd.CLI_PATH, "--stats", path], stdout=dn, stderr=subprocess.PIPE)
+                r = subprocess.run([sid_amd.CLI_PATH, "--stats"] + method_flags(a) + [path], stdout=dn, stderr=subprocess.PIPE)
                 dt = time.perf_counter() - t0
             if r.returncode == 0:
                 try:

@@ -59,7 +59,10 @@ __device__ __forceinline__ void sid_global_insert(unsigned long long* gkeys, uns
 #define SID_HIST_PROBES 32
 
 // counts: n sites; keys of value SID_EMPTY_KEY (all four counts 65535) go to
-// special[0].  stats[0] = distinct keys inserted in the global table.
+// stats[1].  stats[0] = distinct keys inserted in the global table.  With
+// SKIP_DENSE the dense-coded profiles are left out (they were counted by
+// sid_hist_dense_kernel): the overflow path of the fallback list.
+template <bool SKIP_DENSE>
 __global__ __launch_bounds__(256) void sid_hist_kernel(const uint64_t* __restrict__ counts, size_t n,
                                                        size_t per_block, unsigned long long* gkeys,
                                                        unsigned long long* gcnt, uint64_t gmask,
@@ -75,7 +78,9 @@ __global__ __launch_bounds__(256) void sid_hist_kernel(const uint64_t* __restric
     const size_t begin = (size_t)blockIdx.x * per_block;
     const size_t end = begin + per_block < n ? begin + per_block : n;
     for (size_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
-        const uint64_t key = sid_profile_key(counts[i]);
+        const uint64_t w = counts[i];
+        if (SKIP_DENSE && sid_dense_code(w) != SID_DENSE_NONE) continue;
+        const uint64_t key = sid_profile_key(w);
         if (key == SID_EMPTY_KEY) {
             atomicAdd(&stats[1], 1ull);
             continue;
@@ -122,6 +127,113 @@ __global__ void sid_hist_compact_kernel(const unsigned long long* gkeys, const u
             ocnt[k] = gcnt[i];
         }
     }
+}
+
+// ------------------------------------------------ dense histogram ---------
+// countUniqueProfiles (pileup.cpp:169-196) for the dense-coded profiles
+// (sid_math.h): one LDS u32 counter per code, one ds_add per site, no probing;
+// per block one global atomic per non-zero code.  Every other profile (het
+// sites, deep or noisy columns; ~0.1% at 30x) is appended, as its key, to a
+// global fallback list with one atomic per wave, and hashed by
+// sid_hist_list_kernel.  16-B loads of site pairs, lanes contiguous.
+typedef double sid_dvec2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void sid_fallback_append(bool fb, uint64_t key, unsigned long long* __restrict__ list,
+                                                    uint64_t cap, unsigned long long* __restrict__ ctr)
+{
+    const unsigned long long mask = __ballot(fb);
+    if (mask == 0) return;
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__ffsll((long long)mask) - 1u;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(mask));
+    base = (unsigned long long)__shfl((long long)base, (int)leader);
+    if (fb) {
+        const unsigned long long off = base + (unsigned long long)__popcll(mask & ((1ull << lane) - 1ull));
+        if (off < cap) list[off] = key;
+    }
+}
+
+template <bool PAIRS>
+__global__ __launch_bounds__(1024) void sid_hist_dense_kernel(const uint64_t* __restrict__ counts, size_t n,
+                                                              unsigned long long* __restrict__ dense,
+                                                              unsigned long long* __restrict__ list,
+                                                              uint64_t cap, unsigned long long* __restrict__ ctr)
+{
+    __shared__ uint32_t H[SID_DENSE_N];
+    for (uint32_t i = threadIdx.x; i < SID_DENSE_N; i += blockDim.x) H[i] = 0;
+    __syncthreads();
+    if (PAIRS) {
+        const ulonglong2* pairs = (const ulonglong2*)counts;
+        const size_t npairs = n / 2;
+        const size_t stride = (size_t)gridDim.x * blockDim.x;
+        for (size_t base = (size_t)blockIdx.x * blockDim.x; base < npairs; base += 2 * stride) {
+            const size_t p0 = base + threadIdx.x, p1 = p0 + stride;
+            ulonglong2 c0 = {0, 0}, c1 = {0, 0};
+            const bool v0 = p0 < npairs, v1 = p1 < npairs;
+            if (v0) c0 = pairs[p0];
+            if (v1) c1 = pairs[p1];
+            const uint64_t w[4] = {c0.x, c0.y, c1.x, c1.y};
+            const bool v[4] = {v0, v0, v1, v1};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t d = sid_dense_code(w[k]);
+                const bool fb = v[k] && d == SID_DENSE_NONE;
+                if (v[k] && !fb) atomicAdd(&H[sid_dense_slot(d)], 1u);
+                sid_fallback_append(fb, sid_profile_key(w[k]), list, cap, ctr);
+            }
+        }
+        // odd last site
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x < 64) {
+            const bool mine = threadIdx.x == 0;
+            const uint64_t w = mine ? counts[n - 1] : 0;
+            const uint32_t d = sid_dense_code(w);
+            const bool fb = mine && d == SID_DENSE_NONE;
+            if (mine && !fb) atomicAdd(&H[sid_dense_slot(d)], 1u);
+            sid_fallback_append(fb, sid_profile_key(w), list, cap, ctr);
+        }
+    } else {
+        for (size_t base = (size_t)blockIdx.x * blockDim.x; base < n; base += (size_t)gridDim.x * blockDim.x) {
+            const size_t i = base + threadIdx.x;
+            const bool v = i < n;
+            const uint64_t w = v ? counts[i] : 0;
+            const uint32_t d = sid_dense_code(w);
+            const bool fb = v && d == SID_DENSE_NONE;
+            if (v && !fb) atomicAdd(&H[sid_dense_slot(d)], 1u);
+            sid_fallback_append(fb, sid_profile_key(w), list, cap, ctr);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < SID_DENSE_N; i += blockDim.x) {
+        const uint32_t v = H[sid_dense_slot(i)];
+        if (v) atomicAdd(&dense[i], (unsigned long long)v);
+    }
+}
+
+// the fallback list into the global hash (the all-65535 key to stats[1])
+__global__ __launch_bounds__(256) void sid_hist_list_kernel(const unsigned long long* __restrict__ list, uint64_t m,
+                                                            unsigned long long* gkeys, unsigned long long* gcnt,
+                                                            uint64_t gmask, unsigned long long* stats)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = list[i];
+        if (key == SID_EMPTY_KEY) atomicAdd(&stats[1], 1ull);
+        else sid_global_insert(gkeys, gcnt, gmask, &stats[0], key, 1ull);
+    }
+}
+
+// non-zero dense counters -> (key, count), appended after *nout
+__global__ __launch_bounds__(256) void sid_dense_compact_kernel(const unsigned long long* __restrict__ dense,
+                                                                unsigned long long* okeys, unsigned long long* ocnt,
+                                                                unsigned long long* nout)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= SID_DENSE_N) return;
+    const unsigned long long v = dense[i];
+    if (!v) return;
+    const unsigned long long k = atomicAdd(nout, 1ull);
+    okeys[k] = sid_profile_key(sid_dense_word(i));
+    ocnt[k] = v;
 }
 
 // ------------------------------------------------ 10-genotype mixture -----
@@ -201,12 +313,20 @@ __device__ __forceinline__ void sid_two_sum(double a, double b, double& s, doubl
     e = (a - (s - bb)) + (b - bb);
 }
 
-// partial[2*block] = hi, partial[2*block+1] = lo of sum count*ln L
+// One (pi, eps) point per blockIdx.y.  Each block reduces its share of
+// sum count*ln L in double-double into partial[point][block]; the last block of
+// a point (ticket) adds the block partials in block order, again in
+// double-double, and writes {hi, lo} and the call's sequence number to
+// host-mapped memory, so the host reads the result without a copy.
 __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __restrict__ keys,
                                                             const uint32_t* __restrict__ cnt,
                                                             const double* __restrict__ lnM, size_t u,
-                                                            sid_lynch_eval E, double* partial)
+                                                            sid_lynch_evals EV, double* partial,
+                                                            unsigned int* ticket, double* out,
+                                                            volatile unsigned int* seq_out, unsigned int seq)
 {
+    const int pt = blockIdx.y;
+    const sid_lynch_eval& E = EV.e[pt];
     double hi = 0.0, lo = 0.0;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < u;
          i += (size_t)gridDim.x * blockDim.x) {
@@ -227,6 +347,7 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
     }
     // wave64 then block reduction, double-double
     __shared__ double sh_hi[4], sh_lo[4];
+    __shared__ bool last;
     for (int off = 32; off > 0; off >>= 1) {
         double ohi = __shfl_down(hi, off, 64);
         double olo = __shfl_down(lo, off, 64);
@@ -241,6 +362,7 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
         sh_lo[wid] = lo;
     }
     __syncthreads();
+    double* part = partial + (size_t)pt * 2 * gridDim.x;
     if (threadIdx.x == 0) {
         double H = 0.0, Lo = 0.0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
@@ -249,9 +371,30 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
             H = s;
             Lo += sh_lo[w] + e;
         }
-        partial[2 * blockIdx.x] = H;
-        partial[2 * blockIdx.x + 1] = Lo;
+        part[2 * blockIdx.x] = H;
+        part[2 * blockIdx.x + 1] = Lo;
+        __threadfence();
+        last = atomicAdd(&ticket[pt], 1u) == gridDim.x - 1;
     }
+    __syncthreads();
+    if (!last || threadIdx.x != 0) return;
+    __threadfence();
+    double H = 0.0, Lo = 0.0;
+    for (unsigned b = 0; b < gridDim.x; ++b) {
+        const double bh = ((volatile double*)part)[2 * b];
+        const double bl = ((volatile double*)part)[2 * b + 1];
+        double s, e;
+        sid_two_sum(H, bh, s, e);
+        H = s;
+        Lo += bl + e;
+    }
+    ticket[pt] = 0;   // ready for the next launch (stream-ordered)
+    double s, e;
+    sid_two_sum(H, Lo, s, e);   // normalise
+    out[2 * pt] = s;
+    out[2 * pt + 1] = e;
+    __threadfence_system();
+    seq_out[pt] = seq;
 }
 
 // Per-profile L_hom, L_het at eps-hat as emulated long doubles (ln, sign=+).
@@ -374,18 +517,137 @@ __global__ __launch_bounds__(256) void sid_lookup_kernel(const uint64_t* __restr
     }
 }
 
+// The same gather with the dense class index (sid_math.h) in LDS: a typical
+// profile costs one LDS read instead of a hash probe; pairs of sites per lane
+// (16-B count loads, 2-B code and 16-B conf stores, lanes contiguous); the
+// class records (code, {p1, p2}) are L2-resident gathers.
+__device__ __forceinline__ uint32_t sid_class_of(uint64_t w, const uint32_t* T,
+                                                 const unsigned long long* __restrict__ ckeys,
+                                                 const uint32_t* __restrict__ cidx, uint64_t cmask,
+                                                 uint32_t special_idx)
+{
+    const uint32_t d = sid_dense_code(w);
+    if (d != SID_DENSE_NONE) return T[sid_dense_slot(d)];
+    const uint64_t key = sid_profile_key(w);
+    if (key == SID_EMPTY_KEY) return special_idx;
+    uint64_t h = sid_hash64(key) & cmask;
+    for (uint64_t probe = 0; probe <= cmask; ++probe) {
+        const unsigned long long k = ckeys[h];
+        if (k == key) return cidx[h];
+        if (k == SID_EMPTY_KEY) break;
+        h = (h + 1) & cmask;
+    }
+    return 0xFFFFFFFFu;
+}
+
+template <int U>
+__global__ __launch_bounds__(1024) void sid_lookup_dense_kernel(const ulonglong2* __restrict__ pairs, size_t npairs,
+                                                                const uint32_t* __restrict__ g_dense,
+                                                                const unsigned long long* __restrict__ ckeys,
+                                                                const uint32_t* __restrict__ cidx, uint64_t cmask,
+                                                                uint32_t special_idx,
+                                                                const uint8_t* __restrict__ pcode,
+                                                                const sid_dvec2* __restrict__ cc,
+                                                                uint16_t* __restrict__ code2,
+                                                                sid_dvec2* __restrict__ hom,
+                                                                sid_dvec2* __restrict__ het)
+{
+    __shared__ uint32_t T[SID_DENSE_N];
+    for (uint32_t i = threadIdx.x; i < SID_DENSE_N; i += blockDim.x) T[sid_dense_slot(i)] = g_dense[i];
+    __syncthreads();
+    const size_t tile = (size_t)blockDim.x * U;
+    for (size_t base = (size_t)blockIdx.x * tile; base < npairs; base += (size_t)gridDim.x * tile) {
+        ulonglong2 c[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const size_t p = base + (size_t)j * blockDim.x + threadIdx.x;
+            if (p < npairs) c[j] = pairs[p];
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const size_t p = base + (size_t)j * blockDim.x + threadIdx.x;
+            if (p < npairs) {
+                const uint32_t a = sid_class_of(c[j].x, T, ckeys, cidx, cmask, special_idx);
+                const uint32_t b = sid_class_of(c[j].y, T, ckeys, cidx, cmask, special_idx);
+                // profile filtered (coverage < 4): no record
+                const sid_dvec2 zero = {0.0, 0.0};
+                const sid_dvec2 ca = a == 0xFFFFFFFFu ? zero : cc[a];
+                const sid_dvec2 cb = b == 0xFFFFFFFFu ? zero : cc[b];
+                const uint32_t ka = a == 0xFFFFFFFFu ? 0x40u : pcode[a];
+                const uint32_t kb = b == 0xFFFFFFFFu ? 0x40u : pcode[b];
+                code2[p] = (uint16_t)(ka | (kb << 8));
+                hom[p] = sid_dvec2{ca.x, cb.x};
+                het[p] = sid_dvec2{ca.y, cb.y};
+            }
+        }
+    }
+}
+
+// class records packed for the gather: cc[i] = {p1[i], p2[i]}
+__global__ __launch_bounds__(256) void sid_pack_class_kernel(const double* __restrict__ p1,
+                                                             const double* __restrict__ p2, size_t u,
+                                                             sid_dvec2* __restrict__ cc)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < u; i += (size_t)gridDim.x * blockDim.x)
+        cc[i] = sid_dvec2{p1[i], p2[i]};
+}
+
 // ------------------------------------------------------------ launchers --
 extern "C" {
 
 hipError_t sid_launch_hist(const uint16_t* counts, size_t n, unsigned long long* gkeys,
                            unsigned long long* gcnt, uint64_t gmask, unsigned long long* stats,
-                           hipStream_t st)
+                           int skip_dense, hipStream_t st)
 {
     if (n == 0) return hipSuccess;
     const size_t per_block = 16384;
     const size_t grid = (n + per_block - 1) / per_block;
-    sid_hist_kernel<<<(unsigned)grid, 256, 0, st>>>((const uint64_t*)counts, n, per_block, gkeys, gcnt,
-                                                    gmask, stats);
+    if (skip_dense)
+        sid_hist_kernel<true><<<(unsigned)grid, 256, 0, st>>>((const uint64_t*)counts, n, per_block, gkeys, gcnt,
+                                                              gmask, stats);
+    else
+        sid_hist_kernel<false><<<(unsigned)grid, 256, 0, st>>>((const uint64_t*)counts, n, per_block, gkeys, gcnt,
+                                                               gmask, stats);
+    return hipGetLastError();
+}
+
+// dense histogram pass; *ctr (fallback count) must be zero on entry
+hipError_t sid_launch_hist_dense(const uint16_t* counts, size_t n, unsigned long long* dense,
+                                 unsigned long long* list, uint64_t cap, unsigned long long* ctr, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const bool pairs = ((uintptr_t)counts & 15u) == 0 && n >= 2;
+    const size_t units = pairs ? (n / 2 + 1) : n;
+    size_t want = (units + 2 * 1024 - 1) / (2 * 1024);   // >= 2 units per lane
+    const unsigned grid = (unsigned)(want < 512 ? (want ? want : 1) : 512);
+    if (pairs)
+        sid_hist_dense_kernel<true><<<grid, 1024, 0, st>>>((const uint64_t*)counts, n, dense, list, cap, ctr);
+    else
+        sid_hist_dense_kernel<false><<<grid, 1024, 0, st>>>((const uint64_t*)counts, n, dense, list, cap, ctr);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_hist_list(const unsigned long long* list, uint64_t m, unsigned long long* gkeys,
+                                unsigned long long* gcnt, uint64_t gmask, unsigned long long* stats, hipStream_t st)
+{
+    if (m == 0) return hipSuccess;
+    uint64_t g = (m + 255) / 256;
+    sid_hist_list_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(list, m, gkeys, gcnt, gmask, stats);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_dense_compact(const unsigned long long* dense, unsigned long long* okeys,
+                                    unsigned long long* ocnt, unsigned long long* nout, hipStream_t st)
+{
+    sid_dense_compact_kernel<<<SID_DENSE_N / 256, 256, 0, st>>>(dense, okeys, ocnt, nout);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_pack_class(const double* p1, const double* p2, size_t u, double* cc, hipStream_t st)
+{
+    if (u == 0) return hipSuccess;
+    uint64_t g = (u + 255) / 256;
+    sid_pack_class_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(p1, p2, u, (sid_dvec2*)cc);
     return hipGetLastError();
 }
 
@@ -410,9 +672,11 @@ hipError_t sid_launch_compact(const unsigned long long* gkeys, const unsigned lo
 }
 
 hipError_t sid_launch_objective(const uint64_t* keys, const uint32_t* cnt, const double* lnM, size_t u,
-                                const sid_lynch_eval* E, double* partial, int grid, hipStream_t st)
+                                const sid_lynch_evals* EV, int npts, double* partial, unsigned int* ticket,
+                                double* out, unsigned int* seq_out, unsigned int seq, int grid, hipStream_t st)
 {
-    sid_objective_kernel<<<grid, 256, 0, st>>>(keys, cnt, lnM, u, *E, partial);
+    sid_objective_kernel<<<dim3(grid, npts), 256, 0, st>>>(keys, cnt, lnM, u, *EV, partial, ticket, out, seq_out,
+                                                           seq);
     return hipGetLastError();
 }
 
@@ -439,15 +703,31 @@ hipError_t sid_launch_classify(const uint64_t* keys, const double* lhom, const d
 hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned long long* ckeys,
                              const uint32_t* cidx, uint64_t cmask, uint32_t special_idx,
                              const uint8_t* pcode,
-                             const double* p1, const double* p2, uint8_t* code, double* hom,
+                             const double* p1, const double* p2, const uint32_t* dense_cidx,
+                             const double* cc, uint8_t* code, double* hom,
                              double* het, int grid_cap, hipStream_t st)
 {
     if (n == 0) return hipSuccess;
-    uint64_t g = (n + 255) / 256;
-    unsigned grid = (unsigned)(g < (uint64_t)grid_cap ? g : (uint64_t)grid_cap);
-    sid_lookup_kernel<<<grid, 256, 0, st>>>((const uint64_t*)counts, n, ckeys, cidx, cmask, special_idx,
-                                            pcode, p1, p2,
-                                            code, hom, het);
+    size_t done = 0;
+    const bool aligned = (((uintptr_t)counts | (uintptr_t)hom | (uintptr_t)het) & 15u) == 0 &&
+                         (((uintptr_t)code) & 1u) == 0;
+    if (dense_cidx && cc && aligned && n >= 2) {
+        const size_t npairs = n / 2;
+        const int U = 2;
+        size_t want = (npairs + (size_t)1024 * U - 1) / ((size_t)1024 * U);
+        const unsigned grid = (unsigned)(want < 1024 ? want : 1024);
+        sid_lookup_dense_kernel<2><<<grid, 1024, 0, st>>>((const ulonglong2*)counts, npairs, dense_cidx, ckeys, cidx,
+                                                          cmask, special_idx, pcode, (const sid_dvec2*)cc,
+                                                          (uint16_t*)code, (sid_dvec2*)hom, (sid_dvec2*)het);
+        done = 2 * npairs;
+    }
+    if (done < n) {
+        const size_t rest = n - done;
+        uint64_t g = (rest + 255) / 256;
+        unsigned grid = (unsigned)(g < (uint64_t)grid_cap ? g : (uint64_t)grid_cap);
+        sid_lookup_kernel<<<grid, 256, 0, st>>>((const uint64_t*)counts + done, rest, ckeys, cidx, cmask,
+                                                special_idx, pcode, p1, p2, code + done, hom + done, het + done);
+    }
     return hipGetLastError();
 }
 

@@ -10,9 +10,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -24,7 +26,14 @@
 extern "C" {
 hipError_t sid_launch_hist(const uint16_t* counts, size_t n, unsigned long long* gkeys,
                            unsigned long long* gcnt, uint64_t gmask, unsigned long long* stats,
-                           hipStream_t st);
+                           int skip_dense, hipStream_t st);
+hipError_t sid_launch_hist_dense(const uint16_t* counts, size_t n, unsigned long long* dense,
+                                 unsigned long long* list, uint64_t cap, unsigned long long* ctr, hipStream_t st);
+hipError_t sid_launch_hist_list(const unsigned long long* list, uint64_t m, unsigned long long* gkeys,
+                                unsigned long long* gcnt, uint64_t gmask, unsigned long long* stats, hipStream_t st);
+hipError_t sid_launch_dense_compact(const unsigned long long* dense, unsigned long long* okeys,
+                                    unsigned long long* ocnt, unsigned long long* nout, hipStream_t st);
+hipError_t sid_launch_pack_class(const double* p1, const double* p2, size_t u, double* cc, hipStream_t st);
 hipError_t sid_launch_rehash(const unsigned long long* okeys, const unsigned long long* ocnt,
                              uint64_t ocap, unsigned long long* gkeys, unsigned long long* gcnt,
                              uint64_t gmask, unsigned long long* distinct, hipStream_t st);
@@ -32,7 +41,8 @@ hipError_t sid_launch_compact(const unsigned long long* gkeys, const unsigned lo
                               uint64_t cap, unsigned long long* okeys, unsigned long long* ocnt,
                               unsigned long long* nout, hipStream_t st);
 hipError_t sid_launch_objective(const uint64_t* keys, const uint32_t* cnt, const double* lnM, size_t u,
-                                const sid_lynch_eval* E, double* partial, int grid, hipStream_t st);
+                                const sid_lynch_evals* EV, int npts, double* partial, unsigned int* ticket,
+                                double* out, unsigned int* seq_out, unsigned int seq, int grid, hipStream_t st);
 hipError_t sid_launch_profile_lik(const uint64_t* keys, const double* lnM, size_t u,
                                   const sid_lynch_eval* E, double* lhom, double* lhet, hipStream_t st);
 hipError_t sid_launch_classify(const uint64_t* keys, const double* lhom, const double* lhet, size_t u,
@@ -40,7 +50,8 @@ hipError_t sid_launch_classify(const uint64_t* keys, const double* lhom, const d
                                uint8_t* code, hipStream_t st);
 hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned long long* ckeys,
                              const uint32_t* cidx, uint64_t cmask, uint32_t special_idx,
-                             const uint8_t* pcode, const double* p1, const double* p2, uint8_t* code,
+                             const uint8_t* pcode, const double* p1, const double* p2,
+                             const uint32_t* dense_cidx, const double* cc, uint8_t* code,
                              double* hom, double* het, int grid_cap, hipStream_t st);
 }
 
@@ -67,9 +78,15 @@ struct sid_lynch_dev {
     // accumulation hash (device)
     unsigned long long* gkeys = nullptr;
     unsigned long long* gcnt = nullptr;
-    unsigned long long* stats = nullptr;   // [0] distinct, [1] all-65535 profile count
+    unsigned long long* stats = nullptr;   // [0] distinct, [1] all-65535 profile count, [2] fallback sites
     uint64_t cap = 0;
-    uint64_t distinct = 0;
+    uint64_t distinct = 0;                 // upper bound of stats[0]
+    // dense-coded profiles (sid_math.h): one u64 counter per code; the other
+    // profiles' keys go through the fallback list into the hash
+    unsigned long long* dense = nullptr;
+    unsigned long long* list = nullptr;
+    uint64_t list_cap = 0;
+    hipStream_t acc_stream = nullptr;      // stream of the last accumulate
     bool have_hist = false;
     // explicit (merged) table
     bool loaded = false;
@@ -82,10 +99,17 @@ struct sid_lynch_dev {
     uint64_t* d_keys = nullptr;
     uint32_t* d_cnt = nullptr;
     double* d_lnM = nullptr;
-    double* d_partial = nullptr;
-    std::vector<double> h_partial;
+    double* d_partial = nullptr;           // [SID_OBJ_PTS][2 * obj_grid]
     int obj_grid = 0;
     uint64_t evals = 0;
+    // objective results land in host-mapped memory (no copy): {hi, lo} per
+    // point and the launch's sequence number per point
+    unsigned int* d_ticket = nullptr;
+    double* h_out = nullptr;
+    unsigned int* h_seq = nullptr;
+    double* d_out = nullptr;
+    unsigned int* d_seq = nullptr;
+    unsigned int seq = 0;
     // class table
     bool prepared = false;
     double* d_lhom = nullptr;
@@ -95,6 +119,14 @@ struct sid_lynch_dev {
     uint8_t* d_pcode = nullptr;
     unsigned long long* d_ckeys = nullptr;
     uint32_t* d_cidx = nullptr;
+    uint32_t* d_dense_cidx = nullptr;      // dense code -> class index (SID_DENSE_NONE: none)
+    // grow-only capacities of the buffers above (no hipMalloc/hipFree per call)
+    size_t cap_u = 0;                      // U-sized arrays
+    size_t cap_c = 0;                      // class hash
+    size_t cap_x = 0;                      // export buffer (keys, counts)
+    unsigned long long* d_exp = nullptr;   // [cap_x keys][cap_x counts][1 count]
+    std::vector<double> lg;                // lg[k] = GSL lngamma(k + 1), grown on demand
+    double* d_cc = nullptr;                // {p1, p2} per class, packed for the gather
     uint64_t cmask = 0;
     uint32_t special_idx = 0xFFFFFFFFu;
 };
@@ -105,26 +137,31 @@ sid_lynch_dev* sid_lynch_dev_create(int* err)
     return new sid_lynch_dev();
 }
 
-static void free_class(sid_lynch_dev* L)
-{
-    dfree(L->d_lhom);
-    dfree(L->d_lhet);
-    dfree(L->d_c1);
-    dfree(L->d_c2);
-    dfree(L->d_pcode);
-    dfree(L->d_ckeys);
-    dfree(L->d_cidx);
-    L->prepared = false;
-}
+static void free_class(sid_lynch_dev* L) { L->prepared = false; }
 
 static void free_setup(sid_lynch_dev* L)
+{
+    L->setup = false;
+    free_class(L);
+}
+
+static void release_buffers(sid_lynch_dev* L)
 {
     dfree(L->d_keys);
     dfree(L->d_cnt);
     dfree(L->d_lnM);
     dfree(L->d_partial);
-    L->setup = false;
-    free_class(L);
+    dfree(L->d_lhom);
+    dfree(L->d_lhet);
+    dfree(L->d_c1);
+    dfree(L->d_c2);
+    dfree(L->d_pcode);
+    dfree(L->d_cc);
+    dfree(L->d_ckeys);
+    dfree(L->d_cidx);
+    dfree(L->d_dense_cidx);
+    dfree(L->d_exp);
+    L->cap_u = L->cap_c = L->cap_x = 0;
 }
 
 void sid_lynch_dev_destroy(sid_lynch_dev* L)
@@ -133,7 +170,12 @@ void sid_lynch_dev_destroy(sid_lynch_dev* L)
     dfree(L->gkeys);
     dfree(L->gcnt);
     dfree(L->stats);
-    free_setup(L);
+    dfree(L->dense);
+    dfree(L->list);
+    dfree(L->d_ticket);
+    if (L->h_out) (void)hipHostFree(L->h_out);
+    if (L->h_seq) (void)hipHostFree(L->h_seq);
+    release_buffers(L);
     delete L;
 }
 
@@ -171,12 +213,18 @@ extern "C" int sid_profile_reset(sid_ctx* c, void* stream)
     int rc = lynch_of(c, &L);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    dfree(L->gkeys);
-    dfree(L->gcnt);
-    if (!L->stats) HIPCHECK(hipMalloc(&L->stats, 2 * sizeof(unsigned long long)));
-    HIPCHECK(hipMemsetAsync(L->stats, 0, 2 * sizeof(unsigned long long), st));
-    rc = alloc_hash(L, 1ull << 16, st);
-    if (rc) return rc;
+    if (!L->stats) HIPCHECK(hipMalloc(&L->stats, 3 * sizeof(unsigned long long)));
+    if (!L->dense) HIPCHECK(hipMalloc(&L->dense, SID_DENSE_N * sizeof(unsigned long long)));
+    HIPCHECK(hipMemsetAsync(L->stats, 0, 3 * sizeof(unsigned long long), st));
+    HIPCHECK(hipMemsetAsync(L->dense, 0, SID_DENSE_N * sizeof(unsigned long long), st));
+    if (L->gkeys) {   // keep the allocation, clear it
+        HIPCHECK(hipMemsetAsync(L->gkeys, 0xFF, L->cap * sizeof(unsigned long long), st));
+        HIPCHECK(hipMemsetAsync(L->gcnt, 0, L->cap * sizeof(unsigned long long), st));
+    } else {
+        rc = alloc_hash(L, 1ull << 16, st);
+        if (rc) return rc;
+    }
+    L->acc_stream = st;
     L->distinct = 0;
     L->have_hist = true;
     L->loaded = false;
@@ -204,6 +252,10 @@ static int grow_hash(sid_lynch_dev* L, uint64_t need, hipStream_t st)
     return SID_OK;
 }
 
+// countUniqueProfiles (pileup.cpp:169-196), accumulated on the device: the
+// dense pass counts the typical profiles and lists the others; the list is
+// hashed after growing the hash for it (load factor <= 1/2).  One host sync
+// per call (the fallback count).
 extern "C" int sid_profile_accumulate(sid_ctx* c, const uint16_t* counts, size_t n, void* stream)
 {
     sid_lynch_dev* L;
@@ -216,16 +268,35 @@ extern "C" int sid_profile_accumulate(sid_ctx* c, const uint16_t* counts, size_t
     if (n == 0) return SID_OK;
     if (!counts || ((uintptr_t)counts & 7u)) return SID_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    const size_t SUB = 4u << 20;
-    for (size_t off = 0; off < n; off += SUB) {
-        size_t m = std::min(SUB, n - off);
-        rc = grow_hash(L, 2 * (L->distinct + m), st);   // load factor <= 1/2
+    if (L->acc_stream != st) {   // ordered after work queued on another stream
+        HIPCHECK(hipStreamSynchronize(L->acc_stream));
+        L->acc_stream = st;
+    }
+    if (!L->list) {
+        L->list_cap = std::min<uint64_t>(std::max<uint64_t>(n / 64, 1u << 16), 1u << 22);
+        if (const char* e = std::getenv("SID_HIST_LIST_CAP")) L->list_cap = std::max(1ull, std::strtoull(e, nullptr, 10));
+        HIPCHECK(hipMalloc(&L->list, L->list_cap * sizeof(unsigned long long)));
+    }
+    HIPCHECK(hipMemsetAsync(L->stats + 2, 0, sizeof(unsigned long long), st));
+    HIPCHECK(sid_launch_hist_dense(counts, n, L->dense, L->list, L->list_cap, L->stats + 2, st));
+    unsigned long long sv[3] = {0, 0, 0};
+    HIPCHECK(hipMemcpyAsync(sv, L->stats, sizeof(sv), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    const uint64_t F = sv[2];
+    L->distinct = sv[0];
+    if (F) {
+        rc = grow_hash(L, 2 * (L->distinct + F), st);
         if (rc) return rc;
-        HIPCHECK(sid_launch_hist(counts + 4 * off, m, L->gkeys, L->gcnt, L->cap - 1, L->stats, st));
-        unsigned long long d = 0;
-        HIPCHECK(hipMemcpyAsync(&d, L->stats, sizeof(d), hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipStreamSynchronize(st));
-        L->distinct = d;
+        if (F <= L->list_cap) {
+            HIPCHECK(sid_launch_hist_list(L->list, F, L->gkeys, L->gcnt, L->cap - 1, L->stats, st));
+        } else {   // list overflowed: hash the non-dense sites straight from the counts
+            HIPCHECK(sid_launch_hist(counts, n, L->gkeys, L->gcnt, L->cap - 1, L->stats, 1, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            dfree(L->list);
+            L->list_cap = std::min<uint64_t>(F + F / 4, 1ull << 28);
+            HIPCHECK(hipMalloc(&L->list, L->list_cap * sizeof(unsigned long long)));
+        }
+        L->distinct += F;   // upper bound until the next read of stats[0]
     }
     L->setup = false;
     free_class(L);
@@ -238,32 +309,35 @@ static int export_hist(sid_lynch_dev* L, std::vector<uint64_t>& keys, std::vecto
     keys.clear();
     cnt.clear();
     if (!L->have_hist) return SID_OK;
-    unsigned long long *ok = nullptr, *oc = nullptr, *nout = nullptr;
-    size_t m = std::max<uint64_t>(L->distinct, 1);
-    HIPCHECK(hipMalloc(&ok, m * sizeof(unsigned long long)));
-    HIPCHECK(hipMalloc(&oc, m * sizeof(unsigned long long)));
-    HIPCHECK(hipMalloc(&nout, sizeof(unsigned long long)));
-    HIPCHECK(hipMemset(nout, 0, sizeof(unsigned long long)));
+    if (L->acc_stream) HIPCHECK(hipStreamSynchronize(L->acc_stream));
+    const size_t m = L->distinct + SID_DENSE_N;
+    if (m > L->cap_x) {
+        dfree(L->d_exp);
+        L->cap_x = std::max(m, 2 * L->cap_x);
+        HIPCHECK(hipMalloc(&L->d_exp, (2 * L->cap_x + 1) * sizeof(unsigned long long)));
+    }
+    unsigned long long *ok = L->d_exp, *oc = L->d_exp + L->cap_x, *nout = L->d_exp + 2 * L->cap_x;
+    HIPCHECK(hipMemsetAsync(nout, 0, sizeof(unsigned long long), 0));
+    HIPCHECK(sid_launch_dense_compact(L->dense, ok, oc, nout, 0));
     HIPCHECK(sid_launch_compact(L->gkeys, L->gcnt, L->cap, ok, oc, nout, 0));
     unsigned long long nn = 0, stats[2] = {0, 0};
-    HIPCHECK(hipMemcpy(&nn, nout, sizeof(nn), hipMemcpyDeviceToHost));
-    HIPCHECK(hipMemcpy(stats, L->stats, sizeof(stats), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpyAsync(&nn, nout, sizeof(nn), hipMemcpyDeviceToHost, 0));
+    HIPCHECK(hipMemcpyAsync(stats, L->stats, sizeof(stats), hipMemcpyDeviceToHost, 0));
+    HIPCHECK(hipStreamSynchronize(0));
     std::vector<uint64_t> k(nn), v(nn);
     if (nn) {
-        HIPCHECK(hipMemcpy(k.data(), ok, nn * 8, hipMemcpyDeviceToHost));
-        HIPCHECK(hipMemcpy(v.data(), oc, nn * 8, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpyAsync(k.data(), ok, nn * 8, hipMemcpyDeviceToHost, 0));
+        HIPCHECK(hipMemcpyAsync(v.data(), oc, nn * 8, hipMemcpyDeviceToHost, 0));
+        HIPCHECK(hipStreamSynchronize(0));
     }
-    (void)hipFree(ok);
-    (void)hipFree(oc);
-    (void)hipFree(nout);
-    std::vector<size_t> ord(nn);
-    std::iota(ord.begin(), ord.end(), 0);
-    std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return k[a] < k[b]; });
-    keys.reserve(nn + 1);
-    cnt.reserve(nn + 1);
-    for (size_t i : ord) {
-        keys.push_back(k[i]);
-        cnt.push_back(v[i]);
+    std::vector<std::pair<uint64_t, uint64_t>> kv(nn);
+    for (size_t i = 0; i < nn; ++i) kv[i] = {k[i], v[i]};
+    std::sort(kv.begin(), kv.end());   // keys are distinct
+    keys.resize(nn);
+    cnt.resize(nn);
+    for (size_t i = 0; i < nn; ++i) {
+        keys[i] = kv[i].first;
+        cnt[i] = kv[i].second;
     }
     if (stats[1]) {   // the all-65535 profile sorts last
         keys.push_back(EMPTY);
@@ -338,19 +412,29 @@ extern "C" int sid_lynch_setup(sid_ctx* c, sid_estimate* est)
         L->fkeys.clear();
         L->fcnt.clear();
         std::vector<double> lnM;
+        // GSL lngamma(k + 1) for every count that occurs, computed once per
+        // context (the same function values as calling it per profile)
+        auto lgk = [L](uint32_t k) {
+            if (k >= L->lg.size()) {
+                size_t n0 = L->lg.size(), n1 = std::max<size_t>(k + 1, 2 * n0);
+                L->lg.resize(n1);
+                for (size_t i = n0; i < n1; ++i) L->lg[i] = sid_gsl_lngamma((double)(i + 1));
+            }
+            return L->lg[k];
+        };
         // call.cpp:66-70: drop profiles with coverage < 4; UniqueProfile::count
         // is uint32 (pileup.hpp:34)
+        L->fkeys.reserve(k.size());
+        L->fcnt.reserve(k.size());
+        lnM.reserve(k.size());
         for (size_t i = 0; i < k.size(); ++i) {
             uint32_t cov = key_n(k[i], 0) + key_n(k[i], 1) + key_n(k[i], 2) + key_n(k[i], 3);
             if (cov < 4) continue;
             L->fkeys.push_back(k[i]);
             L->fcnt.push_back((uint32_t)v[i]);
             // lynch.hpp:48-55 multinomialCoefficient exponent, double, in order
-            double m = sid_gsl_lngamma((double)(cov + 1));
-            for (int j = 0; j < 4; ++j) {
-                uint32_t nj = key_n(k[i], j);
-                m -= sid_gsl_lngamma((double)(nj + 1));
-            }
+            double m = lgk(cov);
+            for (int j = 0; j < 4; ++j) m -= lgk(key_n(k[i], j));
             lnM.push_back(m);
         }
         // pileup.cpp:198-217 (32-bit products, 64-bit sums)
@@ -363,18 +447,47 @@ extern "C" int sid_lynch_setup(sid_ctx* c, sid_estimate* est)
         }
         for (int j = 0; j < 4; ++j) L->dist[j] = total ? (double)acc[j] / (double)total : 0.25;
         const size_t U = L->fkeys.size();
-        const size_t m = std::max<size_t>(U, 1);
-        HIPCHECK(hipMalloc(&L->d_keys, m * 8));
-        HIPCHECK(hipMalloc(&L->d_cnt, m * 4));
-        HIPCHECK(hipMalloc(&L->d_lnM, m * 8));
+        if (U > L->cap_u || !L->d_keys) {   // every U-sized array, grow-only
+            const size_t m = std::max<size_t>({U, 2 * L->cap_u, 1024});
+            dfree(L->d_keys);
+            dfree(L->d_cnt);
+            dfree(L->d_lnM);
+            dfree(L->d_lhom);
+            dfree(L->d_lhet);
+            dfree(L->d_c1);
+            dfree(L->d_c2);
+            dfree(L->d_pcode);
+            dfree(L->d_cc);
+            HIPCHECK(hipMalloc(&L->d_keys, m * 8));
+            HIPCHECK(hipMalloc(&L->d_cnt, m * 4));
+            HIPCHECK(hipMalloc(&L->d_lnM, m * 8));
+            HIPCHECK(hipMalloc(&L->d_lhom, m * 8));
+            HIPCHECK(hipMalloc(&L->d_lhet, m * 8));
+            HIPCHECK(hipMalloc(&L->d_c1, m * 8));
+            HIPCHECK(hipMalloc(&L->d_c2, m * 8));
+            HIPCHECK(hipMalloc(&L->d_pcode, m));
+            HIPCHECK(hipMalloc(&L->d_cc, m * 16));
+            L->cap_u = m;
+        }
         if (U) {
-            HIPCHECK(hipMemcpy(L->d_keys, L->fkeys.data(), U * 8, hipMemcpyHostToDevice));
-            HIPCHECK(hipMemcpy(L->d_cnt, L->fcnt.data(), U * 4, hipMemcpyHostToDevice));
-            HIPCHECK(hipMemcpy(L->d_lnM, lnM.data(), U * 8, hipMemcpyHostToDevice));
+            HIPCHECK(hipMemcpyAsync(L->d_keys, L->fkeys.data(), U * 8, hipMemcpyHostToDevice, 0));
+            HIPCHECK(hipMemcpyAsync(L->d_cnt, L->fcnt.data(), U * 4, hipMemcpyHostToDevice, 0));
+            HIPCHECK(hipMemcpyAsync(L->d_lnM, lnM.data(), U * 8, hipMemcpyHostToDevice, 0));
+            HIPCHECK(hipStreamSynchronize(0));   // host vectors are pageable and local
         }
         L->obj_grid = (int)std::min<size_t>(1024, std::max<size_t>(1, (U + 255) / 256));
-        HIPCHECK(hipMalloc(&L->d_partial, 2 * L->obj_grid * sizeof(double)));
-        L->h_partial.resize(2 * L->obj_grid);
+        if (!L->d_partial) HIPCHECK(hipMalloc(&L->d_partial, SID_OBJ_PTS * 2 * 1024 * sizeof(double)));
+        if (!L->d_ticket) {
+            HIPCHECK(hipMalloc(&L->d_ticket, SID_OBJ_PTS * sizeof(unsigned int)));
+            HIPCHECK(hipMemset(L->d_ticket, 0, SID_OBJ_PTS * sizeof(unsigned int)));
+            HIPCHECK(hipHostMalloc((void**)&L->h_out, 2 * SID_OBJ_PTS * sizeof(double),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHECK(hipHostMalloc((void**)&L->h_seq, SID_OBJ_PTS * sizeof(unsigned int),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+            std::memset(L->h_seq, 0, SID_OBJ_PTS * sizeof(unsigned int));
+            HIPCHECK(hipHostGetDevicePointer((void**)&L->d_out, L->h_out, 0));
+            HIPCHECK(hipHostGetDevicePointer((void**)&L->d_seq, L->h_seq, 0));
+        }
         L->evals = 0;
         L->setup = true;
     }
@@ -404,31 +517,56 @@ static void make_eval(const double d[4], double pi, double e, sid_lynch_eval* E)
     E->lp = std::log(pi);
 }
 
-// lynch.cpp:37-61
-static int objective(sid_ctx* c, double pi, double eps, double* out)
+// lynch.cpp:37-61 at k <= SID_OBJ_PTS points in one launch.  Out-of-range
+// points return DBL_MAX without evaluation (lynch.cpp:40-42).
+static int objective_batch(sid_ctx* c, const double (*x)[2], int k, double* out)
 {
     sid_lynch_dev* L = c->lynch;
-    L->evals++;
-    if (pi < 0 || pi > 1 || eps < 0 || eps > 1) {
-        *out = DBL_MAX;
-        return SID_OK;
-    }
     const size_t U = L->fkeys.size();
-    if (U == 0) {
-        *out = -0.0;   // static_cast<double>(-0.0L)
-        return SID_OK;
+    sid_lynch_evals EV;
+    int idx[SID_OBJ_PTS];
+    int m = 0;
+    for (int i = 0; i < k; ++i) {
+        const double pi = x[i][0], eps = x[i][1];
+        if (pi < 0 || pi > 1 || eps < 0 || eps > 1) {
+            out[i] = DBL_MAX;
+        } else if (U == 0) {
+            out[i] = -0.0;   // static_cast<double>(-0.0L)
+        } else {
+            make_eval(L->dist, pi, eps, &EV.e[m]);
+            idx[m++] = i;
+        }
     }
-    sid_lynch_eval E;
-    make_eval(L->dist, pi, eps, &E);
-    HIPCHECK(sid_launch_objective(L->d_keys, L->d_cnt, L->d_lnM, U, &E, L->d_partial, L->obj_grid, 0));
-    HIPCHECK(hipMemcpy(L->h_partial.data(), L->d_partial, 2 * L->obj_grid * sizeof(double),
-                       hipMemcpyDeviceToHost));
-    long double sum = 0;
-    for (int b = 0; b < L->obj_grid; ++b) sum += (long double)L->h_partial[2 * b];
-    for (int b = 0; b < L->obj_grid; ++b) sum += (long double)L->h_partial[2 * b + 1];
-    if (std::isinf((double)sum)) sum = sum > 0 ? LDBL_MAX : -LDBL_MAX;
-    *out = (double)(-sum);
+    if (m == 0) return SID_OK;
+    const unsigned int seq = ++L->seq;
+    HIPCHECK(sid_launch_objective(L->d_keys, L->d_cnt, L->d_lnM, U, &EV, m, L->d_partial, L->d_ticket, L->d_out,
+                                  L->d_seq, seq, L->obj_grid, 0));
+    // poll the mapped sequence numbers; the stream status is the backstop
+    auto ready = [&] {
+        for (int j = 0; j < m; ++j)
+            if (__atomic_load_n(&L->h_seq[j], __ATOMIC_ACQUIRE) != seq) return false;
+        return true;
+    };
+    for (uint64_t spin = 0; !ready(); ++spin) {
+        if ((spin & 255) != 255) continue;
+        const hipError_t q = hipStreamQuery(0);
+        if (q == hipErrorNotReady) continue;
+        if (q != hipSuccess) return sid_set_hip_error(q);
+        if (!ready()) return sid_set_hip_error(hipErrorUnknown);   // finished without its result
+        break;
+    }
+    for (int j = 0; j < m; ++j) {
+        long double sum = (long double)L->h_out[2 * j] + (long double)L->h_out[2 * j + 1];
+        if (std::isinf((double)sum)) sum = sum > 0 ? LDBL_MAX : -LDBL_MAX;
+        out[idx[j]] = (double)(-sum);
+    }
     return SID_OK;
+}
+
+static int objective(sid_ctx* c, double pi, double eps, double* out)
+{
+    const double x[1][2] = {{pi, eps}};
+    return objective_batch(c, x, 1, out);
 }
 
 extern "C" int sid_lynch_objective(sid_ctx* c, double pi, double eps, double* out)
@@ -455,8 +593,32 @@ struct Simplex {
     sid_ctx* ctx;
     int err = SID_OK;
 
+    // Objective values of the points the next step may ask for, evaluated in
+    // one launch (prefetch).  The objective is a pure function of the point,
+    // so f() returning a prefetched value changes nothing in the trajectory.
+    double cx[SID_OBJ_PTS][N], cv[SID_OBJ_PTS];
+    int cn = 0;
+
+    void prefetch(const double (*pts)[N], int k)
+    {
+        cn = 0;
+        if (err) return;
+        int rc = objective_batch(ctx, pts, k, cv);
+        if (rc) {
+            err = rc;
+            return;
+        }
+        for (int i = 0; i < k; ++i) {
+            cx[i][0] = pts[i][0];
+            cx[i][1] = pts[i][1];
+        }
+        cn = k;
+    }
     double f(const double* x)
     {
+        ctx->lynch->evals++;
+        for (int i = 0; i < cn; ++i)
+            if (cx[i][0] == x[0] && cx[i][1] == x[1]) return cv[i];
         double v = 0;
         int rc = objective(ctx, x[0], x[1], &v);
         if (rc && !err) err = rc;
@@ -502,13 +664,17 @@ struct Simplex {
         S2 = ss / P;
         return std::sqrt(ss / P);
     }
-    double corner_move(double coeff, int corner, double* xc)
+    void corner_point(double coeff, int corner, double* xc) const
     {
         const size_t p = P;
         double alpha = (1 - coeff) * p / (p - 1.0);
         double beta = (p * coeff - 1.0) / (p - 1.0);
         for (int j = 0; j < N; ++j) xc[j] = center[j] * alpha;
         axpy(beta, x1[corner], xc);
+    }
+    double corner_move(double coeff, int corner, double* xc)
+    {
+        corner_point(coeff, corner, xc);
         return f(xc);
     }
     void update_point(int i, const double* x, double val)
@@ -530,6 +696,14 @@ struct Simplex {
     }
     bool contract_by_best(int best)
     {
+        double pts[P][N];
+        int k = 0;
+        for (int i = 0; i < P; ++i) {
+            if (i == best) continue;
+            for (int j = 0; j < N; ++j) pts[k][j] = 0.5 * (x1[i][j] + x1[best][j]);
+            ++k;
+        }
+        prefetch(pts, k);
         bool ok = true;
         for (int i = 0; i < P; ++i) {
             if (i == best) continue;
@@ -544,6 +718,8 @@ struct Simplex {
     }
     bool set(const double* x, const double* step, double* size)
     {
+        double pts[P][N] = {{x[0], x[1]}, {x[0] + step[0], x[1]}, {x[0], x[1] + step[1]}};
+        prefetch(pts, P);
         double v = f(x);
         if (!std::isfinite(v)) return false;
         x1[0][0] = x[0];
@@ -581,6 +757,17 @@ struct Simplex {
                 ds_hi = v;
                 s_hi = i;
             }
+        }
+        {   // reflection, expansion, and the contraction with and without the
+            // reflected point accepted first
+            double pts[SID_OBJ_PTS][N];
+            corner_point(-1.0, hi, pts[0]);
+            corner_point(-2.0, hi, pts[1]);
+            corner_point(0.5, hi, pts[2]);
+            Simplex T = *this;
+            T.update_point(hi, pts[0], 0.0);
+            T.corner_point(0.5, hi, pts[3]);
+            prefetch(pts, SID_OBJ_PTS);
         }
         double val = corner_move(-1.0, hi, xc);
         if (std::isfinite(val) && val < y1[lo]) {
@@ -664,14 +851,23 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     sid_lynch_dev* L;
     int rc = lynch_of(c, &L);
     if (rc) return rc;
+    // SID_LYNCH_TIMING=1: phase times (ms) on stderr, measurement only
+    static const bool timing = std::getenv("SID_LYNCH_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t0 = now();
     sid_estimate est;
     rc = sid_lynch_setup(c, &est);
     if (rc) return rc;
+    const auto t1 = now();
     const int method = c->opts.method;
     const size_t U = L->fkeys.size();
     if (verbose && method != SID_METHOD_LOCAL) std::fprintf(stderr, "# unique profiles: %zu\n", U);
     rc = run_estimate(c, verbose, &est);
     if (rc) return rc;
+    const auto t2 = now();
     if (est_out) *est_out = est;
     if (method == SID_METHOD_LOCAL) return SID_OK;   // -R local: caller applies the prior
     if (verbose) {
@@ -681,11 +877,6 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     if (U == 0) return SID_EEMPTY;
 
     free_class(L);
-    HIPCHECK(hipMalloc(&L->d_lhom, U * 8));
-    HIPCHECK(hipMalloc(&L->d_lhet, U * 8));
-    HIPCHECK(hipMalloc(&L->d_c1, U * 8));
-    HIPCHECK(hipMalloc(&L->d_c2, U * 8));
-    HIPCHECK(hipMalloc(&L->d_pcode, U));
     sid_lynch_eval E;
     make_eval(L->dist, est.heterozygosity, est.error_rate, &E);
     HIPCHECK(sid_launch_profile_lik(L->d_keys, L->d_lnM, U, &E, L->d_lhom, L->d_lhet, 0));
@@ -698,9 +889,10 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
         // call.cpp:113-127 labels from the adjusted p_het
         std::vector<double> ph(U), pt(U);
         std::vector<uint8_t> code(U);
-        HIPCHECK(hipMemcpy(ph.data(), L->d_c1, U * 8, hipMemcpyDeviceToHost));
-        HIPCHECK(hipMemcpy(pt.data(), L->d_c2, U * 8, hipMemcpyDeviceToHost));
-        HIPCHECK(hipMemcpy(code.data(), L->d_pcode, U, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpyAsync(ph.data(), L->d_c1, U * 8, hipMemcpyDeviceToHost, 0));
+        HIPCHECK(hipMemcpyAsync(pt.data(), L->d_c2, U * 8, hipMemcpyDeviceToHost, 0));
+        HIPCHECK(hipMemcpyAsync(code.data(), L->d_pcode, U, hipMemcpyDeviceToHost, 0));
+        HIPCHECK(hipStreamSynchronize(0));
         auto bh = [U](const std::vector<double>& p) {
             std::vector<size_t> idx(U);
             std::iota(idx.begin(), idx.end(), 0);
@@ -719,10 +911,12 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
             bool het = at[i] < c->opts.significance_level;
             code[i] = (uint8_t)(f | ((het ? s : f) << 2) | (het ? 0x80 : 0));
         }
-        HIPCHECK(hipMemcpy(L->d_c1, ah.data(), U * 8, hipMemcpyHostToDevice));
-        HIPCHECK(hipMemcpy(L->d_c2, at.data(), U * 8, hipMemcpyHostToDevice));
-        HIPCHECK(hipMemcpy(L->d_pcode, code.data(), U, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpyAsync(L->d_c1, ah.data(), U * 8, hipMemcpyHostToDevice, 0));
+        HIPCHECK(hipMemcpyAsync(L->d_c2, at.data(), U * 8, hipMemcpyHostToDevice, 0));
+        HIPCHECK(hipMemcpyAsync(L->d_pcode, code.data(), U, hipMemcpyHostToDevice, 0));
+        HIPCHECK(hipStreamSynchronize(0));   // the host vectors go out of scope
     }
+    const auto t3 = now();
     // compact class hash over the U filtered profiles
     uint64_t cap = 16;
     while (cap < 2 * U) cap <<= 1;
@@ -740,13 +934,35 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
         ck[h] = key;
         ci[h] = (uint32_t)i;
     }
-    HIPCHECK(hipMalloc(&L->d_ckeys, cap * 8));
-    HIPCHECK(hipMalloc(&L->d_cidx, cap * 4));
-    HIPCHECK(hipMemcpy(L->d_ckeys, ck.data(), cap * 8, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(L->d_cidx, ci.data(), cap * 4, hipMemcpyHostToDevice));
+    // dense code -> class index for the typical profiles (lookup fast path)
+    std::vector<uint32_t> dc(SID_DENSE_N, SID_DENSE_NONE);
+    for (size_t i = 0; i < U; ++i) {
+        const uint64_t key = L->fkeys[i];
+        const uint64_t w = (key >> 48) | (((key >> 32) & 0xffff) << 16) | (((key >> 16) & 0xffff) << 32) |
+                           ((key & 0xffff) << 48);
+        const uint32_t d = sid_dense_code(w);
+        if (d != SID_DENSE_NONE) dc[d] = (uint32_t)i;
+    }
+    if (!L->d_dense_cidx) HIPCHECK(hipMalloc(&L->d_dense_cidx, SID_DENSE_N * 4));
+    HIPCHECK(hipMemcpyAsync(L->d_dense_cidx, dc.data(), SID_DENSE_N * 4, hipMemcpyHostToDevice, 0));
+    HIPCHECK(sid_launch_pack_class(L->d_c1, L->d_c2, U, L->d_cc, 0));
+    if (cap > L->cap_c) {
+        dfree(L->d_ckeys);
+        dfree(L->d_cidx);
+        HIPCHECK(hipMalloc(&L->d_ckeys, cap * 8));
+        HIPCHECK(hipMalloc(&L->d_cidx, cap * 4));
+        L->cap_c = cap;
+    }
+    HIPCHECK(hipMemcpyAsync(L->d_ckeys, ck.data(), cap * 8, hipMemcpyHostToDevice, 0));
+    HIPCHECK(hipMemcpyAsync(L->d_cidx, ci.data(), cap * 4, hipMemcpyHostToDevice, 0));
     L->cmask = cap - 1;
-    HIPCHECK(hipDeviceSynchronize());
+    HIPCHECK(hipStreamSynchronize(0));
     L->prepared = true;
+    if (timing)
+        std::fprintf(stderr,
+                     "{\"lynch_prepare_ms\": {\"setup\": %.3f, \"estimate\": %.3f, \"evaluations\": %llu, "
+                     "\"classify_bh\": %.3f, \"class_tables\": %.3f}}\n",
+                     ms(t0, t1), ms(t1, t2), (unsigned long long)est.evaluations, ms(t2, t3), ms(t3, now()));
     return SID_OK;
 }
 
@@ -759,7 +975,7 @@ extern "C" int sid_lookup_sites(sid_ctx* c, const uint16_t* counts, size_t n, ui
     if (n == 0) return SID_OK;
     if (!counts || !code || !hom_conf || !het_conf || ((uintptr_t)counts & 7u)) return SID_EINVAL;
     HIPCHECK(sid_launch_lookup(counts, n, L->d_ckeys, L->d_cidx, L->cmask, L->special_idx, L->d_pcode,
-                               L->d_c1, L->d_c2, code, hom_conf, het_conf, c->grid_cap,
+                               L->d_c1, L->d_c2, L->d_dense_cidx, L->d_cc, code, hom_conf, het_conf, c->grid_cap,
                                (hipStream_t)stream));
     return SID_OK;
 }

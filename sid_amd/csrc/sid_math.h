@@ -55,6 +55,13 @@ struct sid_lynch_eval {
     double l1p, lp;   // ln(1 - pi), ln(pi)
 };
 
+// Up to SID_OBJ_PTS (pi, eps) points per objective launch: Nelder-Mead's
+// candidate points of one iteration are evaluated together.
+#define SID_OBJ_PTS 4
+struct sid_lynch_evals {
+    sid_lynch_eval e[SID_OBJ_PTS];
+};
+
 // x86 prints NaNs made by invalid operations as "-nan" (default NaN has the
 // sign bit set); give every NaN the same sign.
 __device__ __forceinline__ double sid_x86_nan(double v) { return isnan(v) ? -__builtin_nan("") : v; }
@@ -256,6 +263,46 @@ __host__ __device__ __forceinline__ void sid_major(uint64_t w, uint32_t& f, uint
     nf = kf >> 2;
     ns = ks >> 2;
     cov = n0 + n1 + n2 + n3;
+}
+
+// ------------------------------------------- dense profile code (Lynch) --
+// A bijection between the "typical" profiles and 14-bit codes, so that the
+// histogram (countUniqueProfiles, pileup.cpp:169-196) and the per-site class
+// lookup (call.cpp:129-140) index a 16384-entry LDS array instead of hashing.
+// m = max count, f = FIRST index holding it, o0..o2 = the other three counts
+// in index order.  Typical iff m < 64 and every o <= 3: at 30x that is every
+// homozygous site with at most 3 reads of each other base (~99.9% of sites).
+// code = f<<12 | m<<6 | o0<<4 | o1<<2 | o2; decode() inverts it exactly.
+#define SID_DENSE_N 16384u
+#define SID_DENSE_NONE 0xFFFFFFFFu
+
+__host__ __device__ __forceinline__ uint32_t sid_dense_code(uint64_t w)
+{
+    const uint32_t n0 = (uint32_t)(w & 0xffffu), n1 = (uint32_t)((w >> 16) & 0xffffu);
+    const uint32_t n2 = (uint32_t)((w >> 32) & 0xffffu), n3 = (uint32_t)(w >> 48);
+    const uint32_t m = max(max(n0, n1), max(n2, n3));
+    const uint32_t f = n0 == m ? 0u : n1 == m ? 1u : n2 == m ? 2u : 3u;
+    const uint32_t o0 = f == 0 ? n1 : n0, o1 = f <= 1 ? n2 : n1, o2 = f <= 2 ? n3 : n2;
+    if (m >= 64u || (o0 | o1 | o2) >= 4u) return SID_DENSE_NONE;
+    return (f << 12) | (m << 6) | (o0 << 4) | (o1 << 2) | o2;
+}
+
+// LDS slot of a dense code: the low 6 bits XOR-ed with m and f, so that the
+// common codes (o = 0, code = f<<12 | m<<6: all in one bank unswizzled) spread
+// over the LDS banks.  A bijection on [0, SID_DENSE_N).
+__host__ __device__ __forceinline__ uint32_t sid_dense_slot(uint32_t d)
+{
+    return d ^ (((d >> 6) ^ (d >> 11)) & 63u);
+}
+
+// profile word (A,C,G,T little-endian u16) of a dense code
+__host__ __device__ __forceinline__ uint64_t sid_dense_word(uint32_t code)
+{
+    const uint32_t f = code >> 12, m = (code >> 6) & 63u;
+    const uint32_t o[3] = {(code >> 4) & 3u, (code >> 2) & 3u, code & 3u};
+    uint64_t w = 0;
+    for (uint32_t i = 0, k = 0; i < 4; ++i) w |= (uint64_t)(i == f ? m : o[k++]) << (16 * i);
+    return w;
 }
 
 // ------------------------------------------ emulated x87 long double ------

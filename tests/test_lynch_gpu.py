@@ -124,3 +124,61 @@ def test_no_profile_with_coverage_4(gpu, sid):
     assert e.value.status == 9
     code, hom, het, est = gpu.run_method(counts, "local", estimate_prior=True)  # -R local still runs
     assert len(code) == 3
+
+
+def _all_small_profiles():
+    """Every profile with counts <= 5, plus the dense-code borders: max count
+    63/64 with the others 0..4 in every position (sid_math.h sid_dense_code)."""
+    g = np.stack(np.meshgrid(*[np.arange(6)] * 4, indexing="ij"), -1).reshape(-1, 4)
+    rows = [g]
+    for m in (62, 63, 64, 65):
+        o = np.stack(np.meshgrid(*[np.arange(5)] * 3, indexing="ij"), -1).reshape(-1, 3)
+        for f in range(4):
+            p = np.insert(o, f, m, axis=1)
+            rows.append(p)
+    return np.concatenate(rows).astype(np.uint16)
+
+
+def test_histogram_dense_code_borders(gpu, sid):
+    base = _all_small_profiles()
+    rng = np.random.default_rng(5)
+    counts = base[rng.integers(0, len(base), 500_000)]
+    counts[:len(base)] = base   # every profile at least once
+    for lo, hi in ((0, len(counts)), (1, len(counts)), (1, len(counts) - 2)):   # aligned / unaligned / odd
+        k, c = table_via_gpu(gpu, sid, counts[lo:hi])
+        kk, cc = np.unique(sid.profile_key(counts[lo:hi]), return_counts=True)
+        assert k.tolist() == kk.tolist() and c.tolist() == cc.tolist()
+
+
+def test_histogram_fallback_list_overflow(gpu, sid, monkeypatch):
+    monkeypatch.setenv("SID_HIST_LIST_CAP", "16")   # read at the context's first accumulate
+    counts = sid.synth_counts_host(11, 200_000, 30.0)
+    counts[100:20_000:7] = [40, 30, 9, 65535]        # non-dense profiles, far more than 16
+    k, c = table_via_gpu(gpu, sid, counts, chunks=2)
+    kk, cc = np.unique(sid.profile_key(counts), return_counts=True)
+    assert k.tolist() == kk.tolist() and c.tolist() == cc.tolist()
+
+
+def test_context_reuse_and_unaligned_lookup(gpu, sid, oracle):
+    """Two full runs on one context (state cleared by profile_reset); the lookup
+    through an 8-B-offset counts pointer and an odd site count (scalar tail)."""
+    import torch
+    counts = sid.synth_counts_host(13, 60_001, 30.0)
+    ctx = sid.Context(0, method="likelihood_ratio", estimate_prior=True)
+    d = gpu.to_device(np.concatenate([np.zeros((1, 4), np.uint16), counts]))
+    d2 = gpu.to_device(counts)
+    n = len(counts)
+    res = []
+    for ptr, off in ((d.data_ptr() + 8, 1), (d2.data_ptr(), 0)):   # unaligned, then aligned + odd tail
+        ctx.profile_reset(None)
+        ctx.profile_accumulate(ptr, n, None)
+        ctx.lynch_prepare()
+        _, code, hom, het = gpu.device_buffers(n + 1)
+        ctx.lookup_sites(ptr, n, code.data_ptr() + off, hom.data_ptr() + 8 * off, het.data_ptr() + 8 * off, None)
+        torch.cuda.synchronize()
+        res.append((code[off:n + off].cpu().numpy(), hom[off:n + off].cpu().numpy(),
+                    het[off:n + off].cpu().numpy()))
+    ctx.close()
+    rc, rcode, rhom, rhet, rest, u = oracle.call_method(counts, "likelihood_ratio", estimate_prior=True)
+    for code, hom, het in res:
+        assert_parity(code, hom, het, rcode, rhom, rhet, what="reuse/unaligned")

@@ -24,5 +24,11 @@ for s in $STEPS; do
     bench)
       timeout -k 10 900 python3 bench.py ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err
       rc=$?; echo "bench rc=$rc" | tee -a $O/steps.log; [ $rc -eq 0 ] || exit $rc ;;
+    bench_c3)
+      timeout -k 10 900 python3 bench.py --method likelihood_ratio ${BENCH3_ARGS} > $O/bench_c3.json 2> $O/bench_c3.err
+      rc=$?; echo "bench_c3 rc=$rc" | tee -a $O/steps.log; [ $rc -eq 0 ] || exit $rc ;;
+    bench_bayes)
+      timeout -k 10 900 python3 bench.py --method bayes ${BENCH3_ARGS} > $O/bench_bayes.json 2> $O/bench_bayes.err
+      rc=$?; echo "bench_bayes rc=$rc" | tee -a $O/steps.log; [ $rc -eq 0 ] || exit $rc ;;
   esac
 done

@@ -11,12 +11,17 @@ export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
 ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --cpu-sample 0"}
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_trace -o trace -- \
-    python3 bench.py $ARGS > $O/prof_trace.log 2>&1 || { echo "trace rc=$?"; exit 1; }
-echo "trace ok"
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/prof_fetch -o fetch -- \
-    python3 bench.py $ARGS > $O/prof_fetch.log 2>&1 || { echo "fetch rc=$?"; exit 1; }
-echo "fetch ok"
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof_write -o write -- \
-    python3 bench.py $ARGS > $O/prof_write.log 2>&1 || { echo "write rc=$?"; exit 1; }
-echo "write ok"
+P=${PREFIX:-prof}
+PASSES=${PASSES:-"trace fetch write"}
+case " $PASSES " in *" trace "*)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${P}_trace -o trace -- \
+    python3 bench.py $ARGS > $O/${P}_trace.log 2>&1 || { echo "trace rc=$?"; exit 1; }
+echo "trace ok" ;; esac
+case " $PASSES " in *" fetch "*)
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${P}_fetch -o fetch -- \
+    python3 bench.py $ARGS > $O/${P}_fetch.log 2>&1 || { echo "fetch rc=$?"; exit 1; }
+echo "fetch ok" ;; esac
+case " $PASSES " in *" write "*)
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${P}_write -o write -- \
+    python3 bench.py $ARGS > $O/${P}_write.log 2>&1 || { echo "write rc=$?"; exit 1; }
+echo "write ok" ;; esac
