@@ -55,6 +55,22 @@ __device__ __forceinline__ void sid_global_insert(unsigned long long* gkeys, uns
     }
 }
 
+// as sid_global_insert, returning 1 if the key was new instead of counting it
+__device__ __forceinline__ unsigned sid_global_insert_new(unsigned long long* gkeys, unsigned long long* gcnt,
+                                                          uint64_t gmask, uint64_t key, unsigned long long add)
+{
+    uint64_t h = sid_hash64(key) & gmask;
+    for (uint64_t probe = 0; probe <= gmask; ++probe) {
+        unsigned long long prev = atomicCAS(&gkeys[h], SID_EMPTY_KEY, (unsigned long long)key);
+        if (prev == SID_EMPTY_KEY || prev == key) {
+            atomicAdd(&gcnt[h], add);
+            return prev == SID_EMPTY_KEY;
+        }
+        h = (h + 1) & gmask;
+    }
+    return 0;
+}
+
 #define SID_HIST_LCAP 4096
 #define SID_HIST_PROBES 32
 
@@ -131,37 +147,49 @@ __global__ void sid_hist_compact_kernel(const unsigned long long* gkeys, const u
 
 // ------------------------------------------------ dense histogram ---------
 // countUniqueProfiles (pileup.cpp:169-196) for the dense-coded profiles
-// (sid_math.h): one LDS u32 counter per code, one ds_add per site, no probing;
-// per block one global atomic per non-zero code.  Every other profile (het
-// sites, deep or noisy columns; ~0.1% at 30x) is appended, as its key, to a
-// global fallback list with one atomic per wave, and hashed by
-// sid_hist_list_kernel.  16-B loads of site pairs, lanes contiguous.
+// (sid_math.h): one LDS u32 counter per code, one ds_add per site, no probing.
+// Each block writes its 64 KiB of counters to its own row of `part`
+// (coalesced, no atomics: cross-block atomics on the hot codes serialise at
+// the memory side), and sid_hist_reduce_kernel folds the rows into
+// SID_DENSE_ROWS u64 rows.  Every other profile (het sites, deep or noisy
+// columns; ~0.1% at 30x) is appended, as its key, to a global fallback list
+// with one atomic per wave, and hashed by sid_hist_list_kernel.  16-B loads
+// of site pairs, lanes contiguous.
 typedef double sid_dvec2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ void sid_fallback_append(bool fb, uint64_t key, unsigned long long* __restrict__ list,
+// Fallback keys are collected in a per-block LDS list (one LDS atomic per
+// key) and flushed with one global atomic per block: a global atomic per
+// wave on the single list counter serialises at the memory side (measured:
+// 8x the kernel's streaming time, tools/debug/hist_probe.hip).  Keys beyond
+// the LDS capacity take the global counter directly.
+#define SID_HIST_LLIST 1024
+
+__device__ __forceinline__ void sid_fallback_append(bool fb, uint64_t key, unsigned long long* llist,
+                                                    uint32_t* lcnt, unsigned long long* __restrict__ list,
                                                     uint64_t cap, unsigned long long* __restrict__ ctr)
 {
-    const unsigned long long mask = __ballot(fb);
-    if (mask == 0) return;
-    const uint32_t lane = __lane_id();
-    const uint32_t leader = (uint32_t)__ffsll((long long)mask) - 1u;
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(mask));
-    base = (unsigned long long)__shfl((long long)base, (int)leader);
-    if (fb) {
-        const unsigned long long off = base + (unsigned long long)__popcll(mask & ((1ull << lane) - 1ull));
-        if (off < cap) list[off] = key;
+    if (!fb) return;
+    const uint32_t slot = atomicAdd(lcnt, 1u);
+    if (slot < SID_HIST_LLIST) {
+        llist[slot] = key;
+        return;
     }
+    const unsigned long long off = atomicAdd(ctr, 1ull);
+    if (off < cap) list[off] = key;
 }
 
 template <bool PAIRS>
 __global__ __launch_bounds__(1024) void sid_hist_dense_kernel(const uint64_t* __restrict__ counts, size_t n,
-                                                              unsigned long long* __restrict__ dense,
+                                                              uint32_t* __restrict__ part,
                                                               unsigned long long* __restrict__ list,
                                                               uint64_t cap, unsigned long long* __restrict__ ctr)
 {
     __shared__ uint32_t H[SID_DENSE_N];
+    __shared__ unsigned long long llist[SID_HIST_LLIST];
+    __shared__ uint32_t lcnt;
+    __shared__ unsigned long long lbase;
     for (uint32_t i = threadIdx.x; i < SID_DENSE_N; i += blockDim.x) H[i] = 0;
+    if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
     if (PAIRS) {
         const ulonglong2* pairs = (const ulonglong2*)counts;
@@ -180,7 +208,7 @@ __global__ __launch_bounds__(1024) void sid_hist_dense_kernel(const uint64_t* __
                 const uint32_t d = sid_dense_code(w[k]);
                 const bool fb = v[k] && d == SID_DENSE_NONE;
                 if (v[k] && !fb) atomicAdd(&H[sid_dense_slot(d)], 1u);
-                sid_fallback_append(fb, sid_profile_key(w[k]), list, cap, ctr);
+                sid_fallback_append(fb, sid_profile_key(w[k]), llist, &lcnt, list, cap, ctr);
             }
         }
         // odd last site
@@ -190,7 +218,7 @@ __global__ __launch_bounds__(1024) void sid_hist_dense_kernel(const uint64_t* __
             const uint32_t d = sid_dense_code(w);
             const bool fb = mine && d == SID_DENSE_NONE;
             if (mine && !fb) atomicAdd(&H[sid_dense_slot(d)], 1u);
-            sid_fallback_append(fb, sid_profile_key(w), list, cap, ctr);
+            sid_fallback_append(fb, sid_profile_key(w), llist, &lcnt, list, cap, ctr);
         }
     } else {
         for (size_t base = (size_t)blockIdx.x * blockDim.x; base < n; base += (size_t)gridDim.x * blockDim.x) {
@@ -200,14 +228,39 @@ __global__ __launch_bounds__(1024) void sid_hist_dense_kernel(const uint64_t* __
             const uint32_t d = sid_dense_code(w);
             const bool fb = v && d == SID_DENSE_NONE;
             if (v && !fb) atomicAdd(&H[sid_dense_slot(d)], 1u);
-            sid_fallback_append(fb, sid_profile_key(w), list, cap, ctr);
+            sid_fallback_append(fb, sid_profile_key(w), llist, &lcnt, list, cap, ctr);
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < SID_DENSE_N; i += blockDim.x) {
-        const uint32_t v = H[sid_dense_slot(i)];
-        if (v) atomicAdd(&dense[i], (unsigned long long)v);
+    uint32_t* row = part + (size_t)blockIdx.x * SID_DENSE_N;
+    for (uint32_t i = threadIdx.x; i < SID_DENSE_N; i += blockDim.x) row[i] = H[sid_dense_slot(i)];
+    const uint32_t nl = lcnt < SID_HIST_LLIST ? lcnt : SID_HIST_LLIST;
+    if (nl == 0) return;
+    if (threadIdx.x == 0) lbase = atomicAdd(ctr, (unsigned long long)nl);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
+        if (lbase + i < cap) list[lbase + i] = llist[i];
+}
+
+// dense[g][code] += sum of the block rows of row group g (one thread per code
+// and group; no atomics)
+__global__ __launch_bounds__(256) void sid_hist_reduce_kernel(const uint32_t* __restrict__ part, uint32_t nrows,
+                                                              unsigned long long* __restrict__ dense)
+{
+    const uint32_t code = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t g = blockIdx.y;
+    const uint32_t r0 = (uint32_t)((uint64_t)nrows * g / SID_DENSE_ROWS);
+    const uint32_t r1 = (uint32_t)((uint64_t)nrows * (g + 1) / SID_DENSE_ROWS);
+    unsigned long long a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    uint32_t r = r0;
+    for (; r + 4 <= r1; r += 4) {
+        a0 += part[(size_t)r * SID_DENSE_N + code];
+        a1 += part[(size_t)(r + 1) * SID_DENSE_N + code];
+        a2 += part[(size_t)(r + 2) * SID_DENSE_N + code];
+        a3 += part[(size_t)(r + 3) * SID_DENSE_N + code];
     }
+    for (; r < r1; ++r) a0 += part[(size_t)r * SID_DENSE_N + code];
+    dense[(size_t)g * SID_DENSE_N + code] += a0 + a1 + a2 + a3;
 }
 
 // the fallback list into the global hash (the all-65535 key to stats[1])
@@ -215,10 +268,20 @@ __global__ __launch_bounds__(256) void sid_hist_list_kernel(const unsigned long 
                                                             unsigned long long* gkeys, unsigned long long* gcnt,
                                                             uint64_t gmask, unsigned long long* stats)
 {
+    unsigned long long nnew = 0, nspecial = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t key = list[i];
-        if (key == SID_EMPTY_KEY) atomicAdd(&stats[1], 1ull);
-        else sid_global_insert(gkeys, gcnt, gmask, &stats[0], key, 1ull);
+        if (key == SID_EMPTY_KEY) ++nspecial;
+        else nnew += sid_global_insert_new(gkeys, gcnt, gmask, key, 1ull);
+    }
+    // per-wave totals: one atomic per wave instead of one per new key
+    for (int off = 32; off > 0; off >>= 1) {
+        nnew += __shfl_down(nnew, off, 64);
+        nspecial += __shfl_down(nspecial, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (nnew) atomicAdd(&stats[0], nnew);
+        if (nspecial) atomicAdd(&stats[1], nspecial);
     }
 }
 
@@ -229,7 +292,8 @@ __global__ __launch_bounds__(256) void sid_dense_compact_kernel(const unsigned l
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= SID_DENSE_N) return;
-    const unsigned long long v = dense[i];
+    unsigned long long v = 0;
+    for (int g = 0; g < SID_DENSE_ROWS; ++g) v += dense[(size_t)g * SID_DENSE_N + i];
     if (!v) return;
     const unsigned long long k = atomicAdd(nout, 1ull);
     okeys[k] = sid_profile_key(sid_dense_word(i));
@@ -517,17 +581,15 @@ __global__ __launch_bounds__(256) void sid_lookup_kernel(const uint64_t* __restr
     }
 }
 
-// The same gather with the dense class index (sid_math.h) in LDS: a typical
-// profile costs one LDS read instead of a hash probe; pairs of sites per lane
-// (16-B count loads, 2-B code and 16-B conf stores, lanes contiguous); the
-// class records (code, {p1, p2}) are L2-resident gathers.
-__device__ __forceinline__ uint32_t sid_class_of(uint64_t w, const uint32_t* T,
-                                                 const unsigned long long* __restrict__ ckeys,
-                                                 const uint32_t* __restrict__ cidx, uint64_t cmask,
-                                                 uint32_t special_idx)
+// The same lookup with the class records of the record codes (sid_math.h,
+// ~98% of 30x sites) in LDS: such a site costs one LDS read of its
+// (code, {p1, p2}); the others probe the L2-resident class hash and gather.
+// Pairs of sites per lane (16-B count loads, 2-B code and 16-B conf stores,
+// lanes contiguous).
+__device__ __forceinline__ uint32_t sid_class_hash(uint64_t w, const unsigned long long* __restrict__ ckeys,
+                                                   const uint32_t* __restrict__ cidx, uint64_t cmask,
+                                                   uint32_t special_idx)
 {
-    const uint32_t d = sid_dense_code(w);
-    if (d != SID_DENSE_NONE) return T[sid_dense_slot(d)];
     const uint64_t key = sid_profile_key(w);
     if (key == SID_EMPTY_KEY) return special_idx;
     uint64_t h = sid_hash64(key) & cmask;
@@ -540,21 +602,64 @@ __device__ __forceinline__ uint32_t sid_class_of(uint64_t w, const uint32_t* T,
     return 0xFFFFFFFFu;
 }
 
-template <int U>
-__global__ __launch_bounds__(1024) void sid_lookup_dense_kernel(const ulonglong2* __restrict__ pairs, size_t npairs,
-                                                                const uint32_t* __restrict__ g_dense,
-                                                                const unsigned long long* __restrict__ ckeys,
-                                                                const uint32_t* __restrict__ cidx, uint64_t cmask,
-                                                                uint32_t special_idx,
-                                                                const uint8_t* __restrict__ pcode,
-                                                                const sid_dvec2* __restrict__ cc,
-                                                                uint16_t* __restrict__ code2,
-                                                                sid_dvec2* __restrict__ hom,
-                                                                sid_dvec2* __restrict__ het)
+// Sites without a record code are deferred to an LDS list and resolved after
+// the block's streaming loop, all lanes together: inline, every wave holding
+// one such site (~86% of waves at 30x) would stall on the dependent
+// hash-probe and gather loads inside the streaming loop.
+#define SID_LOOKUP_LMISS 2048
+
+__device__ __forceinline__ uint32_t sid_lookup_rec(uint64_t w, const sid_dvec2* R, const uint8_t* C, sid_dvec2& conf)
 {
-    __shared__ uint32_t T[SID_DENSE_N];
-    for (uint32_t i = threadIdx.x; i < SID_DENSE_N; i += blockDim.x) T[sid_dense_slot(i)] = g_dense[i];
+    const uint32_t r = sid_rec_code(sid_dense_code(w));
+    if (r == SID_DENSE_NONE) {
+        conf = sid_dvec2{0.0, 0.0};
+        return 0xFFu;   // deferred
+    }
+    conf = R[r];
+    return C[r];
+}
+
+template <int U>
+__global__ __launch_bounds__(1024) void sid_lookup_rec_kernel(const ulonglong2* __restrict__ pairs, size_t npairs,
+                                                              const sid_dvec2* __restrict__ g_rec,
+                                                              const uint8_t* __restrict__ g_rcode,
+                                                              const unsigned long long* __restrict__ ckeys,
+                                                              const uint32_t* __restrict__ cidx, uint64_t cmask,
+                                                              uint32_t special_idx,
+                                                              const uint8_t* __restrict__ pcode,
+                                                              const sid_dvec2* __restrict__ cc,
+                                                              uint16_t* __restrict__ code2,
+                                                              sid_dvec2* __restrict__ hom,
+                                                              sid_dvec2* __restrict__ het)
+{
+    __shared__ sid_dvec2 R[SID_REC_N];
+    __shared__ uint8_t C[SID_REC_N];
+    __shared__ unsigned long long lmiss[SID_LOOKUP_LMISS];
+    __shared__ uint32_t lcnt;
+    for (uint32_t i = threadIdx.x; i < SID_REC_N; i += blockDim.x) {
+        R[i] = g_rec[i];
+        C[i] = g_rcode[i];
+    }
+    if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
+    const uint64_t* counts = (const uint64_t*)pairs;
+    uint8_t* code = (uint8_t*)code2;
+    double* homd = (double*)hom;
+    double* hetd = (double*)het;
+    auto resolve = [&](size_t i) {   // the general path for site i
+        sid_dvec2 cf;
+        const uint64_t w = counts[i];
+        const uint32_t idx = sid_class_hash(w, ckeys, cidx, cmask, special_idx);
+        uint32_t k = 0x40u;   // profile filtered (coverage < 4): no record
+        cf = sid_dvec2{0.0, 0.0};
+        if (idx != 0xFFFFFFFFu) {
+            cf = cc[idx];
+            k = pcode[idx];
+        }
+        code[i] = (uint8_t)k;
+        homd[i] = cf.x;
+        hetd[i] = cf.y;
+    };
     const size_t tile = (size_t)blockDim.x * U;
     for (size_t base = (size_t)blockIdx.x * tile; base < npairs; base += (size_t)gridDim.x * tile) {
         ulonglong2 c[U];
@@ -567,20 +672,41 @@ __global__ __launch_bounds__(1024) void sid_lookup_dense_kernel(const ulonglong2
         for (int j = 0; j < U; ++j) {
             const size_t p = base + (size_t)j * blockDim.x + threadIdx.x;
             if (p < npairs) {
-                const uint32_t a = sid_class_of(c[j].x, T, ckeys, cidx, cmask, special_idx);
-                const uint32_t b = sid_class_of(c[j].y, T, ckeys, cidx, cmask, special_idx);
-                // profile filtered (coverage < 4): no record
-                const sid_dvec2 zero = {0.0, 0.0};
-                const sid_dvec2 ca = a == 0xFFFFFFFFu ? zero : cc[a];
-                const sid_dvec2 cb = b == 0xFFFFFFFFu ? zero : cc[b];
-                const uint32_t ka = a == 0xFFFFFFFFu ? 0x40u : pcode[a];
-                const uint32_t kb = b == 0xFFFFFFFFu ? 0x40u : pcode[b];
+                sid_dvec2 ca, cb;
+                const uint32_t ka = sid_lookup_rec(c[j].x, R, C, ca);
+                const uint32_t kb = sid_lookup_rec(c[j].y, R, C, cb);
                 code2[p] = (uint16_t)(ka | (kb << 8));
                 hom[p] = sid_dvec2{ca.x, cb.x};
                 het[p] = sid_dvec2{ca.y, cb.y};
+                if (ka == 0xFFu || kb == 0xFFu) {
+                    for (int q = 0; q < 2; ++q) {
+                        if ((q ? kb : ka) != 0xFFu) continue;
+                        const size_t i = 2 * p + q;
+                        const uint32_t slot = atomicAdd(&lcnt, 1u);
+                        if (slot < SID_LOOKUP_LMISS) lmiss[slot] = i;
+                        else resolve(i);   // list full: inline
+                    }
+                }
             }
         }
     }
+    __syncthreads();   // orders the placeholder stores before the resolved ones
+    const uint32_t nl = lcnt < SID_LOOKUP_LMISS ? lcnt : SID_LOOKUP_LMISS;
+    for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) resolve(lmiss[i]);
+}
+
+// record tables from the dense class index: rec[r] = {p1, p2}, rcode[r] =
+// code of the class of record code r (0x40 / zeros: no class)
+__global__ __launch_bounds__(256) void sid_rec_build_kernel(const uint32_t* __restrict__ dense_cidx,
+                                                            const uint8_t* __restrict__ pcode,
+                                                            const sid_dvec2* __restrict__ cc,
+                                                            sid_dvec2* __restrict__ rec, uint8_t* __restrict__ rcode)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= SID_REC_N) return;
+    const uint32_t idx = dense_cidx[sid_rec_dense(r)];
+    rec[r] = idx == SID_DENSE_NONE ? sid_dvec2{0.0, 0.0} : cc[idx];
+    rcode[r] = idx == SID_DENSE_NONE ? (uint8_t)0x40 : pcode[idx];
 }
 
 // class records packed for the gather: cc[i] = {p1[i], p2[i]}
@@ -611,19 +737,24 @@ hipError_t sid_launch_hist(const uint16_t* counts, size_t n, unsigned long long*
     return hipGetLastError();
 }
 
-// dense histogram pass; *ctr (fallback count) must be zero on entry
-hipError_t sid_launch_hist_dense(const uint16_t* counts, size_t n, unsigned long long* dense,
-                                 unsigned long long* list, uint64_t cap, unsigned long long* ctr, hipStream_t st)
+// dense histogram pass; *ctr (fallback count) must be zero on entry.  part
+// holds SID_HIST_GRID_MAX rows of SID_DENSE_N u32.
+#define SID_HIST_GRID_MAX 512
+hipError_t sid_launch_hist_dense(const uint16_t* counts, size_t n, uint32_t* part, unsigned long long* dense,
+                                 unsigned long long* list, uint64_t cap, unsigned long long* ctr, int grid_max,
+                                 hipStream_t st)
 {
     if (n == 0) return hipSuccess;
     const bool pairs = ((uintptr_t)counts & 15u) == 0 && n >= 2;
     const size_t units = pairs ? (n / 2 + 1) : n;
-    size_t want = (units + 2 * 1024 - 1) / (2 * 1024);   // >= 2 units per lane
-    const unsigned grid = (unsigned)(want < 512 ? (want ? want : 1) : 512);
+    const size_t gm = (size_t)(grid_max > 0 && grid_max < SID_HIST_GRID_MAX ? grid_max : SID_HIST_GRID_MAX);
+    size_t want = (units + 8 * 1024 - 1) / (8 * 1024);   // >= 8 units per lane
+    const unsigned grid = (unsigned)(want < gm ? (want ? want : 1) : gm);
     if (pairs)
-        sid_hist_dense_kernel<true><<<grid, 1024, 0, st>>>((const uint64_t*)counts, n, dense, list, cap, ctr);
+        sid_hist_dense_kernel<true><<<grid, 1024, 0, st>>>((const uint64_t*)counts, n, part, list, cap, ctr);
     else
-        sid_hist_dense_kernel<false><<<grid, 1024, 0, st>>>((const uint64_t*)counts, n, dense, list, cap, ctr);
+        sid_hist_dense_kernel<false><<<grid, 1024, 0, st>>>((const uint64_t*)counts, n, part, list, cap, ctr);
+    sid_hist_reduce_kernel<<<dim3(SID_DENSE_N / 256, SID_DENSE_ROWS), 256, 0, st>>>(part, grid, dense);
     return hipGetLastError();
 }
 
@@ -648,6 +779,15 @@ hipError_t sid_launch_pack_class(const double* p1, const double* p2, size_t u, d
     if (u == 0) return hipSuccess;
     uint64_t g = (u + 255) / 256;
     sid_pack_class_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(p1, p2, u, (sid_dvec2*)cc);
+    return hipGetLastError();
+}
+
+// record tables of the lookup (after pack_class); rec: SID_REC_N x 16 B, rcode: SID_REC_N B
+hipError_t sid_launch_rec_build(const uint32_t* dense_cidx, const uint8_t* pcode, const double* cc, double* rec,
+                                uint8_t* rcode, hipStream_t st)
+{
+    sid_rec_build_kernel<<<SID_REC_N / 256, 256, 0, st>>>(dense_cidx, pcode, (const sid_dvec2*)cc, (sid_dvec2*)rec,
+                                                          rcode);
     return hipGetLastError();
 }
 
@@ -703,7 +843,7 @@ hipError_t sid_launch_classify(const uint64_t* keys, const double* lhom, const d
 hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned long long* ckeys,
                              const uint32_t* cidx, uint64_t cmask, uint32_t special_idx,
                              const uint8_t* pcode,
-                             const double* p1, const double* p2, const uint32_t* dense_cidx,
+                             const double* p1, const double* p2, const double* rec, const uint8_t* rcode,
                              const double* cc, uint8_t* code, double* hom,
                              double* het, int grid_cap, hipStream_t st)
 {
@@ -711,14 +851,15 @@ hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned lo
     size_t done = 0;
     const bool aligned = (((uintptr_t)counts | (uintptr_t)hom | (uintptr_t)het) & 15u) == 0 &&
                          (((uintptr_t)code) & 1u) == 0;
-    if (dense_cidx && cc && aligned && n >= 2) {
+    if (rec && rcode && cc && aligned && n >= 2) {
         const size_t npairs = n / 2;
         const int U = 2;
         size_t want = (npairs + (size_t)1024 * U - 1) / ((size_t)1024 * U);
         const unsigned grid = (unsigned)(want < 1024 ? want : 1024);
-        sid_lookup_dense_kernel<2><<<grid, 1024, 0, st>>>((const ulonglong2*)counts, npairs, dense_cidx, ckeys, cidx,
-                                                          cmask, special_idx, pcode, (const sid_dvec2*)cc,
-                                                          (uint16_t*)code, (sid_dvec2*)hom, (sid_dvec2*)het);
+        sid_lookup_rec_kernel<2><<<grid, 1024, 0, st>>>((const ulonglong2*)counts, npairs, (const sid_dvec2*)rec,
+                                                        rcode, ckeys, cidx, cmask, special_idx, pcode,
+                                                        (const sid_dvec2*)cc, (uint16_t*)code, (sid_dvec2*)hom,
+                                                        (sid_dvec2*)het);
         done = 2 * npairs;
     }
     if (done < n) {

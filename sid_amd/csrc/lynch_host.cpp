@@ -27,8 +27,9 @@ extern "C" {
 hipError_t sid_launch_hist(const uint16_t* counts, size_t n, unsigned long long* gkeys,
                            unsigned long long* gcnt, uint64_t gmask, unsigned long long* stats,
                            int skip_dense, hipStream_t st);
-hipError_t sid_launch_hist_dense(const uint16_t* counts, size_t n, unsigned long long* dense,
-                                 unsigned long long* list, uint64_t cap, unsigned long long* ctr, hipStream_t st);
+hipError_t sid_launch_hist_dense(const uint16_t* counts, size_t n, uint32_t* part, unsigned long long* dense,
+                                 unsigned long long* list, uint64_t cap, unsigned long long* ctr, int grid_max,
+                                 hipStream_t st);
 hipError_t sid_launch_hist_list(const unsigned long long* list, uint64_t m, unsigned long long* gkeys,
                                 unsigned long long* gcnt, uint64_t gmask, unsigned long long* stats, hipStream_t st);
 hipError_t sid_launch_dense_compact(const unsigned long long* dense, unsigned long long* okeys,
@@ -50,9 +51,11 @@ hipError_t sid_launch_classify(const uint64_t* keys, const double* lhom, const d
                                uint8_t* code, hipStream_t st);
 hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned long long* ckeys,
                              const uint32_t* cidx, uint64_t cmask, uint32_t special_idx,
-                             const uint8_t* pcode, const double* p1, const double* p2,
-                             const uint32_t* dense_cidx, const double* cc, uint8_t* code,
+                             const uint8_t* pcode, const double* p1, const double* p2, const double* rec,
+                             const uint8_t* rcode, const double* cc, uint8_t* code,
                              double* hom, double* het, int grid_cap, hipStream_t st);
+hipError_t sid_launch_rec_build(const uint32_t* dense_cidx, const uint8_t* pcode, const double* cc, double* rec,
+                                uint8_t* rcode, hipStream_t st);
 }
 
 static const uint64_t EMPTY = 0xFFFFFFFFFFFFFFFFull;
@@ -83,7 +86,9 @@ struct sid_lynch_dev {
     uint64_t distinct = 0;                 // upper bound of stats[0]
     // dense-coded profiles (sid_math.h): one u64 counter per code; the other
     // profiles' keys go through the fallback list into the hash
-    unsigned long long* dense = nullptr;
+    unsigned long long* dense = nullptr;   // [SID_DENSE_ROWS][SID_DENSE_N]
+    uint32_t* part = nullptr;              // per-block rows of the dense pass
+    int hist_grid = 512;                   // SID_HIST_GRID (measurement knob)
     unsigned long long* list = nullptr;
     uint64_t list_cap = 0;
     hipStream_t acc_stream = nullptr;      // stream of the last accumulate
@@ -127,6 +132,8 @@ struct sid_lynch_dev {
     unsigned long long* d_exp = nullptr;   // [cap_x keys][cap_x counts][1 count]
     std::vector<double> lg;                // lg[k] = GSL lngamma(k + 1), grown on demand
     double* d_cc = nullptr;                // {p1, p2} per class, packed for the gather
+    double* d_rec = nullptr;               // {p1, p2} per record code (sid_math.h), SID_REC_N
+    uint8_t* d_rcode = nullptr;            // code per record code
     uint64_t cmask = 0;
     uint32_t special_idx = 0xFFFFFFFFu;
 };
@@ -160,6 +167,8 @@ static void release_buffers(sid_lynch_dev* L)
     dfree(L->d_ckeys);
     dfree(L->d_cidx);
     dfree(L->d_dense_cidx);
+    dfree(L->d_rec);
+    dfree(L->d_rcode);
     dfree(L->d_exp);
     L->cap_u = L->cap_c = L->cap_x = 0;
 }
@@ -171,6 +180,7 @@ void sid_lynch_dev_destroy(sid_lynch_dev* L)
     dfree(L->gcnt);
     dfree(L->stats);
     dfree(L->dense);
+    dfree(L->part);
     dfree(L->list);
     dfree(L->d_ticket);
     if (L->h_out) (void)hipHostFree(L->h_out);
@@ -214,9 +224,13 @@ extern "C" int sid_profile_reset(sid_ctx* c, void* stream)
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     if (!L->stats) HIPCHECK(hipMalloc(&L->stats, 3 * sizeof(unsigned long long)));
-    if (!L->dense) HIPCHECK(hipMalloc(&L->dense, SID_DENSE_N * sizeof(unsigned long long)));
+    if (!L->dense) {
+        HIPCHECK(hipMalloc(&L->dense, SID_DENSE_ROWS * SID_DENSE_N * sizeof(unsigned long long)));
+        if (const char* e = std::getenv("SID_HIST_GRID")) L->hist_grid = std::max(1, std::min(512, std::atoi(e)));
+        HIPCHECK(hipMalloc(&L->part, (size_t)L->hist_grid * SID_DENSE_N * sizeof(uint32_t)));
+    }
     HIPCHECK(hipMemsetAsync(L->stats, 0, 3 * sizeof(unsigned long long), st));
-    HIPCHECK(hipMemsetAsync(L->dense, 0, SID_DENSE_N * sizeof(unsigned long long), st));
+    HIPCHECK(hipMemsetAsync(L->dense, 0, SID_DENSE_ROWS * SID_DENSE_N * sizeof(unsigned long long), st));
     if (L->gkeys) {   // keep the allocation, clear it
         HIPCHECK(hipMemsetAsync(L->gkeys, 0xFF, L->cap * sizeof(unsigned long long), st));
         HIPCHECK(hipMemsetAsync(L->gcnt, 0, L->cap * sizeof(unsigned long long), st));
@@ -278,7 +292,8 @@ extern "C" int sid_profile_accumulate(sid_ctx* c, const uint16_t* counts, size_t
         HIPCHECK(hipMalloc(&L->list, L->list_cap * sizeof(unsigned long long)));
     }
     HIPCHECK(hipMemsetAsync(L->stats + 2, 0, sizeof(unsigned long long), st));
-    HIPCHECK(sid_launch_hist_dense(counts, n, L->dense, L->list, L->list_cap, L->stats + 2, st));
+    HIPCHECK(sid_launch_hist_dense(counts, n, L->part, L->dense, L->list, L->list_cap, L->stats + 2, L->hist_grid,
+                                   st));
     unsigned long long sv[3] = {0, 0, 0};
     HIPCHECK(hipMemcpyAsync(sv, L->stats, sizeof(sv), hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
@@ -946,6 +961,11 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     if (!L->d_dense_cidx) HIPCHECK(hipMalloc(&L->d_dense_cidx, SID_DENSE_N * 4));
     HIPCHECK(hipMemcpyAsync(L->d_dense_cidx, dc.data(), SID_DENSE_N * 4, hipMemcpyHostToDevice, 0));
     HIPCHECK(sid_launch_pack_class(L->d_c1, L->d_c2, U, L->d_cc, 0));
+    if (!L->d_rec) {
+        HIPCHECK(hipMalloc(&L->d_rec, SID_REC_N * 16));
+        HIPCHECK(hipMalloc(&L->d_rcode, SID_REC_N));
+    }
+    HIPCHECK(sid_launch_rec_build(L->d_dense_cidx, L->d_pcode, L->d_cc, L->d_rec, L->d_rcode, 0));
     if (cap > L->cap_c) {
         dfree(L->d_ckeys);
         dfree(L->d_cidx);
@@ -975,7 +995,7 @@ extern "C" int sid_lookup_sites(sid_ctx* c, const uint16_t* counts, size_t n, ui
     if (n == 0) return SID_OK;
     if (!counts || !code || !hom_conf || !het_conf || ((uintptr_t)counts & 7u)) return SID_EINVAL;
     HIPCHECK(sid_launch_lookup(counts, n, L->d_ckeys, L->d_cidx, L->cmask, L->special_idx, L->d_pcode,
-                               L->d_c1, L->d_c2, L->d_dense_cidx, L->d_cc, code, hom_conf, het_conf, c->grid_cap,
+                               L->d_c1, L->d_c2, L->d_rec, L->d_rcode, L->d_cc, code, hom_conf, het_conf, c->grid_cap,
                                (hipStream_t)stream));
     return SID_OK;
 }

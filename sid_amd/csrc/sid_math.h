@@ -275,6 +275,7 @@ __host__ __device__ __forceinline__ void sid_major(uint64_t w, uint32_t& f, uint
 // code = f<<12 | m<<6 | o0<<4 | o1<<2 | o2; decode() inverts it exactly.
 #define SID_DENSE_N 16384u
 #define SID_DENSE_NONE 0xFFFFFFFFu
+#define SID_DENSE_ROWS 16   // u64 rows the per-block dense counters are folded into
 
 __host__ __device__ __forceinline__ uint32_t sid_dense_code(uint64_t w)
 {
@@ -293,6 +294,21 @@ __host__ __device__ __forceinline__ uint32_t sid_dense_code(uint64_t w)
 __host__ __device__ __forceinline__ uint32_t sid_dense_slot(uint32_t d)
 {
     return d ^ (((d >> 6) ^ (d >> 11)) & 63u);
+}
+
+// Record code: the dense codes whose three minor counts are all <= 1 (at 30x
+// ~98% of sites), 11 bits: f<<9 | m<<3 | o0<<2 | o1<<1 | o2.  The per-site
+// lookup keeps one class record (code, p1, p2) per record code in LDS.
+#define SID_REC_N 2048u
+__host__ __device__ __forceinline__ uint32_t sid_rec_code(uint32_t d)
+{
+    const uint32_t o = d & 63u;
+    if (d == SID_DENSE_NONE || (o & 0x2Au)) return SID_DENSE_NONE;
+    return ((d >> 6) << 3) | ((o >> 2) & 4u) | ((o >> 1) & 2u) | (o & 1u);
+}
+__host__ __device__ __forceinline__ uint32_t sid_rec_dense(uint32_t r)
+{
+    return ((r >> 3) << 6) | (((r >> 2) & 1u) << 4) | (((r >> 1) & 1u) << 2) | (r & 1u);
 }
 
 // profile word (A,C,G,T little-endian u16) of a dense code
