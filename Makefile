@@ -9,7 +9,7 @@ SRC := sid_amd/csrc
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-function -Iinclude
 HOSTFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Iinclude
 
-KERNELS := local synth lynch
+KERNELS := local synth lynch textpath
 HOSTSRC := capi lynch_host parse emit
 OBJS := $(KERNELS:%=$(BUILD)/%.o) $(HOSTSRC:%=$(BUILD)/%.o)
 HDRS := include/sid.h $(wildcard $(SRC)/*.h)

@@ -54,6 +54,9 @@ enum {
                             abort (nmsimplex2 set; optimization.hpp:55)            */
     SID_EEMPTY = 9,      /* no profile with coverage >= 4: the reference indexes an
                             empty vector in adjustBenjaminiHochberg (stats.cpp:73) */
+    SID_EIO = 10,        /* the output callback reported a write failure            */
+    SID_ERANGE = 11,     /* a confidence outside the device formatter's range
+                            (|v| >= 2^63; p-values and posteriors never are)        */
 };
 const char* sid_strerror(int status);
 int sid_last_hip_error(void);
@@ -183,6 +186,35 @@ int sid_format_csv(const sid_sites* s, size_t begin, size_t end, const uint8_t* 
                    char* buf, size_t cap, size_t* len);
 /* %g formatting of one double exactly as std::ostream does (precision 6). */
 int sid_format_double(double v, char* buf, size_t cap);
+
+/* ------------------------------------ device text path
+ * The same parse and the same CSV, on the device: the text of one shard is
+ * copied to HBM in line-aligned chunks of `chunk` bytes (0 = 256 MiB), the
+ * copy of each chunk overlapping the parse of the previous one, and stays
+ * resident (the formatter re-reads chrom and pos from it).
+ *
+ * sid_dtext_parse: host text -> device counts (sid_dtext_counts, 4 x u16 per
+ *   non-empty line, as sid_parse_text).  Synchronises.  On a malformed line
+ *   returns SID_EMALFORMED or SID_ENULLCHROM for the first one in file order
+ *   and its byte offset in *err_offset; *out stays NULL.
+ * sid_dtext_format: the records of sites [begin, end) with the given device
+ *   code/confs, formatted on the device and handed to write() in order, in
+ *   pieces valid only during the call (write returns 0, else SID_EIO).
+ *   Synchronises. */
+typedef struct sid_dtext sid_dtext;
+typedef int (*sid_write_fn)(void* user, const char* bytes, size_t len);
+int sid_dtext_parse(sid_ctx* ctx, const char* text, size_t len, size_t chunk, sid_dtext** out,
+                    uint64_t* err_offset, void* stream);
+size_t sid_dtext_count(const sid_dtext* t);
+const uint16_t* sid_dtext_counts(const sid_dtext* t);   /* device */
+int sid_dtext_format(sid_ctx* ctx, const sid_dtext* t, size_t begin, size_t end, const uint8_t* code,
+                     const double* hom_conf, const double* het_conf, const char* conf_type,
+                     sid_write_fn write, void* user, void* stream);
+int sid_dtext_free(sid_dtext* t);
+/* The device formatter's %g, host build (tests) and device batch: out gets
+ * 16 bytes per value, NUL-padded. */
+int sid_format_g6(double v, char* buf, size_t cap);
+int sid_format_g6_device(sid_ctx* ctx, const double* values, size_t n, char* out, void* stream);
 
 #ifdef __cplusplus
 }

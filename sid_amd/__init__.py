@@ -29,7 +29,7 @@ METHODS = {"local": METHOD_LOCAL, "likelihood_ratio": METHOD_LIKELIHOOD_RATIO,
 SID_OK = 0
 STATUS = {0: "SID_OK", 1: "SID_EINVAL", 2: "SID_EHIP", 3: "SID_ENOMEM", 4: "SID_EMALFORMED",
           5: "SID_EMISSING_MQ", 6: "SID_ENULLCHROM", 7: "SID_ESTATE", 8: "SID_EBADFUNC",
-          9: "SID_EEMPTY"}
+          9: "SID_EEMPTY", 10: "SID_EIO", 11: "SID_ERANGE"}
 
 CODE_HET = 0x80
 CODE_DROPPED = 0x40
@@ -60,6 +60,7 @@ _LIB = None
 
 # (name, restype, argtypes) for every entry point of include/sid.h
 _P, _SZ, _U64, _I, _D = C.c_void_p, C.c_size_t, C.c_uint64, C.c_int, C.c_double
+WRITE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_char), C.c_size_t)   # sid_write_fn
 SIGNATURES = [
     ("sid_strerror", C.c_char_p, [_I]),
     ("sid_last_hip_error", _I, []),
@@ -92,6 +93,13 @@ SIGNATURES = [
     ("sid_sites_chrom_name", C.c_char_p, [_P, _SZ, C.POINTER(C.c_uint64)]),
     ("sid_format_csv", _I, [_P, _SZ, _SZ, _P, _P, _P, C.c_char_p, _P, _SZ, C.POINTER(C.c_size_t)]),
     ("sid_format_double", _I, [_D, C.c_char_p, _SZ]),
+    ("sid_dtext_parse", _I, [_P, _P, _SZ, _SZ, C.POINTER(_P), C.POINTER(C.c_uint64), _P]),
+    ("sid_dtext_count", _SZ, [_P]),
+    ("sid_dtext_counts", _P, [_P]),
+    ("sid_dtext_format", _I, [_P, _P, _SZ, _SZ, _P, _P, _P, C.c_char_p, WRITE_FN, _P, _P]),
+    ("sid_dtext_free", _I, [_P]),
+    ("sid_format_g6", _I, [_D, C.c_char_p, _SZ]),
+    ("sid_format_g6_device", _I, [_P, _P, _SZ, _P, _P]),
 ]
 
 
@@ -184,18 +192,18 @@ def parse_text(text: bytes, threads: int = 0) -> Sites:
 
 
 def format_csv(sites: Sites, code: np.ndarray, hom: np.ndarray, het: np.ndarray,
-               conf_type: str = "p_value") -> bytes:
+               conf_type: str = "p_value", begin: int = 0, end: int = None) -> bytes:
     L = lib()
     code = np.ascontiguousarray(code, np.uint8)
     hom = np.ascontiguousarray(hom, np.float64)
     het = np.ascontiguousarray(het, np.float64)
     need = C.c_size_t(0)
-    n = len(sites)
-    L.sid_format_csv(sites.handle, 0, n, _ptr(code), _ptr(hom), _ptr(het), conf_type.encode(),
+    n = len(sites) if end is None else end
+    L.sid_format_csv(sites.handle, begin, n, _ptr(code), _ptr(hom), _ptr(het), conf_type.encode(),
                      None, 0, C.byref(need))
     buf = C.create_string_buffer(max(need.value, 1))
     ln = C.c_size_t(0)
-    check(L.sid_format_csv(sites.handle, 0, n, _ptr(code), _ptr(hom), _ptr(het), conf_type.encode(),
+    check(L.sid_format_csv(sites.handle, begin, n, _ptr(code), _ptr(hom), _ptr(het), conf_type.encode(),
                            buf, need.value, C.byref(ln)), "format")
     return buf.raw[: ln.value]
 
@@ -204,6 +212,63 @@ def format_double(v: float) -> str:
     buf = C.create_string_buffer(48)
     k = lib().sid_format_double(float(v), buf, 48)
     return buf.value.decode()
+
+
+def format_g6(v: float) -> str:
+    """The device formatter's %g (fmt.h), host build."""
+    buf = C.create_string_buffer(48)
+    k = lib().sid_format_g6(float(v), buf, 48)
+    if k < 0:
+        raise SidError(-k, "format_g6")
+    return buf.value.decode()
+
+
+class DText:
+    """One shard of pileup text parsed on the device (sid_dtext_*)."""
+
+    def __init__(self, ctx: "Context", text: bytes, chunk: int = 0, stream=None):
+        self.ctx = ctx
+        self._text = text   # the host text must outlive the (synchronous) parse only
+        h = C.c_void_p()
+        off = C.c_uint64(0)
+        buf = C.c_char_p(text)
+        rc = lib().sid_dtext_parse(ctx.h, C.cast(buf, C.c_void_p), len(text), chunk, C.byref(h), C.byref(off),
+                                   stream)
+        if rc != 0:
+            err = SidError(rc, "sid_dtext_parse")
+            err.offset = off.value   # byte offset of the first malformed line
+            raise err
+        self.h = h
+
+    def __len__(self):
+        return lib().sid_dtext_count(self.h)
+
+    @property
+    def counts_ptr(self):
+        return lib().sid_dtext_counts(self.h)
+
+    def format(self, code_ptr, hom_ptr, het_ptr, conf_type="p_value", begin=0, end=None, stream=None) -> bytes:
+        end = len(self) if end is None else end
+        parts = []
+
+        def w(_user, data, n):
+            parts.append(C.string_at(data, n))
+            return 0
+        cb = WRITE_FN(w)
+        check(lib().sid_dtext_format(self.ctx.h, self.h, begin, end, code_ptr, hom_ptr, het_ptr,
+                                     conf_type.encode(), cb, None, stream), "sid_dtext_format")
+        return b"".join(parts)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sid_dtext_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def synth_text(seed: int, n: int, depth: float = 30.0, first: int = 0,

@@ -38,6 +38,8 @@ extern "C" const char* sid_strerror(int status)
     case SID_ESTATE: return "call order violated";
     case SID_EBADFUNC: return "non-finite function value encountered";
     case SID_EEMPTY: return "no profile with coverage >= 4";
+    case SID_EIO: return "output write failed";
+    case SID_ERANGE: return "value outside the device formatter's range";
     default: return "unknown status";
     }
 }

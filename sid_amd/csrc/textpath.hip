@@ -1,0 +1,727 @@
+// textpath.hip — pileup text -> counts and records -> CSV on the device
+// (SURVEY.md §8(f) #1 GPU-side tokenisation, #4 GPU-side CSV formatting).
+//
+// The host hands over the raw text (e.g. a file mapping); it is copied to HBM
+// in line-aligned chunks and, chunk by chunk while the next one is in flight:
+//
+//   sid_lines_count_kernel   line starts per 4 KiB tile (16-B loads, lanes
+//                            contiguous)
+//   sid_scan_kernel          exclusive scan of the tile counts (one block),
+//                            continuing the running site count of the shard
+//   sid_lines_emit_kernel    the byte offset of every non-empty line
+//                            (call.cpp:14 skips empty lines)
+//   sid_parse_kernel         one lane per line: parsePileupLine +
+//                            parseReadBases (pileup.cpp:13-153) into
+//                            profile_t counts; the first malformed line in
+//                            file order is kept as min(offset*4 + status)
+//
+// and for output, per piece of sites:
+//
+//   sid_fmt_len_kernel       record length per site (call.hpp:29-38), block sums
+//   sid_scan_kernel          block offsets
+//   sid_fmt_write_kernel     records assembled in LDS, written with 16-B stores
+//
+// chrom and pos are re-tokenised from the resident text when formatting, so
+// parsing stores only the 8-B counts (and 8-B line offsets) per site.
+// Semantics are those of parse.cpp (the host parser, tested against the
+// reference's own pileup.cpp) and emit.cpp; the %g digits come from fmt.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/sid.h"
+#include "fmt.h"
+#include "sid_internal.h"
+
+namespace {
+
+constexpr int TB = 256;                 // threads per block (4 waves)
+constexpr int TILE = TB * 16;           // bytes per line-index tile
+constexpr int SCAN_TB = 1024;
+
+// ------------------------------------------------------------ block scan --
+// exclusive scan of one u32 per thread over a 256-thread block; returns the
+// prefix, *total = block sum
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* total)
+{
+    __shared__ uint32_t wsum[TB / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (int w = 0; w < TB / 64; ++w) {
+        if (w < wid) base += wsum[w];
+        tot += wsum[w];
+    }
+    __syncthreads();   // wsum reused by the next call
+    *total = tot;
+    return base + x - v;
+}
+
+// exclusive scan of m u32 values into u64 offsets, continuing from *base;
+// *base advances by the sum (stream-ordered running total); range (if set)
+// receives {*base before, *base after}
+__global__ __launch_bounds__(SCAN_TB) void sid_scan_kernel(const uint32_t* __restrict__ in, uint64_t m,
+                                                          uint64_t* __restrict__ out, uint64_t* base,
+                                                          uint64_t* __restrict__ range)
+{
+    __shared__ uint64_t part[SCAN_TB];
+    const uint64_t per = (m + SCAN_TB - 1) / SCAN_TB;
+    const uint64_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
+    uint64_t s = 0;
+    for (uint64_t i = lo; i < hi; ++i) s += in[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {   // 1024 partials: sequential is cheap next to the launch
+        uint64_t acc = *base;
+        if (range) range[0] = acc;
+        for (int t = 0; t < SCAN_TB; ++t) {
+            const uint64_t v = part[t];
+            part[t] = acc;
+            acc += v;
+        }
+        *base = acc;
+        if (range) range[1] = acc;
+    }
+    __syncthreads();
+    uint64_t acc = part[threadIdx.x];
+    for (uint64_t i = lo; i < hi; ++i) {
+        out[i] = acc;
+        acc += in[i];
+    }
+}
+
+// ------------------------------------------------------------ line index --
+// 16 bytes per lane; bit j of the result = byte j starts a non-empty line.
+// Bytes outside [c0, c1) never start a line; c0 is a line start.
+__device__ __forceinline__ uint32_t line_start_mask(const char* __restrict__ text, uint64_t tile0, uint64_t c0,
+                                                    uint64_t c1)
+{
+    const uint64_t at = tile0 + (uint64_t)threadIdx.x * 16;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (at < c1 && at + 16 > c0) v = *(const uint4*)(text + at);
+    // previous byte: the neighbour lane's last byte, or a load at a wave start
+    uint32_t last = (v.w >> 24) & 0xffu;
+    uint32_t prev = (uint32_t)__shfl_up((int)last, 1, 64);
+    if ((threadIdx.x & 63) == 0) prev = (at > c0 && at - 1 < c1) ? (uint8_t)text[at - 1] : (uint32_t)'\n';
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t mask = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+        const uint64_t pos = at + j;
+        const bool in = pos >= c0 && pos < c1;
+        const uint32_t p = pos == c0 ? (uint32_t)'\n' : prev;
+        if (in && b != '\n' && p == '\n') mask |= 1u << j;
+        prev = b;
+    }
+    return mask;
+}
+
+__global__ __launch_bounds__(TB) void sid_lines_count_kernel(const char* __restrict__ text, uint64_t tile_base,
+                                                             uint64_t c0, uint64_t c1, uint32_t* __restrict__ cnt)
+{
+    const uint64_t tile0 = tile_base + (uint64_t)blockIdx.x * TILE;
+    const uint32_t m = __popc(line_start_mask(text, tile0, c0, c1));
+    uint32_t tot;
+    block_exscan(m, &tot);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(TB) void sid_lines_emit_kernel(const char* __restrict__ text, uint64_t tile_base,
+                                                            uint64_t c0, uint64_t c1,
+                                                            const uint64_t* __restrict__ toff,
+                                                            uint64_t* __restrict__ starts)
+{
+    const uint64_t tile0 = tile_base + (uint64_t)blockIdx.x * TILE;
+    uint32_t mask = line_start_mask(text, tile0, c0, c1);
+    uint32_t tot;
+    uint64_t o = toff[blockIdx.x] + block_exscan(__popc(mask), &tot);
+    const uint64_t at = tile0 + (uint64_t)threadIdx.x * 16;
+    while (mask) {
+        const int j = __ffs(mask) - 1;
+        starts[o++] = at + j;
+        mask &= mask - 1;
+    }
+}
+
+// ----------------------------------------------------------------- parse --
+// Byte reader over the resident text with a 16-B window.
+struct Reader {
+    const char* text;
+    uint64_t limit;    // first byte not to read (end of text)
+    uint64_t wpos = ~0ull;
+    uint4 win;
+    __device__ __forceinline__ uint32_t at(uint64_t i)
+    {
+        const uint64_t w = i & ~15ull;
+        if (w != wpos) {
+            wpos = w;
+            win = *(const uint4*)(text + w);   // text is padded to a 16-B multiple
+        }
+        const uint32_t k = (uint32_t)(i & 15);
+        const uint32_t word = k < 8 ? (k < 4 ? win.x : win.y) : (k < 12 ? win.z : win.w);
+        return (word >> (8 * (k & 3))) & 0xffu;
+    }
+};
+
+__device__ __forceinline__ bool is_sep(uint32_t c) { return c == ' ' || c == '\t'; }
+__device__ __forceinline__ bool is_c_space(uint32_t c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+__device__ __forceinline__ bool is_digit(uint32_t c) { return c >= '0' && c <= '9'; }
+
+// parse.cpp ClassTable: 1..4 = A C G T (either case), 5 = '^', 6 = '+'/'-', 0 = other
+__device__ __forceinline__ uint32_t base_class(uint32_t c)
+{
+    switch (c) {
+    case 'A': case 'a': return 1;
+    case 'C': case 'c': return 2;
+    case 'G': case 'g': return 3;
+    case 'T': case 't': return 4;
+    case '^': return 5;
+    case '+': case '-': return 6;
+    default: return 0;
+    }
+}
+
+// end of the line starting at s: the '\n' or the end of the text; and the
+// end of its C string (first NUL), as parsePileupLine sees it
+struct Line {
+    uint64_t s, le, end;
+};
+
+// tokens on ' '/'\t' runs within [s, end): up to `want` tokens
+__device__ __forceinline__ int tokenize(Reader& R, uint64_t s, uint64_t end, int want, uint64_t* tb, uint64_t* te)
+{
+    uint64_t q = s;
+    int nt = 0;
+    while (nt < want) {
+        while (q < end && is_sep(R.at(q))) ++q;
+        if (q >= end) break;
+        tb[nt] = q;
+        while (q < end && !is_sep(R.at(q))) ++q;
+        te[nt] = q;
+        ++nt;
+    }
+    return nt;
+}
+
+__device__ __forceinline__ Line find_line(Reader& R, uint64_t s)
+{
+    Line L;
+    L.s = s;
+    uint64_t q = s, z = ~0ull;
+    while (q < R.limit) {
+        const uint32_t c = R.at(q);
+        if (c == '\n') break;
+        if (c == 0 && z == ~0ull) z = q;
+        ++q;
+    }
+    L.le = q;
+    L.end = z < q ? z : q;
+    return L;
+}
+
+// (int)strtol over [b, e) (parse.cpp atoi_like)
+__device__ int atoi_like(Reader& R, uint64_t b, uint64_t e)
+{
+    while (b < e && is_c_space(R.at(b))) ++b;
+    bool neg = false;
+    if (b < e && (R.at(b) == '+' || R.at(b) == '-')) {
+        neg = R.at(b) == '-';
+        ++b;
+    }
+    unsigned long long v = 0;
+    bool ovf = false;
+    while (b < e && is_digit(R.at(b))) {
+        const unsigned d = R.at(b) - '0';
+        if (v > (ULLONG_MAX - d) / 10) ovf = true;
+        else v = v * 10 + d;
+        ++b;
+    }
+    long r;
+    if (!neg) r = (ovf || v > (unsigned long long)LONG_MAX) ? LONG_MAX : (long)v;
+    else r = (ovf || v > (unsigned long long)LONG_MAX + 1ull) ? LONG_MIN : (long)(0ull - v);
+    return (int)(unsigned)(unsigned long)r;
+}
+
+__global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ text, uint64_t len,
+                                                       const uint64_t* __restrict__ starts,
+                                                       const uint64_t* __restrict__ range,   // [lo, hi)
+                                                       uint64_t* __restrict__ counts,
+                                                       unsigned long long* __restrict__ err)
+{
+    const uint64_t lo = range[0], hi = range[1];
+    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        Reader R{text, len};
+        const Line L = find_line(R, starts[i]);
+        uint64_t tb[5], te[5];
+        const int nt = tokenize(R, L.s, L.end, 5, tb, te);
+        int code = SID_OK;
+        if (nt < 1) code = SID_ENULLCHROM;
+        else if (nt < 3 || (te[2] - tb[2]) != 1 || nt < 5) code = SID_EMALFORMED;
+        if (code != SID_OK) {   // first in file order: min(offset * 4 + kind)
+            atomicMin(err, (unsigned long long)(L.s * 4 + (code == SID_EMALFORMED ? 1u : 2u)));
+            counts[i] = 0;
+            continue;
+        }
+        // parseReadBases over token 4 with reference tb[2] (parse.cpp read_bases)
+        const uint32_t ref = R.at(tb[2]);
+        const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
+        const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
+        const uint32_t cdot = base_class(up), ccomma = base_class(lw);
+        uint32_t n[5] = {0, 0, 0, 0, 0};
+        const uint64_t b = tb[4], e = te[4];
+        for (uint64_t q = b; q < e; ++q) {
+            const uint32_t c = R.at(q);
+            const uint32_t k = c == '.' ? cdot : (c == ',' ? ccomma : base_class(c));
+            if (k <= 4) {
+                n[k]++;
+            } else if (k == 5) {
+                ++q;
+            } else if (q + 1 < e && is_digit(R.at(q + 1))) {   // '+'/'-' and a number
+                uint64_t p = q + 1;
+                unsigned long long v = 0;
+                bool ovf = false;
+                while (p < e && is_digit(R.at(p))) {
+                    const unsigned d = R.at(p) - '0';
+                    if (!ovf) {
+                        if (v > ((unsigned long long)LONG_MAX - d) / 10) ovf = true;
+                        else v = v * 10 + d;
+                    }
+                    ++p;
+                }
+                const unsigned long long length = ovf ? (unsigned long long)LONG_MAX : v;
+                // i = after + length - 1, then ++i
+                q = (length > e - p) ? e : p + length - 1;
+                if (q >= e) break;
+            }
+        }
+        counts[i] = (uint64_t)(uint16_t)n[1] | ((uint64_t)(uint16_t)n[2] << 16) | ((uint64_t)(uint16_t)n[3] << 32) |
+                    ((uint64_t)(uint16_t)n[4] << 48);
+    }
+}
+
+// ---------------------------------------------------------------- format --
+struct Rec {
+    uint64_t cb, ce;   // chrom token
+    int32_t pos;
+    bool skip;
+    int len;
+};
+
+// the record of site i (call.hpp:29-38); writes it to out when out != null
+__device__ __forceinline__ int record(Reader& R, uint64_t start, uint8_t c, double h, double t,
+                                      const char* ctype, int tlen, char* out)
+{
+    if (c & 0x40) return 0;   // filtered profile: no record (call.cpp:131-140)
+    const Line L = find_line(R, start);
+    uint64_t tb[2], te[2];
+    const int nt = tokenize(R, L.s, L.end, 2, tb, te);
+    const int32_t pos = nt >= 2 ? atoi_like(R, tb[1], te[1]) : 0;
+    char buf[64];
+    int n = 0;
+    const int clen = (int)(te[0] - tb[0]);
+    if (out) {
+        for (int k = 0; k < clen; ++k) out[k] = (char)R.at(tb[0] + k);
+        out += clen;
+    }
+    n += clen;
+    buf[0] = ',';
+    int m = 1;
+    m += sid_fmt_i32(pos, buf + m);
+    buf[m++] = ',';
+    const bool het = c & 0x80;
+    buf[m++] = 'h';
+    buf[m++] = het ? 'e' : 'o';
+    buf[m++] = het ? 't' : 'm';
+    buf[m++] = ',';
+    buf[m++] = "ACGT"[c & 3];
+    buf[m++] = "ACGT"[(c >> 2) & 3];
+    buf[m++] = ',';
+    const int a = sid_fmt_g6(h, buf + m);
+    m += a < 0 ? 0 : a;
+    buf[m++] = ',';
+    const int b = sid_fmt_g6(t, buf + m);
+    m += b < 0 ? 0 : b;
+    buf[m++] = ',';
+    if (out) {
+        for (int k = 0; k < m; ++k) out[k] = buf[k];
+        out += m;
+        for (int k = 0; k < tlen; ++k) out[k] = ctype[k];
+        out[tlen] = '\n';
+    }
+    return (a < 0 || b < 0) ? -1 : n + m + tlen + 1;
+}
+
+struct CType {
+    char s[16];
+    int len;
+};
+
+__global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict__ text, uint64_t len,
+                                                         const uint64_t* __restrict__ starts, uint64_t s0,
+                                                         uint64_t s1, const uint8_t* __restrict__ code,
+                                                         const double* __restrict__ hom,
+                                                         const double* __restrict__ het, CType ct,
+                                                         uint32_t* __restrict__ bsum, int* __restrict__ bad)
+{
+    const uint64_t i = s0 + (uint64_t)blockIdx.x * TB + threadIdx.x;
+    int l = 0;
+    if (i < s1) {
+        Reader R{text, len};
+        l = record(R, starts[i], code[i], hom[i], het[i], ct.s, ct.len, nullptr);
+        if (l < 0) {
+            atomicExch(bad, 1);
+            l = 0;
+        }
+    }
+    uint32_t tot;
+    block_exscan((uint32_t)l, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+constexpr int FMT_LDS = 24 * 1024;
+
+__global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restrict__ text, uint64_t len,
+                                                           const uint64_t* __restrict__ starts, uint64_t s0,
+                                                           uint64_t s1, const uint8_t* __restrict__ code,
+                                                           const double* __restrict__ hom,
+                                                           const double* __restrict__ het, CType ct,
+                                                           const uint64_t* __restrict__ boff, uint64_t out0,
+                                                           char* __restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) char buf[FMT_LDS + 32];
+    const uint64_t i = s0 + (uint64_t)blockIdx.x * TB + threadIdx.x;
+    Reader R{text, len};
+    int l = 0;
+    uint8_t c = 0x40;
+    double h = 0, t = 0;
+    uint64_t st = 0;
+    if (i < s1) {
+        st = starts[i];
+        c = code[i];
+        h = hom[i];
+        t = het[i];
+        l = record(R, st, c, h, t, ct.s, ct.len, nullptr);
+        if (l < 0) l = 0;
+    }
+    uint32_t tot;
+    const uint32_t my = block_exscan((uint32_t)l, &tot);
+    const uint64_t base = boff[blockIdx.x] - out0;   // offset of this block in `out`
+    if (tot > FMT_LDS) {   // long records (long chromosome names): straight to global
+        if (l) record(R, st, c, h, t, ct.s, ct.len, out + base + my);
+        return;
+    }
+    // assemble in LDS at the same 16-B phase as the destination, then 16-B stores
+    const uint32_t phase = (uint32_t)((uintptr_t)(out + base) & 15u);
+    if (l) record(R, st, c, h, t, ct.s, ct.len, buf + phase + my);
+    __syncthreads();
+    char* dst = out + base - phase;   // 16-B aligned
+    const uint32_t span = phase + tot;
+    for (uint32_t k = threadIdx.x * 16; k < span; k += TB * 16) {
+        if (k >= phase && k + 16 <= span) {
+            *(uint4*)(dst + k) = *(const uint4*)(buf + k);
+        } else {
+            for (uint32_t j = k; j < k + 16 && j < span; ++j)
+                if (j >= phase) dst[j] = buf[j];
+        }
+    }
+}
+
+// host build of the device formatter over an array (tests)
+__global__ __launch_bounds__(TB) void sid_fmt_g6_kernel(const double* __restrict__ v, size_t n, char* __restrict__ out)
+{
+    const size_t i = (size_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n) return;
+    char b[SID_FMT_MAX];
+    const int l = sid_fmt_g6(v[i], b);
+    char* o = out + i * SID_FMT_MAX;
+    for (int k = 0; k < SID_FMT_MAX; ++k) o[k] = k < l ? b[k] : 0;
+}
+
+}  // namespace
+
+// ============================================================== C ABI ======
+struct sid_dtext {
+    int device = 0;
+    char* d_text = nullptr;
+    uint64_t len = 0;
+    uint64_t* d_starts = nullptr;
+    uint64_t* d_counts = nullptr;
+    uint64_t nsites = 0;
+    uint64_t* d_state = nullptr;   // [0] running site count, [1..2] chunk range
+    unsigned long long* d_err = nullptr;
+    uint32_t* d_tcnt = nullptr;
+    uint64_t* d_toff = nullptr;
+    uint64_t tcap = 0;
+};
+
+#define TCHECK(x)                                                   \
+    do {                                                            \
+        hipError_t e_ = (x);                                        \
+        if (e_ != hipSuccess) return sid_set_hip_error(e_);         \
+    } while (0)
+
+extern "C" int sid_dtext_free(sid_dtext* t)
+{
+    if (!t) return SID_OK;
+    (void)hipSetDevice(t->device);
+    for (void* p : {(void*)t->d_text, (void*)t->d_starts, (void*)t->d_counts, (void*)t->d_state, (void*)t->d_err,
+                    (void*)t->d_tcnt, (void*)t->d_toff})
+        if (p) (void)hipFree(p);
+    delete t;
+    return SID_OK;
+}
+
+extern "C" size_t sid_dtext_count(const sid_dtext* t) { return t ? t->nsites : 0; }
+extern "C" const uint16_t* sid_dtext_counts(const sid_dtext* t) { return t ? (const uint16_t*)t->d_counts : nullptr; }
+
+extern "C" int sid_dtext_parse(sid_ctx* ctx, const char* text, size_t len, size_t chunk, sid_dtext** out,
+                               uint64_t* err_offset, void* stream)
+{
+    if (!ctx || !out || (!text && len)) return SID_EINVAL;
+    *out = nullptr;
+    const int dev = ctx->device;
+    TCHECK(hipSetDevice(dev));
+    hipStream_t st = (hipStream_t)stream;
+    if (chunk == 0) chunk = 256u << 20;
+    chunk = std::max<size_t>(chunk, TILE);
+    sid_dtext* T = new sid_dtext();
+    T->device = dev;
+    T->len = len;
+    auto fail = [&](int rc) {
+        sid_dtext_free(T);
+        return rc;
+    };
+    // line-aligned chunk boundaries
+    std::vector<uint64_t> cut{0};
+    while (cut.back() < len) {
+        uint64_t c = cut.back() + chunk;
+        if (c >= len) {
+            c = len;
+        } else {
+            const char* nl = (const char*)std::memchr(text + c, '\n', len - c);
+            c = nl ? (uint64_t)(nl - text) + 1 : len;
+        }
+        cut.push_back(c);
+    }
+    const size_t nch = cut.size() - 1;
+    size_t maxtiles = 0;
+    for (size_t k = 0; k < nch; ++k) {
+        const uint64_t tb = cut[k] & ~(uint64_t)15;
+        maxtiles = std::max<size_t>(maxtiles, (size_t)((cut[k + 1] - tb + TILE - 1) / TILE));
+    }
+    // worst case one site per 2 bytes ("x\n"); sized exactly after counting
+    hipError_t e;
+    if ((e = hipMalloc(&T->d_text, ((len + 15) & ~(size_t)15) + 128)) != hipSuccess) return fail(sid_set_hip_error(e));
+    if ((e = hipMalloc(&T->d_state, 4 * sizeof(uint64_t))) != hipSuccess) return fail(sid_set_hip_error(e));
+    if ((e = hipMalloc(&T->d_err, sizeof(unsigned long long))) != hipSuccess) return fail(sid_set_hip_error(e));
+    if ((e = hipMalloc(&T->d_tcnt, std::max<size_t>(maxtiles, 1) * 4)) != hipSuccess) return fail(sid_set_hip_error(e));
+    if ((e = hipMalloc(&T->d_toff, std::max<size_t>(maxtiles, 1) * 8)) != hipSuccess) return fail(sid_set_hip_error(e));
+    T->tcap = maxtiles;
+    if ((e = hipMemsetAsync(T->d_state, 0, 4 * sizeof(uint64_t), st)) != hipSuccess) return fail(sid_set_hip_error(e));
+    if ((e = hipMemsetAsync(T->d_err, 0xFF, sizeof(unsigned long long), st)) != hipSuccess)
+        return fail(sid_set_hip_error(e));
+    if ((e = hipMemsetAsync(T->d_text + (len & ~(size_t)15), 0, 80, st)) != hipSuccess)
+        return fail(sid_set_hip_error(e));
+    // pass 1: copy + count lines per chunk (the copies overlap the counting of
+    // the previous chunk: DMA and kernels on one stream still pipeline, the
+    // count kernels are short)
+    hipStream_t cs;
+    if ((e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) return fail(sid_set_hip_error(e));
+    std::vector<hipEvent_t> copied(nch);
+    for (auto& ev : copied) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    hipEvent_t ready;
+    (void)hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+    (void)hipEventRecord(ready, st);
+    (void)hipStreamWaitEvent(cs, ready, 0);   // the memsets above come first
+    int rc = SID_OK;
+    for (size_t k = 0; k < nch && rc == SID_OK; ++k) {
+        if ((e = hipMemcpyAsync(T->d_text + cut[k], text + cut[k], cut[k + 1] - cut[k], hipMemcpyHostToDevice, cs)) !=
+            hipSuccess)
+            rc = sid_set_hip_error(e);
+        (void)hipEventRecord(copied[k], cs);
+    }
+    // site counts per chunk -> total (one host sync), then starts + parse
+    std::vector<uint64_t> sites_before(nch + 1, 0);
+    for (size_t k = 0; k < nch && rc == SID_OK; ++k) {
+        (void)hipStreamWaitEvent(st, copied[k], 0);
+        const uint64_t tb = cut[k] & ~(uint64_t)15;
+        const unsigned tiles = (unsigned)((cut[k + 1] - tb + TILE - 1) / TILE);
+        sid_lines_count_kernel<<<tiles, TB, 0, st>>>(T->d_text, tb, cut[k], cut[k + 1], T->d_tcnt);
+        sid_scan_kernel<<<1, SCAN_TB, 0, st>>>(T->d_tcnt, tiles, T->d_toff, T->d_state, nullptr);
+        if ((e = hipGetLastError()) != hipSuccess) rc = sid_set_hip_error(e);
+    }
+    uint64_t total = 0;
+    if (rc == SID_OK) {
+        if ((e = hipMemcpyAsync(&total, T->d_state, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            rc = sid_set_hip_error(e);
+    }
+    if (rc == SID_OK) {
+        T->nsites = total;
+        const size_t m = std::max<uint64_t>(total, 1);
+        if ((e = hipMalloc(&T->d_starts, m * 8)) != hipSuccess || (e = hipMalloc(&T->d_counts, m * 8)) != hipSuccess)
+            rc = sid_set_hip_error(e);
+    }
+    if (rc == SID_OK) (void)hipMemsetAsync(T->d_state, 0, 8, st);
+    for (size_t k = 0; k < nch && rc == SID_OK; ++k) {
+        const uint64_t tb = cut[k] & ~(uint64_t)15;
+        const unsigned tiles = (unsigned)((cut[k + 1] - tb + TILE - 1) / TILE);
+        // recount (cheap) so the offsets of this chunk are in d_toff, then emit
+        sid_lines_count_kernel<<<tiles, TB, 0, st>>>(T->d_text, tb, cut[k], cut[k + 1], T->d_tcnt);
+        // d_state[1..2] = the chunk's site range (the scan advances d_state[0])
+        sid_scan_kernel<<<1, SCAN_TB, 0, st>>>(T->d_tcnt, tiles, T->d_toff, T->d_state, T->d_state + 1);
+        sid_lines_emit_kernel<<<tiles, TB, 0, st>>>(T->d_text, tb, cut[k], cut[k + 1], T->d_toff, T->d_starts);
+        const uint64_t approx = (cut[k + 1] - cut[k]) / 32 + 1;
+        const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((approx + TB - 1) / TB, 1), 8192);
+        sid_parse_kernel<<<pg, TB, 0, st>>>(T->d_text, len, T->d_starts, T->d_state + 1, T->d_counts, T->d_err);
+        if ((e = hipGetLastError()) != hipSuccess) rc = sid_set_hip_error(e);
+    }
+    unsigned long long ek = ~0ull;
+    if (rc == SID_OK) {
+        if ((e = hipMemcpyAsync(&ek, T->d_err, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            rc = sid_set_hip_error(e);
+    }
+    (void)hipStreamSynchronize(cs);
+    for (auto& ev : copied) (void)hipEventDestroy(ev);
+    (void)hipEventDestroy(ready);
+    (void)hipStreamDestroy(cs);
+    if (rc != SID_OK) return fail(rc);
+    if (ek != ~0ull) {
+        if (err_offset) *err_offset = ek >> 2;
+        return fail((ek & 3) == 1 ? SID_EMALFORMED : SID_ENULLCHROM);
+    }
+    *out = T;
+    return SID_OK;
+}
+
+// CSV records of sites [begin, end) (code bit 6: skipped) into pinned staging
+// buffers piece by piece; write() receives them in order.
+extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, size_t end, const uint8_t* d_code,
+                                const double* d_hom, const double* d_het, const char* conf_type,
+                                sid_write_fn write, void* user, void* stream)
+{
+    if (!ctx || !T || !d_code || !d_hom || !d_het || !conf_type || !write) return SID_EINVAL;
+    if (end > T->nsites || begin > end) return SID_EINVAL;
+    CType ct{};
+    ct.len = (int)std::strlen(conf_type);
+    if (ct.len >= (int)sizeof ct.s) return SID_EINVAL;
+    std::memcpy(ct.s, conf_type, ct.len);
+    TCHECK(hipSetDevice(T->device));
+    hipStream_t st = (hipStream_t)stream;
+    const size_t PIECE = 4u << 20;   // sites per piece
+    const size_t nb_max = (PIECE + TB - 1) / TB;
+    uint32_t* d_bsum = nullptr;
+    uint64_t* d_boff = nullptr;
+    uint64_t* d_base = nullptr;
+    int* d_bad = nullptr;
+    char* d_out[2] = {nullptr, nullptr};
+    char* h_out[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
+    hipEvent_t done[2], written;
+    (void)hipEventCreateWithFlags(&done[0], hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&done[1], hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&written, hipEventDisableTiming);
+    hipStream_t cs = nullptr;   // D2H of piece k overlaps the formatting of piece k+1
+    (void)hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+    int rc = SID_OK;
+    hipError_t e;
+    auto hip = [&](hipError_t x) {
+        if (x != hipSuccess && rc == SID_OK) rc = sid_set_hip_error(x);
+        return rc == SID_OK;
+    };
+    hip(hipMalloc(&d_bsum, nb_max * 4));
+    hip(hipMalloc(&d_boff, nb_max * 8));
+    hip(hipMalloc(&d_base, 8));
+    hip(hipMalloc(&d_bad, 4));
+    if (rc == SID_OK) hip(hipMemsetAsync(d_bad, 0, 4, st));
+    size_t pending_len[2] = {0, 0};
+    bool pending[2] = {false, false};
+    int k = 0;
+    auto flush = [&](int b) {   // hand piece b to the writer
+        if (!pending[b]) return;
+        pending[b] = false;
+        if (!hip(hipEventSynchronize(done[b]))) return;
+        if (pending_len[b] && write(user, h_out[b], pending_len[b]) != 0 && rc == SID_OK) rc = SID_EIO;
+    };
+    for (size_t s0 = begin; s0 < end && rc == SID_OK; s0 += PIECE, k ^= 1) {
+        const size_t s1 = std::min(end, s0 + PIECE);
+        const unsigned nb = (unsigned)((s1 - s0 + TB - 1) / TB);
+        sid_fmt_len_kernel<<<nb, TB, 0, st>>>(T->d_text, T->len, T->d_starts, s0, s1, d_code, d_hom, d_het, ct, d_bsum,
+                                               d_bad);
+        hip(hipMemsetAsync(d_base, 0, 8, st));
+        sid_scan_kernel<<<1, SCAN_TB, 0, st>>>(d_bsum, nb, d_boff, d_base, nullptr);
+        uint64_t bytes = 0;
+        hip(hipMemcpyAsync(&bytes, d_base, 8, hipMemcpyDeviceToHost, st));
+        hip(hipStreamSynchronize(st));
+        if (rc != SID_OK) break;
+        flush(k);   // buffer k is about to be reused
+        if (rc != SID_OK) break;
+        if (bytes + 64 > cap[k]) {
+            if (d_out[k]) (void)hipFree(d_out[k]);
+            if (h_out[k]) (void)hipHostFree(h_out[k]);
+            d_out[k] = nullptr;
+            h_out[k] = nullptr;
+            cap[k] = bytes + bytes / 4 + 4096;
+            if (!hip(hipMalloc(&d_out[k], cap[k]))) break;
+            if (!hip(hipHostMalloc((void**)&h_out[k], cap[k], hipHostMallocDefault))) break;
+        }
+        sid_fmt_write_kernel<<<nb, TB, 0, st>>>(T->d_text, T->len, T->d_starts, s0, s1, d_code, d_hom, d_het, ct,
+                                                 d_boff, 0, d_out[k]);
+        if (!hip(hipGetLastError())) break;
+        hip(hipEventRecord(written, st));
+        hip(hipStreamWaitEvent(cs, written, 0));
+        if (bytes) hip(hipMemcpyAsync(h_out[k], d_out[k], bytes, hipMemcpyDeviceToHost, cs));
+        hip(hipEventRecord(done[k], cs));
+        pending[k] = true;
+        pending_len[k] = bytes;
+        flush(k ^ 1);   // the previous piece, while this one copies
+    }
+    flush(k ^ 1);
+    flush(k);
+    int bad = 0;
+    if (rc == SID_OK && hip(hipMemcpy(&bad, d_bad, 4, hipMemcpyDeviceToHost)) && bad) rc = SID_ERANGE;
+    (void)hipStreamSynchronize(cs);
+    for (int b = 0; b < 2; ++b) {
+        if (d_out[b]) (void)hipFree(d_out[b]);
+        if (h_out[b]) (void)hipHostFree(h_out[b]);
+        (void)hipEventDestroy(done[b]);
+    }
+    (void)hipEventDestroy(written);
+    (void)hipStreamDestroy(cs);
+    for (void* p : {(void*)d_bsum, (void*)d_boff, (void*)d_base, (void*)d_bad})
+        if (p) (void)hipFree(p);
+    (void)e;
+    return rc;
+}
+
+extern "C" int sid_format_g6(double v, char* buf, size_t cap)
+{
+    char tmp[SID_FMT_MAX];
+    const int n = sid_fmt_g6(v, tmp);
+    if (n < 0) return -SID_ERANGE;
+    if (!buf || cap < (size_t)n + 1) return -(n + 1);
+    std::memcpy(buf, tmp, n);
+    buf[n] = '\0';
+    return n;
+}
+
+extern "C" int sid_format_g6_device(sid_ctx* ctx, const double* d_v, size_t n, char* d_out, void* stream)
+{
+    if (!ctx || (n && (!d_v || !d_out))) return SID_EINVAL;
+    if (n == 0) return SID_OK;
+    TCHECK(hipSetDevice(ctx->device));
+    sid_fmt_g6_kernel<<<(unsigned)((n + TB - 1) / TB), TB, 0, (hipStream_t)stream>>>(d_v, n, d_out);
+    TCHECK(hipGetLastError());
+    return SID_OK;
+}

@@ -34,6 +34,18 @@ def stream_handle(device: int = 0):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+class _CAI:
+    def __init__(self, ptr, shape, typestr):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 2}
+
+
+def device_view(ptr: int, shape, typestr: str = "<i2", device: int = 0):
+    """A torch tensor viewing library-owned device memory (no copy)."""
+    torch = _torch()
+    return torch.as_tensor(_CAI(ptr, shape, typestr), device=torch.device("cuda", device))
+
+
 def to_device(counts_np: np.ndarray, device: int = 0):
     torch = _torch()
     a = np.ascontiguousarray(counts_np, np.uint16).view(np.int16)
