@@ -4,13 +4,18 @@
 // reference's defaults, help text, error messages and exit codes; CSV on
 // stdout, "# ..." diagnostics on stderr.  Behind it:
 //
-//   mmap(file) -> sid_parse_text (N host threads) -> counts resident in HBM
-//   (one shard per GPU) -> sid_call_local | sid_profile_* + sid_lynch_prepare
-//   + sid_lookup_sites -> code/confs back to pinned host memory ->
-//   sid_format_csv (N host threads) -> stdout in input order.
+//   mmap(file) -> text to HBM, parsed there (sid_dtext_parse; one line-aligned
+//   shard per GPU) -> sid_call_local | sid_profile_* + sid_lynch_prepare +
+//   sid_lookup_sites -> records formatted on the device (sid_dtext_format) ->
+//   stdout in input order.
 //
 // Extra long options (no short letter, so they cannot collide with the
-// reference's flags): --devices N, --threads N, --stats.
+// reference's flags): --devices N, --threads N, --stats, --host-parse.
+//
+// Default path: the text itself goes to each device (sid_dtext_parse: a
+// line-aligned byte range per device, parsed in HBM), and the CSV records
+// come back formatted by the device (sid_dtext_format).  --host-parse keeps
+// the host parser and emitter (sid_parse_text / sid_format_csv) instead.
 //
 // As in the reference, the whole input is parsed before anything is written
 // to stdout, so a malformed line aborts with no CSV output (call.cpp:11-20
@@ -44,6 +49,7 @@ struct Options {
     int devices = 1;
     int threads = 0;
     bool stats = false;
+    bool host_parse = false;   // parse and format on the host (sid_parse_text / sid_format_csv)
 };
 
 // sid.cpp:26-58; std::map<char,...> iterates E R h m p r
@@ -149,9 +155,11 @@ bool open_input(const char* path, Input& in)
 }
 
 struct Shard {
-    size_t begin = 0, end = 0;
+    size_t begin = 0, end = 0;            // global site range
     sid_ctx* ctx = nullptr;
-    uint16_t* d_counts = nullptr;
+    const uint16_t* d_counts = nullptr;   // the shard's counts (owned below or by `text`)
+    uint16_t* d_own_counts = nullptr;     // host-parse path: uploaded counts
+    sid_dtext* text = nullptr;            // device-parse path: resident text + counts
     uint8_t* d_code = nullptr;
     double* d_hom = nullptr;
     double* d_het = nullptr;
@@ -167,6 +175,7 @@ int main(int argc, char** argv)
     static const struct option LONG[] = {{"devices", required_argument, nullptr, 1},
                                          {"threads", required_argument, nullptr, 2},
                                          {"stats", no_argument, nullptr, 3},
+                                         {"host-parse", no_argument, nullptr, 4},
                                          {nullptr, 0, nullptr, 0}};
     int flag;
     while ((flag = getopt_long(argc, argv, "E:Rhm:p:r:", LONG, nullptr)) != -1) {
@@ -187,6 +196,7 @@ int main(int argc, char** argv)
         case 1: opt.devices = std::max(1, std::atoi(optarg)); break;
         case 2: opt.threads = std::max(1, std::atoi(optarg)); break;
         case 3: opt.stats = true; break;
+        case 4: opt.host_parse = true; break;
         default: std::exit(EXIT_FAILURE);
         }
     }
@@ -220,29 +230,6 @@ int main(int argc, char** argv)
     const int T = opt.threads > 0 ? opt.threads
                                   : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
 
-    // ---------------------------------------------------------------- parse --
-    double t0 = now();
-    sid_sites* sites = nullptr;
-    uint64_t bad = 0;
-    int prc = sid_parse_text(in.data, in.len, T, &sites, &bad);
-    if (prc == SID_EMALFORMED) terminate_like("std::invalid_argument", "Malformed pileup line");
-    if (prc == SID_ENULLCHROM) {
-        // pileup.cpp:18 assigns a NULL char* to std::string: the reference
-        // dies in strlen() with SIGSEGV, printing nothing
-        std::fflush(stdout);
-        std::signal(SIGSEGV, SIG_DFL);
-        std::raise(SIGSEGV);
-    }
-    CHECK(prc, "parse");
-    if (in.map) munmap(in.map, in.len);
-    in.map = nullptr;
-    const size_t n = sid_sites_count(sites);
-    const uint16_t* h_counts = sid_sites_counts(sites);
-    double t1 = now();
-
-    // -------------------------------------------------------------- compute --
-    uint8_t* h_code = nullptr;
-    double *h_hom = nullptr, *h_het = nullptr;
     int ndev = 0;
     CHECK(sid_device_count(&ndev), "device query");
     if (ndev <= 0) {
@@ -250,63 +237,127 @@ int main(int argc, char** argv)
         std::fputs("sid: no HIP device available\n", stderr);
         std::exit(EXIT_FAILURE);
     }
-    const int D = std::max(1, std::min(opt.devices, ndev));
-    const size_t nn = std::max<size_t>(n, 1);
-    if (hipHostMalloc((void**)&h_code, nn, hipHostMallocDefault) != hipSuccess) h_code = (uint8_t*)std::malloc(nn);
-    if (hipHostMalloc((void**)&h_hom, nn * 8, hipHostMallocDefault) != hipSuccess) h_hom = (double*)std::malloc(nn * 8);
-    if (hipHostMalloc((void**)&h_het, nn * 8, hipHostMallocDefault) != hipSuccess) h_het = (double*)std::malloc(nn * 8);
-
-    std::vector<Shard> sh(D);
-    for (int d = 0; d < D; ++d) {
-        sh[d].begin = n * d / D;
-        sh[d].end = n * (d + 1) / D;
-    }
+    // shard d runs on device d % ndev (more shards than devices: a
+    // multi-device run's splitting and merging on fewer GPUs)
+    const int D = std::max(1, opt.devices);
     const bool lynch = method != SID_METHOD_LOCAL || opt.o.estimate_prior;
-    auto upload = [&](int d) {
+    const char* conf_type = method == SID_METHOD_BAYES ? "probability" : "p_value";
+    std::vector<Shard> sh(D);
+    auto on_parse_error = [&](int prc) {
+        if (prc == SID_EMALFORMED) terminate_like("std::invalid_argument", "Malformed pileup line");
+        if (prc == SID_ENULLCHROM) {
+            // pileup.cpp:18 assigns a NULL char* to std::string: the reference
+            // dies in strlen() with SIGSEGV, printing nothing
+            std::fflush(stdout);
+            std::signal(SIGSEGV, SIG_DFL);
+            std::raise(SIGSEGV);
+        }
+        CHECK(prc, "parse");
+    };
+    auto make_ctx = [&](int d) {
         Shard& s = sh[d];
-        CHECK(sid_create(d, &opt.o, &s.ctx), "context");
+        CHECK(sid_create(d % ndev, &opt.o, &s.ctx), "context");
         HCHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "stream");
+    };
+    auto alloc_out = [&](Shard& s) {
         const size_t m = std::max<size_t>(s.end - s.begin, 1);
-        HCHECK(hipMalloc(&s.d_counts, m * 8), "device counts");
         HCHECK(hipMalloc(&s.d_code, m), "device code");
         HCHECK(hipMalloc(&s.d_hom, m * 8), "device hom_conf");
         HCHECK(hipMalloc(&s.d_het, m * 8), "device het_conf");
-        if (s.end > s.begin)
-            HCHECK(hipMemcpyAsync(s.d_counts, h_counts + 4 * s.begin, (s.end - s.begin) * 8,
-                                  hipMemcpyHostToDevice, s.stream),
-                   "H2D");
-        if (lynch) {
+    };
+    auto parallel = [&](auto fn) {
+        std::vector<std::thread> th;
+        for (int d = 1; d < D; ++d) th.emplace_back(fn, d);
+        fn(0);
+        for (auto& x : th) x.join();
+    };
+
+    // ---------------------------------------------------------------- parse --
+    double t0 = now();
+    sid_sites* sites = nullptr;   // host path only
+    size_t n = 0;
+    if (opt.host_parse) {
+        uint64_t bad = 0;
+        int prc = sid_parse_text(in.data, in.len, T, &sites, &bad);
+        on_parse_error(prc);
+        if (in.map) munmap(in.map, in.len);
+        in.map = nullptr;
+        n = sid_sites_count(sites);
+        const uint16_t* h_counts = sid_sites_counts(sites);
+        for (int d = 0; d < D; ++d) {
+            sh[d].begin = n * d / D;
+            sh[d].end = n * (d + 1) / D;
+        }
+        parallel([&](int d) {
+            make_ctx(d);
+            Shard& s = sh[d];
+            HCHECK(hipMalloc(&s.d_own_counts, std::max<size_t>(s.end - s.begin, 1) * 8), "device counts");
+            s.d_counts = s.d_own_counts;
+            if (s.end > s.begin)
+                HCHECK(hipMemcpyAsync(s.d_own_counts, h_counts + 4 * s.begin, (s.end - s.begin) * 8,
+                                      hipMemcpyHostToDevice, s.stream),
+                       "H2D");
+            alloc_out(s);
+            HCHECK(hipStreamSynchronize(s.stream), "H2D");
+        });
+    } else {
+        // one line-aligned byte range of the text per device, parsed there
+        std::vector<size_t> cut(D + 1, 0);
+        cut[D] = in.len;
+        for (int d = 1; d < D; ++d) {
+            size_t c = std::max(cut[d - 1], in.len / D * d);
+            const char* nl = c < in.len ? (const char*)std::memchr(in.data + c, '\n', in.len - c) : nullptr;
+            cut[d] = nl ? (size_t)(nl - in.data) + 1 : in.len;
+        }
+        std::vector<int> rcs(D, SID_OK);
+        std::vector<uint64_t> eoff(D, 0);
+        parallel([&](int d) {
+            make_ctx(d);
+            Shard& s = sh[d];
+            rcs[d] = sid_dtext_parse(s.ctx, in.data + cut[d], cut[d + 1] - cut[d], 0, &s.text, &eoff[d], s.stream);
+            if (rcs[d] == SID_OK) {
+                s.d_counts = sid_dtext_counts(s.text);
+                s.end = sid_dtext_count(s.text);
+                alloc_out(s);
+            }
+        });
+        // the first malformed line in file order decides
+        int prc = SID_OK;
+        uint64_t first = UINT64_MAX;
+        for (int d = 0; d < D; ++d) {
+            if (rcs[d] == SID_EMALFORMED || rcs[d] == SID_ENULLCHROM) {
+                if (cut[d] + eoff[d] < first) {
+                    first = cut[d] + eoff[d];
+                    prc = rcs[d];
+                }
+            } else if (rcs[d] != SID_OK && prc == SID_OK) {
+                prc = rcs[d];
+            }
+        }
+        on_parse_error(prc);
+        size_t off = 0;
+        for (int d = 0; d < D; ++d) {   // global site index ranges
+            const size_t m = sh[d].end;
+            sh[d].begin = off;
+            sh[d].end = off + m;
+            off += m;
+        }
+        n = off;
+    }
+    double t1 = now();
+
+    // -------------------------------------------------------------- compute --
+    if (lynch) {
+        parallel([&](int d) {
+            Shard& s = sh[d];
+            (void)hipSetDevice(d % ndev);
             CHECK(sid_profile_reset(s.ctx, s.stream), "histogram");
             CHECK(sid_profile_accumulate(s.ctx, s.d_counts, s.end - s.begin, s.stream), "histogram");
-        }
-        HCHECK(hipStreamSynchronize(s.stream), "H2D");
-    };
-    auto finish = [&](int d) {
-        Shard& s = sh[d];
-        (void)hipSetDevice(d);
-        const size_t m = s.end - s.begin;
-        if (method == SID_METHOD_LOCAL)
-            CHECK(sid_call_local(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "local");
-        else
-            CHECK(sid_lookup_sites(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "lookup");
-        if (m) {
-            HCHECK(hipMemcpyAsync(h_code + s.begin, s.d_code, m, hipMemcpyDeviceToHost, s.stream), "D2H");
-            HCHECK(hipMemcpyAsync(h_hom + s.begin, s.d_hom, m * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
-            HCHECK(hipMemcpyAsync(h_het + s.begin, s.d_het, m * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
-        }
-        HCHECK(hipStreamSynchronize(s.stream), "D2H");
-    };
-    {
-        std::vector<std::thread> th;
-        for (int d = 1; d < D; ++d) th.emplace_back(upload, d);
-        upload(0);
-        for (auto& x : th) x.join();
-    }
-    if (lynch) {
+        });
         // merge the per-device histograms (the single exchange of the path)
         std::vector<uint64_t> keys, cnts;
         for (int d = 0; d < D; ++d) {
-            (void)hipSetDevice(d);
+            (void)hipSetDevice(d % ndev);
             size_t u = 0;
             CHECK(sid_profile_table(sh[d].ctx, nullptr, nullptr, 0, &u), "profile table");
             size_t at = keys.size();
@@ -317,10 +368,13 @@ int main(int argc, char** argv)
         std::vector<int> rcs(D, SID_OK);
         std::vector<sid_estimate> est(D);
         auto prep = [&](int d) {
-            (void)hipSetDevice(d);
+            (void)hipSetDevice(d % ndev);
             if (D > 1) {
                 int rc = sid_profile_load(sh[d].ctx, keys.data(), cnts.data(), keys.size());
-                if (rc) { rcs[d] = rc; return; }
+                if (rc) {
+                    rcs[d] = rc;
+                    return;
+                }
             }
             rcs[d] = sid_lynch_prepare(sh[d].ctx, d == 0, &est[d]);
             if (rcs[d] == SID_OK && method == SID_METHOD_LOCAL)
@@ -346,40 +400,79 @@ int main(int argc, char** argv)
         for (auto& x : th) x.join();
         for (int d = 1; d < D; ++d) CHECK(rcs[d], "estimate");
     }
-    {
-        std::vector<std::thread> th;
-        for (int d = 1; d < D; ++d) th.emplace_back(finish, d);
-        finish(0);
-        for (auto& x : th) x.join();
-    }
+    parallel([&](int d) {
+        Shard& s = sh[d];
+        (void)hipSetDevice(d % ndev);
+        const size_t m = s.end - s.begin;
+        if (method == SID_METHOD_LOCAL)
+            CHECK(sid_call_local(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "local");
+        else
+            CHECK(sid_lookup_sites(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "lookup");
+        HCHECK(hipStreamSynchronize(s.stream), "compute");
+    });
     double t2 = now();
 
     // ----------------------------------------------------------------- emit --
     std::fputs("chrom,pos,label,gt,hom_conf,het_conf,conf_type\n", stdout);
     std::fflush(stdout);
-    const char* conf_type = method == SID_METHOD_BAYES ? "probability" : "p_value";
-    const size_t BLOCK = 1u << 18;
-    const size_t nblocks = (n + BLOCK - 1) / BLOCK;
-    std::vector<std::vector<char>> bufs(nblocks);
-    std::vector<size_t> lens(nblocks, 0);
-    std::vector<std::atomic<int>> ready(nblocks);
-    for (auto& r : ready) r.store(0);
-    std::atomic<size_t> next{0};
-    auto worker = [&] {
-        for (;;) {
-            size_t b = next.fetch_add(1);
-            if (b >= nblocks) return;
-            size_t lo = b * BLOCK, hi = std::min(n, lo + BLOCK);
-            size_t need = 0;
-            sid_format_csv(sites, lo, hi, h_code, h_hom, h_het, conf_type, nullptr, 0, &need);
-            bufs[b].resize(need);
-            size_t len = 0;
-            int rc = sid_format_csv(sites, lo, hi, h_code, h_hom, h_het, conf_type, bufs[b].data(), need, &len);
-            lens[b] = rc == SID_OK ? len : 0;
-            ready[b].store(1, std::memory_order_release);
+    if (!opt.host_parse) {
+        // records formatted on each device, written in device (= file) order
+        auto write_all = [](void*, const char* p, size_t len) -> int {
+            size_t off = 0;
+            while (off < len) {
+                ssize_t w = ::write(1, p + off, len - off);
+                if (w <= 0) return -1;
+                off += (size_t)w;
+            }
+            return 0;
+        };
+        for (int d = 0; d < D; ++d) {
+            Shard& s = sh[d];
+            (void)hipSetDevice(d % ndev);
+            int rc = sid_dtext_format(s.ctx, s.text, 0, s.end - s.begin, s.d_code, s.d_hom, s.d_het, conf_type,
+                                      write_all, nullptr, s.stream);
+            if (rc == SID_EIO) std::exit(EXIT_FAILURE);
+            CHECK(rc, "format");
         }
-    };
-    {
+    } else {
+        uint8_t* h_code = nullptr;
+        double *h_hom = nullptr, *h_het = nullptr;
+        const size_t nn = std::max<size_t>(n, 1);
+        if (hipHostMalloc((void**)&h_code, nn, hipHostMallocDefault) != hipSuccess) h_code = (uint8_t*)std::malloc(nn);
+        if (hipHostMalloc((void**)&h_hom, nn * 8, hipHostMallocDefault) != hipSuccess) h_hom = (double*)std::malloc(nn * 8);
+        if (hipHostMalloc((void**)&h_het, nn * 8, hipHostMallocDefault) != hipSuccess) h_het = (double*)std::malloc(nn * 8);
+        parallel([&](int d) {
+            Shard& s = sh[d];
+            (void)hipSetDevice(d % ndev);
+            const size_t m = s.end - s.begin;
+            if (m) {
+                HCHECK(hipMemcpyAsync(h_code + s.begin, s.d_code, m, hipMemcpyDeviceToHost, s.stream), "D2H");
+                HCHECK(hipMemcpyAsync(h_hom + s.begin, s.d_hom, m * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
+                HCHECK(hipMemcpyAsync(h_het + s.begin, s.d_het, m * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
+            }
+            HCHECK(hipStreamSynchronize(s.stream), "D2H");
+        });
+        const size_t BLOCK = 1u << 18;
+        const size_t nblocks = (n + BLOCK - 1) / BLOCK;
+        std::vector<std::vector<char>> bufs(nblocks);
+        std::vector<size_t> lens(nblocks, 0);
+        std::vector<std::atomic<int>> ready(nblocks);
+        for (auto& r : ready) r.store(0);
+        std::atomic<size_t> next{0};
+        auto worker = [&] {
+            for (;;) {
+                size_t b = next.fetch_add(1);
+                if (b >= nblocks) return;
+                size_t lo = b * BLOCK, hi = std::min(n, lo + BLOCK);
+                size_t need = 0;
+                sid_format_csv(sites, lo, hi, h_code, h_hom, h_het, conf_type, nullptr, 0, &need);
+                bufs[b].resize(need);
+                size_t len = 0;
+                int rc = sid_format_csv(sites, lo, hi, h_code, h_hom, h_het, conf_type, bufs[b].data(), need, &len);
+                lens[b] = rc == SID_OK ? len : 0;
+                ready[b].store(1, std::memory_order_release);
+            }
+        };
         std::vector<std::thread> th;
         for (int t = 0; t < T; ++t) th.emplace_back(worker);
         for (size_t b = 0; b < nblocks; ++b) {
@@ -397,19 +490,23 @@ int main(int argc, char** argv)
     double t3 = now();
     if (opt.stats) {
         std::fprintf(stderr,
-                     "{\"sites\": %zu, \"devices\": %d, \"threads\": %d, \"parse_s\": %.6f, "
+                     "{\"sites\": %zu, \"devices\": %d, \"threads\": %d, \"path\": \"%s\", \"parse_s\": %.6f, "
                      "\"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, \"sites_per_s\": %.1f}\n",
-                     n, D, T, t1 - t0, t2 - t1, t3 - t2, t3 - t0, n / std::max(1e-9, t3 - t0));
+                     n, D, T, opt.host_parse ? "host" : "device", t1 - t0, t2 - t1, t3 - t2, t3 - t0,
+                     n / std::max(1e-9, t3 - t0));
     }
-    for (auto& s : sh) {
-        (void)hipSetDevice((int)(&s - sh.data()));
-        (void)hipFree(s.d_counts);
+    for (int d = 0; d < D; ++d) {
+        Shard& s = sh[d];
+        (void)hipSetDevice(d % ndev);
+        if (s.d_own_counts) (void)hipFree(s.d_own_counts);
         (void)hipFree(s.d_code);
         (void)hipFree(s.d_hom);
         (void)hipFree(s.d_het);
+        if (s.text) sid_dtext_free(s.text);
         if (s.stream) (void)hipStreamDestroy(s.stream);
         sid_destroy(s.ctx);
     }
-    sid_sites_free(sites);
+    if (in.map) munmap(in.map, in.len);
+    if (sites) sid_sites_free(sites);
     return 0;
 }

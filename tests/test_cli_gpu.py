@@ -71,3 +71,37 @@ def test_cli_error_paths(sid, oracle, tmp_path):
         assert a.stdout == b.stdout, args
         # getopt prefixes its messages with argv[0]
         assert a.stderr.replace(sid.CLI_PATH.encode(), b"P") == b.stderr.replace(oracle.CLI.encode(), b"P"), args
+
+
+@pytest.mark.parametrize("extra", [["--devices", "3"], ["--host-parse"], ["--host-parse", "--devices", "2"]],
+                         ids=lambda e: " ".join(e))
+@pytest.mark.parametrize("flags", [[], ["-R", "-m", "likelihood_ratio"], ["-m", "bayes"], ["-R", "-m", "local"]],
+                         ids=lambda f: " ".join(f) or "default")
+@pytest.mark.parametrize("name", ["c1", "deep"])
+def test_cli_shards_and_host_path_match_oracle(sid, oracle, inputs, name, flags, extra):
+    """More shards than GPUs (shard d on device d % n: the multi-device split,
+    histogram merge and ordered output) and the host parse/emit path."""
+    a = run(sid.CLI_PATH, extra + flags + [inputs[name]])
+    b = oracle.run_cli(flags + [inputs[name]])
+    assert a.returncode == b.returncode == 0, a.stderr
+    assert a.stdout == b.stdout
+    assert a.stderr == b.stderr
+
+
+def test_cli_first_error_across_shards(sid, oracle, tmp_path):
+    good = b"".join(b"chr1\t%d\tA\t3\t.,.\tIII\n" % i for i in range(1, 4000))
+    cases = {
+        # malformed line in a late shard, blank (SIGSEGV) line even later
+        "late": good + b"chr1\t1\tAC\t3\t...\tIII\n" + good + b" \t\n" + good,
+        # blank line first, malformed later: the reference dies with SIGSEGV
+        "blank_first": good + b" \t\n" + good + b"chr1\t1\tAC\t3\t...\tIII\n",
+    }
+    for tag, text in cases.items():
+        p = tmp_path / f"{tag}.plp"
+        p.write_bytes(text)
+        b = oracle.run_cli([str(p)])
+        for extra in ([], ["--devices", "4"], ["--host-parse", "--devices", "3"]):
+            a = run(sid.CLI_PATH, extra + [str(p)])
+            assert a.returncode == b.returncode, (tag, extra, a.returncode, b.returncode)
+            assert a.stdout == b.stdout == b"", (tag, extra)
+            assert a.stderr == b.stderr, (tag, extra)
