@@ -189,12 +189,12 @@ int sid_format_double(double v, char* buf, size_t cap);
 
 /* ------------------------------------ device text path
  * The same parse and the same CSV, on the device: the text of one shard is
- * copied to HBM in line-aligned chunks of `chunk` bytes (0 = 256 MiB), the
- * copy of each chunk overlapping the parse of the previous one, and stays
- * resident (the formatter re-reads chrom and pos from it).
+ * copied to HBM, indexed (line starts) and parsed there, and stays resident
+ * (the formatter re-reads chrom and pos from it).
  *
  * sid_dtext_parse: host text -> device counts (sid_dtext_counts, 4 x u16 per
- *   non-empty line, as sid_parse_text).  Synchronises.  On a malformed line
+ *   non-empty line, as sid_parse_text).  Synchronises.  `chunk` (0 = 256 MiB)
+ *   is the size of the individual host-to-device copies.  On a malformed line
  *   returns SID_EMALFORMED or SID_ENULLCHROM for the first one in file order
  *   and its byte offset in *err_offset; *out stays NULL.
  * sid_dtext_format: the records of sites [begin, end) with the given device
@@ -205,6 +205,11 @@ typedef struct sid_dtext sid_dtext;
 typedef int (*sid_write_fn)(void* user, const char* bytes, size_t len);
 int sid_dtext_parse(sid_ctx* ctx, const char* text, size_t len, size_t chunk, sid_dtext** out,
                     uint64_t* err_offset, void* stream);
+/* The same for bytes [offset, offset+len) of an open file (offset at a line
+ * start): `threads` host threads (0 = 8) pread() into pinned staging owned by
+ * the context, each buffer DMA'd to HBM as it fills -- no file mapping. */
+int sid_dtext_parse_fd(sid_ctx* ctx, int fd, uint64_t offset, uint64_t len, int threads, sid_dtext** out,
+                       uint64_t* err_offset, void* stream);
 size_t sid_dtext_count(const sid_dtext* t);
 const uint16_t* sid_dtext_counts(const sid_dtext* t);   /* device */
 int sid_dtext_format(sid_ctx* ctx, const sid_dtext* t, size_t begin, size_t end, const uint8_t* code,

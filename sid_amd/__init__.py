@@ -94,6 +94,7 @@ SIGNATURES = [
     ("sid_format_csv", _I, [_P, _SZ, _SZ, _P, _P, _P, C.c_char_p, _P, _SZ, C.POINTER(C.c_size_t)]),
     ("sid_format_double", _I, [_D, C.c_char_p, _SZ]),
     ("sid_dtext_parse", _I, [_P, _P, _SZ, _SZ, C.POINTER(_P), C.POINTER(C.c_uint64), _P]),
+    ("sid_dtext_parse_fd", _I, [_P, _I, _U64, _U64, _I, C.POINTER(_P), C.POINTER(C.c_uint64), _P]),
     ("sid_dtext_count", _SZ, [_P]),
     ("sid_dtext_counts", _P, [_P]),
     ("sid_dtext_format", _I, [_P, _P, _SZ, _SZ, _P, _P, _P, C.c_char_p, WRITE_FN, _P, _P]),
@@ -226,14 +227,17 @@ def format_g6(v: float) -> str:
 class DText:
     """One shard of pileup text parsed on the device (sid_dtext_*)."""
 
-    def __init__(self, ctx: "Context", text: bytes, chunk: int = 0, stream=None):
+    def __init__(self, ctx: "Context", text: bytes = None, chunk: int = 0, stream=None, fd: int = None,
+                 offset: int = 0, length: int = None, threads: int = 0):
         self.ctx = ctx
-        self._text = text   # the host text must outlive the (synchronous) parse only
         h = C.c_void_p()
         off = C.c_uint64(0)
-        buf = C.c_char_p(text)
-        rc = lib().sid_dtext_parse(ctx.h, C.cast(buf, C.c_void_p), len(text), chunk, C.byref(h), C.byref(off),
-                                   stream)
+        if fd is not None:   # bytes [offset, offset+length) of an open file
+            rc = lib().sid_dtext_parse_fd(ctx.h, fd, offset, length, threads, C.byref(h), C.byref(off), stream)
+        else:
+            buf = C.c_char_p(text)
+            rc = lib().sid_dtext_parse(ctx.h, C.cast(buf, C.c_void_p), len(text), chunk, C.byref(h), C.byref(off),
+                                       stream)
         if rc != 0:
             err = SidError(rc, "sid_dtext_parse")
             err.offset = off.value   # byte offset of the first malformed line

@@ -164,6 +164,12 @@ extern "C" int sid_destroy(sid_ctx* c)
     if (c->ws.miss) (void)hipFree(c->ws.miss);
     if (c->ws.ctr) (void)hipFree(c->ws.ctr);
     if (c->lynch) sid_lynch_dev_destroy(c->lynch);
+    for (int b = 0; b < 2; ++b) {
+        if (c->fmt_d[b]) (void)hipFree(c->fmt_d[b]);
+        if (c->fmt_h[b]) (void)hipHostFree(c->fmt_h[b]);
+    }
+    for (char* p : c->in_h)
+        if (p) (void)hipHostFree(p);
     for (auto& v : {c->ev_pool, c->ev_pending})
         for (auto& ev : v) {
             (void)hipEventDestroy(ev.start);

@@ -105,11 +105,34 @@ double now()
 }
 
 struct Input {
-    const char* data = nullptr;
+    const char* data = nullptr;   // the text in memory (pipes, or mapped for --host-parse)
     size_t len = 0;
     void* map = nullptr;
     std::string owned;
+    int fd = -1;                  // regular file: read by the device path with pread()
 };
+
+void map_input(Input& in, bool populate)
+{
+    if (in.data || in.fd < 0 || !in.len) return;
+    in.map = mmap(nullptr, in.len, PROT_READ, MAP_PRIVATE | (populate ? MAP_POPULATE : 0), in.fd, 0);
+    if (in.map == MAP_FAILED) {
+        in.map = nullptr;
+        in.owned.resize(in.len);
+        size_t off = 0;
+        while (off < in.len) {
+            ssize_t r = ::pread(in.fd, &in.owned[off], in.len - off, (off_t)off);
+            if (r <= 0) break;
+            off += (size_t)r;
+        }
+        in.owned.resize(off);
+        in.data = in.owned.data();
+        in.len = off;
+    } else {
+        madvise(in.map, in.len, MADV_SEQUENTIAL);
+        in.data = (const char*)in.map;
+    }
+}
 
 // std::ifstream semantics: open failure -> "Could not open file" (sid.cpp:86-89)
 bool open_input(const char* path, Input& in)
@@ -119,28 +142,10 @@ bool open_input(const char* path, Input& in)
     struct stat st;
     if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
         in.len = (size_t)st.st_size;
-        if (in.len) {
-            in.map = mmap(nullptr, in.len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
-            if (in.map == MAP_FAILED) {
-                in.map = nullptr;
-            } else {
-                madvise(in.map, in.len, MADV_SEQUENTIAL);
-                in.data = (const char*)in.map;
-            }
-        }
-        if (in.len && !in.map) {   // fall back to read()
-            in.owned.resize(in.len);
-            size_t off = 0;
-            while (off < in.len) {
-                ssize_t r = ::read(fd, &in.owned[off], in.len - off);
-                if (r <= 0) break;
-                off += (size_t)r;
-            }
-            in.owned.resize(off);
-            in.data = in.owned.data();
-            in.len = off;
-        }
-    } else if (fstat(fd, &st) == 0 && S_ISDIR(st.st_mode)) {
+        in.fd = fd;   // kept open
+        return true;
+    }
+    if (fstat(fd, &st) == 0 && S_ISDIR(st.st_mode)) {
         // std::ifstream opens a directory, getline then fails: no records
         in.len = 0;
     } else {   // pipe / character device
@@ -152,6 +157,24 @@ bool open_input(const char* path, Input& in)
     }
     ::close(fd);
     return true;
+}
+
+// first line start at or after c: one past the next '\n' (pread in windows)
+size_t next_line_start(const Input& in, size_t c)
+{
+    if (c == 0 || c >= in.len) return std::min(c, in.len);
+    if (in.data) {
+        const char* nl = (const char*)std::memchr(in.data + c - 1, '\n', in.len - c + 1);
+        return nl ? (size_t)(nl - in.data) + 1 : in.len;
+    }
+    std::vector<char> w(1 << 20);
+    for (size_t at = c - 1; at < in.len; at += w.size()) {
+        const ssize_t r = ::pread(in.fd, w.data(), std::min(w.size(), in.len - at), (off_t)at);
+        if (r <= 0) break;
+        const char* nl = (const char*)std::memchr(w.data(), '\n', (size_t)r);
+        if (nl) return at + (size_t)(nl - w.data()) + 1;
+    }
+    return in.len;
 }
 
 struct Shard {
@@ -278,6 +301,7 @@ int main(int argc, char** argv)
     size_t n = 0;
     if (opt.host_parse) {
         uint64_t bad = 0;
+        map_input(in, true);
         int prc = sid_parse_text(in.data, in.len, T, &sites, &bad);
         on_parse_error(prc);
         if (in.map) munmap(in.map, in.len);
@@ -302,19 +326,24 @@ int main(int argc, char** argv)
         });
     } else {
         // one line-aligned byte range of the text per device, parsed there
+        // a populated mapping, copied by one stream per device, measured
+        // fastest end to end (SID_READ_FD=1: pread into pinned staging instead)
+        const bool use_fd = std::getenv("SID_READ_FD") != nullptr;
+        if (!use_fd) map_input(in, true);
         std::vector<size_t> cut(D + 1, 0);
         cut[D] = in.len;
-        for (int d = 1; d < D; ++d) {
-            size_t c = std::max(cut[d - 1], in.len / D * d);
-            const char* nl = c < in.len ? (const char*)std::memchr(in.data + c, '\n', in.len - c) : nullptr;
-            cut[d] = nl ? (size_t)(nl - in.data) + 1 : in.len;
-        }
+        for (int d = 1; d < D; ++d) cut[d] = next_line_start(in, std::max(cut[d - 1], in.len / D * d));
         std::vector<int> rcs(D, SID_OK);
         std::vector<uint64_t> eoff(D, 0);
         parallel([&](int d) {
             make_ctx(d);
             Shard& s = sh[d];
-            rcs[d] = sid_dtext_parse(s.ctx, in.data + cut[d], cut[d + 1] - cut[d], 0, &s.text, &eoff[d], s.stream);
+            if (in.fd >= 0 && !in.data)
+                rcs[d] = sid_dtext_parse_fd(s.ctx, in.fd, cut[d], cut[d + 1] - cut[d], std::max(1, std::min(8, T / D)),
+                                            &s.text, &eoff[d], s.stream);
+            else
+                rcs[d] = sid_dtext_parse(s.ctx, in.data + cut[d], cut[d + 1] - cut[d], 0, &s.text, &eoff[d],
+                                         s.stream);
             if (rcs[d] == SID_OK) {
                 s.d_counts = sid_dtext_counts(s.text);
                 s.end = sid_dtext_count(s.text);
@@ -495,18 +524,7 @@ int main(int argc, char** argv)
                      n, D, T, opt.host_parse ? "host" : "device", t1 - t0, t2 - t1, t3 - t2, t3 - t0,
                      n / std::max(1e-9, t3 - t0));
     }
-    for (int d = 0; d < D; ++d) {
-        Shard& s = sh[d];
-        (void)hipSetDevice(d % ndev);
-        if (s.d_own_counts) (void)hipFree(s.d_own_counts);
-        (void)hipFree(s.d_code);
-        (void)hipFree(s.d_hom);
-        (void)hipFree(s.d_het);
-        if (s.text) sid_dtext_free(s.text);
-        if (s.stream) (void)hipStreamDestroy(s.stream);
-        sid_destroy(s.ctx);
-    }
-    if (in.map) munmap(in.map, in.len);
-    if (sites) sid_sites_free(sites);
+    // device memory, pinned staging and mappings go with the process: freeing
+    // gigabytes of HBM and pinned host memory one by one only delays the exit
     return 0;
 }

@@ -43,6 +43,9 @@ struct sid_lynch_dev;
 sid_lynch_dev* sid_lynch_dev_create(int* err);
 void sid_lynch_dev_destroy(sid_lynch_dev* L);
 
+#define SID_STAGE_N 8                   // reader threads / pinned input buffers
+#define SID_STAGE_BYTES (16u << 20)     // bytes per input buffer
+
 struct sid_ctx {
     int device = 0;
     sid_opts opts{};
@@ -59,6 +62,13 @@ struct sid_ctx {
     std::vector<sid_timing_ev> ev_pool, ev_pending;
     // Lynch path
     sid_lynch_dev* lynch = nullptr;
+    // device CSV formatter (textpath.hip): staging kept for the context's
+    // lifetime (pinning host memory costs ~5 GB/s, too slow per call)
+    char* fmt_d[2] = {nullptr, nullptr};
+    char* fmt_h[2] = {nullptr, nullptr};
+    size_t fmt_cap[2] = {0, 0};
+    // sid_dtext_parse_fd: pinned read staging, one buffer per reader thread
+    char* in_h[SID_STAGE_N] = {};
 };
 
 // host helpers (capi.cpp)

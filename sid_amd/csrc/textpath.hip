@@ -26,9 +26,14 @@
 // Semantics are those of parse.cpp (the host parser, tested against the
 // reference's own pileup.cpp) and emit.cpp; the %g digits come from fmt.h.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/sid.h"
@@ -322,10 +327,17 @@ __device__ __forceinline__ int record(Reader& R, uint64_t start, uint8_t c, doub
                                       const char* ctype, int tlen, char* out)
 {
     if (c & 0x40) return 0;   // filtered profile: no record (call.cpp:131-140)
-    const Line L = find_line(R, start);
+    // the line parsed (>= 5 tokens before any NUL or newline), so its first
+    // two tokens are plain separator-delimited runs
     uint64_t tb[2], te[2];
-    const int nt = tokenize(R, L.s, L.end, 2, tb, te);
-    const int32_t pos = nt >= 2 ? atoi_like(R, tb[1], te[1]) : 0;
+    uint64_t q = start;
+    for (int k = 0; k < 2; ++k) {
+        while (is_sep(R.at(q))) ++q;
+        tb[k] = q;
+        while (!is_sep(R.at(q))) ++q;
+        te[k] = q;
+    }
+    const int32_t pos = atoi_like(R, tb[1], te[1]);
     char buf[64];
     int n = 0;
     const int clen = (int)(te[0] - tb[0]);
@@ -450,6 +462,17 @@ __global__ __launch_bounds__(TB) void sid_fmt_g6_kernel(const double* __restrict
 }  // namespace
 
 // ============================================================== C ABI ======
+// SID_TEXT_TIMING=1: phase times on stderr (measurement only)
+static bool text_timing()
+{
+    static const bool on = std::getenv("SID_TEXT_TIMING") != nullptr;
+    return on;
+}
+static double wall()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct sid_dtext {
     int device = 0;
     char* d_text = nullptr;
@@ -484,122 +507,174 @@ extern "C" int sid_dtext_free(sid_dtext* t)
 extern "C" size_t sid_dtext_count(const sid_dtext* t) { return t ? t->nsites : 0; }
 extern "C" const uint16_t* sid_dtext_counts(const sid_dtext* t) { return t ? (const uint16_t*)t->d_counts : nullptr; }
 
+static sid_dtext* dtext_alloc(int dev, uint64_t len, int* rc)
+{
+    sid_dtext* T = new sid_dtext();
+    T->device = dev;
+    T->len = len;
+    hipError_t e;
+    // padded: 16-B window reads past the end stay inside the allocation
+    if ((e = hipMalloc(&T->d_text, ((len + 15) & ~(size_t)15) + 128)) != hipSuccess ||
+        (e = hipMalloc(&T->d_state, 4 * sizeof(uint64_t))) != hipSuccess ||
+        (e = hipMalloc(&T->d_err, sizeof(unsigned long long))) != hipSuccess) {
+        *rc = sid_set_hip_error(e);
+        sid_dtext_free(T);
+        return nullptr;
+    }
+    *rc = SID_OK;
+    return T;
+}
+
+// Line index + parse over the resident text [0, len) (a line start at 0):
+// count per tile -> scan -> (sync: the site count) -> line offsets -> parse.
+static int dtext_index_parse(sid_dtext* T, hipStream_t st, uint64_t* err_offset)
+{
+    const uint64_t len = T->len;
+    hipError_t e;
+    const size_t tiles = std::max<size_t>((len + TILE - 1) / TILE, 1);
+    if ((e = hipMalloc(&T->d_tcnt, tiles * 4)) != hipSuccess || (e = hipMalloc(&T->d_toff, tiles * 8)) != hipSuccess)
+        return sid_set_hip_error(e);
+    T->tcap = tiles;
+    if ((e = hipMemsetAsync(T->d_state, 0, 4 * sizeof(uint64_t), st)) != hipSuccess ||
+        (e = hipMemsetAsync(T->d_err, 0xFF, sizeof(unsigned long long), st)) != hipSuccess)
+        return sid_set_hip_error(e);
+    sid_lines_count_kernel<<<(unsigned)tiles, TB, 0, st>>>(T->d_text, 0, 0, len, T->d_tcnt);
+    sid_scan_kernel<<<1, SCAN_TB, 0, st>>>(T->d_tcnt, tiles, T->d_toff, T->d_state, T->d_state + 1);
+    if ((e = hipGetLastError()) != hipSuccess) return sid_set_hip_error(e);
+    uint64_t total = 0;
+    if ((e = hipMemcpyAsync(&total, T->d_state, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return sid_set_hip_error(e);
+    T->nsites = total;
+    const size_t m = std::max<uint64_t>(total, 1);
+    if ((e = hipMalloc(&T->d_starts, m * 8)) != hipSuccess || (e = hipMalloc(&T->d_counts, m * 8)) != hipSuccess)
+        return sid_set_hip_error(e);
+    sid_lines_emit_kernel<<<(unsigned)tiles, TB, 0, st>>>(T->d_text, 0, 0, len, T->d_toff, T->d_starts);
+    const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((total + TB - 1) / TB, 1), 16384);
+    sid_parse_kernel<<<pg, TB, 0, st>>>(T->d_text, len, T->d_starts, T->d_state + 1, T->d_counts, T->d_err);
+    if ((e = hipGetLastError()) != hipSuccess) return sid_set_hip_error(e);
+    unsigned long long ek = ~0ull;
+    if ((e = hipMemcpyAsync(&ek, T->d_err, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return sid_set_hip_error(e);
+    if (ek != ~0ull) {
+        if (err_offset) *err_offset = ek >> 2;
+        return (ek & 3) == 1 ? SID_EMALFORMED : SID_ENULLCHROM;
+    }
+    return SID_OK;
+}
+
 extern "C" int sid_dtext_parse(sid_ctx* ctx, const char* text, size_t len, size_t chunk, sid_dtext** out,
                                uint64_t* err_offset, void* stream)
 {
     if (!ctx || !out || (!text && len)) return SID_EINVAL;
     *out = nullptr;
-    const int dev = ctx->device;
-    TCHECK(hipSetDevice(dev));
+    const double w0 = wall();
+    TCHECK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    int rc;
+    sid_dtext* T = dtext_alloc(ctx->device, len, &rc);
+    if (!T) return rc;
+    // the padding first, then the text in `chunk`-sized copies.  (Measured on
+    // a page-cache file mapping: one stream from a populated mapping beats
+    // parallel copies that fault the pages in, and pread() into pinned staging.)
+    hipError_t e = hipMemsetAsync(T->d_text + (len & ~(uint64_t)15), 0,
+                                  ((len + 15) & ~(uint64_t)15) - (len & ~(uint64_t)15) + 128, st);
     if (chunk == 0) chunk = 256u << 20;
-    chunk = std::max<size_t>(chunk, TILE);
-    sid_dtext* T = new sid_dtext();
-    T->device = dev;
-    T->len = len;
-    auto fail = [&](int rc) {
+    for (uint64_t off = 0; off < len && e == hipSuccess; off += chunk)
+        e = hipMemcpyAsync(T->d_text + off, text + off, std::min<uint64_t>(chunk, len - off), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        sid_dtext_free(T);
+        return sid_set_hip_error(e);
+    }
+    const double w1 = wall();
+    rc = dtext_index_parse(T, st, err_offset);
+    if (text_timing())
+        std::fprintf(stderr, "{\"dtext_parse\": {\"bytes\": %llu, \"upload_s\": %.6f, \"index_parse_s\": %.6f}}\n",
+                     (unsigned long long)len, w1 - w0, wall() - w1);
+    if (rc != SID_OK) {
         sid_dtext_free(T);
         return rc;
-    };
-    // line-aligned chunk boundaries
-    std::vector<uint64_t> cut{0};
-    while (cut.back() < len) {
-        uint64_t c = cut.back() + chunk;
-        if (c >= len) {
-            c = len;
-        } else {
-            const char* nl = (const char*)std::memchr(text + c, '\n', len - c);
-            c = nl ? (uint64_t)(nl - text) + 1 : len;
+    }
+    *out = T;
+    return SID_OK;
+}
+
+// Text straight from a file descriptor: pread() by `threads` host threads into
+// a ring of pinned buffers (context-owned), each DMA'd to HBM as it fills.
+// No mapping of the file: no page-table population for gigabytes of page cache.
+extern "C" int sid_dtext_parse_fd(sid_ctx* ctx, int fd, uint64_t offset, uint64_t len, int threads, sid_dtext** out,
+                                  uint64_t* err_offset, void* stream)
+{
+    if (!ctx || !out || fd < 0) return SID_EINVAL;
+    *out = nullptr;
+    const double w0 = wall();
+    TCHECK(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    int rc;
+    sid_dtext* T = dtext_alloc(ctx->device, len, &rc);
+    if (!T) return rc;
+    const int R = std::max(1, std::min(threads > 0 ? threads : 8, SID_STAGE_N));
+    const size_t B = SID_STAGE_BYTES;
+    hipError_t e = hipSuccess;
+    for (int b = 0; b < R && e == hipSuccess; ++b)
+        if (!ctx->in_h[b]) e = hipHostMalloc((void**)&ctx->in_h[b], B, hipHostMallocDefault);
+    if (e == hipSuccess)
+        e = hipMemsetAsync(T->d_text + (len & ~(uint64_t)15), 0,
+                           ((len + 15) & ~(uint64_t)15) - (len & ~(uint64_t)15) + 128, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        sid_dtext_free(T);
+        return sid_set_hip_error(e);
+    }
+    // reader r owns buffer r and chunks r, r+R, r+2R, ...: pread, DMA on its
+    // own stream, wait for the DMA before refilling the buffer
+    std::vector<int> rcs(R, SID_OK);
+    std::vector<std::thread> th;
+    const uint64_t nch = (len + B - 1) / B;
+    for (int r = 0; r < R; ++r)
+        th.emplace_back([&, r] {
+            (void)hipSetDevice(T->device);
+            hipStream_t rs;
+            if (hipStreamCreateWithFlags(&rs, hipStreamNonBlocking) != hipSuccess) {
+                rcs[r] = SID_EHIP;
+                return;
+            }
+            char* buf = ctx->in_h[r];
+            for (uint64_t c = r; c < nch && rcs[r] == SID_OK; c += R) {
+                const uint64_t off = c * B, n = std::min<uint64_t>(B, len - off);
+                uint64_t got = 0;
+                while (got < n) {
+                    const ssize_t k = ::pread(fd, buf + got, n - got, (off_t)(offset + off + got));
+                    if (k <= 0) break;
+                    got += (uint64_t)k;
+                }
+                if (got != n) {
+                    rcs[r] = SID_EIO;
+                    break;
+                }
+                hipError_t x = hipMemcpyAsync(T->d_text + off, buf, n, hipMemcpyHostToDevice, rs);
+                if (x == hipSuccess) x = hipStreamSynchronize(rs);
+                if (x != hipSuccess) rcs[r] = sid_set_hip_error(x);
+            }
+            (void)hipStreamDestroy(rs);
+        });
+    for (auto& x : th) x.join();
+    for (int r : rcs)
+        if (r != SID_OK) {
+            sid_dtext_free(T);
+            return r;
         }
-        cut.push_back(c);
-    }
-    const size_t nch = cut.size() - 1;
-    size_t maxtiles = 0;
-    for (size_t k = 0; k < nch; ++k) {
-        const uint64_t tb = cut[k] & ~(uint64_t)15;
-        maxtiles = std::max<size_t>(maxtiles, (size_t)((cut[k + 1] - tb + TILE - 1) / TILE));
-    }
-    // worst case one site per 2 bytes ("x\n"); sized exactly after counting
-    hipError_t e;
-    if ((e = hipMalloc(&T->d_text, ((len + 15) & ~(size_t)15) + 128)) != hipSuccess) return fail(sid_set_hip_error(e));
-    if ((e = hipMalloc(&T->d_state, 4 * sizeof(uint64_t))) != hipSuccess) return fail(sid_set_hip_error(e));
-    if ((e = hipMalloc(&T->d_err, sizeof(unsigned long long))) != hipSuccess) return fail(sid_set_hip_error(e));
-    if ((e = hipMalloc(&T->d_tcnt, std::max<size_t>(maxtiles, 1) * 4)) != hipSuccess) return fail(sid_set_hip_error(e));
-    if ((e = hipMalloc(&T->d_toff, std::max<size_t>(maxtiles, 1) * 8)) != hipSuccess) return fail(sid_set_hip_error(e));
-    T->tcap = maxtiles;
-    if ((e = hipMemsetAsync(T->d_state, 0, 4 * sizeof(uint64_t), st)) != hipSuccess) return fail(sid_set_hip_error(e));
-    if ((e = hipMemsetAsync(T->d_err, 0xFF, sizeof(unsigned long long), st)) != hipSuccess)
-        return fail(sid_set_hip_error(e));
-    if ((e = hipMemsetAsync(T->d_text + (len & ~(size_t)15), 0, 80, st)) != hipSuccess)
-        return fail(sid_set_hip_error(e));
-    // pass 1: copy + count lines per chunk (the copies overlap the counting of
-    // the previous chunk: DMA and kernels on one stream still pipeline, the
-    // count kernels are short)
-    hipStream_t cs;
-    if ((e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) return fail(sid_set_hip_error(e));
-    std::vector<hipEvent_t> copied(nch);
-    for (auto& ev : copied) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    hipEvent_t ready;
-    (void)hipEventCreateWithFlags(&ready, hipEventDisableTiming);
-    (void)hipEventRecord(ready, st);
-    (void)hipStreamWaitEvent(cs, ready, 0);   // the memsets above come first
-    int rc = SID_OK;
-    for (size_t k = 0; k < nch && rc == SID_OK; ++k) {
-        if ((e = hipMemcpyAsync(T->d_text + cut[k], text + cut[k], cut[k + 1] - cut[k], hipMemcpyHostToDevice, cs)) !=
-            hipSuccess)
-            rc = sid_set_hip_error(e);
-        (void)hipEventRecord(copied[k], cs);
-    }
-    // site counts per chunk -> total (one host sync), then starts + parse
-    std::vector<uint64_t> sites_before(nch + 1, 0);
-    for (size_t k = 0; k < nch && rc == SID_OK; ++k) {
-        (void)hipStreamWaitEvent(st, copied[k], 0);
-        const uint64_t tb = cut[k] & ~(uint64_t)15;
-        const unsigned tiles = (unsigned)((cut[k + 1] - tb + TILE - 1) / TILE);
-        sid_lines_count_kernel<<<tiles, TB, 0, st>>>(T->d_text, tb, cut[k], cut[k + 1], T->d_tcnt);
-        sid_scan_kernel<<<1, SCAN_TB, 0, st>>>(T->d_tcnt, tiles, T->d_toff, T->d_state, nullptr);
-        if ((e = hipGetLastError()) != hipSuccess) rc = sid_set_hip_error(e);
-    }
-    uint64_t total = 0;
-    if (rc == SID_OK) {
-        if ((e = hipMemcpyAsync(&total, T->d_state, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-            (e = hipStreamSynchronize(st)) != hipSuccess)
-            rc = sid_set_hip_error(e);
-    }
-    if (rc == SID_OK) {
-        T->nsites = total;
-        const size_t m = std::max<uint64_t>(total, 1);
-        if ((e = hipMalloc(&T->d_starts, m * 8)) != hipSuccess || (e = hipMalloc(&T->d_counts, m * 8)) != hipSuccess)
-            rc = sid_set_hip_error(e);
-    }
-    if (rc == SID_OK) (void)hipMemsetAsync(T->d_state, 0, 8, st);
-    for (size_t k = 0; k < nch && rc == SID_OK; ++k) {
-        const uint64_t tb = cut[k] & ~(uint64_t)15;
-        const unsigned tiles = (unsigned)((cut[k + 1] - tb + TILE - 1) / TILE);
-        // recount (cheap) so the offsets of this chunk are in d_toff, then emit
-        sid_lines_count_kernel<<<tiles, TB, 0, st>>>(T->d_text, tb, cut[k], cut[k + 1], T->d_tcnt);
-        // d_state[1..2] = the chunk's site range (the scan advances d_state[0])
-        sid_scan_kernel<<<1, SCAN_TB, 0, st>>>(T->d_tcnt, tiles, T->d_toff, T->d_state, T->d_state + 1);
-        sid_lines_emit_kernel<<<tiles, TB, 0, st>>>(T->d_text, tb, cut[k], cut[k + 1], T->d_toff, T->d_starts);
-        const uint64_t approx = (cut[k + 1] - cut[k]) / 32 + 1;
-        const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((approx + TB - 1) / TB, 1), 8192);
-        sid_parse_kernel<<<pg, TB, 0, st>>>(T->d_text, len, T->d_starts, T->d_state + 1, T->d_counts, T->d_err);
-        if ((e = hipGetLastError()) != hipSuccess) rc = sid_set_hip_error(e);
-    }
-    unsigned long long ek = ~0ull;
-    if (rc == SID_OK) {
-        if ((e = hipMemcpyAsync(&ek, T->d_err, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-            (e = hipStreamSynchronize(st)) != hipSuccess)
-            rc = sid_set_hip_error(e);
-    }
-    (void)hipStreamSynchronize(cs);
-    for (auto& ev : copied) (void)hipEventDestroy(ev);
-    (void)hipEventDestroy(ready);
-    (void)hipStreamDestroy(cs);
-    if (rc != SID_OK) return fail(rc);
-    if (ek != ~0ull) {
-        if (err_offset) *err_offset = ek >> 2;
-        return fail((ek & 3) == 1 ? SID_EMALFORMED : SID_ENULLCHROM);
+    const double w1 = wall();
+    rc = dtext_index_parse(T, st, err_offset);
+    if (text_timing())
+        std::fprintf(stderr,
+                     "{\"dtext_parse_fd\": {\"bytes\": %llu, \"readers\": %d, \"upload_s\": %.6f, \"index_parse_s\": %.6f}}\n",
+                     (unsigned long long)len, R, w1 - w0, wall() - w1);
+    if (rc != SID_OK) {
+        sid_dtext_free(T);
+        return rc;
     }
     *out = T;
     return SID_OK;
@@ -619,15 +694,16 @@ extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, 
     std::memcpy(ct.s, conf_type, ct.len);
     TCHECK(hipSetDevice(T->device));
     hipStream_t st = (hipStream_t)stream;
-    const size_t PIECE = 4u << 20;   // sites per piece
-    const size_t nb_max = (PIECE + TB - 1) / TB;
+    const size_t n = end - begin;
+    const size_t PB = 4096;                          // blocks (of TB sites) per piece: 1 Mi sites
+    const size_t nb = (n + TB - 1) / TB;
     uint32_t* d_bsum = nullptr;
     uint64_t* d_boff = nullptr;
     uint64_t* d_base = nullptr;
     int* d_bad = nullptr;
-    char* d_out[2] = {nullptr, nullptr};
-    char* h_out[2] = {nullptr, nullptr};
-    size_t cap[2] = {0, 0};
+    char** d_out = ctx->fmt_d;   // staging owned by the context
+    char** h_out = ctx->fmt_h;
+    size_t* cap = ctx->fmt_cap;
     hipEvent_t done[2], written;
     (void)hipEventCreateWithFlags(&done[0], hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&done[1], hipEventDisableTiming);
@@ -635,49 +711,82 @@ extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, 
     hipStream_t cs = nullptr;   // D2H of piece k overlaps the formatting of piece k+1
     (void)hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
     int rc = SID_OK;
-    hipError_t e;
     auto hip = [&](hipError_t x) {
         if (x != hipSuccess && rc == SID_OK) rc = sid_set_hip_error(x);
         return rc == SID_OK;
     };
-    hip(hipMalloc(&d_bsum, nb_max * 4));
-    hip(hipMalloc(&d_boff, nb_max * 8));
+    double t_wait = 0, t_write = 0, t_size = 0, t_alloc = 0;
+    const double f0 = wall();
+    // staging for a piece of ~64 B records, pinned on another thread while the
+    // lengths are computed (pinning runs at a few GB/s)
+    auto stage = [d_out, h_out, cap](size_t need) {
+        hipError_t err = hipSuccess;
+        for (int b = 0; b < 2 && err == hipSuccess; ++b) {
+            if (need <= cap[b]) continue;
+            if (d_out[b]) (void)hipFree(d_out[b]);
+            if (h_out[b]) (void)hipHostFree(h_out[b]);
+            d_out[b] = nullptr;
+            h_out[b] = nullptr;
+            cap[b] = 0;
+            const size_t want = need + need / 8 + 4096;
+            if ((err = hipMalloc(&d_out[b], want)) != hipSuccess) break;
+            if ((err = hipHostMalloc((void**)&h_out[b], want, hipHostMallocDefault)) != hipSuccess) break;
+            cap[b] = want;
+        }
+        return err;
+    };
+    hipError_t stage_err = hipSuccess;
+    std::thread stager([&, dev = T->device] {
+        (void)hipSetDevice(dev);
+        stage_err = stage(std::min<size_t>(n, PB * TB) * 64 + 64);
+    });
+    // record lengths of every site and their block offsets: one pass, one sync
+    std::vector<uint64_t> boff(nb + 1, 0);
+    hip(hipMalloc(&d_bsum, std::max<size_t>(nb, 1) * 4));
+    hip(hipMalloc(&d_boff, (nb + 1) * 8));
     hip(hipMalloc(&d_base, 8));
     hip(hipMalloc(&d_bad, 4));
-    if (rc == SID_OK) hip(hipMemsetAsync(d_bad, 0, 4, st));
+    if (rc == SID_OK && nb) {
+        hip(hipMemsetAsync(d_bad, 0, 4, st));
+        hip(hipMemsetAsync(d_base, 0, 8, st));
+        sid_fmt_len_kernel<<<(unsigned)nb, TB, 0, st>>>(T->d_text, T->len, T->d_starts, begin, end, d_code, d_hom,
+                                                        d_het, ct, d_bsum, d_bad);
+        sid_scan_kernel<<<1, SCAN_TB, 0, st>>>(d_bsum, nb, d_boff, d_base, nullptr);
+        hip(hipGetLastError());
+        hip(hipMemcpyAsync(boff.data(), d_boff, nb * 8, hipMemcpyDeviceToHost, st));
+        hip(hipMemcpyAsync(&boff[nb], d_base, 8, hipMemcpyDeviceToHost, st));
+        hip(hipStreamSynchronize(st));
+    }
+    t_size = wall() - f0;
+    const double al = wall();
+    stager.join();
+    hip(stage_err);
+    // exact size of the largest piece (long chromosome names can exceed the guess)
+    size_t need = 64;
+    for (size_t b0 = 0; b0 < nb; b0 += PB) need = std::max<size_t>(need, boff[std::min(nb, b0 + PB)] - boff[b0] + 64);
+    if (rc == SID_OK) hip(stage(need));
+    t_alloc = wall() - al;
     size_t pending_len[2] = {0, 0};
     bool pending[2] = {false, false};
-    int k = 0;
     auto flush = [&](int b) {   // hand piece b to the writer
         if (!pending[b]) return;
         pending[b] = false;
+        const double a = wall();
         if (!hip(hipEventSynchronize(done[b]))) return;
+        const double m = wall();
         if (pending_len[b] && write(user, h_out[b], pending_len[b]) != 0 && rc == SID_OK) rc = SID_EIO;
+        t_wait += m - a;
+        t_write += wall() - m;
     };
-    for (size_t s0 = begin; s0 < end && rc == SID_OK; s0 += PIECE, k ^= 1) {
-        const size_t s1 = std::min(end, s0 + PIECE);
-        const unsigned nb = (unsigned)((s1 - s0 + TB - 1) / TB);
-        sid_fmt_len_kernel<<<nb, TB, 0, st>>>(T->d_text, T->len, T->d_starts, s0, s1, d_code, d_hom, d_het, ct, d_bsum,
-                                               d_bad);
-        hip(hipMemsetAsync(d_base, 0, 8, st));
-        sid_scan_kernel<<<1, SCAN_TB, 0, st>>>(d_bsum, nb, d_boff, d_base, nullptr);
-        uint64_t bytes = 0;
-        hip(hipMemcpyAsync(&bytes, d_base, 8, hipMemcpyDeviceToHost, st));
-        hip(hipStreamSynchronize(st));
-        if (rc != SID_OK) break;
+    int k = 0;
+    for (size_t b0 = 0; b0 < nb && rc == SID_OK; b0 += PB, k ^= 1) {
+        const size_t b1 = std::min(nb, b0 + PB);
+        const size_t s0 = begin + b0 * TB, s1 = std::min(end, begin + b1 * TB);
+        const uint64_t bytes = boff[b1] - boff[b0];
         flush(k);   // buffer k is about to be reused
         if (rc != SID_OK) break;
-        if (bytes + 64 > cap[k]) {
-            if (d_out[k]) (void)hipFree(d_out[k]);
-            if (h_out[k]) (void)hipHostFree(h_out[k]);
-            d_out[k] = nullptr;
-            h_out[k] = nullptr;
-            cap[k] = bytes + bytes / 4 + 4096;
-            if (!hip(hipMalloc(&d_out[k], cap[k]))) break;
-            if (!hip(hipHostMalloc((void**)&h_out[k], cap[k], hipHostMallocDefault))) break;
-        }
-        sid_fmt_write_kernel<<<nb, TB, 0, st>>>(T->d_text, T->len, T->d_starts, s0, s1, d_code, d_hom, d_het, ct,
-                                                 d_boff, 0, d_out[k]);
+        sid_fmt_write_kernel<<<(unsigned)(b1 - b0), TB, 0, st>>>(T->d_text, T->len, T->d_starts, s0, s1, d_code, d_hom,
+                                                                 d_het, ct, d_boff + b0, boff[b0], d_out[k]);
         if (!hip(hipGetLastError())) break;
         hip(hipEventRecord(written, st));
         hip(hipStreamWaitEvent(cs, written, 0));
@@ -691,17 +800,17 @@ extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, 
     flush(k);
     int bad = 0;
     if (rc == SID_OK && hip(hipMemcpy(&bad, d_bad, 4, hipMemcpyDeviceToHost)) && bad) rc = SID_ERANGE;
+    if (text_timing())
+        std::fprintf(stderr,
+                     "{\"dtext_format\": {\"sites\": %zu, \"total_s\": %.6f, \"lengths_s\": %.6f, "
+                     "\"alloc_s\": %.6f, \"d2h_wait_s\": %.6f, \"write_s\": %.6f}}\n",
+                     n, wall() - f0, t_size, t_alloc, t_wait, t_write);
     (void)hipStreamSynchronize(cs);
-    for (int b = 0; b < 2; ++b) {
-        if (d_out[b]) (void)hipFree(d_out[b]);
-        if (h_out[b]) (void)hipHostFree(h_out[b]);
-        (void)hipEventDestroy(done[b]);
-    }
+    for (int b = 0; b < 2; ++b) (void)hipEventDestroy(done[b]);
     (void)hipEventDestroy(written);
     (void)hipStreamDestroy(cs);
     for (void* p : {(void*)d_bsum, (void*)d_boff, (void*)d_base, (void*)d_bad})
         if (p) (void)hipFree(p);
-    (void)e;
     return rc;
 }
 

@@ -157,3 +157,25 @@ def test_c1_golden_end_to_end_on_device(gpu, sid):
     torch.cuda.synchronize()
     body = t.format(code.data_ptr(), hom.data_ptr(), het.data_ptr(), "p_value")
     assert b"chrom,pos,label,gt,hom_conf,het_conf,conf_type\n" + body == want
+
+
+@pytest.mark.parametrize("n,threads,offset_lines", [(2_500, 1, 0), (2_200_000, 8, 0), (300_000, 3, 1234)])
+def test_parse_fd_equals_host(gpu, sid, tmp_path, n, threads, offset_lines):
+    """sid_dtext_parse_fd: pread into pinned staging (more chunks than readers
+    for the large case), from a line-aligned offset into the file."""
+    text = sid.synth_text(23, n, 30.0, sites_per_chrom=n // 2 + 1)
+    p = tmp_path / "in.plp"
+    p.write_bytes(text)
+    off = 0
+    for _ in range(offset_lines):
+        off = text.index(b"\n", off) + 1
+    ctx = sid.Context(0)
+    fd = os.open(str(p), os.O_RDONLY)
+    try:
+        t = sid.DText(ctx, fd=fd, offset=off, length=len(text) - off, threads=threads)
+    finally:
+        os.close(fd)
+    s = sid.parse_text(text[off:])
+    assert len(t) == len(s)
+    counts = gpu.device_view(t.counts_ptr, (len(t), 4)).cpu().numpy().view(np.uint16)
+    assert np.array_equal(counts, s.counts)
