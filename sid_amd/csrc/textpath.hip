@@ -29,6 +29,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <climits>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -256,61 +257,122 @@ __device__ int atoi_like(Reader& R, uint64_t b, uint64_t e)
     return (int)(unsigned)(unsigned long)r;
 }
 
+// One pass over each line, stopping at the end of the fifth token (the
+// quality and mapping-quality fields are never read): tokenisation on ' '/'\t'
+// runs up to a NUL or '\n' (parsePileupLine sees a C string), and the read
+// bases of token 4 counted on the fly with the reference's skip rules
+// (pileup.cpp:70-153, parse.cpp read_bases):
+//   '^' skips the next byte; '+'/'-' followed by a digit skips the digits and
+//   then strtol(digits) more bytes; '.'/',' count as toupper/tolower(ref);
+//   the skips end with the token.
+// Byte classes come from a 256-entry LDS table; the counts are updated without
+// branches on the class.
+enum : uint32_t { K_IGN = 0, K_A = 1, K_C = 2, K_G = 3, K_T = 4, K_CARET = 5, K_INDEL = 6 };
+
 __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ text, uint64_t len,
                                                        const uint64_t* __restrict__ starts,
                                                        const uint64_t* __restrict__ range,   // [lo, hi)
                                                        uint64_t* __restrict__ counts,
                                                        unsigned long long* __restrict__ err)
 {
+    __shared__ uint8_t cls[256];
+    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    __syncthreads();
     const uint64_t lo = range[0], hi = range[1];
     for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
          i += (uint64_t)gridDim.x * blockDim.x) {
         Reader R{text, len};
-        const Line L = find_line(R, starts[i]);
-        uint64_t tb[5], te[5];
-        const int nt = tokenize(R, L.s, L.end, 5, tb, te);
+        const uint64_t s0 = starts[i];
+        int nt = 0;              // tokens started
+        bool in_tok = false;
+        uint64_t tb2 = 0, te2 = 0;
+        uint32_t cdot = 0, ccomma = 0;
+        uint32_t nA = 0, nC = 0, nG = 0, nT = 0;
+        uint64_t skip = 0;       // bytes of token 4 still to skip
+        int ind = 0;             // 1: after '+'/'-'; 2: in its number
+        uint64_t num = 0;
+        bool ovf = false;
+        for (uint64_t q = s0; q < len; ++q) {
+            const uint32_t c = R.at(q);
+            if (c == '\n' || c == 0) break;   // end of the line / of the C string
+            const bool sep = c == ' ' || c == '\t';
+            if (!in_tok) {
+                if (sep) continue;
+                in_tok = true;
+                ++nt;
+                if (nt == 3) tb2 = q;
+                if (nt == 5) {   // token 2 is complete: the '.'/',' classes
+                    const uint32_t ref = R.at(tb2);
+                    const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
+                    const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
+                    cdot = cls[up];
+                    ccomma = cls[lw];
+                }
+            } else if (sep) {
+                in_tok = false;
+                if (nt == 3) te2 = q;
+                if (nt == 5) break;            // token 4 done: the rest is never read
+                continue;
+            }
+            if (nt != 5) continue;
+            // ---- a byte of the read-bases token
+            if (ind == 1) {   // byte after '+'/'-'
+                ind = 0;
+                if (c >= '0' && c <= '9') {
+                    ind = 2;
+                    num = c - '0';
+                    ovf = false;
+                    continue;
+                }
+            } else if (ind == 2) {
+                if (c >= '0' && c <= '9') {
+                    const unsigned d = c - '0';
+                    if (!ovf) {
+                        if (num > ((unsigned long long)LONG_MAX - d) / 10) ovf = true;
+                        else num = num * 10 + d;
+                    }
+                    continue;
+                }
+                ind = 0;
+                skip = ovf ? (uint64_t)LONG_MAX : num;   // this byte is the first skipped
+            }
+            if (skip) {
+                --skip;
+                continue;
+            }
+            const uint32_t k = c == '.' ? cdot : (c == ',' ? ccomma : cls[c]);
+            nA += k == K_A;
+            nC += k == K_C;
+            nG += k == K_G;
+            nT += k == K_T;
+            if (k == K_CARET) skip = 1;
+            else if (k == K_INDEL) ind = 1;
+        }
+        if (in_tok && nt == 3) te2 = ~0ull;   // token 2 ran to the end: length checked below
         int code = SID_OK;
         if (nt < 1) code = SID_ENULLCHROM;
-        else if (nt < 3 || (te[2] - tb[2]) != 1 || nt < 5) code = SID_EMALFORMED;
+        else if (nt < 3) code = SID_EMALFORMED;
+        else {
+            // token 2 length: its end is te2, or (if the line ended inside it) the
+            // first '\n'/NUL/end after tb2
+            uint64_t e2 = te2;
+            if (e2 == 0 || e2 == ~0ull) {
+                e2 = tb2;
+                while (e2 < len) {
+                    const uint32_t c = R.at(e2);
+                    if (c == '\n' || c == 0 || c == ' ' || c == '\t') break;
+                    ++e2;
+                }
+            }
+            if (e2 - tb2 != 1 || nt < 5) code = SID_EMALFORMED;
+        }
         if (code != SID_OK) {   // first in file order: min(offset * 4 + kind)
-            atomicMin(err, (unsigned long long)(L.s * 4 + (code == SID_EMALFORMED ? 1u : 2u)));
+            atomicMin(err, (unsigned long long)(s0 * 4 + (code == SID_EMALFORMED ? 1u : 2u)));
             counts[i] = 0;
             continue;
         }
-        // parseReadBases over token 4 with reference tb[2] (parse.cpp read_bases)
-        const uint32_t ref = R.at(tb[2]);
-        const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
-        const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
-        const uint32_t cdot = base_class(up), ccomma = base_class(lw);
-        uint32_t n[5] = {0, 0, 0, 0, 0};
-        const uint64_t b = tb[4], e = te[4];
-        for (uint64_t q = b; q < e; ++q) {
-            const uint32_t c = R.at(q);
-            const uint32_t k = c == '.' ? cdot : (c == ',' ? ccomma : base_class(c));
-            if (k <= 4) {
-                n[k]++;
-            } else if (k == 5) {
-                ++q;
-            } else if (q + 1 < e && is_digit(R.at(q + 1))) {   // '+'/'-' and a number
-                uint64_t p = q + 1;
-                unsigned long long v = 0;
-                bool ovf = false;
-                while (p < e && is_digit(R.at(p))) {
-                    const unsigned d = R.at(p) - '0';
-                    if (!ovf) {
-                        if (v > ((unsigned long long)LONG_MAX - d) / 10) ovf = true;
-                        else v = v * 10 + d;
-                    }
-                    ++p;
-                }
-                const unsigned long long length = ovf ? (unsigned long long)LONG_MAX : v;
-                // i = after + length - 1, then ++i
-                q = (length > e - p) ? e : p + length - 1;
-                if (q >= e) break;
-            }
-        }
-        counts[i] = (uint64_t)(uint16_t)n[1] | ((uint64_t)(uint16_t)n[2] << 16) | ((uint64_t)(uint16_t)n[3] << 32) |
-                    ((uint64_t)(uint16_t)n[4] << 48);
+        counts[i] = (uint64_t)(uint16_t)nA | ((uint64_t)(uint16_t)nC << 16) | ((uint64_t)(uint16_t)nG << 32) |
+                    ((uint64_t)(uint16_t)nT << 48);
     }
 }
 
