@@ -57,6 +57,8 @@ enum {
     SID_EIO = 10,        /* the output callback reported a write failure            */
     SID_ERANGE = 11,     /* a confidence outside the device formatter's range
                             (|v| >= 2^63; p-values and posteriors never are)        */
+    SID_ENOBQ = 12,      /* -m quality, no base-quality field: parseQualities(NULL)
+                            dereferences NULL (pileup.cpp:54,158): SIGSEGV          */
 };
 const char* sid_strerror(int status);
 int sid_last_hip_error(void);
@@ -64,7 +66,7 @@ int sid_last_hip_error(void);
 const char* sid_version(void);
 
 /* --------------------------------------------------------------- options -- */
-enum { SID_METHOD_LOCAL = 0, SID_METHOD_LIKELIHOOD_RATIO = 1, SID_METHOD_BAYES = 2 };
+enum { SID_METHOD_LOCAL = 0, SID_METHOD_LIKELIHOOD_RATIO = 1, SID_METHOD_BAYES = 2, SID_METHOD_QUALITY = 3 };
 
 /* GlobalOptions, sid.cpp:11-17 */
 typedef struct {
@@ -155,6 +157,10 @@ int sid_synth_counts(sid_ctx* ctx, uint64_t seed, double mean_depth, uint64_t fi
  * *len; writes at most cap bytes (call with buf == NULL to size). */
 int sid_synth_text(uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
                    uint64_t sites_per_chrom, char* buf, size_t cap, size_t* len);
+/* The same text with a 7th column of mapping qualities (samtools mpileup -s,
+ * uniform 0..60 per read), as the quality method requires. */
+int sid_synth_text_mq(uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
+                      uint64_t sites_per_chrom, char* buf, size_t cap, size_t* len);
 /* Host counts of the same sites (for tests; no GPU needed). */
 int sid_synth_counts_host(uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
                           uint16_t* counts);
@@ -216,6 +222,12 @@ int sid_dtext_format(sid_ctx* ctx, const sid_dtext* t, size_t begin, size_t end,
                      const double* hom_conf, const double* het_conf, const char* conf_type,
                      sid_write_fn write, void* user, void* stream);
 int sid_dtext_free(sid_dtext* t);
+/* -m quality (call.cpp:291-372) over a shard parsed by a context whose method
+ * is SID_METHOD_QUALITY (7 fields per line): the read bases and both quality
+ * fields are read from the resident text.  snp_prior / significance_level
+ * from the context's options (sid_set_prior after a -R estimate). */
+int sid_call_quality(sid_ctx* ctx, const sid_dtext* t, uint8_t* code, double* hom_conf, double* het_conf,
+                     void* stream);
 /* The device formatter's %g, host build (tests) and device batch: out gets
  * 16 bytes per value, NUL-padded. */
 int sid_format_g6(double v, char* buf, size_t cap);

@@ -64,6 +64,11 @@ def lib():
                                                  C.c_double]
         L.oracle_filter_min_coverage.restype = C.c_size_t
         L.oracle_filter_min_coverage.argtypes = [C.POINTER(Profile), C.c_size_t]
+        L.oracle_read_bases_seq.restype = C.c_int
+        L.oracle_read_bases_seq.argtypes = [C.c_char_p, C.c_char, C.c_char_p, C.c_int]
+        L.oracle_call_quality_text.restype = C.c_int
+        L.oracle_call_quality_text.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_double, C.c_double, P, P, P,
+                                               C.c_size_t, C.POINTER(C.c_size_t), C.c_int]
         _L = L
     return _L
 
@@ -109,6 +114,33 @@ def call_method(counts: np.ndarray, method="local", estimate_prior=False, snp_pr
                                   site_error_threshold, significance_level, _p(counts), n, _p(code),
                                   _p(h), _p(t), C.byref(est), C.byref(u), int(verbose))
     return rc, code[:n], h[:n], t[:n], est, u.value
+
+
+def read_bases_seq(s: bytes, ref: bytes) -> bytes:
+    """pileup.cpp:70-153 bases vector (upper case, read order)."""
+    n = lib().oracle_read_bases_seq(s, ref, None, 0)
+    buf = C.create_string_buffer(max(n, 1))
+    lib().oracle_read_bases_seq(s, ref, buf, n)
+    return buf.raw[:n]
+
+
+def call_quality(text: bytes, estimate_prior=False, snp_prior=-1.0, significance_level=0.05):
+    """call.cpp:291-372 over a pileup text (7 fields).  Returns (rc, code, hom, het):
+    rc = 0, or 1 malformed / 2 missing mapping qualities / 3 no chromosome /
+    4 no base qualities (the first bad line), or 10 + the -R estimate's rc."""
+    n = C.c_size_t(0)
+    L = lib()
+    rc = L.oracle_call_quality_text(text, len(text), int(estimate_prior), snp_prior, significance_level,
+                                    None, None, None, 0, C.byref(n), 0)
+    if rc:
+        return rc, None, None, None
+    m = n.value
+    code = np.zeros(max(m, 1), np.uint8)
+    h = np.zeros(max(m, 1), np.float64)
+    t = np.zeros(max(m, 1), np.float64)
+    rc = L.oracle_call_quality_text(text, len(text), int(estimate_prior), snp_prior, significance_level, _p(code),
+                                    _p(h), _p(t), m, C.byref(n), 0)
+    return rc, code[:m], h[:m], t[:m]
 
 
 def read_bases(s: bytes, ref: bytes) -> np.ndarray:

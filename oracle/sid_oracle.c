@@ -64,6 +64,44 @@ void oracle_read_bases(const char* read_bases, char reference, uint16_t counts[4
     }
 }
 
+/* pileup.cpp:70-153: the bases vector -- upper-case A/C/G/T in read order,
+ * the same walk as oracle_read_bases.  Returns the count; writes up to cap. */
+int oracle_read_bases_seq(const char* read_bases, char reference, char* out, int cap)
+{
+    int n = 0;
+    for (size_t i = 0; i < strlen(read_bases); ++i) {
+        char base = read_bases[i];
+        if (base == '.') {
+            base = (char)toupper(reference);
+        } else if (base == ',') {
+            base = (char)tolower(reference);
+        }
+        char b = 0;
+        switch (base) {
+        case 'a': case 'A': b = 'A'; break;
+        case 'c': case 'C': b = 'C'; break;
+        case 'g': case 'G': b = 'G'; break;
+        case 't': case 'T': b = 'T'; break;
+        case '^': ++i; break;
+        case '+':
+        case '-': {
+            if (!isdigit((unsigned char)read_bases[i + 1])) break;
+            char* first_after_number;
+            unsigned long length = (unsigned long)strtol(read_bases + i + 1, &first_after_number, 10);
+            if (SIZE_MAX - length < i) i = SIZE_MAX;
+            else i = (size_t)(first_after_number - read_bases) + length - 1;
+            break;
+        }
+        default: break;
+        }
+        if (b) {
+            if (out && n < cap) out[n] = b;
+            ++n;
+        }
+    }
+    return n;
+}
+
 /* pileup.cpp:155-167 parseQualities */
 int oracle_parse_qualities(const char* q, uint8_t* out, int cap)
 {
@@ -108,15 +146,18 @@ int oracle_parse_line(char* line, int parse_bq, int parse_mq, oracle_line* out)
     oracle_read_bases(read_bases, out->reference, out->counts);
 
     char* base_qualities = strtok_r(NULL, FIELD_SEPARATORS, &saveptr);
+    out->read_bases = read_bases;
     if (parse_bq) {
         /* pileup.cpp:51-54 checks read_bases (never NULL here) and then
-         * dereferences base_qualities, which crashes when it is NULL. */
-        if (base_qualities == NULL) return ORACLE_EMALFORMED;
+         * parseQualities dereferences base_qualities: SIGSEGV when it is NULL. */
+        if (base_qualities == NULL) return ORACLE_ENOBQ;
+        out->base_qualities = base_qualities;
         out->n_bq = oracle_parse_qualities(base_qualities, NULL, 0);
     }
     if (parse_mq) {
         char* mapping_qualities = strtok_r(NULL, FIELD_SEPARATORS, &saveptr);
         if (mapping_qualities == NULL) return ORACLE_EMISSING_MQ;
+        out->mapping_qualities = mapping_qualities;
         out->n_mq = oracle_parse_qualities(mapping_qualities, NULL, 0);
     }
     return ORACLE_OK;
@@ -965,4 +1006,141 @@ void oracle_call_local(const uint16_t* counts, size_t n, double snp_prior, doubl
     for (size_t i = 0; i < n; ++i)
         oracle_local_profile(counts + 4 * i, snp_prior, error_threshold, significance_level,
                              &code[i], &hom_conf[i], &het_conf[i]);
+}
+
+/* ------------------------------------------------------------------------ */
+/* call.cpp:311-369 callQualityBasedSimple, one site.  bases / bq / mq as    */
+/* pileup.cpp parses them; the j-th counted base pairs with the j-th quality */
+/* characters (the reference's index alignment).  Past the end of bq or mq   */
+/* the reference reads outside the vectors (undefined); quality 1 is used.   */
+/* ------------------------------------------------------------------------ */
+void oracle_quality_site(const uint16_t counts[4], const char* bases, int nb, const uint8_t* bq, int nbq,
+                         const uint8_t* mq, int nmq, double snp_prior, double significance_level,
+                         uint8_t* code, double* p1, double* p2)
+{
+    static const char ACGT[] = "ACGT";
+    int ref0, ref1;
+    oracle_major(counts, &ref0, &ref1);
+    long double lph = 0, lpt = 0;
+    for (int j = 0; j < nb; ++j) {
+        const uint8_t b = j < nbq ? bq[j] : 1, m = j < nmq ? mq[j] : 1;
+        const double error = pow(10., (b < m ? b : m) / -10.);
+        if (bases[j] == ACGT[ref0]) lph += log(1 - error);
+        else lph += log(error);
+        if (bases[j] == ACGT[ref0] || bases[j] == ACGT[ref1]) lpt += log(1 - 2. / 3. * error);
+        else lpt += log(2. / 3. * error);
+    }
+    const int n = counts[ref0] + counts[ref1];
+    const int k = counts[ref1];
+    const double logbinom = oracle_log_gamma(n + 1) - oracle_log_gamma(n - k + 1) - oracle_log_gamma(k + 1);
+    lpt += logbinom - n * logl(2);
+    long double pp1 = expl(lph), pp2 = expl(lpt);
+    if (snp_prior > 0) {
+        pp1 *= (1 - snp_prior);
+        pp2 *= snp_prior;
+    }
+    *p1 = oracle_lrt(pp2, pp1);
+    *p2 = oracle_lrt(pp1, pp2);
+    const int het = *p2 < significance_level;
+    *code = (uint8_t)(ref0 | ((het ? ref1 : ref0) << 2) | (het ? 0x80 : 0));
+}
+
+/* quality method over a whole text (readFile(in, true, true) + the per-site
+ * loop); returns ORACLE_* of the first malformed line, or 10 + oracle_call_method's rc */
+int oracle_call_quality_text(const char* text, size_t len, int estimate_prior, double snp_prior,
+                             double significance_level, uint8_t* code, double* hom, double* het,
+                             size_t cap, size_t* n_out, int verbose)
+{
+    size_t n = 0, ncap = 1024;
+    uint16_t* counts = (uint16_t*)malloc(ncap * 8);
+    char* line = NULL;
+    size_t lcap = 0;
+    /* pass 1: parse (errors first, as readFile does), counts */
+    const char* p = text;
+    const char* end = text + len;
+    int rc = ORACLE_OK;
+    while (p < end) {
+        const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+        size_t ll = nl ? (size_t)(nl - p) : (size_t)(end - p);
+        if (ll > 0) {
+            if (ll + 1 > lcap) {
+                lcap = 2 * (ll + 1);
+                line = (char*)realloc(line, lcap);
+            }
+            memcpy(line, p, ll);
+            line[ll] = 0;
+            oracle_line L;
+            rc = oracle_parse_line(line, 1, 1, &L);
+            if (rc != ORACLE_OK) break;
+            if (n == ncap) {
+                ncap *= 2;
+                counts = (uint16_t*)realloc(counts, ncap * 8);
+            }
+            memcpy(counts + 4 * n, L.counts, 8);
+            ++n;
+        }
+        p = nl ? nl + 1 : end;
+    }
+    if (rc != ORACLE_OK) {
+        free(counts);
+        free(line);
+        return rc;
+    }
+    *n_out = n;
+    if (estimate_prior) {   /* call.cpp:294-305: the -R estimate of the local method */
+        uint8_t* c = (uint8_t*)malloc(n ? n : 1);
+        double* a = (double*)malloc((n ? n : 1) * 8);
+        double* b = (double*)malloc((n ? n : 1) * 8);
+        oracle_est_t est;
+        int r = oracle_call_method(ORACLE_LOCAL, 1, -1, 0.1, significance_level, counts, n, c, a, b, &est, NULL,
+                                   verbose);
+        free(c);
+        free(a);
+        free(b);
+        if (r) {
+            free(counts);
+            free(line);
+            return 10 + r;
+        }
+        snp_prior = est.heterozygosity;
+    }
+    /* pass 2: per site */
+    size_t i = 0;
+    char* bases = NULL;
+    uint8_t *bq = NULL, *mq = NULL;
+    int bcap = 0;
+    p = text;
+    while (p < end && i < n) {
+        const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+        size_t ll = nl ? (size_t)(nl - p) : (size_t)(end - p);
+        if (ll > 0) {
+            memcpy(line, p, ll);
+            line[ll] = 0;
+            oracle_line L;
+            oracle_parse_line(line, 1, 1, &L);
+            int nb = oracle_read_bases_seq(L.read_bases, L.reference, NULL, 0);
+            int need = nb > L.n_bq ? nb : L.n_bq;
+            if (L.n_mq > need) need = L.n_mq;
+            if (need + 1 > bcap) {
+                bcap = 2 * (need + 1);
+                bases = (char*)realloc(bases, bcap);
+                bq = (uint8_t*)realloc(bq, bcap);
+                mq = (uint8_t*)realloc(mq, bcap);
+            }
+            oracle_read_bases_seq(L.read_bases, L.reference, bases, bcap);
+            oracle_parse_qualities(L.base_qualities, bq, bcap);
+            oracle_parse_qualities(L.mapping_qualities, mq, bcap);
+            if (i < cap)
+                oracle_quality_site(counts + 4 * i, bases, nb, bq, L.n_bq, mq, L.n_mq, snp_prior,
+                                    significance_level, &code[i], &hom[i], &het[i]);
+            ++i;
+        }
+        p = nl ? nl + 1 : end;
+    }
+    free(bases);
+    free(bq);
+    free(mq);
+    free(counts);
+    free(line);
+    return ORACLE_OK;
 }

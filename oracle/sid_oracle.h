@@ -36,6 +36,8 @@ enum {
     ORACLE_EMALFORMED = 1,        /* "Malformed pileup line"                 pileup.cpp:9   */
     ORACLE_EMISSING_MQ = 2,       /* "... or missing mapping qualities"      pileup.cpp:10  */
     ORACLE_ENULLCHROM = 3,        /* std::string = (char*)NULL: SIGSEGV      pileup.cpp:18 */
+    ORACLE_ENOBQ = 4,             /* quality mode, no 6th field: parseQualities(NULL)
+                                     dereferences NULL: SIGSEGV          pileup.cpp:54,158 */
 };
 
 enum { ORACLE_LOCAL = 0, ORACLE_LIKELIHOOD_RATIO = 1, ORACLE_BAYES = 2 };
@@ -47,6 +49,7 @@ typedef struct {
     int coverage;        /* atoi(), only a reserve() hint         pileup.cpp:36 */
     uint16_t counts[4];  /* profile_t A,C,G,T                     pileup.hpp:7  */
     int n_bq, n_mq;      /* number of parsed quality values (when requested)   */
+    const char* read_bases, *base_qualities, *mapping_qualities;   /* tokens */
 } oracle_line;
 
 /* pileup.cpp:13-68.  Mutates `line` like strtok_r does.  Returns ORACLE_*. */
@@ -55,6 +58,18 @@ int oracle_parse_line(char* line, int parse_bq, int parse_mq, oracle_line* out);
 void oracle_read_bases(const char* read_bases, char reference, uint16_t counts[4]);
 /* pileup.cpp:155-167. Writes up to `cap` values, returns the count. */
 int oracle_parse_qualities(const char* q, uint8_t* out, int cap);
+/* pileup.cpp:70-153 bases vector (upper case, read order); returns the count */
+int oracle_read_bases_seq(const char* read_bases, char reference, char* out, int cap);
+/* call.cpp:311-369, one site */
+void oracle_quality_site(const uint16_t counts[4], const char* bases, int nb, const uint8_t* bq, int nbq,
+                         const uint8_t* mq, int nmq, double snp_prior, double significance_level,
+                         uint8_t* code, double* p1, double* p2);
+/* call.cpp:291-372 over a text: ORACLE_* of the first bad line, 10 + rc of the
+ * -R estimate on failure, else ORACLE_OK with *n_out sites (results for the
+ * first `cap`) */
+int oracle_call_quality_text(const char* text, size_t len, int estimate_prior, double snp_prior,
+                             double significance_level, uint8_t* code, double* hom, double* het,
+                             size_t cap, size_t* n_out, int verbose);
 
 /* call.cpp:52-60 */
 void oracle_major(const uint16_t p[4], int* first, int* second);

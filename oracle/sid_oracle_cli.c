@@ -131,16 +131,51 @@ int main(int argc, char** argv)
     if (strcmp(o.method, "local") == 0) method = ORACLE_LOCAL;
     else if (strcmp(o.method, "bayes") == 0) method = ORACLE_BAYES;
     else if (strcmp(o.method, "likelihood_ratio") == 0) method = ORACLE_LIKELIHOOD_RATIO;
-    else if (strcmp(o.method, "quality") == 0) {
-        fputs("sid_oracle: -m quality is not restated by the oracle\n", stderr);
-        return 3;
-    }
+    else if (strcmp(o.method, "quality") == 0) method = 3;   /* call.cpp:291-372 */
 
     sites_t s = {0};
     uint8_t* code = NULL;
     double *h = NULL, *t = NULL;
     const char* conf_type = method == ORACLE_BAYES ? "probability" : "p_value";
-    if (method >= 0) {
+    if (method == 3) {
+        /* readFile(in, true, true): the whole text, errors first */
+        char* text = NULL;
+        size_t len = 0, tcap = 0;
+        char buf[1 << 16];
+        size_t r;
+        while ((r = fread(buf, 1, sizeof buf, in)) > 0) {
+            if (len + r > tcap) {
+                tcap = 2 * (len + r);
+                text = (char*)realloc(text, tcap);
+            }
+            memcpy(text + len, buf, r);
+            len += r;
+        }
+        size_t nq = 0;
+        int rc = oracle_call_quality_text(text, len, o.estimate_prior, o.snp_prior, o.significance_level,
+                                          NULL, NULL, NULL, 0, &nq, 1);
+        if (rc == ORACLE_EMALFORMED) die_terminate("std::invalid_argument", "Malformed pileup line");
+        if (rc == ORACLE_EMISSING_MQ)
+            die_terminate("std::invalid_argument", "Malformed pileup line or missing mapping qualities");
+        if (rc == ORACLE_ENULLCHROM || rc == ORACLE_ENOBQ) {
+            fflush(stdout);
+            signal(SIGSEGV, SIG_DFL);
+            raise(SIGSEGV);
+        }
+        if (rc == 11) {
+            fputs("gsl: nmsimplex2.c: ERROR: non-finite function value encountered\n"
+                  "Default GSL error handler invoked.\n", stderr);
+            abort();
+        }
+        code = (uint8_t*)malloc(nq ? nq : 1);
+        h = (double*)malloc((nq ? nq : 1) * sizeof(double));
+        t = (double*)malloc((nq ? nq : 1) * sizeof(double));
+        oracle_call_quality_text(text, len, o.estimate_prior, o.snp_prior, o.significance_level, code, h, t, nq,
+                                 &nq, 0);
+        rewind(in);
+        read_file(in, &s);   /* chrom and pos; cannot fail after the quality parse */
+        free(text);
+    } else if (method >= 0) {
         read_file(in, &s);
         code = (uint8_t*)malloc(s.n ? s.n : 1);
         h = (double*)malloc((s.n ? s.n : 1) * sizeof(double));

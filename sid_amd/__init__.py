@@ -22,14 +22,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(ROOT, "build", "libsid.so")
 CLI_PATH = os.path.join(ROOT, "build", "sid")
 
-METHOD_LOCAL, METHOD_LIKELIHOOD_RATIO, METHOD_BAYES = 0, 1, 2
+METHOD_LOCAL, METHOD_LIKELIHOOD_RATIO, METHOD_BAYES, METHOD_QUALITY = 0, 1, 2, 3
 METHODS = {"local": METHOD_LOCAL, "likelihood_ratio": METHOD_LIKELIHOOD_RATIO,
-           "bayes": METHOD_BAYES}
+           "bayes": METHOD_BAYES, "quality": METHOD_QUALITY}
 
 SID_OK = 0
 STATUS = {0: "SID_OK", 1: "SID_EINVAL", 2: "SID_EHIP", 3: "SID_ENOMEM", 4: "SID_EMALFORMED",
           5: "SID_EMISSING_MQ", 6: "SID_ENULLCHROM", 7: "SID_ESTATE", 8: "SID_EBADFUNC",
-          9: "SID_EEMPTY", 10: "SID_EIO", 11: "SID_ERANGE"}
+          9: "SID_EEMPTY", 10: "SID_EIO", 11: "SID_ERANGE", 12: "SID_ENOBQ"}
 
 CODE_HET = 0x80
 CODE_DROPPED = 0x40
@@ -84,6 +84,7 @@ SIGNATURES = [
     ("sid_synth_counts", _I, [_P, _U64, _D, _U64, _SZ, _P, _P]),
     ("sid_synth_text", _I, [_U64, _D, _U64, _SZ, _U64, _P, _SZ, C.POINTER(C.c_size_t)]),
     ("sid_synth_counts_host", _I, [_U64, _D, _U64, _SZ, _P]),
+    ("sid_synth_text_mq", _I, [_U64, _D, _U64, _SZ, _U64, _P, _SZ, C.POINTER(C.c_size_t)]),
     ("sid_parse_text", _I, [C.c_char_p, _SZ, _I, C.POINTER(_P), C.POINTER(C.c_uint64)]),
     ("sid_sites_free", None, [_P]),
     ("sid_sites_count", _SZ, [_P]),
@@ -99,6 +100,7 @@ SIGNATURES = [
     ("sid_dtext_counts", _P, [_P]),
     ("sid_dtext_format", _I, [_P, _P, _SZ, _SZ, _P, _P, _P, C.c_char_p, WRITE_FN, _P, _P]),
     ("sid_dtext_free", _I, [_P]),
+    ("sid_call_quality", _I, [_P, _P, _P, _P, _P, _P]),
     ("sid_format_g6", _I, [_D, C.c_char_p, _SZ]),
     ("sid_format_g6_device", _I, [_P, _P, _SZ, _P, _P]),
 ]
@@ -276,12 +278,14 @@ class DText:
 
 
 def synth_text(seed: int, n: int, depth: float = 30.0, first: int = 0,
-               sites_per_chrom: int = 0) -> bytes:
+               sites_per_chrom: int = 0, mapq: bool = False) -> bytes:
+    """Synthetic pileup text; mapq=True adds the 7th (mapping quality) column."""
     L = lib()
+    fn = L.sid_synth_text_mq if mapq else L.sid_synth_text
     ln = C.c_size_t(0)
-    check(L.sid_synth_text(seed, depth, first, n, sites_per_chrom, None, 0, C.byref(ln)), "synth")
+    check(fn(seed, depth, first, n, sites_per_chrom, None, 0, C.byref(ln)), "synth")
     buf = C.create_string_buffer(max(ln.value, 1))
-    check(L.sid_synth_text(seed, depth, first, n, sites_per_chrom, buf, ln.value, C.byref(ln)), "synth")
+    check(fn(seed, depth, first, n, sites_per_chrom, buf, ln.value, C.byref(ln)), "synth")
     return buf.raw[: ln.value]
 
 

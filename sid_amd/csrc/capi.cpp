@@ -40,6 +40,7 @@ extern "C" const char* sid_strerror(int status)
     case SID_EEMPTY: return "no profile with coverage >= 4";
     case SID_EIO: return "output write failed";
     case SID_ERANGE: return "value outside the device formatter's range";
+    case SID_ENOBQ: return "no base-quality field";
     default: return "unknown status";
     }
 }
@@ -170,6 +171,8 @@ extern "C" int sid_destroy(sid_ctx* c)
     }
     for (char* p : c->in_h)
         if (p) (void)hipHostFree(p);
+    for (void* p : {(void*)c->d_qtab, (void*)c->d_lg, (void*)c->d_scratch})
+        if (p) (void)hipFree(p);
     for (auto& v : {c->ev_pool, c->ev_pending})
         for (auto& ev : v) {
             (void)hipEventDestroy(ev.start);
@@ -312,13 +315,13 @@ extern "C" int sid_synth_counts_host(uint64_t seed, double mean_depth, uint64_t 
 }
 
 static void synth_text_range(uint64_t seed, const std::vector<uint64_t>& cdf, uint64_t first,
-                             size_t n, uint64_t spc, std::string& out)
+                             size_t n, uint64_t spc, bool mq, std::string& out)
 {
     static const char UP[] = "ACGT", LO[] = "acgt";
     out.clear();
     out.reserve(n * 96);
     char num[32];
-    std::string bases, quals;
+    std::string bases, quals, mquals;
     const uint32_t k = (uint32_t)cdf.size();
     for (size_t i = 0; i < n; ++i) {
         const uint64_t site = first + i;
@@ -335,11 +338,12 @@ static void synth_text_range(uint64_t seed, const std::vector<uint64_t>& cdf, ui
         out.append(num, (size_t)std::snprintf(num, sizeof num, "%u", s.depth));
         out += '\t';
         if (s.depth == 0) {
-            out += "*\t*\n";
+            out += mq ? "*\t*\t*\n" : "*\t*\n";
             continue;
         }
         bases.clear();
         quals.clear();
+        mquals.clear();
         for (uint32_t r = 0; r < s.depth; ++r) {
             uint32_t strand;
             uint32_t b = sid_synth_read_base(&s, r, &strand);
@@ -353,16 +357,36 @@ static void synth_text_range(uint64_t seed, const std::vector<uint64_t>& cdf, ui
                 bases += strand ? UP[b] : LO[b];
             if (en) bases += '$';
             quals += (char)('!' + q);
+            if (mq) mquals += (char)('!' + sid_synth_read_mapq(&s, r));
         }
         out += bases;
         out += '\t';
         out += quals;
+        if (mq) {
+            out += '\t';
+            out += mquals;
+        }
         out += '\n';
     }
 }
 
+static int synth_text(uint64_t seed, double mean_depth, uint64_t first_site, size_t n, uint64_t sites_per_chrom,
+                      bool mq, char* buf, size_t cap, size_t* len);
+
 extern "C" int sid_synth_text(uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
                               uint64_t sites_per_chrom, char* buf, size_t cap, size_t* len)
+{
+    return synth_text(seed, mean_depth, first_site, n, sites_per_chrom, false, buf, cap, len);
+}
+
+extern "C" int sid_synth_text_mq(uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
+                                 uint64_t sites_per_chrom, char* buf, size_t cap, size_t* len)
+{
+    return synth_text(seed, mean_depth, first_site, n, sites_per_chrom, true, buf, cap, len);
+}
+
+static int synth_text(uint64_t seed, double mean_depth, uint64_t first_site, size_t n, uint64_t sites_per_chrom,
+                      bool mq, char* buf, size_t cap, size_t* len)
 {
     if (!len || !(mean_depth >= 0) || mean_depth > 600) return SID_EINVAL;
     std::vector<uint64_t> cdf;
@@ -377,7 +401,7 @@ extern "C" int sid_synth_text(uint64_t seed, double mean_depth, uint64_t first_s
     for (unsigned t = 0; t < T; ++t) {
         size_t b = t * per, e = std::min(n, b + per);
         if (b >= e) continue;
-        th.emplace_back([&, t, b, e] { synth_text_range(seed, cdf, first_site + b, e - b, sites_per_chrom, parts[t]); });
+        th.emplace_back([&, t, b, e] { synth_text_range(seed, cdf, first_site + b, e - b, sites_per_chrom, mq, parts[t]); });
     }
     for (auto& x : th) x.join();
     size_t total = 0;

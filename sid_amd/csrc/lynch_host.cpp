@@ -879,12 +879,14 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     const auto t1 = now();
     const int method = c->opts.method;
     const size_t U = L->fkeys.size();
-    if (verbose && method != SID_METHOD_LOCAL) std::fprintf(stderr, "# unique profiles: %zu\n", U);
+    // the -R estimate of local and quality prints only the minimiser's line
+    const bool local_like = method == SID_METHOD_LOCAL || method == SID_METHOD_QUALITY;
+    if (verbose && !local_like) std::fprintf(stderr, "# unique profiles: %zu\n", U);
     rc = run_estimate(c, verbose, &est);
     if (rc) return rc;
     const auto t2 = now();
     if (est_out) *est_out = est;
-    if (method == SID_METHOD_LOCAL) return SID_OK;   // -R local: caller applies the prior
+    if (local_like) return SID_OK;   // -R local / quality: the caller applies the prior
     if (verbose) {
         std::fprintf(stderr, "# heterozygosity: %e\n", est.heterozygosity);
         std::fprintf(stderr, "# error: %e\n", est.error_rate);

@@ -239,11 +239,7 @@ int main(int argc, char** argv)
     if (opt.method == "local") method = SID_METHOD_LOCAL;
     else if (opt.method == "bayes") method = SID_METHOD_BAYES;
     else if (opt.method == "likelihood_ratio") method = SID_METHOD_LIKELIHOOD_RATIO;
-    else if (opt.method == "quality") {
-        std::fflush(stdout);
-        std::fputs("sid: -m quality is not implemented in this build (SURVEY.md §8(f) rank 3)\n", stderr);
-        std::exit(EXIT_FAILURE);
-    }
+    else if (opt.method == "quality") method = SID_METHOD_QUALITY;   // call.cpp:291-372
     if (method < 0) {   // sid.cpp:92-102: unknown method -> header only
         std::printf("chrom,pos,label,gt,hom_conf,het_conf,conf_type\n");
         return 0;
@@ -263,14 +259,21 @@ int main(int argc, char** argv)
     // shard d runs on device d % ndev (more shards than devices: a
     // multi-device run's splitting and merging on fewer GPUs)
     const int D = std::max(1, opt.devices);
-    const bool lynch = method != SID_METHOD_LOCAL || opt.o.estimate_prior;
+    const bool quality = method == SID_METHOD_QUALITY;
+    // the Lynch estimate: LR and bayes always, local and quality with -R
+    const bool lynch = method == SID_METHOD_LIKELIHOOD_RATIO || method == SID_METHOD_BAYES || opt.o.estimate_prior;
+    // per-read qualities live in the text: -m quality always takes the device text path
+    if (quality) opt.host_parse = false;
     const char* conf_type = method == SID_METHOD_BAYES ? "probability" : "p_value";
     std::vector<Shard> sh(D);
     auto on_parse_error = [&](int prc) {
         if (prc == SID_EMALFORMED) terminate_like("std::invalid_argument", "Malformed pileup line");
-        if (prc == SID_ENULLCHROM) {
-            // pileup.cpp:18 assigns a NULL char* to std::string: the reference
-            // dies in strlen() with SIGSEGV, printing nothing
+        if (prc == SID_EMISSING_MQ)   // pileup.cpp:10,63
+            terminate_like("std::invalid_argument", "Malformed pileup line or missing mapping qualities");
+        if (prc == SID_ENULLCHROM || prc == SID_ENOBQ) {
+            // pileup.cpp:18 assigns a NULL char* to std::string (or, for
+            // -m quality, pileup.cpp:158 reads a NULL field): the reference
+            // dies with SIGSEGV, printing nothing
             std::fflush(stdout);
             std::signal(SIGSEGV, SIG_DFL);
             std::raise(SIGSEGV);
@@ -354,7 +357,8 @@ int main(int argc, char** argv)
         int prc = SID_OK;
         uint64_t first = UINT64_MAX;
         for (int d = 0; d < D; ++d) {
-            if (rcs[d] == SID_EMALFORMED || rcs[d] == SID_ENULLCHROM) {
+            if (rcs[d] == SID_EMALFORMED || rcs[d] == SID_ENULLCHROM || rcs[d] == SID_EMISSING_MQ ||
+                rcs[d] == SID_ENOBQ) {
                 if (cut[d] + eoff[d] < first) {
                     first = cut[d] + eoff[d];
                     prc = rcs[d];
@@ -406,8 +410,8 @@ int main(int argc, char** argv)
                 }
             }
             rcs[d] = sid_lynch_prepare(sh[d].ctx, d == 0, &est[d]);
-            if (rcs[d] == SID_OK && method == SID_METHOD_LOCAL)
-                rcs[d] = sid_set_prior(sh[d].ctx, est[d].heterozygosity);   // call.cpp:233
+            if (rcs[d] == SID_OK && (method == SID_METHOD_LOCAL || quality))
+                rcs[d] = sid_set_prior(sh[d].ctx, est[d].heterozygosity);   // call.cpp:233, :305
         };
         // device 0 prints the reference's diagnostics; the others run the same
         // deterministic estimate silently
@@ -433,7 +437,9 @@ int main(int argc, char** argv)
         Shard& s = sh[d];
         (void)hipSetDevice(d % ndev);
         const size_t m = s.end - s.begin;
-        if (method == SID_METHOD_LOCAL)
+        if (quality)
+            CHECK(sid_call_quality(s.ctx, s.text, s.d_code, s.d_hom, s.d_het, s.stream), "quality");
+        else if (method == SID_METHOD_LOCAL)
             CHECK(sid_call_local(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "local");
         else
             CHECK(sid_lookup_sites(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "lookup");

@@ -69,6 +69,11 @@ struct sid_ctx {
     size_t fmt_cap[2] = {0, 0};
     // sid_dtext_parse_fd: pinned read staging, one buffer per reader thread
     char* in_h[SID_STAGE_N] = {};
+    // -m quality (textpath.hip): per-quality terms and log_gamma, host-computed
+    double* d_qtab = nullptr;   // 4 x 256
+    double* d_lg = nullptr;     // log_gamma(x), x < lg_n
+    size_t lg_n = 0;
+    uint32_t* d_scratch = nullptr;
 };
 
 // host helpers (capi.cpp)

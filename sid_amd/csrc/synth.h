@@ -102,6 +102,12 @@ SID_HD void sid_synth_read_marks(const struct sid_synth_site* s, uint32_t r, int
     *qual = 20u + (uint32_t)((u3 >> 40) % 21u);
 }
 
+// Mapping quality of read r (samtools mpileup -s 7th column): uniform 0..60.
+SID_HD uint32_t sid_synth_read_mapq(const struct sid_synth_site* s, uint32_t r)
+{
+    return (uint32_t)(sid_draw(s->key, 0x40000000u + r) % 61u);
+}
+
 // Counts (A,C,G,T) packed as profile_t little-endian u64 (pileup.hpp:7).
 // Synthetic depth is < 65536, so the per-base 16-bit fields never carry.
 SID_HD uint64_t sid_synth_counts(uint64_t seed, uint64_t site, const uint64_t* cdf, uint32_t kmax)

@@ -29,6 +29,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <climits>
 #include <chrono>
 #include <cstdio>
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
                                                        const uint64_t* __restrict__ starts,
                                                        const uint64_t* __restrict__ range,   // [lo, hi)
                                                        uint64_t* __restrict__ counts,
-                                                       unsigned long long* __restrict__ err)
+                                                       unsigned long long* __restrict__ err, int qmode)
 {
     __shared__ uint8_t cls[256];
     if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
@@ -300,6 +301,7 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
                 if (sep) continue;
                 in_tok = true;
                 ++nt;
+                if (nt == 7) break;                // quality mode: both quality fields exist
                 if (nt == 3) tb2 = q;
                 if (nt == 5) {   // token 2 is complete: the '.'/',' classes
                     const uint32_t ref = R.at(tb2);
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
             } else if (sep) {
                 in_tok = false;
                 if (nt == 3) te2 = q;
-                if (nt == 5) break;            // token 4 done: the rest is never read
+                if (nt == 5 && !qmode) break;  // token 4 done: the rest is never read
                 continue;
             }
             if (nt != 5) continue;
@@ -365,9 +367,15 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
                 }
             }
             if (e2 - tb2 != 1 || nt < 5) code = SID_EMALFORMED;
+            // readFile(in, true, true) (call.cpp:292): parseQualities(NULL) on a
+            // missing 6th field (SIGSEGV), then the mapping-quality check
+            else if (qmode && nt == 5) code = SID_ENOBQ;
+            else if (qmode && nt == 6) code = SID_EMISSING_MQ;
         }
-        if (code != SID_OK) {   // first in file order: min(offset * 4 + kind)
-            atomicMin(err, (unsigned long long)(s0 * 4 + (code == SID_EMALFORMED ? 1u : 2u)));
+        if (code != SID_OK) {   // first in file order: min(offset * 8 + kind)
+            const uint32_t kind = code == SID_EMALFORMED ? 1u : code == SID_ENULLCHROM ? 2u
+                                : code == SID_EMISSING_MQ ? 3u : 4u;
+            atomicMin(err, (unsigned long long)(s0 * 8 + kind));
             counts[i] = 0;
             continue;
         }
@@ -510,6 +518,171 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
     }
 }
 
+// ------------------------------------------------------------ -m quality --
+// call.cpp:311-369 callQualityBasedSimple, one lane per site, reading the
+// read bases and both quality fields straight from the resident text.  The
+// j-th counted base pairs with the j-th characters of the base- and
+// mapping-quality fields (the reference's index alignment; past their end the
+// reference reads outside its vectors -- undefined -- and quality 1 is used).
+// Every per-read term is a function of q = min(bq, mq) only, so the four of
+// them come from a host table built with the same glibc pow/log the reference
+// calls (bit-identical doubles); the long-double sums are double-double here.
+struct QParams {
+    double sig;
+    double prior;
+    int prior_on;
+    int prior_ld;      // prior >= 1: emulated long-double path
+    sid_dd lp1, lp2;   // ln(1 - prior), ln(prior) to ~1e-19
+    double lg15;
+};
+
+__device__ __forceinline__ void dd_acc(sid_dd& a, double t)
+{
+    const double s = a.hi + t;
+    const double bb = s - a.hi;
+    const double e = (a.hi - (s - bb)) + (t - bb);
+    a.hi = s;
+    a.lo += e;
+}
+
+__global__ __launch_bounds__(TB) void sid_quality_kernel(const char* __restrict__ text, uint64_t len,
+                                                         const uint64_t* __restrict__ starts,
+                                                         const uint64_t* __restrict__ counts, uint64_t n,
+                                                         const double* __restrict__ g_qtab,
+                                                         const double* __restrict__ lg, QParams P,
+                                                         uint8_t* __restrict__ code, double* __restrict__ hom,
+                                                         double* __restrict__ het)
+{
+    __shared__ double T[4 * 256];
+    __shared__ uint8_t cls[256];
+    for (uint32_t i = threadIdx.x; i < 4 * 256; i += blockDim.x) T[i] = g_qtab[i];
+    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    __syncthreads();
+    const sid_dd LN2_LD = {0.6931471805599453, 2.3201926491189795e-17};   // x87 logl(2), exactly
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t w = counts[i];
+        uint32_t f, s2, nf, ns, cov;
+        sid_major(w, f, s2, nf, ns, cov);   // getMajorAlleleIndices (same std::sort)
+        Reader R{text, len};
+        // tokens 4, 5, 6 (the line parsed with 7 fields)
+        uint64_t tb[7], te[7];
+        {
+            uint64_t q = starts[i];
+            for (int t = 0; t < 7; ++t) {
+                while (is_sep(R.at(q))) ++q;
+                tb[t] = q;
+                uint32_t c;
+                while ((c = R.at(q)) != ' ' && c != '\t' && c != '\n' && c != 0 && q < len) ++q;
+                te[t] = q;
+            }
+        }
+        const uint32_t ref = R.at(tb[2]);
+        const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
+        const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
+        const uint32_t cdot = cls[up], ccomma = cls[lw];
+        Reader RB{text, len}, RM{text, len};
+        const uint64_t nbq = te[5] - tb[5], nmq = te[6] - tb[6];
+        sid_dd lph = {0.0, 0.0}, lpt = {0.0, 0.0};
+        uint64_t j = 0, skip = 0, num = 0;
+        int ind = 0;
+        bool ovf = false;
+        for (uint64_t q = tb[4]; q < te[4]; ++q) {
+            const uint32_t c = R.at(q);
+            if (ind == 1) {
+                ind = 0;
+                if (c >= '0' && c <= '9') {
+                    ind = 2;
+                    num = c - '0';
+                    ovf = false;
+                    continue;
+                }
+            } else if (ind == 2) {
+                if (c >= '0' && c <= '9') {
+                    const unsigned d = c - '0';
+                    if (!ovf) {
+                        if (num > ((unsigned long long)LONG_MAX - d) / 10) ovf = true;
+                        else num = num * 10 + d;
+                    }
+                    continue;
+                }
+                ind = 0;
+                skip = ovf ? (uint64_t)LONG_MAX : num;
+            }
+            if (skip) {
+                --skip;
+                continue;
+            }
+            const uint32_t k = c == '.' ? cdot : (c == ',' ? ccomma : cls[c]);
+            if (k >= K_A && k <= K_T) {
+                // parseQualities: uint8_t(c - 33), at least 1
+                uint32_t bq = 1, mq = 1;
+                if (j < nbq) {
+                    bq = (RB.at(tb[5] + j) - 33u) & 0xffu;
+                    bq = bq < 1 ? 1 : bq;
+                }
+                if (j < nmq) {
+                    mq = (RM.at(tb[6] + j) - 33u) & 0xffu;
+                    mq = mq < 1 ? 1 : mq;
+                }
+                const uint32_t qv = bq < mq ? bq : mq;
+                const uint32_t b = k - 1;
+                dd_acc(lph, T[(b == f ? 0 : 256) + qv]);
+                dd_acc(lpt, T[(b == f || b == s2 ? 512 : 768) + qv]);
+                ++j;
+            } else if (k == K_CARET) {
+                skip = 1;
+            } else if (k == K_INDEL) {
+                ind = 1;
+            }
+        }
+        lph = dd_norm(lph.hi, lph.lo);
+        // log_probability_heterozygous += logbinom(n, k) - n * logl(2)
+        const uint32_t nn = nf + ns, kk = ns;
+        const double lb = lg[nn + 1] - lg[nn - kk + 1] - lg[kk + 1];
+        sid_dd t = dd_add(sid_dd{lb, 0.0}, dd_neg(dd_mul_d(LN2_LD, (double)nn)));
+        lpt = dd_add(dd_norm(lpt.hi, lpt.lo), t);
+        double p1, p2;
+        if (!P.prior_ld && lph.hi >= SID_FAST_FLOOR && lpt.hi >= SID_FAST_FLOOR) {
+            // pp = expl(lp) (* prior) are normal long doubles: the LRTs from
+            // the log difference, in double-double
+            sid_dd a = lph, b = lpt;
+            if (P.prior_on) {
+                a = dd_add(a, P.lp1);
+                b = dd_add(b, P.lp2);
+            }
+            const sid_dd dd = dd_add(a, dd_neg(b));
+            const double d = dd.hi + dd.lo;
+            p1 = sid_chisq_Q(d > 0.0 ? 2.0 * d : 0.0, P.lg15);    // LRT(pp2, pp1)
+            p2 = sid_chisq_Q(d < 0.0 ? -2.0 * d : 0.0, P.lg15);   // LRT(pp1, pp2)
+        } else {
+            sid_ld l1 = ld_round(sid_ld{lph.hi, 0}), l2 = ld_round(sid_ld{lpt.hi, 0});
+            if (P.prior_on) {
+                l1 = ld_mul(l1, ld_from_double(1 - P.prior));
+                l2 = ld_mul(l2, ld_from_double(P.prior));
+            }
+            p1 = ld_lrt(l2, l1, P.lg15);
+            p2 = ld_lrt(l1, l2, P.lg15);
+        }
+        const bool hz = p2 < P.sig;   // call.cpp:362
+        code[i] = (uint8_t)(f | ((hz ? s2 : f) << 2) | (hz ? 0x80u : 0u));
+        hom[i] = p1;
+        het[i] = p2;
+    }
+}
+
+__global__ __launch_bounds__(TB) void sid_max_major_kernel(const uint64_t* __restrict__ counts, uint64_t n,
+                                                           uint32_t* __restrict__ mx)
+{
+    uint32_t m = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t f, s, nf, ns, cov;
+        sid_major(counts[i], f, s, nf, ns, cov);
+        m = max(m, nf + ns);
+    }
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_down((int)m, off, 64));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
+}
+
 // host build of the device formatter over an array (tests)
 __global__ __launch_bounds__(TB) void sid_fmt_g6_kernel(const double* __restrict__ v, size_t n, char* __restrict__ out)
 {
@@ -537,6 +710,7 @@ static double wall()
 
 struct sid_dtext {
     int device = 0;
+    int quality = 0;               // parsed for -m quality (7 fields required)
     char* d_text = nullptr;
     uint64_t len = 0;
     uint64_t* d_starts = nullptr;
@@ -569,10 +743,11 @@ extern "C" int sid_dtext_free(sid_dtext* t)
 extern "C" size_t sid_dtext_count(const sid_dtext* t) { return t ? t->nsites : 0; }
 extern "C" const uint16_t* sid_dtext_counts(const sid_dtext* t) { return t ? (const uint16_t*)t->d_counts : nullptr; }
 
-static sid_dtext* dtext_alloc(int dev, uint64_t len, int* rc)
+static sid_dtext* dtext_alloc(const sid_ctx* ctx, uint64_t len, int* rc)
 {
     sid_dtext* T = new sid_dtext();
-    T->device = dev;
+    T->device = ctx->device;
+    T->quality = ctx->opts.method == SID_METHOD_QUALITY;
     T->len = len;
     hipError_t e;
     // padded: 16-B window reads past the end stay inside the allocation
@@ -613,15 +788,17 @@ static int dtext_index_parse(sid_dtext* T, hipStream_t st, uint64_t* err_offset)
         return sid_set_hip_error(e);
     sid_lines_emit_kernel<<<(unsigned)tiles, TB, 0, st>>>(T->d_text, 0, 0, len, T->d_toff, T->d_starts);
     const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((total + TB - 1) / TB, 1), 16384);
-    sid_parse_kernel<<<pg, TB, 0, st>>>(T->d_text, len, T->d_starts, T->d_state + 1, T->d_counts, T->d_err);
+    sid_parse_kernel<<<pg, TB, 0, st>>>(T->d_text, len, T->d_starts, T->d_state + 1, T->d_counts, T->d_err,
+                                        T->quality);
     if ((e = hipGetLastError()) != hipSuccess) return sid_set_hip_error(e);
     unsigned long long ek = ~0ull;
     if ((e = hipMemcpyAsync(&ek, T->d_err, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return sid_set_hip_error(e);
     if (ek != ~0ull) {
-        if (err_offset) *err_offset = ek >> 2;
-        return (ek & 3) == 1 ? SID_EMALFORMED : SID_ENULLCHROM;
+        if (err_offset) *err_offset = ek >> 3;
+        const unsigned kind = (unsigned)(ek & 7);
+        return kind == 1 ? SID_EMALFORMED : kind == 2 ? SID_ENULLCHROM : kind == 3 ? SID_EMISSING_MQ : SID_ENOBQ;
     }
     return SID_OK;
 }
@@ -635,7 +812,7 @@ extern "C" int sid_dtext_parse(sid_ctx* ctx, const char* text, size_t len, size_
     TCHECK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
     int rc;
-    sid_dtext* T = dtext_alloc(ctx->device, len, &rc);
+    sid_dtext* T = dtext_alloc(ctx, len, &rc);
     if (!T) return rc;
     // the padding first, then the text in `chunk`-sized copies.  (Measured on
     // a page-cache file mapping: one stream from a populated mapping beats
@@ -675,7 +852,7 @@ extern "C" int sid_dtext_parse_fd(sid_ctx* ctx, int fd, uint64_t offset, uint64_
     TCHECK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
     int rc;
-    sid_dtext* T = dtext_alloc(ctx->device, len, &rc);
+    sid_dtext* T = dtext_alloc(ctx, len, &rc);
     if (!T) return rc;
     const int R = std::max(1, std::min(threads > 0 ? threads : 8, SID_STAGE_N));
     const size_t B = SID_STAGE_BYTES;
@@ -893,6 +1070,72 @@ extern "C" int sid_format_g6_device(sid_ctx* ctx, const double* d_v, size_t n, c
     if (n == 0) return SID_OK;
     TCHECK(hipSetDevice(ctx->device));
     sid_fmt_g6_kernel<<<(unsigned)((n + TB - 1) / TB), TB, 0, (hipStream_t)stream>>>(d_v, n, d_out);
+    TCHECK(hipGetLastError());
+    return SID_OK;
+}
+
+// call.cpp:291-372 over a shard parsed with the context's method = quality.
+// Host tables: the four per-quality terms (glibc pow/log through volatile
+// pointers, so no compiler rewrite of pow(10, x)) and log_gamma up to the
+// largest n = count[ref0] + count[ref1] of the shard.
+extern "C" int sid_call_quality(sid_ctx* ctx, const sid_dtext* T, uint8_t* code, double* hom_conf,
+                                double* het_conf, void* stream)
+{
+    if (!ctx || !T) return SID_EINVAL;
+    if (!T->quality || ctx->opts.method != SID_METHOD_QUALITY) return SID_ESTATE;
+    const uint64_t n = T->nsites;
+    if (n == 0) return SID_OK;
+    if (!code || !hom_conf || !het_conf) return SID_EINVAL;
+    TCHECK(hipSetDevice(T->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (!ctx->d_qtab) {
+        double (*volatile powp)(double, double) = pow;
+        double (*volatile logp)(double) = log;
+        std::vector<double> q(4 * 256);
+        for (int v = 0; v < 256; ++v) {
+            const double error = powp(10., v / -10.);            // call.cpp:329
+            q[v] = logp(1 - error);                              // :331
+            q[256 + v] = logp(error);                            // :333
+            q[512 + v] = logp(1 - 2. / 3. * error);              // :336
+            q[768 + v] = logp(2. / 3. * error);                  // :338
+        }
+        TCHECK(hipMalloc(&ctx->d_qtab, q.size() * 8));
+        TCHECK(hipMemcpy(ctx->d_qtab, q.data(), q.size() * 8, hipMemcpyHostToDevice));
+    }
+    if (!ctx->d_scratch) TCHECK(hipMalloc(&ctx->d_scratch, 16));
+    TCHECK(hipMemsetAsync(ctx->d_scratch, 0, 4, st));
+    sid_max_major_kernel<<<(unsigned)std::min<uint64_t>((n + TB - 1) / TB, 2048), TB, 0, st>>>(T->d_counts, n,
+                                                                                             ctx->d_scratch);
+    uint32_t mx = 0;
+    TCHECK(hipMemcpyAsync(&mx, ctx->d_scratch, 4, hipMemcpyDeviceToHost, st));
+    TCHECK(hipStreamSynchronize(st));
+    const size_t need = (size_t)mx + 2;
+    if (need > ctx->lg_n) {   // lynch.hpp:11-31 MemoizedLogGamma (x == 0 -> 0)
+        const size_t m = std::max<size_t>(need, 1024);
+        std::vector<double> lg(m);
+        for (size_t x = 0; x < m; ++x) lg[x] = x == 0 ? 0.0 : sid_gsl_lngamma((double)x);
+        if (ctx->d_lg) (void)hipFree(ctx->d_lg);
+        ctx->d_lg = nullptr;
+        ctx->lg_n = 0;
+        TCHECK(hipMalloc(&ctx->d_lg, m * 8));
+        TCHECK(hipMemcpy(ctx->d_lg, lg.data(), m * 8, hipMemcpyHostToDevice));
+        ctx->lg_n = m;
+    }
+    QParams P{};
+    P.sig = ctx->opts.significance_level;
+    P.prior = ctx->opts.snp_prior;
+    P.prior_on = P.prior > 0;
+    P.prior_ld = P.prior_on && P.prior >= 1;
+    if (P.prior_on && !P.prior_ld) {
+        // pp1 *= (1 - snp_prior): the factor is the double 1 - prior (call.cpp:354-357)
+        const long double a = logl((long double)(1.0 - P.prior)), b = logl((long double)P.prior);
+        P.lp1 = {(double)a, (double)(a - (long double)(double)a)};
+        P.lp2 = {(double)b, (double)(b - (long double)(double)b)};
+    }
+    P.lg15 = ctx->K.lg15;
+    const unsigned grid = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, 16384);
+    sid_quality_kernel<<<grid, TB, 0, st>>>(T->d_text, T->len, T->d_starts, T->d_counts, n, ctx->d_qtab, ctx->d_lg,
+                                            P, code, hom_conf, het_conf);
     TCHECK(hipGetLastError());
     return SID_OK;
 }

@@ -141,3 +141,43 @@ def test_survey_observed_outputs(oracle, tmp_path):
     assert out[0] == "chrom,pos,label,gt,hom_conf,het_conf,conf_type"
     got = {l.split(",")[1]: ",".join(l.split(",")[2:6]) for l in out[1:]}
     assert got == want
+
+
+def test_bases_vector_kat(oracle):
+    # test/test-pileup_parser.cpp:23-35: parseReadBases("AgACgt", 'N').bases
+    assert oracle.read_bases_seq(b"AgACgt", b"N") == b"AGACGT"
+    # '.'/',' map to the reference; '^' skips the mapping quality; indels skip
+    assert oracle.read_bases_seq(b".,^]A$+2CCg-1at", b"c") == b"CCAGT"
+
+
+def test_quality_line_fields_kat(oracle):
+    # test/test-pileup_parser.cpp:37-56: the 7-field line parses (quality mode)
+    text = b"chr19\t1337\tA\t6\tAgACgt\t++5D5\tDD55D\n"
+    rc, code, hom, het = oracle.call_quality(text)
+    assert rc == 0 and len(code) == 1
+    # 6 fields: missing mapping qualities; 5 fields: the reference dereferences NULL
+    assert oracle.call_quality(b"chr19\t1337\tA\t6\tAgACgt\t++5D5\n")[0] == 2
+    assert oracle.call_quality(b"chr19\t1337\tA\t6\tAgACgt\n")[0] == 4
+    assert oracle.call_quality(b"chr19\t1337\tAC\t6\tAgACgt\t++5D5\n")[0] == 1
+
+
+def test_quality_site_by_hand(oracle):
+    """call.cpp:311-369 for one site, recomputed with numpy long double."""
+    import numpy as np
+    from scipy.special import chdtrc
+    text = b"c1\t5\tA\t4\tAAAC\tIIII\t5555\n"   # bq 40, mq 20 -> q = 20, e = 0.01
+    rc, code, hom, het = oracle.call_quality(text)
+    e = 10 ** (20 / -10.)
+    lph = np.longdouble(0)
+    lpt = np.longdouble(0)
+    for b in b"AAAC":
+        lph += np.log(1 - e) if b == ord("A") else np.log(e)
+        lpt += np.log(1 - 2. / 3. * e)
+    n, k = 4, 1
+    lb = oracle.lngamma(5) - oracle.lngamma(4) - oracle.lngamma(2)
+    lpt += np.longdouble(lb) - n * np.log(np.longdouble(2))
+    # here the het model wins: p_hom = LRT(pp2, pp1) = 1, p_het = Q(2 (lpt - lph))
+    assert lpt > lph and hom[0] == 1.0
+    p = chdtrc(1, float(2 * (lpt - lph)))
+    assert abs(het[0] - p) < 1e-12 * p
+    assert code[0] == (0 | (1 << 2) | 0x80) if p < 0.05 else code[0] == 0
