@@ -13,7 +13,7 @@
 //   sid_parse_kernel         one lane per line: parsePileupLine +
 //                            parseReadBases (pileup.cpp:13-153) into
 //                            profile_t counts; the first malformed line in
-//                            file order is kept as min(offset*4 + status)
+//                            file order is kept as min(offset*8 + kind)
 //
 // and for output, per piece of sites:
 //
