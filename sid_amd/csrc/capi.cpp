@@ -112,7 +112,7 @@ extern "C" int sid_device_count(int* n)
 static hipError_t sid_build_table(sid_ctx* c)
 {
     if (c->K.general) return hipSuccess;
-    hipError_t e = sid_launch_local_table_build(&c->K, c->d_lnt, c->ws.table, nullptr);
+    hipError_t e = sid_launch_local_table_build(&c->K, c->d_lnt, c->ws.table, c->ws.table2, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     return e;
 }
@@ -133,6 +133,7 @@ extern "C" int sid_create(int device, const sid_opts* opts, sid_ctx** out)
     if (const char* g = std::getenv("SID_LOCAL_DIRECT")) c->ws.direct = std::atoi(g) != 0;
     if (const char* g = std::getenv("SID_TABLE_UNROLL")) c->ws.unroll = std::atoi(g);
     if (const char* g = std::getenv("SID_TABLE_NT")) c->ws.nt = std::atoi(g) != 0;
+    if (const char* g = std::getenv("SID_TABLE_TAIL")) c->ws.tail = std::atoi(g) != 0;
 
     std::vector<double> lnt(SID_LUTN);
     lnt[0] = -INFINITY;
@@ -142,6 +143,7 @@ extern "C" int sid_create(int device, const sid_opts* opts, sid_ctx** out)
     e = hipMalloc(&c->d_lnt, SID_LUTN * sizeof(double));
     if (e == hipSuccess) e = hipMemcpy(c->d_lnt, lnt.data(), SID_LUTN * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&c->ws.table, tab * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&c->ws.table2, 65536 * sizeof(double));   // SID_TAB2_N (local.hip)
     if (e == hipSuccess) e = hipMalloc(&c->ws.miss, (size_t)c->ws.cap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&c->ws.ctr, 2 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c->ws.ctr, 0, 2 * sizeof(uint32_t));
@@ -162,6 +164,7 @@ extern "C" int sid_destroy(sid_ctx* c)
     if (c->d_lnt) (void)hipFree(c->d_lnt);
     if (c->d_cdf) (void)hipFree(c->d_cdf);
     if (c->ws.table) (void)hipFree(c->ws.table);
+    if (c->ws.table2) (void)hipFree(c->ws.table2);
     if (c->ws.miss) (void)hipFree(c->ws.miss);
     if (c->ws.ctr) (void)hipFree(c->ws.ctr);
     if (c->lynch) sid_lynch_dev_destroy(c->lynch);

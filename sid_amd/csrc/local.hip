@@ -182,12 +182,23 @@ __global__ __launch_bounds__(256) void sid_local_kernel_x1(const uint64_t* __res
 #define SID_TAB_NR 4
 #define SID_TAB_N (SID_TAB_NF * SID_TAB_NS * SID_TAB_NR)
 
+// Second-level table for the fix-up (L2-resident, 512 KiB): the 30x het sites
+// the LDS table leaves out (ns >= 8) have nf, ns < 64 and few other reads.
+#define SID_TAB2_NF 128
+#define SID_TAB2_NS 64
+#define SID_TAB2_NR 8
+#define SID_TAB2_N (SID_TAB2_NF * SID_TAB2_NS * SID_TAB2_NR)
+
+// Table entry for (nf, ns, r2): v >= +0 -> p1 = v, p2 = 1; v <= -0 -> p1 = 1,
+// p2 = -v; NaN -> both 0 (NaN-free: the reference's 0/0 never reaches here);
+// +inf -> not covered (the site needs the fast or emulated path).
 __global__ __launch_bounds__(256) void sid_local_table_build(sid_local_k K, const double* __restrict__ lnt,
-                                                            double* __restrict__ table)
+                                                            double* __restrict__ table, uint32_t NF, uint32_t NS,
+                                                            uint32_t NR)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= SID_TAB_N) return;
-    const uint32_t r2 = i % SID_TAB_NR, ns = (i / SID_TAB_NR) % SID_TAB_NS, nf = i / (SID_TAB_NR * SID_TAB_NS);
+    if (i >= NF * NS * NR) return;
+    const uint32_t r2 = i % NR, ns = (i / NR) % NS, nf = i / (NR * NS);
     double v = __builtin_inf();
     double p1, p2;
     bool gt;
@@ -200,19 +211,11 @@ __global__ __launch_bounds__(256) void sid_local_table_build(sid_local_k K, cons
     table[i] = v;
 }
 
-__device__ __forceinline__ uint32_t table_site(uint64_t w, const double* __restrict__ T, double sig,
-                                               double& p1, double& p2)
+// outputs of a site from its table value v (not +inf); returns the code
+__device__ __forceinline__ uint32_t table_decode(double v, uint32_t f, uint32_t s, double sig, double& p1,
+                                                 double& p2)
 {
-    uint32_t f, s, nf, ns, cov;
-    sid_major(w, f, s, nf, ns, cov);
-    const uint32_t r2 = cov - nf - ns;
-    double v = __builtin_inf();
-    if (nf < SID_TAB_NF && ns < SID_TAB_NS && r2 < SID_TAB_NR) v = T[(nf * SID_TAB_NS + ns) * SID_TAB_NR + r2];
     bool het = false;
-    if (isinf(v)) {
-        p1 = p2 = 0.0;
-        return 0xFFu;   // miss marker (not a valid code: bits 4-5 are never set)
-    }
     if (isnan(v)) {
         p1 = p2 = 0.0;
     } else if (signbit(v)) {
@@ -224,6 +227,21 @@ __device__ __forceinline__ uint32_t table_site(uint64_t w, const double* __restr
         p2 = 1.0;
     }
     return f | ((het ? s : f) << 2) | (het ? 0x80u : 0u);
+}
+
+__device__ __forceinline__ uint32_t table_site(uint64_t w, const double* __restrict__ T, double sig,
+                                               double& p1, double& p2)
+{
+    uint32_t f, s, nf, ns, cov;
+    sid_major(w, f, s, nf, ns, cov);
+    const uint32_t r2 = cov - nf - ns;
+    double v = __builtin_inf();
+    if (nf < SID_TAB_NF && ns < SID_TAB_NS && r2 < SID_TAB_NR) v = T[(nf * SID_TAB_NS + ns) * SID_TAB_NR + r2];
+    if (isinf(v)) {
+        p1 = p2 = 0.0;
+        return 0xFFu;   // miss marker (not a valid code: bits 4-5 are never set)
+    }
+    return table_decode(v, f, s, sig, p1, p2);
 }
 
 // Sites are processed in pairs (one 16-B profile_t load per lane), U pairs
@@ -247,6 +265,7 @@ __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __r
                                                            uint16_t* __restrict__ code2, sid_dvec2* __restrict__ hom,
                                                            sid_dvec2* __restrict__ het,
                                                            const double* __restrict__ g_table, double sig,
+                                                           const double* __restrict__ T2,
                                                            uint32_t* __restrict__ miss, uint32_t cap,
                                                            uint32_t* __restrict__ ctr)
 {
@@ -294,9 +313,35 @@ __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __r
             }
         }
     }
-    __syncthreads();
+    __syncthreads();   // orders the pair stores before the tail's site stores
     const uint32_t nl = lcnt < SID_LMISS ? lcnt : SID_LMISS;
     if (nl == 0) return;
+    if (T2) {
+        // the block's own misses through the L2-resident second-level table
+        // (the 30x het sites); only what it does not cover goes to the fix-up
+        const uint64_t* counts = (const uint64_t*)pairs;
+        uint8_t* code = (uint8_t*)code2;
+        double* homd = (double*)hom;
+        double* hetd = (double*)het;
+        for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) {
+            const uint32_t idx = lmiss[i];
+            uint32_t f, s, nf, ns, cov;
+            sid_major(counts[idx], f, s, nf, ns, cov);
+            const uint32_t r2 = cov - nf - ns;
+            double v = __builtin_inf();
+            if (nf < SID_TAB2_NF && ns < SID_TAB2_NS && r2 < SID_TAB2_NR) v = T2[(nf * SID_TAB2_NS + ns) * SID_TAB2_NR + r2];
+            if (!isinf(v)) {
+                double h, t;
+                code[idx] = (uint8_t)table_decode(v, f, s, sig, h, t);
+                homd[idx] = h;
+                hetd[idx] = t;
+            } else {
+                const uint32_t g = atomicAdd(ctr, 1u);
+                if (g < cap) miss[g] = idx;
+            }
+        }
+        return;
+    }
     if (threadIdx.x == 0) gbase = atomicAdd(ctr, nl);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
@@ -330,10 +375,29 @@ __global__ __launch_bounds__(1024) void sid_local_table_x1(const uint64_t* __res
 // Sites the table does not cover: the miss list (or, if it overflowed, a
 // scan for the 0xFF marker).  Resets the other parity's counter for the next
 // call on this stream.
+// the fix-up of one missed site: the second-level table, else the fast /
+// emulated evaluation
+__device__ __forceinline__ uint32_t fixup_site(uint64_t w, const double* __restrict__ T2, const sid_local_k& K,
+                                               const double* __restrict__ lnt, double& h, double& t)
+{
+    uint32_t f, s, nf, ns, cov;
+    sid_major(w, f, s, nf, ns, cov);
+    const uint32_t r2 = cov - nf - ns;
+    if (T2 && nf < SID_TAB2_NF && ns < SID_TAB2_NS && r2 < SID_TAB2_NR) {
+        const double v = T2[(nf * SID_TAB2_NS + ns) * SID_TAB2_NR + r2];
+        if (!isinf(v)) return table_decode(v, f, s, K.sig, h, t);
+    }
+    return local_site<false>(w, K, lnt, h, t);
+}
+
+// Sites the table does not cover: the miss list (or, if it overflowed, a
+// scan for the 0xFF marker).  Resets the other parity's counter for the next
+// call on this stream.
 __global__ __launch_bounds__(256) void sid_local_fixup(const uint64_t* __restrict__ counts, size_t n,
                                                        uint8_t* __restrict__ code, double* __restrict__ hom,
                                                        double* __restrict__ het, sid_local_k K,
                                                        const double* __restrict__ lnt,
+                                                       const double* __restrict__ T2,
                                                        const uint32_t* __restrict__ miss, uint32_t cap,
                                                        uint32_t* __restrict__ ctr, int parity)
 {
@@ -345,7 +409,7 @@ __global__ __launch_bounds__(256) void sid_local_fixup(const uint64_t* __restric
         for (size_t j = t0; j < m; j += stride) {
             const uint32_t i = miss[j];
             double h, t;
-            code[i] = (uint8_t)local_site<false>(counts[i], K, lnt, h, t);
+            code[i] = (uint8_t)fixup_site(counts[i], T2, K, lnt, h, t);
             hom[i] = h;
             het[i] = t;
         }
@@ -353,7 +417,7 @@ __global__ __launch_bounds__(256) void sid_local_fixup(const uint64_t* __restric
         for (size_t i = t0; i < n; i += stride) {
             if (code[i] != 0xFFu) continue;
             double h, t;
-            code[i] = (uint8_t)local_site<false>(counts[i], K, lnt, h, t);
+            code[i] = (uint8_t)fixup_site(counts[i], T2, K, lnt, h, t);
             hom[i] = h;
             het[i] = t;
         }
@@ -368,9 +432,13 @@ __global__ __launch_bounds__(256) void sid_local_fixup(const uint64_t* __restric
 // arrays allow 16-B accesses, x1 otherwise) + fix-up kernel.  General option
 // sets (E < 0, prior > 1): the direct kernels with the emulated path.
 extern "C" hipError_t sid_launch_local_table_build(const sid_local_k* K, const double* d_lnt, double* d_table,
-                                                   hipStream_t stream)
+                                                   double* d_table2, hipStream_t stream)
 {
-    sid_local_table_build<<<SID_TAB_N / 256, 256, 0, stream>>>(*K, d_lnt, d_table);
+    sid_local_table_build<<<SID_TAB_N / 256, 256, 0, stream>>>(*K, d_lnt, d_table, SID_TAB_NF, SID_TAB_NS,
+                                                               SID_TAB_NR);
+    if (d_table2)
+        sid_local_table_build<<<SID_TAB2_N / 256, 256, 0, stream>>>(*K, d_lnt, d_table2, SID_TAB2_NF, SID_TAB2_NS,
+                                                                    SID_TAB2_NR);
     return hipGetLastError();
 }
 
@@ -398,12 +466,13 @@ extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t
             auto* C2 = (uint16_t*)code;
             auto* H = (sid_dvec2*)hom;
             auto* Q = (sid_dvec2*)het;
-            if (U == 1 && !ws->nt) sid_local_table_p2<1, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
-            else if (U == 1) sid_local_table_p2<1, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
-            else if (U == 4 && !ws->nt) sid_local_table_p2<4, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
-            else if (U == 4) sid_local_table_p2<4, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
-            else if (!ws->nt) sid_local_table_p2<2, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
-            else sid_local_table_p2<2, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, ws->miss, cap, ctr);
+            const double* T2 = ws->tail ? ws->table2 : nullptr;
+            if (U == 1 && !ws->nt) sid_local_table_p2<1, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
+            else if (U == 1) sid_local_table_p2<1, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
+            else if (U == 4 && !ws->nt) sid_local_table_p2<4, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
+            else if (U == 4) sid_local_table_p2<4, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
+            else if (!ws->nt) sid_local_table_p2<2, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
+            else sid_local_table_p2<2, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
             done = npairs * 2;
         }
         if (done < n) {
@@ -416,7 +485,7 @@ extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t
                                                         ws->miss, cap, ctr, done);
         }
         if (ws->ev_mid) (void)hipEventRecord(ws->ev_mid, stream);   // measurement: main | fix-up
-        sid_local_fixup<<<256, 256, 0, stream>>>((const uint64_t*)counts, n, code, hom, het, *K, d_lnt,
+        sid_local_fixup<<<256, 256, 0, stream>>>((const uint64_t*)counts, n, code, hom, het, *K, d_lnt, ws->table2,
                                                  ws->miss, cap, ws->ctr, ws->parity);
         return hipGetLastError();
     }

@@ -11,7 +11,8 @@
 
 // -m local workspace (class table + miss list), one per context
 struct sid_local_ws {
-    double* table = nullptr;     // SID_TAB_N entries (local.hip)
+    double* table = nullptr;     // SID_TAB_N entries (local.hip), copied to LDS
+    double* table2 = nullptr;    // SID_TAB2_N entries, the fix-up's L2-resident table
     uint32_t* miss = nullptr;    // miss list
     uint32_t cap = 0;            // miss list capacity
     uint32_t* ctr = nullptr;     // [2] miss counters, alternating per call
@@ -20,6 +21,7 @@ struct sid_local_ws {
     int direct = 0;              // SID_LOCAL_DIRECT=1: bypass the table (A/B)
     int unroll = 2;              // SID_TABLE_UNROLL: pairs per thread per tile (1, 2, 4)
     int nt = 0;                  // SID_TABLE_NT=1: non-temporal output stores
+    int tail = 1;                // SID_TABLE_TAIL=0: leave every miss to the fix-up kernel (A/B)
     hipEvent_t ev_mid = nullptr; // set only while timing: recorded between main and fix-up
 };
 
@@ -33,7 +35,7 @@ extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t
                                        const double* d_lnt, const sid_local_ws* ws, int grid_cap,
                                        hipStream_t stream);
 extern "C" hipError_t sid_launch_local_table_build(const sid_local_k* K, const double* d_lnt,
-                                                   double* d_table, hipStream_t stream);
+                                                   double* d_table, double* d_table2, hipStream_t stream);
 extern "C" hipError_t sid_launch_synth(uint64_t seed, uint64_t first, size_t n,
                                        const uint64_t* d_cdf, uint32_t kmax, uint16_t* counts,
                                        hipStream_t stream);
