@@ -16,6 +16,7 @@
 //                        (call.cpp:129-140) through a compact,
 //                        L2/MALL-resident hash of the U profiles.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include "sid_math.h"
 
@@ -441,16 +442,40 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
         last = atomicAdd(&ticket[pt], 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    if (!last || threadIdx.x != 0) return;
+    if (!last) return;
     __threadfence();
-    double H = 0.0, Lo = 0.0;
-    for (unsigned b = 0; b < gridDim.x; ++b) {
-        const double bh = ((volatile double*)part)[2 * b];
-        const double bl = ((volatile double*)part)[2 * b + 1];
+    // the block partials, one per thread (in parallel: a serial walk of
+    // volatile loads cost most of the kernel), reduced by a fixed tree
+    double bh = 0.0, bl = 0.0;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+        const double x = ((volatile double*)part)[2 * b];
+        const double y = ((volatile double*)part)[2 * b + 1];
         double s, e;
-        sid_two_sum(H, bh, s, e);
+        sid_two_sum(bh, x, s, e);
+        bh = s;
+        bl += y + e;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ohi = __shfl_down(bh, off, 64);
+        const double olo = __shfl_down(bl, off, 64);
+        double s, e;
+        sid_two_sum(bh, ohi, s, e);
+        bh = s;
+        bl += olo + e;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        sh_hi[wid] = bh;
+        sh_lo[wid] = bl;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double H = 0.0, Lo = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        double s, e;
+        sid_two_sum(H, sh_hi[w], s, e);
         H = s;
-        Lo += bl + e;
+        Lo += sh_lo[w] + e;
     }
     ticket[pt] = 0;   // ready for the next launch (stream-ordered)
     double s, e;
@@ -718,6 +743,67 @@ __global__ __launch_bounds__(256) void sid_pack_class_kernel(const double* __res
         cc[i] = sid_dvec2{p1[i], p2[i]};
 }
 
+// ------------------------------------------------ Benjamini-Hochberg ------
+// stats.cpp:58-80 on the device: p sorted descending (radix sort, with the
+// original indices), adj[0] = p[0], adj[i] = min(adj[i-1], p[i] * m / (m - i)),
+// capped at 1, scattered back.  The tie order is irrelevant (equal p get equal
+// adj), so any sort gives the reference's values.  NaN or -0 p-values (their
+// order or sign could differ from std::sort's) flag `odd`; the host then
+// takes its own BH.
+__global__ __launch_bounds__(256) void sid_bh_check_kernel(const double* __restrict__ p, size_t m,
+                                                           uint32_t* __restrict__ idx, int* __restrict__ odd)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x) {
+        idx[i] = (uint32_t)i;
+        const double v = p[i];
+        if (isnan(v) || (v == 0.0 && signbit(v))) atomicExch(odd, 1);
+    }
+}
+
+#define SID_BH_TB 1024
+__global__ __launch_bounds__(SID_BH_TB) void sid_bh_scan_kernel(const double* __restrict__ ps,
+                                                                const uint32_t* __restrict__ is, size_t m,
+                                                                double* __restrict__ adj)
+{
+    __shared__ double part[SID_BH_TB];
+    const size_t per = (m + SID_BH_TB - 1) / SID_BH_TB;
+    const size_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
+    const double dm = (double)m;
+    double mn = __builtin_inf();
+    for (size_t i = lo; i < hi; ++i) {
+        const double v = i == 0 ? ps[0] : ps[i] * dm / (double)(m - i);   // stats.cpp:74-76
+        mn = fmin(mn, v);
+    }
+    part[threadIdx.x] = mn;
+    __syncthreads();
+    if (threadIdx.x == 0) {   // exclusive min-scan of the 1024 chunk minima
+        double acc = __builtin_inf();
+        for (int t = 0; t < SID_BH_TB; ++t) {
+            const double v = part[t];
+            part[t] = acc;
+            acc = fmin(acc, v);
+        }
+    }
+    __syncthreads();
+    double acc = part[threadIdx.x];
+    for (size_t i = lo; i < hi; ++i) {
+        const double v = i == 0 ? ps[0] : ps[i] * dm / (double)(m - i);
+        acc = fmin(acc, v);
+        adj[is[i]] = acc > 1 ? 1.0 : acc;   // stats.cpp:77-79
+    }
+}
+
+// call.cpp:113-127: the label from the adjusted p_het
+__global__ __launch_bounds__(256) void sid_bh_label_kernel(const double* __restrict__ adj_het, size_t m, double sig,
+                                                           uint8_t* __restrict__ code)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t c = code[i], f = c & 3u, s = (c >> 2) & 3u;
+        const bool het = adj_het[i] < sig;
+        code[i] = (uint8_t)(f | ((het ? s : f) << 2) | (het ? 0x80u : 0u));
+    }
+}
+
 // ------------------------------------------------------------ launchers --
 extern "C" {
 
@@ -783,6 +869,44 @@ hipError_t sid_launch_pack_class(const double* p1, const double* p2, size_t u, d
 }
 
 // record tables of the lookup (after pack_class); rec: SID_REC_N x 16 B, rcode: SID_REC_N B
+// BH of p[0..m) into adj (p untouched); ws: device scratch of sid_bh_ws_bytes(m)
+size_t sid_bh_ws_bytes(size_t m)
+{
+    size_t t = 0;
+    (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, t, (const double*)nullptr, (double*)nullptr,
+                                                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)m);
+    return ((t + 255) & ~(size_t)255) + m * (8 + 4 + 4) + 256;
+}
+
+hipError_t sid_launch_bh(const double* p, size_t m, double* adj, void* ws, size_t ws_bytes, int* odd, hipStream_t st)
+{
+    if (m == 0) return hipSuccess;
+    size_t t = 0;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, t, p, (double*)nullptr, (const uint32_t*)nullptr,
+                                                                (uint32_t*)nullptr, (int)m, 0, 64, st);
+    if (e != hipSuccess) return e;
+    char* w = (char*)ws;
+    const size_t tb = (t + 255) & ~(size_t)255;
+    if (tb + m * 16 > ws_bytes) return hipErrorInvalidValue;
+    double* ps = (double*)(w + tb);
+    uint32_t* idx = (uint32_t*)(w + tb + m * 8);
+    uint32_t* is = (uint32_t*)(w + tb + m * 12);
+    uint64_t g = (m + 255) / 256;
+    sid_bh_check_kernel<<<(unsigned)(g < 1024 ? g : 1024), 256, 0, st>>>(p, m, idx, odd);
+    e = hipcub::DeviceRadixSort::SortPairsDescending(w, t, p, ps, idx, is, (int)m, 0, 64, st);
+    if (e != hipSuccess) return e;
+    sid_bh_scan_kernel<<<1, SID_BH_TB, 0, st>>>(ps, is, m, adj);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_bh_label(const double* adj_het, size_t m, double sig, uint8_t* code, hipStream_t st)
+{
+    if (m == 0) return hipSuccess;
+    uint64_t g = (m + 255) / 256;
+    sid_bh_label_kernel<<<(unsigned)(g < 1024 ? g : 1024), 256, 0, st>>>(adj_het, m, sig, code);
+    return hipGetLastError();
+}
+
 hipError_t sid_launch_rec_build(const uint32_t* dense_cidx, const uint8_t* pcode, const double* cc, double* rec,
                                 uint8_t* rcode, hipStream_t st)
 {

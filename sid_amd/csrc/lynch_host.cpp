@@ -56,6 +56,9 @@ hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned lo
                              double* hom, double* het, int grid_cap, hipStream_t st);
 hipError_t sid_launch_rec_build(const uint32_t* dense_cidx, const uint8_t* pcode, const double* cc, double* rec,
                                 uint8_t* rcode, hipStream_t st);
+size_t sid_bh_ws_bytes(size_t m);
+hipError_t sid_launch_bh(const double* p, size_t m, double* adj, void* ws, size_t ws_bytes, int* odd, hipStream_t st);
+hipError_t sid_launch_bh_label(const double* adj_het, size_t m, double sig, uint8_t* code, hipStream_t st);
 }
 
 static const uint64_t EMPTY = 0xFFFFFFFFFFFFFFFFull;
@@ -134,6 +137,9 @@ struct sid_lynch_dev {
     double* d_cc = nullptr;                // {p1, p2} per class, packed for the gather
     double* d_rec = nullptr;               // {p1, p2} per record code (sid_math.h), SID_REC_N
     uint8_t* d_rcode = nullptr;            // code per record code
+    void* d_bhws = nullptr;                // device BH scratch (radix sort)
+    size_t bhws_bytes = 0;
+    int* d_odd = nullptr;                  // BH saw NaN / -0 p-values: host BH instead
     uint64_t cmask = 0;
     uint32_t special_idx = 0xFFFFFFFFu;
 };
@@ -169,6 +175,9 @@ static void release_buffers(sid_lynch_dev* L)
     dfree(L->d_dense_cidx);
     dfree(L->d_rec);
     dfree(L->d_rcode);
+    dfree(L->d_bhws);
+    dfree(L->d_odd);
+    L->bhws_bytes = 0;
     dfree(L->d_exp);
     L->cap_u = L->cap_c = L->cap_x = 0;
 }
@@ -901,7 +910,32 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     HIPCHECK(sid_launch_classify(L->d_keys, L->d_lhom, L->d_lhet, U, mode,
                                  method == SID_METHOD_LIKELIHOOD_RATIO && c->opts.estimate_prior,
                                  est.heterozygosity, c->K.lg15, L->d_c1, L->d_c2, L->d_pcode, 0));
+    bool host_bh = mode == 0;
     if (mode == 0) {
+        // stats.cpp:58-80 on the device (radix sort + min-scan), adjusted
+        // values into the likelihood arrays (no longer needed), then swapped in
+        const size_t need = sid_bh_ws_bytes(U);
+        if (need > L->bhws_bytes) {
+            dfree(L->d_bhws);
+            L->bhws_bytes = 0;
+            HIPCHECK(hipMalloc(&L->d_bhws, need));
+            L->bhws_bytes = need;
+        }
+        if (!L->d_odd) HIPCHECK(hipMalloc(&L->d_odd, sizeof(int)));
+        HIPCHECK(hipMemsetAsync(L->d_odd, 0, sizeof(int), 0));
+        HIPCHECK(sid_launch_bh(L->d_c1, U, L->d_lhom, L->d_bhws, L->bhws_bytes, L->d_odd, 0));
+        HIPCHECK(sid_launch_bh(L->d_c2, U, L->d_lhet, L->d_bhws, L->bhws_bytes, L->d_odd, 0));
+        int odd = 0;
+        HIPCHECK(hipMemcpyAsync(&odd, L->d_odd, sizeof(int), hipMemcpyDeviceToHost, 0));
+        HIPCHECK(hipStreamSynchronize(0));
+        if (!odd) {
+            HIPCHECK(sid_launch_bh_label(L->d_lhet, U, c->opts.significance_level, L->d_pcode, 0));
+            std::swap(L->d_c1, L->d_lhom);
+            std::swap(L->d_c2, L->d_lhet);
+            host_bh = false;
+        }
+    }
+    if (host_bh) {
         // stats.cpp:58-80 Benjamini-Hochberg over the U p-values, then
         // call.cpp:113-127 labels from the adjusted p_het
         std::vector<double> ph(U), pt(U);
