@@ -318,11 +318,12 @@ __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __r
     if (nl == 0) return;
     if (T2) {
         // the block's own misses through the L2-resident second-level table
-        // (the 30x het sites); only what it does not cover goes to the fix-up
+        // (the 30x het sites); resolved entries are struck from the list
         const uint64_t* counts = (const uint64_t*)pairs;
         uint8_t* code = (uint8_t*)code2;
         double* homd = (double*)hom;
         double* hetd = (double*)het;
+        uint32_t kept = 0;
         for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) {
             const uint32_t idx = lmiss[i];
             uint32_t f, s, nf, ns, cov;
@@ -335,10 +336,35 @@ __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __r
                 code[idx] = (uint8_t)table_decode(v, f, s, sig, h, t);
                 homd[idx] = h;
                 hetd[idx] = t;
+                lmiss[i] = 0xFFFFFFFFu;
             } else {
-                const uint32_t g = atomicAdd(ctr, 1u);
-                if (g < cap) miss[g] = idx;
+                ++kept;
             }
+        }
+        // the rest to the fix-up: one global atomic per block
+        const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        uint32_t x = kept;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        __shared__ uint32_t wsum[32];
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
+        uint32_t wbase = 0, tot = 0;
+        for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
+            if (w < wid) wbase += wsum[w];
+            tot += wsum[w];
+        }
+        if (tot == 0) return;
+        if (threadIdx.x == 0) gbase = atomicAdd(ctr, tot);
+        __syncthreads();
+        uint32_t o = gbase + wbase + x - kept;
+        for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) {
+            const uint32_t idx = lmiss[i];
+            if (idx == 0xFFFFFFFFu) continue;
+            if (o < cap) miss[o] = idx;
+            ++o;
         }
         return;
     }
