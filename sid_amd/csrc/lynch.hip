@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "sid_math.h"
 
 #define SID_EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
@@ -743,6 +745,95 @@ __global__ __launch_bounds__(256) void sid_pack_class_kernel(const double* __res
         cc[i] = sid_dvec2{p1[i], p2[i]};
 }
 
+// ------------------------------------------------ setup on the device -----
+// call.cpp:66-70 + pileup.cpp:198-217 + lynch.hpp:48-55 over the sorted
+// (key, count) table: keep coverage >= 4 (flag + select), count as uint32
+// (UniqueProfile::count), lnM from the host's GSL lnGamma table in the
+// reference's order, and the nucleotide-distribution sums with 32-bit products
+// (integer sums: order-free).  sums: [0..3] per base, [4] total.
+__device__ __forceinline__ uint32_t sid_key_n(uint64_t key, int i) { return (uint32_t)((key >> (48 - 16 * i)) & 0xffff); }
+
+__global__ __launch_bounds__(256) void sid_setup_flag_kernel(const unsigned long long* __restrict__ keys, size_t n,
+                                                             uint8_t* __restrict__ flags, uint32_t* __restrict__ maxcov)
+{
+    uint32_t mx = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        const uint32_t cov = sid_key_n(k, 0) + sid_key_n(k, 1) + sid_key_n(k, 2) + sid_key_n(k, 3);
+        flags[i] = cov >= 4;
+        mx = cov > mx ? cov : mx;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_down((int)mx, off, 64);
+        mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(maxcov, mx);
+}
+
+__global__ __launch_bounds__(256) void sid_setup_gather_kernel(const unsigned long long* __restrict__ keys,
+                                                               const unsigned long long* __restrict__ cnts,
+                                                               const uint32_t* __restrict__ sel,
+                                                               const uint32_t* __restrict__ nsel,
+                                                               const double* __restrict__ lgk,
+                                                               uint64_t* __restrict__ okeys, uint32_t* __restrict__ ocnt,
+                                                               double* __restrict__ olnM,
+                                                               unsigned long long* __restrict__ sums)
+{
+    const uint32_t U = *nsel;
+    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < U; j += gridDim.x * blockDim.x) {
+        const uint32_t i = sel[j];
+        const uint64_t k = keys[i];
+        const uint32_t c = (uint32_t)cnts[i];
+        const uint32_t n0 = sid_key_n(k, 0), n1 = sid_key_n(k, 1), n2 = sid_key_n(k, 2), n3 = sid_key_n(k, 3);
+        const uint32_t cov = n0 + n1 + n2 + n3;
+        okeys[j] = k;
+        ocnt[j] = c;
+        double m = lgk[cov];   // lgk[x] = GSL lngamma(x + 1)
+        m -= lgk[n0];
+        m -= lgk[n1];
+        m -= lgk[n2];
+        m -= lgk[n3];
+        olnM[j] = m;
+        acc[0] += (uint32_t)(c * n0);
+        acc[1] += (uint32_t)(c * n1);
+        acc[2] += (uint32_t)(c * n2);
+        acc[3] += (uint32_t)(c * n3);
+        acc[4] += (uint32_t)(c * cov);
+    }
+    for (int q = 0; q < 5; ++q) {
+        unsigned long long v = acc[q];
+        for (int off = 32; off > 0; off >>= 1) v += (unsigned long long)__shfl_down((long long)v, off, 64);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&sums[q], v);
+    }
+}
+
+// class tables of the lookup: dense code -> class index, and the compact
+// class hash (any insertion order: lookups match whole keys)
+__global__ __launch_bounds__(256) void sid_class_tables_kernel(const uint64_t* __restrict__ keys, uint32_t U,
+                                                               uint32_t* __restrict__ dense_cidx,
+                                                               unsigned long long* __restrict__ ckeys,
+                                                               uint32_t* __restrict__ cidx, uint64_t cmask)
+{
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < U; j += gridDim.x * blockDim.x) {
+        const uint64_t key = keys[j];
+        if (key == SID_EMPTY_KEY) continue;   // the all-65535 profile: special_idx
+        const uint64_t w = (key >> 48) | (((key >> 32) & 0xffff) << 16) | (((key >> 16) & 0xffff) << 32) |
+                           ((key & 0xffff) << 48);
+        const uint32_t d = sid_dense_code(w);
+        if (d != SID_DENSE_NONE) dense_cidx[d] = j;
+        uint64_t h = sid_hash64(key) & cmask;
+        for (uint64_t probe = 0; probe <= cmask; ++probe) {
+            const unsigned long long prev = atomicCAS(&ckeys[h], SID_EMPTY_KEY, (unsigned long long)key);
+            if (prev == SID_EMPTY_KEY) {
+                cidx[h] = j;
+                break;
+            }
+            h = (h + 1) & cmask;
+        }
+    }
+}
+
 // ------------------------------------------------ Benjamini-Hochberg ------
 // stats.cpp:58-80 on the device: p sorted descending (radix sort, with the
 // original indices), adj[0] = p[0], adj[i] = min(adj[i-1], p[i] * m / (m - i)),
@@ -869,6 +960,87 @@ hipError_t sid_launch_pack_class(const double* p1, const double* p2, size_t u, d
 }
 
 // record tables of the lookup (after pack_class); rec: SID_REC_N x 16 B, rcode: SID_REC_N B
+// setup: sort the exported table, select coverage >= 4, gather.  ws: scratch of
+// sid_setup_ws_bytes(n); keys/cnts (n entries) are sorted into skeys/scnts.
+size_t sid_setup_ws_bytes(size_t n)
+{
+    size_t a = 0, b = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                             (const unsigned long long*)nullptr, (unsigned long long*)nullptr, (int)n);
+    (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0), (const uint8_t*)nullptr,
+                                        (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+    return ((std::max(a, b) + 255) & ~(size_t)255) + n * (1 + 4) + 520;
+}
+
+static size_t setup_sel_offset(size_t n)
+{
+    size_t a = 0, b = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                             (const unsigned long long*)nullptr, (unsigned long long*)nullptr, (int)n);
+    (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0), (const uint8_t*)nullptr,
+                                        (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+    const size_t tb = (std::max(a, b) + 255) & ~(size_t)255;
+    return (tb + n + 3) & ~(size_t)3;
+}
+
+// phase 1: sort (unless already sorted), flag coverage >= 4 (and the largest
+// coverage, for the lnGamma table), select the indices; the table stays in
+// skeys/scnts and the selection in ws for phase 2
+hipError_t sid_launch_setup_select(const unsigned long long* keys, const unsigned long long* cnts, size_t n, bool sort,
+                                   unsigned long long* skeys, unsigned long long* scnts, void* ws, size_t ws_bytes,
+                                   uint32_t* nsel, uint32_t* maxcov, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(maxcov, 0, 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(nsel, 0, 4, st);
+    if (e != hipSuccess || n == 0) return e;
+    size_t a = 0, b = 0;
+    e = hipcub::DeviceRadixSort::SortPairs(nullptr, a, keys, skeys, cnts, scnts, (int)n, 0, 64, st);
+    if (e == hipSuccess)
+        e = hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0), (const uint8_t*)nullptr,
+                                          (uint32_t*)nullptr, nsel, (int)n, st);
+    if (e != hipSuccess) return e;
+    char* w = (char*)ws;
+    const size_t tb = (std::max(a, b) + 255) & ~(size_t)255;
+    if (setup_sel_offset(n) + n * 4 > ws_bytes) return hipErrorInvalidValue;
+    uint8_t* flags = (uint8_t*)(w + tb);
+    uint32_t* sel = (uint32_t*)(w + setup_sel_offset(n));
+    if (sort) {
+        e = hipcub::DeviceRadixSort::SortPairs(w, a, keys, skeys, cnts, scnts, (int)n, 0, 64, st);
+        if (e != hipSuccess) return e;
+    }
+    const unsigned long long* k = sort ? skeys : keys;
+    uint64_t g = (n + 255) / 256;
+    sid_setup_flag_kernel<<<(unsigned)(g < 1024 ? g : 1024), 256, 0, st>>>(k, n, flags, maxcov);
+    e = hipcub::DeviceSelect::Flagged(w, b, hipcub::CountingInputIterator<uint32_t>(0), flags, sel, nsel, (int)n, st);
+    if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+// phase 2: gather the selected profiles (lnM from lgk, distribution sums)
+hipError_t sid_launch_setup_gather(const unsigned long long* skeys, const unsigned long long* scnts, size_t n,
+                                   const void* ws, const uint32_t* nsel, const double* lgk, uint64_t* okeys,
+                                   uint32_t* ocnt, double* olnM, unsigned long long* sums, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(sums, 0, 5 * sizeof(unsigned long long), st);
+    if (e != hipSuccess || n == 0) return e;
+    const uint32_t* sel = (const uint32_t*)((const char*)ws + setup_sel_offset(n));
+    uint64_t g = (n + 255) / 256;
+    sid_setup_gather_kernel<<<(unsigned)(g < 1024 ? g : 1024), 256, 0, st>>>(skeys, scnts, sel, nsel, lgk, okeys, ocnt,
+                                                                              olnM, sums);
+    return hipGetLastError();
+}
+
+hipError_t sid_launch_class_tables(const uint64_t* keys, uint32_t U, uint32_t* dense_cidx, unsigned long long* ckeys,
+                                   uint32_t* cidx, uint64_t cmask, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(dense_cidx, 0xFF, SID_DENSE_N * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(ckeys, 0xFF, (cmask + 1) * 8, st);
+    if (e != hipSuccess || U == 0) return e;
+    uint64_t g = (U + 255) / 256;
+    sid_class_tables_kernel<<<(unsigned)(g < 1024 ? g : 1024), 256, 0, st>>>(keys, U, dense_cidx, ckeys, cidx, cmask);
+    return hipGetLastError();
+}
+
 // BH of p[0..m) into adj (p untouched); ws: device scratch of sid_bh_ws_bytes(m)
 size_t sid_bh_ws_bytes(size_t m)
 {

@@ -4,9 +4,10 @@
 // Nelder-Mead driver (GSL 2.7.1 nmsimplex2 restated; GSL is not vendored in the
 // reference), Benjamini-Hochberg, and the compact class hash used by the
 // per-site lookup kernel.  The O(sites) work (histogram, lookup) and the
-// O(U) per-profile arithmetic (objective, likelihoods, LRT/posteriors) run on
-// the GPU; only O(U) bookkeeping (sort, BH step-up) and the 2-parameter
-// simplex stay on the host.
+// O(U) work (table sort and filter, lnM, objective, likelihoods,
+// LRT/posteriors, BH, class tables) run on the GPU; the host drives the
+// 2-parameter simplex, computes the lnGamma table once per context, and
+// takes BH over only when NaN / -0 p-values occur.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -59,19 +60,18 @@ hipError_t sid_launch_rec_build(const uint32_t* dense_cidx, const uint8_t* pcode
 size_t sid_bh_ws_bytes(size_t m);
 hipError_t sid_launch_bh(const double* p, size_t m, double* adj, void* ws, size_t ws_bytes, int* odd, hipStream_t st);
 hipError_t sid_launch_bh_label(const double* adj_het, size_t m, double sig, uint8_t* code, hipStream_t st);
+size_t sid_setup_ws_bytes(size_t n);
+hipError_t sid_launch_setup_select(const unsigned long long* keys, const unsigned long long* cnts, size_t n, bool sort,
+                                   unsigned long long* skeys, unsigned long long* scnts, void* ws, size_t ws_bytes,
+                                   uint32_t* nsel, uint32_t* maxcov, hipStream_t st);
+hipError_t sid_launch_setup_gather(const unsigned long long* skeys, const unsigned long long* scnts, size_t n,
+                                   const void* ws, const uint32_t* nsel, const double* lgk, uint64_t* okeys,
+                                   uint32_t* ocnt, double* olnM, unsigned long long* sums, hipStream_t st);
+hipError_t sid_launch_class_tables(const uint64_t* keys, uint32_t U, uint32_t* dense_cidx, unsigned long long* ckeys,
+                                   uint32_t* cidx, uint64_t cmask, hipStream_t st);
 }
 
 static const uint64_t EMPTY = 0xFFFFFFFFFFFFFFFFull;
-
-static uint64_t host_hash64(uint64_t k)   // == sid_hash64 (lynch.hip)
-{
-    k ^= k >> 33;
-    k *= 0xFF51AFD7ED558CCDull;
-    k ^= k >> 33;
-    k *= 0xC4CEB9FE1A85EC53ull;
-    k ^= k >> 33;
-    return k;
-}
 
 template <class T>
 static void dfree(T*& p)
@@ -99,10 +99,10 @@ struct sid_lynch_dev {
     // explicit (merged) table
     bool loaded = false;
     std::vector<uint64_t> tkeys, tcnt;
-    // filtered profiles (host + device)
+    // filtered profiles (device): U of them, sorted by key
     bool setup = false;
-    std::vector<uint64_t> fkeys;
-    std::vector<uint32_t> fcnt;
+    size_t nU = 0;
+    bool has_special = false;              // the all-65535 profile is the last one
     double dist[4] = {0.25, 0.25, 0.25, 0.25};
     uint64_t* d_keys = nullptr;
     uint32_t* d_cnt = nullptr;
@@ -133,7 +133,13 @@ struct sid_lynch_dev {
     size_t cap_c = 0;                      // class hash
     size_t cap_x = 0;                      // export buffer (keys, counts)
     unsigned long long* d_exp = nullptr;   // [cap_x keys][cap_x counts][1 count]
+    unsigned long long* d_sexp = nullptr;  // sorted table: [cap_x keys][cap_x counts]
+    void* d_setws = nullptr;               // setup scratch (sort, select)
+    size_t setws_bytes = 0;
+    uint32_t* d_setsc = nullptr;           // {nsel, maxcov} + 5 u64 sums (8-aligned at +8)
     std::vector<double> lg;                // lg[k] = GSL lngamma(k + 1), grown on demand
+    double* d_lg = nullptr;                // device copy of lg
+    size_t d_lg_n = 0;
     double* d_cc = nullptr;                // {p1, p2} per class, packed for the gather
     double* d_rec = nullptr;               // {p1, p2} per record code (sid_math.h), SID_REC_N
     uint8_t* d_rcode = nullptr;            // code per record code
@@ -179,6 +185,11 @@ static void release_buffers(sid_lynch_dev* L)
     dfree(L->d_odd);
     L->bhws_bytes = 0;
     dfree(L->d_exp);
+    dfree(L->d_sexp);
+    dfree(L->d_setws);
+    dfree(L->d_setsc);
+    dfree(L->d_lg);
+    L->setws_bytes = L->d_lg_n = 0;
     L->cap_u = L->cap_c = L->cap_x = 0;
 }
 
@@ -327,57 +338,105 @@ extern "C" int sid_profile_accumulate(sid_ctx* c, const uint16_t* counts, size_t
     return SID_OK;
 }
 
-// sorted (key, count) of the accumulated histogram
-static int export_hist(sid_lynch_dev* L, std::vector<uint64_t>& keys, std::vector<uint64_t>& cnt)
+// The current profile table, sorted by key, on the device: *n entries at
+// *keys / *cnts (inside d_sexp or d_exp), with the coverage >= 4 selection
+// (call.cpp:66-70) left in d_setws and {nsel, maxcov} in d_setsc.  The
+// accumulated histogram is compacted (dense codes, then the hash), the
+// all-65535 profile appended (it sorts last), and radix-sorted; a loaded
+// table is uploaded already sorted.  Two host syncs (the compacted count,
+// then nsel/maxcov).
+static int device_table(sid_lynch_dev* L, size_t* n, const unsigned long long** keys,
+                        const unsigned long long** cnts, uint32_t* nsel, uint32_t* maxcov)
 {
-    keys.clear();
-    cnt.clear();
-    if (!L->have_hist) return SID_OK;
-    if (L->acc_stream) HIPCHECK(hipStreamSynchronize(L->acc_stream));
-    const size_t m = L->distinct + SID_DENSE_N;
+    *n = 0;
+    *nsel = *maxcov = 0;
+    size_t m = 1;
+    if (L->loaded) m = std::max<size_t>(L->tkeys.size(), 1);
+    else if (L->have_hist) m = L->distinct + SID_DENSE_N + 1;
     if (m > L->cap_x) {
         dfree(L->d_exp);
+        dfree(L->d_sexp);
         L->cap_x = std::max(m, 2 * L->cap_x);
         HIPCHECK(hipMalloc(&L->d_exp, (2 * L->cap_x + 1) * sizeof(unsigned long long)));
+        HIPCHECK(hipMalloc(&L->d_sexp, 2 * L->cap_x * sizeof(unsigned long long)));
     }
-    unsigned long long *ok = L->d_exp, *oc = L->d_exp + L->cap_x, *nout = L->d_exp + 2 * L->cap_x;
-    HIPCHECK(hipMemsetAsync(nout, 0, sizeof(unsigned long long), 0));
-    HIPCHECK(sid_launch_dense_compact(L->dense, ok, oc, nout, 0));
-    HIPCHECK(sid_launch_compact(L->gkeys, L->gcnt, L->cap, ok, oc, nout, 0));
-    unsigned long long nn = 0, stats[2] = {0, 0};
-    HIPCHECK(hipMemcpyAsync(&nn, nout, sizeof(nn), hipMemcpyDeviceToHost, 0));
-    HIPCHECK(hipMemcpyAsync(stats, L->stats, sizeof(stats), hipMemcpyDeviceToHost, 0));
-    HIPCHECK(hipStreamSynchronize(0));
-    std::vector<uint64_t> k(nn), v(nn);
-    if (nn) {
-        HIPCHECK(hipMemcpyAsync(k.data(), ok, nn * 8, hipMemcpyDeviceToHost, 0));
-        HIPCHECK(hipMemcpyAsync(v.data(), oc, nn * 8, hipMemcpyDeviceToHost, 0));
+    if (!L->d_setsc) HIPCHECK(hipMalloc(&L->d_setsc, 8 + 5 * sizeof(unsigned long long)));
+    unsigned long long *ek = L->d_exp, *ec = L->d_exp + L->cap_x, *nout = L->d_exp + 2 * L->cap_x;
+    unsigned long long *sk = L->d_sexp, *sc = L->d_sexp + L->cap_x;
+    size_t nn = 0;
+    bool sort = true;
+    if (L->loaded) {
+        nn = L->tkeys.size();
+        if (nn) {
+            HIPCHECK(hipMemcpyAsync(sk, L->tkeys.data(), nn * 8, hipMemcpyHostToDevice, 0));
+            HIPCHECK(hipMemcpyAsync(sc, L->tcnt.data(), nn * 8, hipMemcpyHostToDevice, 0));
+        }
+        sort = false;
+        ek = sk;
+        ec = sc;
+    } else if (L->have_hist) {
+        if (L->acc_stream) HIPCHECK(hipStreamSynchronize(L->acc_stream));
+        HIPCHECK(hipMemsetAsync(nout, 0, sizeof(unsigned long long), 0));
+        HIPCHECK(sid_launch_dense_compact(L->dense, ek, ec, nout, 0));
+        HIPCHECK(sid_launch_compact(L->gkeys, L->gcnt, L->cap, ek, ec, nout, 0));
+        unsigned long long hv[3] = {0, 0, 0};   // nout, distinct, special count
+        HIPCHECK(hipMemcpyAsync(&hv[0], nout, 8, hipMemcpyDeviceToHost, 0));
+        HIPCHECK(hipMemcpyAsync(&hv[1], L->stats, 16, hipMemcpyDeviceToHost, 0));
         HIPCHECK(hipStreamSynchronize(0));
+        nn = hv[0];
+        if (hv[2]) {
+            const unsigned long long sp[2] = {EMPTY, hv[2]};
+            HIPCHECK(hipMemcpyAsync(ek + nn, &sp[0], 8, hipMemcpyHostToDevice, 0));
+            HIPCHECK(hipMemcpyAsync(ec + nn, &sp[1], 8, hipMemcpyHostToDevice, 0));
+            ++nn;
+        }
     }
-    std::vector<std::pair<uint64_t, uint64_t>> kv(nn);
-    for (size_t i = 0; i < nn; ++i) kv[i] = {k[i], v[i]};
-    std::sort(kv.begin(), kv.end());   // keys are distinct
-    keys.resize(nn);
-    cnt.resize(nn);
-    for (size_t i = 0; i < nn; ++i) {
-        keys[i] = kv[i].first;
-        cnt[i] = kv[i].second;
+    if (nn == 0) return SID_OK;
+    const size_t need = sid_setup_ws_bytes(nn);
+    if (need > L->setws_bytes) {
+        dfree(L->d_setws);
+        L->setws_bytes = 0;
+        const size_t sz = std::max(need, 2 * L->setws_bytes);
+        L->setws_bytes = 0;
+        HIPCHECK(hipMalloc(&L->d_setws, sz));
+        L->setws_bytes = sz;
     }
-    if (stats[1]) {   // the all-65535 profile sorts last
-        keys.push_back(EMPTY);
-        cnt.push_back(stats[1]);
-    }
+    HIPCHECK(sid_launch_setup_select(ek, ec, nn, sort, sk, sc, L->d_setws, L->setws_bytes, L->d_setsc,
+                                     L->d_setsc + 1, 0));
+    uint32_t hs[2] = {0, 0};
+    HIPCHECK(hipMemcpyAsync(hs, L->d_setsc, 8, hipMemcpyDeviceToHost, 0));
+    HIPCHECK(hipStreamSynchronize(0));   // also orders the pageable uploads above
+    *n = nn;
+    *keys = sk;
+    *cnts = sc;
+    *nsel = hs[0];
+    *maxcov = hs[1];
     return SID_OK;
 }
 
 static int current_table(sid_lynch_dev* L, std::vector<uint64_t>& keys, std::vector<uint64_t>& cnt)
 {
+    keys.clear();
+    cnt.clear();
     if (L->loaded) {
         keys = L->tkeys;
         cnt = L->tcnt;
         return SID_OK;
     }
-    return export_hist(L, keys, cnt);
+    if (!L->have_hist) return SID_OK;
+    size_t n;
+    const unsigned long long *k, *v;
+    uint32_t ns, mc;
+    int rc = device_table(L, &n, &k, &v, &ns, &mc);
+    if (rc) return rc;
+    keys.resize(n);
+    cnt.resize(n);
+    if (n) {
+        HIPCHECK(hipMemcpyAsync(keys.data(), k, n * 8, hipMemcpyDeviceToHost, 0));
+        HIPCHECK(hipMemcpyAsync(cnt.data(), v, n * 8, hipMemcpyDeviceToHost, 0));
+        HIPCHECK(hipStreamSynchronize(0));
+    }
+    return SID_OK;
 }
 
 extern "C" int sid_profile_table(sid_ctx* c, uint64_t* keys, uint64_t* counts64, size_t cap, size_t* u)
@@ -421,56 +480,33 @@ extern "C" int sid_profile_load(sid_ctx* c, const uint64_t* keys, const uint64_t
     return SID_OK;
 }
 
-static inline uint32_t key_n(uint64_t key, int i) { return (uint32_t)((key >> (48 - 16 * i)) & 0xffff); }
-
 extern "C" int sid_lynch_setup(sid_ctx* c, sid_estimate* est)
 {
     sid_lynch_dev* L;
     int rc = lynch_of(c, &L);
     if (rc) return rc;
     if (!L->setup) {
-        std::vector<uint64_t> k, v;
-        rc = current_table(L, k, v);
-        if (rc) return rc;
         free_setup(L);
-        L->fkeys.clear();
-        L->fcnt.clear();
-        std::vector<double> lnM;
-        // GSL lngamma(k + 1) for every count that occurs, computed once per
-        // context (the same function values as calling it per profile)
-        auto lgk = [L](uint32_t k) {
-            if (k >= L->lg.size()) {
-                size_t n0 = L->lg.size(), n1 = std::max<size_t>(k + 1, 2 * n0);
-                L->lg.resize(n1);
-                for (size_t i = n0; i < n1; ++i) L->lg[i] = sid_gsl_lngamma((double)(i + 1));
-            }
-            return L->lg[k];
-        };
-        // call.cpp:66-70: drop profiles with coverage < 4; UniqueProfile::count
-        // is uint32 (pileup.hpp:34)
-        L->fkeys.reserve(k.size());
-        L->fcnt.reserve(k.size());
-        lnM.reserve(k.size());
-        for (size_t i = 0; i < k.size(); ++i) {
-            uint32_t cov = key_n(k[i], 0) + key_n(k[i], 1) + key_n(k[i], 2) + key_n(k[i], 3);
-            if (cov < 4) continue;
-            L->fkeys.push_back(k[i]);
-            L->fcnt.push_back((uint32_t)v[i]);
-            // lynch.hpp:48-55 multinomialCoefficient exponent, double, in order
-            double m = lgk(cov);
-            for (int j = 0; j < 4; ++j) m -= lgk(key_n(k[i], j));
-            lnM.push_back(m);
+        size_t n = 0;
+        const unsigned long long *k = nullptr, *v = nullptr;
+        uint32_t U32 = 0, maxcov = 0;
+        rc = device_table(L, &n, &k, &v, &U32, &maxcov);
+        if (rc) return rc;
+        const size_t U = U32;
+        // GSL lngamma(k + 1) for every count that occurs (the coverages bound
+        // them), computed once per context on the host and kept on the device
+        if (U && maxcov >= L->lg.size()) {
+            size_t n0 = L->lg.size(), n1 = std::max<size_t>(maxcov + 1, 2 * n0);
+            L->lg.resize(n1);
+            for (size_t i = n0; i < n1; ++i) L->lg[i] = sid_gsl_lngamma((double)(i + 1));
         }
-        // pileup.cpp:198-217 (32-bit products, 64-bit sums)
-        uint64_t acc[4] = {0, 0, 0, 0}, total = 0;
-        for (size_t i = 0; i < L->fkeys.size(); ++i) {
-            uint32_t cov = key_n(L->fkeys[i], 0) + key_n(L->fkeys[i], 1) + key_n(L->fkeys[i], 2) +
-                           key_n(L->fkeys[i], 3);
-            total += (uint32_t)(L->fcnt[i] * cov);
-            for (int j = 0; j < 4; ++j) acc[j] += (uint32_t)(L->fcnt[i] * key_n(L->fkeys[i], j));
+        if (U && L->lg.size() > L->d_lg_n) {
+            dfree(L->d_lg);
+            L->d_lg_n = 0;
+            HIPCHECK(hipMalloc(&L->d_lg, L->lg.size() * 8));
+            HIPCHECK(hipMemcpy(L->d_lg, L->lg.data(), L->lg.size() * 8, hipMemcpyHostToDevice));
+            L->d_lg_n = L->lg.size();
         }
-        for (int j = 0; j < 4; ++j) L->dist[j] = total ? (double)acc[j] / (double)total : 0.25;
-        const size_t U = L->fkeys.size();
         if (U > L->cap_u || !L->d_keys) {   // every U-sized array, grow-only
             const size_t m = std::max<size_t>({U, 2 * L->cap_u, 1024});
             dfree(L->d_keys);
@@ -493,12 +529,23 @@ extern "C" int sid_lynch_setup(sid_ctx* c, sid_estimate* est)
             HIPCHECK(hipMalloc(&L->d_cc, m * 16));
             L->cap_u = m;
         }
+        // pileup.cpp:198-217 distribution (32-bit products, 64-bit sums) and
+        // lynch.hpp:48-55 lnM per profile, gathered in key order
+        unsigned long long acc[5] = {0, 0, 0, 0, 0};
+        bool special = false;
         if (U) {
-            HIPCHECK(hipMemcpyAsync(L->d_keys, L->fkeys.data(), U * 8, hipMemcpyHostToDevice, 0));
-            HIPCHECK(hipMemcpyAsync(L->d_cnt, L->fcnt.data(), U * 4, hipMemcpyHostToDevice, 0));
-            HIPCHECK(hipMemcpyAsync(L->d_lnM, lnM.data(), U * 8, hipMemcpyHostToDevice, 0));
-            HIPCHECK(hipStreamSynchronize(0));   // host vectors are pageable and local
+            unsigned long long* sums = (unsigned long long*)(L->d_setsc + 2);
+            HIPCHECK(sid_launch_setup_gather(k, v, n, L->d_setws, L->d_setsc, L->d_lg, L->d_keys, L->d_cnt,
+                                             L->d_lnM, sums, 0));
+            uint64_t last = 0;
+            HIPCHECK(hipMemcpyAsync(acc, sums, sizeof(acc), hipMemcpyDeviceToHost, 0));
+            HIPCHECK(hipMemcpyAsync(&last, L->d_keys + (U - 1), 8, hipMemcpyDeviceToHost, 0));
+            HIPCHECK(hipStreamSynchronize(0));
+            special = last == EMPTY;
         }
+        for (int j = 0; j < 4; ++j) L->dist[j] = acc[4] ? (double)acc[j] / (double)acc[4] : 0.25;
+        L->nU = U;
+        L->has_special = special;
         L->obj_grid = (int)std::min<size_t>(1024, std::max<size_t>(1, (U + 255) / 256));
         if (!L->d_partial) HIPCHECK(hipMalloc(&L->d_partial, SID_OBJ_PTS * 2 * 1024 * sizeof(double)));
         if (!L->d_ticket) {
@@ -518,7 +565,7 @@ extern "C" int sid_lynch_setup(sid_ctx* c, sid_estimate* est)
     if (est) {
         std::memset(est, 0, sizeof(*est));
         std::memcpy(est->dist, L->dist, sizeof(L->dist));
-        est->n_unique = L->fkeys.size();
+        est->n_unique = L->nU;
     }
     return SID_OK;
 }
@@ -546,7 +593,7 @@ static void make_eval(const double d[4], double pi, double e, sid_lynch_eval* E)
 static int objective_batch(sid_ctx* c, const double (*x)[2], int k, double* out)
 {
     sid_lynch_dev* L = c->lynch;
-    const size_t U = L->fkeys.size();
+    const size_t U = L->nU;
     sid_lynch_evals EV;
     int idx[SID_OBJ_PTS];
     int m = 0;
@@ -887,7 +934,7 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     if (rc) return rc;
     const auto t1 = now();
     const int method = c->opts.method;
-    const size_t U = L->fkeys.size();
+    const size_t U = L->nU;
     // the -R estimate of local and quality prints only the minimiser's line
     const bool local_like = method == SID_METHOD_LOCAL || method == SID_METHOD_QUALITY;
     if (verbose && !local_like) std::fprintf(stderr, "# unique profiles: %zu\n", U);
@@ -968,50 +1015,28 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
         HIPCHECK(hipStreamSynchronize(0));   // the host vectors go out of scope
     }
     const auto t3 = now();
-    // compact class hash over the U filtered profiles
+    // compact class hash over the U filtered profiles (the all-65535 one is
+    // special_idx) and dense code -> class index for the lookup fast path
     uint64_t cap = 16;
     while (cap < 2 * U) cap <<= 1;
-    std::vector<uint64_t> ck(cap, EMPTY);
-    std::vector<uint32_t> ci(cap, 0xFFFFFFFFu);
-    L->special_idx = 0xFFFFFFFFu;
-    for (size_t i = 0; i < U; ++i) {
-        uint64_t key = L->fkeys[i];
-        if (key == EMPTY) {
-            L->special_idx = (uint32_t)i;
-            continue;
-        }
-        uint64_t h = host_hash64(key) & (cap - 1);
-        while (ck[h] != EMPTY) h = (h + 1) & (cap - 1);
-        ck[h] = key;
-        ci[h] = (uint32_t)i;
-    }
-    // dense code -> class index for the typical profiles (lookup fast path)
-    std::vector<uint32_t> dc(SID_DENSE_N, SID_DENSE_NONE);
-    for (size_t i = 0; i < U; ++i) {
-        const uint64_t key = L->fkeys[i];
-        const uint64_t w = (key >> 48) | (((key >> 32) & 0xffff) << 16) | (((key >> 16) & 0xffff) << 32) |
-                           ((key & 0xffff) << 48);
-        const uint32_t d = sid_dense_code(w);
-        if (d != SID_DENSE_NONE) dc[d] = (uint32_t)i;
+    if (cap > L->cap_c) {
+        dfree(L->d_ckeys);
+        dfree(L->d_cidx);
+        L->cap_c = 0;
+        HIPCHECK(hipMalloc(&L->d_ckeys, cap * 8));
+        HIPCHECK(hipMalloc(&L->d_cidx, cap * 4));
+        L->cap_c = cap;
     }
     if (!L->d_dense_cidx) HIPCHECK(hipMalloc(&L->d_dense_cidx, SID_DENSE_N * 4));
-    HIPCHECK(hipMemcpyAsync(L->d_dense_cidx, dc.data(), SID_DENSE_N * 4, hipMemcpyHostToDevice, 0));
+    L->cmask = cap - 1;
+    L->special_idx = L->has_special ? (uint32_t)(U - 1) : 0xFFFFFFFFu;
+    HIPCHECK(sid_launch_class_tables(L->d_keys, (uint32_t)U, L->d_dense_cidx, L->d_ckeys, L->d_cidx, L->cmask, 0));
     HIPCHECK(sid_launch_pack_class(L->d_c1, L->d_c2, U, L->d_cc, 0));
     if (!L->d_rec) {
         HIPCHECK(hipMalloc(&L->d_rec, SID_REC_N * 16));
         HIPCHECK(hipMalloc(&L->d_rcode, SID_REC_N));
     }
     HIPCHECK(sid_launch_rec_build(L->d_dense_cidx, L->d_pcode, L->d_cc, L->d_rec, L->d_rcode, 0));
-    if (cap > L->cap_c) {
-        dfree(L->d_ckeys);
-        dfree(L->d_cidx);
-        HIPCHECK(hipMalloc(&L->d_ckeys, cap * 8));
-        HIPCHECK(hipMalloc(&L->d_cidx, cap * 4));
-        L->cap_c = cap;
-    }
-    HIPCHECK(hipMemcpyAsync(L->d_ckeys, ck.data(), cap * 8, hipMemcpyHostToDevice, 0));
-    HIPCHECK(hipMemcpyAsync(L->d_cidx, ci.data(), cap * 4, hipMemcpyHostToDevice, 0));
-    L->cmask = cap - 1;
     HIPCHECK(hipStreamSynchronize(0));
     L->prepared = true;
     if (timing)
