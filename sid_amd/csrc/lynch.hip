@@ -134,17 +134,77 @@ __global__ void sid_hist_rehash_kernel(const unsigned long long* okeys, const un
         if (okeys[i] != SID_EMPTY_KEY) sid_global_insert(gkeys, gcnt, gmask, distinct, okeys[i], ocnt[i]);
 }
 
-__global__ void sid_hist_compact_kernel(const unsigned long long* gkeys, const unsigned long long* gcnt,
-                                        uint64_t cap, unsigned long long* okeys,
-                                        unsigned long long* ocnt, unsigned long long* nout)
+// output slot of this lane in an append to *ctr by the lanes with take set:
+// one atomic per wave (same-address atomics serialise at the memory side)
+__device__ __forceinline__ unsigned long long sid_wave_append(bool take, unsigned long long* ctr)
 {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        if (gkeys[i] != SID_EMPTY_KEY) {
-            unsigned long long k = atomicAdd(nout, 1ull);
-            okeys[k] = gkeys[i];
-            ocnt[k] = gcnt[i];
+    const unsigned long long mask = __ballot(take);
+    if (mask == 0) return 0;
+    const uint32_t lane = __lane_id();
+    const uint32_t leader = (uint32_t)__ffsll((long long)mask) - 1u;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(mask));
+    base = (unsigned long long)__shfl((long long)base, (int)leader);
+    return base + (unsigned long long)__popcll(mask & ((1ull << lane) - 1ull));
+}
+
+// Compaction of a table into (key, count) pairs after *nout: each block owns a
+// contiguous range, counts its entries, takes its output range with ONE
+// global atomic (same-address device atomics cost ~13 ns each, serialised:
+// one per wave was 27 us for a 128k-slot hash) and writes them in order.
+// SRC::at(i, key, cnt) -> whether slot i holds an entry.
+struct sid_hash_src {
+    const unsigned long long* keys;
+    const unsigned long long* cnt;
+    __device__ bool at(uint64_t i, unsigned long long& k, unsigned long long& c) const
+    {
+        k = keys[i];
+        if (k == SID_EMPTY_KEY) return false;
+        c = cnt[i];
+        return true;
+    }
+};
+
+template <class SRC>
+__global__ __launch_bounds__(256) void sid_compact_kernel(SRC src, uint64_t n, unsigned long long* __restrict__ okeys,
+                                                          unsigned long long* __restrict__ ocnt,
+                                                          unsigned long long* nout)
+{
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+    __shared__ uint32_t wc[4];
+    __shared__ unsigned long long base;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t c = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        unsigned long long k, v;
+        c += src.at(i, k, v) ? 1u : 0u;
+    }
+    for (int off = 32; off > 0; off >>= 1) c += (uint32_t)__shfl_down((int)c, off, 64);
+    if (lane == 0) wc[wid] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = wc[0] + wc[1] + wc[2] + wc[3];
+        base = t ? atomicAdd(nout, (unsigned long long)t) : 0ull;
+    }
+    __syncthreads();
+    unsigned long long off0 = base;
+    for (uint64_t b = lo; b < hi; b += 256) {
+        const uint64_t i = b + threadIdx.x;
+        unsigned long long k = 0, v = 0;
+        const bool take = i < hi && src.at(i, k, v);
+        const unsigned long long mask = __ballot(take);
+        __syncthreads();   // wc of the previous tile consumed
+        if (lane == 0) wc[wid] = (uint32_t)__popcll(mask);
+        __syncthreads();
+        uint32_t before = 0;
+        for (int w = 0; w < wid; ++w) before += wc[w];
+        if (take) {
+            const unsigned long long o = off0 + before + (unsigned long long)__popcll(mask & ((1ull << lane) - 1ull));
+            okeys[o] = k;
+            ocnt[o] = v;
         }
+        off0 += wc[0] + wc[1] + wc[2] + wc[3];
     }
 }
 
@@ -267,41 +327,76 @@ __global__ __launch_bounds__(256) void sid_hist_reduce_kernel(const uint32_t* __
 }
 
 // the fallback list into the global hash (the all-65535 key to stats[1])
+// The fallback keys: each block pre-aggregates its contiguous range (at most
+// SID_LIST_PER keys) in an LDS table, so hot keys (common het profiles) reach
+// the global hash once per block, and the new-key / special counts take one
+// atomic per block.
+#define SID_LIST_PER 1024
+#define SID_LIST_LDS 2048
 __global__ __launch_bounds__(256) void sid_hist_list_kernel(const unsigned long long* __restrict__ list, uint64_t m,
                                                             unsigned long long* gkeys, unsigned long long* gcnt,
                                                             uint64_t gmask, unsigned long long* stats)
 {
-    unsigned long long nnew = 0, nspecial = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t key = list[i];
-        if (key == SID_EMPTY_KEY) ++nspecial;
-        else nnew += sid_global_insert_new(gkeys, gcnt, gmask, key, 1ull);
+    __shared__ unsigned long long lk[SID_LIST_LDS];
+    __shared__ uint32_t lc[SID_LIST_LDS];
+    __shared__ unsigned long long red[2][4];
+    for (int i = threadIdx.x; i < SID_LIST_LDS; i += blockDim.x) {
+        lk[i] = SID_EMPTY_KEY;
+        lc[i] = 0;
     }
-    // per-wave totals: one atomic per wave instead of one per new key
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * SID_LIST_PER;
+    const uint64_t hi = lo + SID_LIST_PER < m ? lo + SID_LIST_PER : m;
+    unsigned long long nnew = 0, nspecial = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const uint64_t key = list[i];
+        if (key == SID_EMPTY_KEY) {
+            ++nspecial;
+            continue;
+        }
+        // at most SID_LIST_PER distinct keys in 2x as many slots: always lands
+        uint32_t h = (uint32_t)sid_hash64(key) & (SID_LIST_LDS - 1);
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&lk[h], SID_EMPTY_KEY, (unsigned long long)key);
+            if (prev == SID_EMPTY_KEY || prev == key) {
+                atomicAdd(&lc[h], 1u);
+                break;
+            }
+            h = (h + 1) & (SID_LIST_LDS - 1);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SID_LIST_LDS; i += blockDim.x)
+        if (lk[i] != SID_EMPTY_KEY) nnew += sid_global_insert_new(gkeys, gcnt, gmask, lk[i], lc[i]);
     for (int off = 32; off > 0; off >>= 1) {
         nnew += __shfl_down(nnew, off, 64);
         nspecial += __shfl_down(nspecial, off, 64);
     }
     if ((threadIdx.x & 63) == 0) {
-        if (nnew) atomicAdd(&stats[0], nnew);
-        if (nspecial) atomicAdd(&stats[1], nspecial);
+        red[0][threadIdx.x >> 6] = nnew;
+        red[1][threadIdx.x >> 6] = nspecial;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] +
+                                     red[threadIdx.x][3];
+        if (v) atomicAdd(&stats[threadIdx.x], v);
     }
 }
 
-// non-zero dense counters -> (key, count), appended after *nout
-__global__ __launch_bounds__(256) void sid_dense_compact_kernel(const unsigned long long* __restrict__ dense,
-                                                                unsigned long long* okeys, unsigned long long* ocnt,
-                                                                unsigned long long* nout)
-{
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= SID_DENSE_N) return;
-    unsigned long long v = 0;
-    for (int g = 0; g < SID_DENSE_ROWS; ++g) v += dense[(size_t)g * SID_DENSE_N + i];
-    if (!v) return;
-    const unsigned long long k = atomicAdd(nout, 1ull);
-    okeys[k] = sid_profile_key(sid_dense_word(i));
-    ocnt[k] = v;
-}
+// non-zero dense counters (summed over the SID_DENSE_ROWS rows) -> (key, count)
+struct sid_dense_src {
+    const unsigned long long* dense;
+    __device__ bool at(uint64_t i, unsigned long long& k, unsigned long long& c) const
+    {
+        unsigned long long v = 0;
+        for (int g = 0; g < SID_DENSE_ROWS; ++g) v += dense[(size_t)g * SID_DENSE_N + i];
+        if (!v) return false;
+        k = sid_profile_key(sid_dense_word((uint32_t)i));
+        c = v;
+        return true;
+    }
+};
 
 // ------------------------------------------------ 10-genotype mixture -----
 // sid_lynch_eval: sid_math.h
@@ -381,19 +476,29 @@ __device__ __forceinline__ void sid_two_sum(double a, double b, double& s, doubl
 }
 
 // One (pi, eps) point per blockIdx.y.  Each block reduces its share of
-// sum count*ln L in double-double into partial[point][block]; the last block of
-// a point (ticket) adds the block partials in block order, again in
-// double-double, and writes {hi, lo} and the call's sequence number to
-// host-mapped memory, so the host reads the result without a copy.
+// sum count*ln L in double-double into partial[point][block]; a second kernel
+// (sid_objective_fold_kernel) adds the block partials in block order.  Two
+// launches cost less than a last-block ticket (per-block device-scope fence +
+// same-address atomic: +7 us per launch at 188 blocks) and than block
+// partials written straight to host-mapped memory and folded by the host
+// (+1.7 us per round trip) (tools/debug/obj_probe.hip).
 __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __restrict__ keys,
                                                             const uint32_t* __restrict__ cnt,
                                                             const double* __restrict__ lnM, size_t u,
-                                                            sid_lynch_evals EV, double* partial,
-                                                            unsigned int* ticket, double* out,
-                                                            volatile unsigned int* seq_out, unsigned int seq)
+                                                            sid_lynch_evals EV, double* __restrict__ partial)
 {
     const int pt = blockIdx.y;
-    const sid_lynch_eval& E = EV.e[pt];
+    sid_lynch_eval E;
+    E.la = EV.p[pt].la;
+    E.lb = EV.p[pt].lb;
+    E.lh = EV.p[pt].lh;
+    E.l1p = EV.p[pt].l1p;
+    E.lp = EV.p[pt].lp;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) E.ld[i] = EV.ld[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) E.ldd[i] = EV.ldd[i];
+    E.lnorm = EV.lnorm;
     double hi = 0.0, lo = 0.0;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < u;
          i += (size_t)gridDim.x * blockDim.x) {
@@ -414,7 +519,6 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
     }
     // wave64 then block reduction, double-double
     __shared__ double sh_hi[4], sh_lo[4];
-    __shared__ bool last;
     for (int off = 32; off > 0; off >>= 1) {
         double ohi = __shfl_down(hi, off, 64);
         double olo = __shfl_down(lo, off, 64);
@@ -429,7 +533,6 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
         sh_lo[wid] = lo;
     }
     __syncthreads();
-    double* part = partial + (size_t)pt * 2 * gridDim.x;
     if (threadIdx.x == 0) {
         double H = 0.0, Lo = 0.0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
@@ -438,24 +541,27 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
             H = s;
             Lo += sh_lo[w] + e;
         }
-        part[2 * blockIdx.x] = H;
-        part[2 * blockIdx.x + 1] = Lo;
-        __threadfence();
-        last = atomicAdd(&ticket[pt], 1u) == gridDim.x - 1;
+        double* part = partial + ((size_t)pt * gridDim.x + blockIdx.x) * 2;
+        part[0] = H;
+        part[1] = Lo;
     }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    // the block partials, one per thread (in parallel: a serial walk of
-    // volatile loads cost most of the kernel), reduced by a fixed tree
+}
+
+// One block per point: the nb block partials (in parallel, then a fixed
+// tree), {hi, lo} and the call's sequence number into host-mapped memory, so
+// the host reads the result without a copy.
+__global__ __launch_bounds__(256) void sid_objective_fold_kernel(const double* __restrict__ partial, int nb,
+                                                                 double* out, volatile unsigned int* seq_out,
+                                                                 unsigned int seq)
+{
+    const int pt = blockIdx.x;
+    const double* part = partial + (size_t)pt * nb * 2;
     double bh = 0.0, bl = 0.0;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
-        const double x = ((volatile double*)part)[2 * b];
-        const double y = ((volatile double*)part)[2 * b + 1];
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
         double s, e;
-        sid_two_sum(bh, x, s, e);
+        sid_two_sum(bh, part[2 * b], s, e);
         bh = s;
-        bl += y + e;
+        bl += part[2 * b + 1] + e;
     }
     for (int off = 32; off > 0; off >>= 1) {
         const double ohi = __shfl_down(bh, off, 64);
@@ -465,7 +571,8 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
         bh = s;
         bl += olo + e;
     }
-    __syncthreads();
+    __shared__ double sh_hi[4], sh_lo[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (lane == 0) {
         sh_hi[wid] = bh;
         sh_lo[wid] = bl;
@@ -479,7 +586,6 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
         H = s;
         Lo += sh_lo[w] + e;
     }
-    ticket[pt] = 0;   // ready for the next launch (stream-ordered)
     double s, e;
     sid_two_sum(H, Lo, s, e);   // normalise
     out[2 * pt] = s;
@@ -801,10 +907,17 @@ __global__ __launch_bounds__(256) void sid_setup_gather_kernel(const unsigned lo
         acc[3] += (uint32_t)(c * n3);
         acc[4] += (uint32_t)(c * cov);
     }
+    __shared__ unsigned long long red[4][5];
     for (int q = 0; q < 5; ++q) {
         unsigned long long v = acc[q];
         for (int off = 32; off > 0; off >>= 1) v += (unsigned long long)__shfl_down((long long)v, off, 64);
-        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&sums[q], v);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) {   // one atomic per (block, sum)
+        const unsigned long long v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                     red[3][threadIdx.x];
+        if (v) atomicAdd(&sums[threadIdx.x], v);
     }
 }
 
@@ -841,46 +954,84 @@ __global__ __launch_bounds__(256) void sid_class_tables_kernel(const uint64_t* _
 // adj), so any sort gives the reference's values.  NaN or -0 p-values (their
 // order or sign could differ from std::sort's) flag `odd`; the host then
 // takes its own BH.
-__global__ __launch_bounds__(256) void sid_bh_check_kernel(const double* __restrict__ p, size_t m,
-                                                           uint32_t* __restrict__ idx, int* __restrict__ odd)
+// Both p arrays in one sort: key = the p's bit pattern (monotonic for
+// p >= +0) with bit 63 marking the second array, so a descending sort gives
+// array 2 then array 1, each descending in p.
+__global__ __launch_bounds__(256) void sid_bh_key_kernel(const double* __restrict__ p1, const double* __restrict__ p2,
+                                                         size_t m, unsigned long long* __restrict__ keys,
+                                                         uint32_t* __restrict__ idx, int* __restrict__ odd)
 {
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (size_t)gridDim.x * blockDim.x) {
-        idx[i] = (uint32_t)i;
-        const double v = p[i];
-        if (isnan(v) || (v == 0.0 && signbit(v))) atomicExch(odd, 1);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * m; i += (size_t)gridDim.x * blockDim.x) {
+        const bool second = i >= m;
+        const double v = second ? p2[i - m] : p1[i];
+        if (isnan(v) || signbit(v)) atomicExch(odd, 1);   // NaN, -0 or < 0: host BH
+        keys[i] = (unsigned long long)__double_as_longlong(v) | (second ? 1ull << 63 : 0ull);
+        idx[i] = (uint32_t)(second ? i - m : i);
     }
 }
 
+// One block per array (blockIdx.x 0: array 2, sorted first; 1: array 1).
+// Per-thread chunk minima, a parallel exclusive min-scan of them (fmin is
+// exact, so any scan order gives the serial result), then the chunk walk.
 #define SID_BH_TB 1024
-__global__ __launch_bounds__(SID_BH_TB) void sid_bh_scan_kernel(const double* __restrict__ ps,
+__global__ __launch_bounds__(SID_BH_TB) void sid_bh_scan_kernel(const unsigned long long* __restrict__ ks,
                                                                 const uint32_t* __restrict__ is, size_t m,
-                                                                double* __restrict__ adj)
+                                                                double* __restrict__ adj1, double* __restrict__ adj2)
 {
-    __shared__ double part[SID_BH_TB];
+    const unsigned long long* k = ks + (size_t)blockIdx.x * m;
+    const uint32_t* ix = is + (size_t)blockIdx.x * m;
+    double* adj = blockIdx.x == 0 ? adj2 : adj1;
+    __shared__ double wmin[SID_BH_TB / 64];
     const size_t per = (m + SID_BH_TB - 1) / SID_BH_TB;
     const size_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
     const double dm = (double)m;
+    auto val = [&](size_t i) {
+        const double p = __longlong_as_double((long long)(k[i] & ~(1ull << 63)));
+        return i == 0 ? p : p * dm / (double)(m - i);   // stats.cpp:74-76
+    };
+    // up to 16 per thread: every load issued at once into registers (a
+    // chunk walk of dependent trips was latency-bound)
+    constexpr int R = 16;
+    double rv[R];
+    uint32_t ri[R];
+    const bool regs = per <= R;
     double mn = __builtin_inf();
-    for (size_t i = lo; i < hi; ++i) {
-        const double v = i == 0 ? ps[0] : ps[i] * dm / (double)(m - i);   // stats.cpp:74-76
-        mn = fmin(mn, v);
-    }
-    part[threadIdx.x] = mn;
-    __syncthreads();
-    if (threadIdx.x == 0) {   // exclusive min-scan of the 1024 chunk minima
-        double acc = __builtin_inf();
-        for (int t = 0; t < SID_BH_TB; ++t) {
-            const double v = part[t];
-            part[t] = acc;
-            acc = fmin(acc, v);
+    if (regs) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t i = lo + r;
+            rv[r] = i < hi ? val(i) : __builtin_inf();
+            ri[r] = i < hi ? ix[i] : 0u;
+            mn = fmin(mn, rv[r]);
         }
+    } else {
+        for (size_t i = lo; i < hi; ++i) mn = fmin(mn, val(i));
     }
+    // inclusive min-scan in the wave, then over the wave totals
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double v = mn;
+    for (int off = 1; off < 64; off <<= 1) {
+        const double t = __shfl_up(v, off, 64);
+        if (lane >= off) v = fmin(v, t);
+    }
+    if (lane == 63) wmin[wid] = v;
     __syncthreads();
-    double acc = part[threadIdx.x];
-    for (size_t i = lo; i < hi; ++i) {
-        const double v = i == 0 ? ps[0] : ps[i] * dm / (double)(m - i);
-        acc = fmin(acc, v);
-        adj[is[i]] = acc > 1 ? 1.0 : acc;   // stats.cpp:77-79
+    double before = __builtin_inf();
+    for (int w = 0; w < wid; ++w) before = fmin(before, wmin[w]);
+    double excl = __shfl_up(v, 1, 64);
+    excl = lane == 0 ? before : fmin(before, excl);
+    double acc = excl;
+    if (regs) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            acc = fmin(acc, rv[r]);
+            if (lo + r < hi) adj[ri[r]] = acc > 1 ? 1.0 : acc;   // stats.cpp:77-79
+        }
+    } else {
+        for (size_t i = lo; i < hi; ++i) {
+            acc = fmin(acc, val(i));
+            adj[ix[i]] = acc > 1 ? 1.0 : acc;
+        }
     }
 }
 
@@ -939,15 +1090,16 @@ hipError_t sid_launch_hist_list(const unsigned long long* list, uint64_t m, unsi
                                 unsigned long long* gcnt, uint64_t gmask, unsigned long long* stats, hipStream_t st)
 {
     if (m == 0) return hipSuccess;
-    uint64_t g = (m + 255) / 256;
-    sid_hist_list_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(list, m, gkeys, gcnt, gmask, stats);
+    const uint64_t g = (m + SID_LIST_PER - 1) / SID_LIST_PER;
+    if (g > 0x7fffffffull) return hipErrorInvalidValue;
+    sid_hist_list_kernel<<<(unsigned)g, 256, 0, st>>>(list, m, gkeys, gcnt, gmask, stats);
     return hipGetLastError();
 }
 
 hipError_t sid_launch_dense_compact(const unsigned long long* dense, unsigned long long* okeys,
                                     unsigned long long* ocnt, unsigned long long* nout, hipStream_t st)
 {
-    sid_dense_compact_kernel<<<SID_DENSE_N / 256, 256, 0, st>>>(dense, okeys, ocnt, nout);
+    sid_compact_kernel<<<32, 256, 0, st>>>(sid_dense_src{dense}, SID_DENSE_N, okeys, ocnt, nout);
     return hipGetLastError();
 }
 
@@ -1041,33 +1193,39 @@ hipError_t sid_launch_class_tables(const uint64_t* keys, uint32_t U, uint32_t* d
     return hipGetLastError();
 }
 
-// BH of p[0..m) into adj (p untouched); ws: device scratch of sid_bh_ws_bytes(m)
+// BH of p1[0..m) into adj1 and of p2 into adj2 (p untouched); ws: device
+// scratch of sid_bh_ws_bytes(m); *odd must be zero on entry
 size_t sid_bh_ws_bytes(size_t m)
 {
     size_t t = 0;
-    (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, t, (const double*)nullptr, (double*)nullptr,
-                                                       (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)m);
-    return ((t + 255) & ~(size_t)255) + m * (8 + 4 + 4) + 256;
+    (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, t, (const unsigned long long*)nullptr,
+                                                       (unsigned long long*)nullptr, (const uint32_t*)nullptr,
+                                                       (uint32_t*)nullptr, (int)(2 * m));
+    return ((t + 255) & ~(size_t)255) + 2 * m * (8 + 8 + 4 + 4) + 256;
 }
 
-hipError_t sid_launch_bh(const double* p, size_t m, double* adj, void* ws, size_t ws_bytes, int* odd, hipStream_t st)
+hipError_t sid_launch_bh(const double* p1, const double* p2, size_t m, double* adj1, double* adj2, void* ws,
+                         size_t ws_bytes, int* odd, hipStream_t st)
 {
     if (m == 0) return hipSuccess;
+    const int n = (int)(2 * m);
     size_t t = 0;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, t, p, (double*)nullptr, (const uint32_t*)nullptr,
-                                                                (uint32_t*)nullptr, (int)m, 0, 64, st);
+    hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, t, (const unsigned long long*)nullptr,
+                                                                (unsigned long long*)nullptr, (const uint32_t*)nullptr,
+                                                                (uint32_t*)nullptr, n, 0, 64, st);
     if (e != hipSuccess) return e;
     char* w = (char*)ws;
     const size_t tb = (t + 255) & ~(size_t)255;
-    if (tb + m * 16 > ws_bytes) return hipErrorInvalidValue;
-    double* ps = (double*)(w + tb);
-    uint32_t* idx = (uint32_t*)(w + tb + m * 8);
-    uint32_t* is = (uint32_t*)(w + tb + m * 12);
-    uint64_t g = (m + 255) / 256;
-    sid_bh_check_kernel<<<(unsigned)(g < 1024 ? g : 1024), 256, 0, st>>>(p, m, idx, odd);
-    e = hipcub::DeviceRadixSort::SortPairsDescending(w, t, p, ps, idx, is, (int)m, 0, 64, st);
+    if (tb + 2 * m * 24 > ws_bytes) return hipErrorInvalidValue;
+    unsigned long long* keys = (unsigned long long*)(w + tb);
+    unsigned long long* ks = keys + 2 * m;
+    uint32_t* idx = (uint32_t*)(ks + 2 * m);
+    uint32_t* is = idx + 2 * m;
+    uint64_t g = (2 * m + 255) / 256;
+    sid_bh_key_kernel<<<(unsigned)(g < 1024 ? g : 1024), 256, 0, st>>>(p1, p2, m, keys, idx, odd);
+    e = hipcub::DeviceRadixSort::SortPairsDescending(w, t, keys, ks, idx, is, n, 0, 64, st);
     if (e != hipSuccess) return e;
-    sid_bh_scan_kernel<<<1, SID_BH_TB, 0, st>>>(ps, is, m, adj);
+    sid_bh_scan_kernel<<<2, SID_BH_TB, 0, st>>>(ks, is, m, adj1, adj2);
     return hipGetLastError();
 }
 
@@ -1101,18 +1259,19 @@ hipError_t sid_launch_compact(const unsigned long long* gkeys, const unsigned lo
                               uint64_t cap, unsigned long long* okeys, unsigned long long* ocnt,
                               unsigned long long* nout, hipStream_t st)
 {
-    uint64_t g = (cap + 255) / 256;
-    sid_hist_compact_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(gkeys, gcnt, cap, okeys,
-                                                                             ocnt, nout);
+    const uint64_t g = (cap + 2047) / 2048;   // >= 8 tiles per block, one atomic per block
+    sid_compact_kernel<<<(unsigned)(g < 256 ? (g ? g : 1) : 256), 256, 0, st>>>(sid_hash_src{gkeys, gcnt}, cap, okeys,
+                                                                                ocnt, nout);
     return hipGetLastError();
 }
 
 hipError_t sid_launch_objective(const uint64_t* keys, const uint32_t* cnt, const double* lnM, size_t u,
-                                const sid_lynch_evals* EV, int npts, double* partial, unsigned int* ticket,
-                                double* out, unsigned int* seq_out, unsigned int seq, int grid, hipStream_t st)
+                                const sid_lynch_evals* EV, int npts, double* partial, double* out,
+                                unsigned int* seq_out, unsigned int seq, int grid, hipStream_t st)
 {
-    sid_objective_kernel<<<dim3(grid, npts), 256, 0, st>>>(keys, cnt, lnM, u, *EV, partial, ticket, out, seq_out,
-                                                           seq);
+    if (npts < 1 || npts > SID_OBJ_PTS || grid < 1 || grid > 1024) return hipErrorInvalidValue;
+    sid_objective_kernel<<<dim3(grid, npts), 256, 0, st>>>(keys, cnt, lnM, u, *EV, partial);
+    sid_objective_fold_kernel<<<npts, 256, 0, st>>>(partial, grid, out, seq_out, seq);
     return hipGetLastError();
 }
 

@@ -43,8 +43,8 @@ hipError_t sid_launch_compact(const unsigned long long* gkeys, const unsigned lo
                               uint64_t cap, unsigned long long* okeys, unsigned long long* ocnt,
                               unsigned long long* nout, hipStream_t st);
 hipError_t sid_launch_objective(const uint64_t* keys, const uint32_t* cnt, const double* lnM, size_t u,
-                                const sid_lynch_evals* EV, int npts, double* partial, unsigned int* ticket,
-                                double* out, unsigned int* seq_out, unsigned int seq, int grid, hipStream_t st);
+                                const sid_lynch_evals* EV, int npts, double* partial, double* out,
+                                unsigned int* seq_out, unsigned int seq, int grid, hipStream_t st);
 hipError_t sid_launch_profile_lik(const uint64_t* keys, const double* lnM, size_t u,
                                   const sid_lynch_eval* E, double* lhom, double* lhet, hipStream_t st);
 hipError_t sid_launch_classify(const uint64_t* keys, const double* lhom, const double* lhet, size_t u,
@@ -58,7 +58,8 @@ hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned lo
 hipError_t sid_launch_rec_build(const uint32_t* dense_cidx, const uint8_t* pcode, const double* cc, double* rec,
                                 uint8_t* rcode, hipStream_t st);
 size_t sid_bh_ws_bytes(size_t m);
-hipError_t sid_launch_bh(const double* p, size_t m, double* adj, void* ws, size_t ws_bytes, int* odd, hipStream_t st);
+hipError_t sid_launch_bh(const double* p1, const double* p2, size_t m, double* adj1, double* adj2, void* ws,
+                         size_t ws_bytes, int* odd, hipStream_t st);
 hipError_t sid_launch_bh_label(const double* adj_het, size_t m, double sig, uint8_t* code, hipStream_t st);
 size_t sid_setup_ws_bytes(size_t n);
 hipError_t sid_launch_setup_select(const unsigned long long* keys, const unsigned long long* cnts, size_t n, bool sort,
@@ -107,12 +108,13 @@ struct sid_lynch_dev {
     uint64_t* d_keys = nullptr;
     uint32_t* d_cnt = nullptr;
     double* d_lnM = nullptr;
-    double* d_partial = nullptr;           // [SID_OBJ_PTS][2 * obj_grid]
     int obj_grid = 0;
+    bool lookahead = false;                // NM prefetches two iterations' candidates
     uint64_t evals = 0;
+    uint64_t launches = 0;
+    double* d_partial = nullptr;           // [SID_OBJ_PTS][obj_grid][2]
     // objective results land in host-mapped memory (no copy): {hi, lo} per
     // point and the launch's sequence number per point
-    unsigned int* d_ticket = nullptr;
     double* h_out = nullptr;
     unsigned int* h_seq = nullptr;
     double* d_out = nullptr;
@@ -169,13 +171,13 @@ static void release_buffers(sid_lynch_dev* L)
     dfree(L->d_keys);
     dfree(L->d_cnt);
     dfree(L->d_lnM);
-    dfree(L->d_partial);
     dfree(L->d_lhom);
     dfree(L->d_lhet);
     dfree(L->d_c1);
     dfree(L->d_c2);
     dfree(L->d_pcode);
     dfree(L->d_cc);
+    dfree(L->d_partial);
     dfree(L->d_ckeys);
     dfree(L->d_cidx);
     dfree(L->d_dense_cidx);
@@ -202,7 +204,6 @@ void sid_lynch_dev_destroy(sid_lynch_dev* L)
     dfree(L->dense);
     dfree(L->part);
     dfree(L->list);
-    dfree(L->d_ticket);
     if (L->h_out) (void)hipHostFree(L->h_out);
     if (L->h_seq) (void)hipHostFree(L->h_seq);
     release_buffers(L);
@@ -547,10 +548,13 @@ extern "C" int sid_lynch_setup(sid_ctx* c, sid_estimate* est)
         L->nU = U;
         L->has_special = special;
         L->obj_grid = (int)std::min<size_t>(1024, std::max<size_t>(1, (U + 255) / 256));
+        // two-iteration prefetch (up to 28 points per launch) while the points
+        // still fit the chip alongside each other (U x 28 profile-points);
+        // SID_NM_LOOKAHEAD=0/1 overrides (measurement)
+        L->lookahead = U <= 32768;
+        if (const char* e = std::getenv("SID_NM_LOOKAHEAD")) L->lookahead = std::atoi(e) != 0;
         if (!L->d_partial) HIPCHECK(hipMalloc(&L->d_partial, SID_OBJ_PTS * 2 * 1024 * sizeof(double)));
-        if (!L->d_ticket) {
-            HIPCHECK(hipMalloc(&L->d_ticket, SID_OBJ_PTS * sizeof(unsigned int)));
-            HIPCHECK(hipMemset(L->d_ticket, 0, SID_OBJ_PTS * sizeof(unsigned int)));
+        if (!L->h_out) {
             HIPCHECK(hipHostMalloc((void**)&L->h_out, 2 * SID_OBJ_PTS * sizeof(double),
                                    hipHostMallocMapped | hipHostMallocCoherent));
             HIPCHECK(hipHostMalloc((void**)&L->h_seq, SID_OBJ_PTS * sizeof(unsigned int),
@@ -597,6 +601,7 @@ static int objective_batch(sid_ctx* c, const double (*x)[2], int k, double* out)
     sid_lynch_evals EV;
     int idx[SID_OBJ_PTS];
     int m = 0;
+    if (k > SID_OBJ_PTS) return SID_EINVAL;
     for (int i = 0; i < k; ++i) {
         const double pi = x[i][0], eps = x[i][1];
         if (pi < 0 || pi > 1 || eps < 0 || eps > 1) {
@@ -604,14 +609,22 @@ static int objective_batch(sid_ctx* c, const double (*x)[2], int k, double* out)
         } else if (U == 0) {
             out[i] = -0.0;   // static_cast<double>(-0.0L)
         } else {
-            make_eval(L->dist, pi, eps, &EV.e[m]);
+            sid_lynch_eval E;
+            make_eval(L->dist, pi, eps, &E);
+            if (m == 0) {
+                std::memcpy(EV.ld, E.ld, sizeof(EV.ld));
+                std::memcpy(EV.ldd, E.ldd, sizeof(EV.ldd));
+                EV.lnorm = E.lnorm;
+            }
+            EV.p[m] = {E.la, E.lb, E.lh, E.l1p, E.lp};
             idx[m++] = i;
         }
     }
     if (m == 0) return SID_OK;
     const unsigned int seq = ++L->seq;
-    HIPCHECK(sid_launch_objective(L->d_keys, L->d_cnt, L->d_lnM, U, &EV, m, L->d_partial, L->d_ticket, L->d_out,
-                                  L->d_seq, seq, L->obj_grid, 0));
+    L->launches++;
+    HIPCHECK(sid_launch_objective(L->d_keys, L->d_cnt, L->d_lnM, U, &EV, m, L->d_partial, L->d_out, L->d_seq, seq,
+                                  L->obj_grid, 0));
     // poll the mapped sequence numbers; the stream status is the backstop
     auto ready = [&] {
         for (int j = 0; j < m; ++j)
@@ -674,6 +687,7 @@ struct Simplex {
     {
         cn = 0;
         if (err) return;
+        k = std::min(k, (int)SID_OBJ_PTS);
         int rc = objective_batch(ctx, pts, k, cv);
         if (rc) {
             err = rc;
@@ -684,6 +698,12 @@ struct Simplex {
             cx[i][1] = pts[i][1];
         }
         cn = k;
+    }
+    bool cached(const double* x) const
+    {
+        for (int i = 0; i < cn; ++i)
+            if (cx[i][0] == x[0] && cx[i][1] == x[1]) return true;
+        return false;
     }
     double f(const double* x)
     {
@@ -742,6 +762,28 @@ struct Simplex {
         double beta = (p * coeff - 1.0) / (p - 1.0);
         for (int j = 0; j < N; ++j) xc[j] = center[j] * alpha;
         axpy(beta, x1[corner], xc);
+    }
+    // candidate points of an iteration whose worst vertex is h: reflection,
+    // expansion, inside contraction, and the contraction after the reflected
+    // point is accepted (optimization.hpp -> nmsimplex2_iterate)
+    void candidates(int h, double (*pts)[N]) const
+    {
+        corner_point(-1.0, h, pts[0]);
+        corner_point(-2.0, h, pts[1]);
+        corner_point(0.5, h, pts[2]);
+        Simplex T = *this;
+        T.update_point(h, pts[0], 0.0);
+        T.corner_point(0.5, h, pts[3]);
+    }
+    static void add_point(double (*pts)[N], int& k, const double* x)
+    {
+        for (int i = 0; i < k; ++i)
+            if (pts[i][0] == x[0] && pts[i][1] == x[1]) return;
+        if (k < SID_OBJ_PTS) {
+            pts[k][0] = x[0];
+            pts[k][1] = x[1];
+            ++k;
+        }
     }
     double corner_move(double coeff, int corner, double* xc)
     {
@@ -829,16 +871,39 @@ struct Simplex {
                 s_hi = i;
             }
         }
-        {   // reflection, expansion, and the contraction with and without the
-            // reflected point accepted first
-            double pts[SID_OBJ_PTS][N];
-            corner_point(-1.0, hi, pts[0]);
-            corner_point(-2.0, hi, pts[1]);
-            corner_point(0.5, hi, pts[2]);
-            Simplex T = *this;
-            T.update_point(hi, pts[0], 0.0);
-            T.corner_point(0.5, hi, pts[3]);
-            prefetch(pts, SID_OBJ_PTS);
+        {
+            double c1[4][N];
+            candidates(hi, c1);
+            if (!(cached(c1[0]) && cached(c1[1]) && cached(c1[2]) && cached(c1[3]))) {
+                double pts[SID_OBJ_PTS][N];
+                int k = 0;
+                for (int i = 0; i < 4; ++i) add_point(pts, k, c1[i]);
+                if (ctx->lynch->lookahead) {
+                    // the next iteration's candidates after each outcome of
+                    // this one (only the worst vertex moves, so the new
+                    // worst is the old second worst, or the moved vertex
+                    // after a contraction); the trajectory does not depend
+                    // on what is prefetched
+                    for (int o = 0; o < 4; ++o) {
+                        Simplex T = *this;
+                        T.cn = 0;
+                        if (o == 0) T.update_point(hi, c1[0], 0.0);   // reflection accepted
+                        if (o == 1) T.update_point(hi, c1[1], 0.0);   // expansion accepted
+                        if (o == 2) {                                 // outside contraction
+                            T.update_point(hi, c1[0], 0.0);
+                            T.update_point(hi, c1[3], 0.0);
+                        }
+                        if (o == 3) T.update_point(hi, c1[2], 0.0);   // inside contraction
+                        for (int h2 : {s_hi, hi}) {
+                            if (h2 == hi && o < 2) continue;
+                            double c2[4][N];
+                            T.candidates(h2, c2);
+                            for (int i = 0; i < 4; ++i) add_point(pts, k, c2[i]);
+                        }
+                    }
+                }
+                prefetch(pts, k);
+            }
         }
         double val = corner_move(-1.0, hi, xc);
         if (std::isfinite(val) && val < y1[lo]) {
@@ -890,6 +955,7 @@ static int run_estimate(sid_ctx* c, int verbose, sid_estimate* est)
     const double step[2] = {1e-4, 1e-4}; // DEFAULT_STEPSIZE
     double x[2] = {x0[0], x0[1]}, size = 0, fval = 0;
     L->evals = 0;
+    L->launches = 0;
     if (!S.set(x0, step, &size)) return S.err ? S.err : SID_EBADFUNC;
     if (S.err) return S.err;
     int i = 0, status = 0;
@@ -970,8 +1036,7 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
         }
         if (!L->d_odd) HIPCHECK(hipMalloc(&L->d_odd, sizeof(int)));
         HIPCHECK(hipMemsetAsync(L->d_odd, 0, sizeof(int), 0));
-        HIPCHECK(sid_launch_bh(L->d_c1, U, L->d_lhom, L->d_bhws, L->bhws_bytes, L->d_odd, 0));
-        HIPCHECK(sid_launch_bh(L->d_c2, U, L->d_lhet, L->d_bhws, L->bhws_bytes, L->d_odd, 0));
+        HIPCHECK(sid_launch_bh(L->d_c1, L->d_c2, U, L->d_lhom, L->d_lhet, L->d_bhws, L->bhws_bytes, L->d_odd, 0));
         int odd = 0;
         HIPCHECK(hipMemcpyAsync(&odd, L->d_odd, sizeof(int), hipMemcpyDeviceToHost, 0));
         HIPCHECK(hipStreamSynchronize(0));
@@ -1042,8 +1107,9 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     if (timing)
         std::fprintf(stderr,
                      "{\"lynch_prepare_ms\": {\"setup\": %.3f, \"estimate\": %.3f, \"evaluations\": %llu, "
-                     "\"classify_bh\": %.3f, \"class_tables\": %.3f}}\n",
-                     ms(t0, t1), ms(t1, t2), (unsigned long long)est.evaluations, ms(t2, t3), ms(t3, now()));
+                     "\"launches\": %llu, \"classify_bh\": %.3f, \"class_tables\": %.3f}}\n",
+                     ms(t0, t1), ms(t1, t2), (unsigned long long)est.evaluations, (unsigned long long)L->launches,
+                     ms(t2, t3), ms(t3, now()));
     return SID_OK;
 }
 

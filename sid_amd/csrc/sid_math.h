@@ -56,10 +56,18 @@ struct sid_lynch_eval {
 };
 
 // Up to SID_OBJ_PTS (pi, eps) points per objective launch: Nelder-Mead's
-// candidate points of one iteration are evaluated together.
-#define SID_OBJ_PTS 4
+// candidate points of one iteration (and of the next one, lynch_host.cpp) are
+// evaluated together.  The dist-only constants are shared; per point only the
+// eps- and pi-dependent logs differ (kernel arguments stay small).
+#define SID_OBJ_PTS 32
+struct sid_lynch_pt {
+    double la, lb, lh, l1p, lp;
+};
 struct sid_lynch_evals {
-    sid_lynch_eval e[SID_OBJ_PTS];
+    double ld[4];
+    double ldd[6];
+    double lnorm;
+    sid_lynch_pt p[SID_OBJ_PTS];
 };
 
 // x86 prints NaNs made by invalid operations as "-nan" (default NaN has the
