@@ -143,7 +143,7 @@ extern "C" int sid_create(int device, const sid_opts* opts, sid_ctx** out)
     e = hipMalloc(&c->d_lnt, SID_LUTN * sizeof(double));
     if (e == hipSuccess) e = hipMemcpy(c->d_lnt, lnt.data(), SID_LUTN * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&c->ws.table, tab * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&c->ws.table2, 65536 * sizeof(double));   // SID_TAB2_N (local.hip)
+    if (e == hipSuccess) e = hipMalloc(&c->ws.table2, SID_TAB2_N * sizeof(double));
     if (e == hipSuccess) e = hipMalloc(&c->ws.miss, (size_t)c->ws.cap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&c->ws.ctr, 2 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c->ws.ctr, 0, 2 * sizeof(uint32_t));

@@ -182,19 +182,25 @@ __global__ __launch_bounds__(256) void sid_local_kernel_x1(const uint64_t* __res
 #define SID_TAB_NR 4
 #define SID_TAB_N (SID_TAB_NF * SID_TAB_NS * SID_TAB_NR)
 
-// Second-level table for the fix-up (L2-resident, 512 KiB): the 30x het sites
-// the LDS table leaves out (ns >= 8) have nf, ns < 64 and few other reads.
-#define SID_TAB2_NF 128
-#define SID_TAB2_NS 64
-#define SID_TAB2_NR 8
-#define SID_TAB2_N (SID_TAB2_NF * SID_TAB2_NS * SID_TAB2_NR)
+// Second-level table (SID_TAB2_*, sid_internal.h): looked up inline by the
+// table kernel for its LDS misses, and by the fix-up.
+
+// LDS slot of (nf, ns, r2): one 256-B bank row per nf (8 ns x 4 r2 entries of
+// 8 B), the position in the row XOR-ed with nf.  Linear, every nf's entry of a
+// class fell on the same two banks, so a 32-lane half reading the (ns, r2) =
+// (0, 0) class at k distinct depths was a k-way conflict (ds_read_b64 banks:
+// MI355X_MICROARCH.md §LDS); swizzled, distinct nf mod 32 never collide.
+__device__ __forceinline__ uint32_t sid_tab_slot(uint32_t nf, uint32_t ns, uint32_t r2)
+{
+    return nf * (SID_TAB_NS * SID_TAB_NR) + ((ns * SID_TAB_NR + r2) ^ (nf & (SID_TAB_NS * SID_TAB_NR - 1)));
+}
 
 // Table entry for (nf, ns, r2): v >= +0 -> p1 = v, p2 = 1; v <= -0 -> p1 = 1,
 // p2 = -v; NaN -> both 0 (NaN-free: the reference's 0/0 never reaches here);
 // +inf -> not covered (the site needs the fast or emulated path).
 __global__ __launch_bounds__(256) void sid_local_table_build(sid_local_k K, const double* __restrict__ lnt,
                                                             double* __restrict__ table, uint32_t NF, uint32_t NS,
-                                                            uint32_t NR)
+                                                            uint32_t NR, bool swz)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= NF * NS * NR) return;
@@ -208,7 +214,7 @@ __global__ __launch_bounds__(256) void sid_local_table_build(sid_local_k K, cons
         else if (gt) v = -p2;       // p1 == 1
         else v = p1;                // p2 == 1
     }
-    table[i] = v;
+    table[swz ? sid_tab_slot(nf, ns, r2) : i] = v;
 }
 
 // outputs of a site from its table value v (not +inf); returns the code
@@ -236,10 +242,27 @@ __device__ __forceinline__ uint32_t table_site(uint64_t w, const double* __restr
     sid_major(w, f, s, nf, ns, cov);
     const uint32_t r2 = cov - nf - ns;
     double v = __builtin_inf();
-    if (nf < SID_TAB_NF && ns < SID_TAB_NS && r2 < SID_TAB_NR) v = T[(nf * SID_TAB_NS + ns) * SID_TAB_NR + r2];
+    if (nf < SID_TAB_NF && ns < SID_TAB_NS && r2 < SID_TAB_NR) v = T[sid_tab_slot(nf, ns, r2)];
     if (isinf(v)) {
         p1 = p2 = 0.0;
         return 0xFFu;   // miss marker (not a valid code: bits 4-5 are never set)
+    }
+    return table_decode(v, f, s, sig, p1, p2);
+}
+
+// a site the LDS table missed, through the L2-resident second-level table
+// (0xFF: still not covered)
+__device__ __forceinline__ uint32_t table2_site(uint64_t w, const double* __restrict__ T2, double sig, double& p1,
+                                                double& p2)
+{
+    uint32_t f, s, nf, ns, cov;
+    sid_major(w, f, s, nf, ns, cov);
+    const uint32_t r2 = cov - nf - ns;
+    double v = __builtin_inf();
+    if (nf < SID_TAB2_NF && ns < SID_TAB2_NS && r2 < SID_TAB2_NR) v = T2[(nf * SID_TAB2_NS + ns) * SID_TAB2_NR + r2];
+    if (isinf(v)) {
+        p1 = p2 = 0.0;
+        return 0xFFu;
     }
     return table_decode(v, f, s, sig, p1, p2);
 }
@@ -292,8 +315,15 @@ __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __r
             const size_t p = base + (size_t)j * blockDim.x + threadIdx.x;
             if (p < npairs) {
                 double h0, h1, t0, t1;
-                const uint32_t a = table_site(c[j].x, T, sig, h0, t0);
-                const uint32_t b = table_site(c[j].y, T, sig, h1, t1);
+                uint32_t a = table_site(c[j].x, T, sig, h0, t0);
+                uint32_t b = table_site(c[j].y, T, sig, h1, t1);
+                // LDS misses (30x het sites, 200x sites with r2 >= 4) through
+                // the second-level table before the stores: an L2 hit the
+                // other waves hide, instead of a scattered rewrite later
+                if (T2 && (a == 0xFFu || b == 0xFFu)) {
+                    if (a == 0xFFu) a = table2_site(c[j].x, T2, sig, h0, t0);
+                    if (b == 0xFFu) b = table2_site(c[j].y, T2, sig, h1, t1);
+                }
                 st_stream(code2 + p, (uint16_t)(a | (b << 8)), NT);
                 st_stream(hom + p, sid_dvec2{h0, h1}, NT);
                 st_stream(het + p, sid_dvec2{t0, t1}, NT);
@@ -313,61 +343,9 @@ __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __r
             }
         }
     }
-    __syncthreads();   // orders the pair stores before the tail's site stores
+    __syncthreads();
     const uint32_t nl = lcnt < SID_LMISS ? lcnt : SID_LMISS;
     if (nl == 0) return;
-    if (T2) {
-        // the block's own misses through the L2-resident second-level table
-        // (the 30x het sites); resolved entries are struck from the list
-        const uint64_t* counts = (const uint64_t*)pairs;
-        uint8_t* code = (uint8_t*)code2;
-        double* homd = (double*)hom;
-        double* hetd = (double*)het;
-        uint32_t kept = 0;
-        for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) {
-            const uint32_t idx = lmiss[i];
-            uint32_t f, s, nf, ns, cov;
-            sid_major(counts[idx], f, s, nf, ns, cov);
-            const uint32_t r2 = cov - nf - ns;
-            double v = __builtin_inf();
-            if (nf < SID_TAB2_NF && ns < SID_TAB2_NS && r2 < SID_TAB2_NR) v = T2[(nf * SID_TAB2_NS + ns) * SID_TAB2_NR + r2];
-            if (!isinf(v)) {
-                double h, t;
-                code[idx] = (uint8_t)table_decode(v, f, s, sig, h, t);
-                homd[idx] = h;
-                hetd[idx] = t;
-                lmiss[i] = 0xFFFFFFFFu;
-            } else {
-                ++kept;
-            }
-        }
-        // the rest to the fix-up: one global atomic per block
-        const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-        uint32_t x = kept;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(x, off, 64);
-            if (lane >= off) x += y;
-        }
-        __shared__ uint32_t wsum[32];
-        if (lane == 63) wsum[wid] = x;
-        __syncthreads();
-        uint32_t wbase = 0, tot = 0;
-        for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
-            if (w < wid) wbase += wsum[w];
-            tot += wsum[w];
-        }
-        if (tot == 0) return;
-        if (threadIdx.x == 0) gbase = atomicAdd(ctr, tot);
-        __syncthreads();
-        uint32_t o = gbase + wbase + x - kept;
-        for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) {
-            const uint32_t idx = lmiss[i];
-            if (idx == 0xFFFFFFFFu) continue;
-            if (o < cap) miss[o] = idx;
-            ++o;
-        }
-        return;
-    }
     if (threadIdx.x == 0) gbase = atomicAdd(ctr, nl);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
@@ -461,10 +439,10 @@ extern "C" hipError_t sid_launch_local_table_build(const sid_local_k* K, const d
                                                    double* d_table2, hipStream_t stream)
 {
     sid_local_table_build<<<SID_TAB_N / 256, 256, 0, stream>>>(*K, d_lnt, d_table, SID_TAB_NF, SID_TAB_NS,
-                                                               SID_TAB_NR);
+                                                               SID_TAB_NR, true);
     if (d_table2)
         sid_local_table_build<<<SID_TAB2_N / 256, 256, 0, stream>>>(*K, d_lnt, d_table2, SID_TAB2_NF, SID_TAB2_NS,
-                                                                    SID_TAB2_NR);
+                                                                    SID_TAB2_NR, false);
     return hipGetLastError();
 }
 

@@ -9,6 +9,14 @@
 #include "../../include/sid.h"
 #include "sid_math.h"
 
+// Second-level class table of -m local (L2-resident, 2 MiB): (nf, ns, r2)
+// with nf < 512, ns < 64, r2 < 8 covers the 30x het sites (ns >= 8) and the
+// 200x sites with r2 >= 4 that the LDS table (nf < 256, ns < 8, r2 < 4) leaves out.
+#define SID_TAB2_NF 512
+#define SID_TAB2_NS 64
+#define SID_TAB2_NR 8
+#define SID_TAB2_N (SID_TAB2_NF * SID_TAB2_NS * SID_TAB2_NR)
+
 // -m local workspace (class table + miss list), one per context
 struct sid_local_ws {
     double* table = nullptr;     // SID_TAB_N entries (local.hip), copied to LDS
@@ -21,7 +29,7 @@ struct sid_local_ws {
     int direct = 0;              // SID_LOCAL_DIRECT=1: bypass the table (A/B)
     int unroll = 2;              // SID_TABLE_UNROLL: pairs per thread per tile (1, 2, 4)
     int nt = 0;                  // SID_TABLE_NT=1: non-temporal output stores
-    int tail = 1;                // SID_TABLE_TAIL=0: leave every miss to the fix-up kernel (A/B)
+    int tail = 1;                // SID_TABLE_TAIL=0: no inline second-level lookup, every miss to the fix-up (A/B)
     hipEvent_t ev_mid = nullptr; // set only while timing: recorded between main and fix-up
 };
 
