@@ -9,11 +9,11 @@
 #include "../../include/sid.h"
 #include "sid_math.h"
 
-// Second-level class table of -m local (L2-resident, 2 MiB): (nf, ns, r2)
-// with nf < 512, ns < 64, r2 < 8 covers the 30x het sites (ns >= 8) and the
+// Second-level class table of -m local (L2-resident, 4 MiB): (nf, ns, r2)
+// with nf < 512, ns < 128, r2 < 8 covers the 30x and 200x het sites (ns >= 8) and the
 // 200x sites with r2 >= 4 that the LDS table (nf < 256, ns < 8, r2 < 4) leaves out.
 #define SID_TAB2_NF 512
-#define SID_TAB2_NS 64
+#define SID_TAB2_NS 128
 #define SID_TAB2_NR 8
 #define SID_TAB2_N (SID_TAB2_NF * SID_TAB2_NS * SID_TAB2_NR)
 
