@@ -24,7 +24,11 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
                 of the same workload, rank 0 at N=1 only;
   e2e           the product CLI (build/sid) on the same sample file, text
                 in -> CSV out, device text path and --host-parse (wall clock
-                of the whole process and the CLI's own clock), informational.
+                of the whole process and the CLI's own clock), informational;
+  pipeline      SURVEY.md §8(d) throughput 2: counts in pinned host memory ->
+                H2D -> sid_call_local -> D2H of code + confs, in chunks over
+                three streams (PCIe-bound, 25 B/site cross the link),
+                informational.
 """
 import argparse
 import json
@@ -177,6 +181,8 @@ def main():
             "het_sites_last_step": nhet,
             "kernel_path": "direct" if a.direct else "class-table + fix-up",
         }
+        if world == 1 and not a.no_e2e:
+            out["pipeline"] = bench_pipeline(a, torch, dev, counts, code, hom, het)
         if world == 1 and a.cpu_sample > 0:
             out["cpu_baseline"], e2e = cpu_and_e2e(a)
             if e2e is not None:
@@ -185,6 +191,55 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_pipeline(a, torch, dev, counts, code, hom, het):
+    """Pinned host counts -> H2D -> sid_call_local -> D2H (code, hom, het) for
+    the whole shard, 4M-site chunks round-robin over three streams, one
+    context per stream (a context's miss list is per call)."""
+    import sid_amd
+    n = a.sites
+    chunk = 1 << 22
+    nstreams = 3
+    h_counts = counts.cpu().pin_memory()
+    h_code = torch.empty(n, dtype=torch.uint8).pin_memory()
+    h_hom = torch.empty(n, dtype=torch.float64).pin_memory()
+    h_het = torch.empty(n, dtype=torch.float64).pin_memory()
+    lanes = []
+    for _ in range(nstreams):
+        lanes.append((torch.cuda.Stream(dev), sid_amd.Context(dev.index),
+                      torch.empty((chunk, 4), dtype=torch.int16, device=dev),
+                      torch.empty(chunk, dtype=torch.uint8, device=dev),
+                      torch.empty(chunk, dtype=torch.float64, device=dev),
+                      torch.empty(chunk, dtype=torch.float64, device=dev)))
+
+    def run():
+        for k, lo in enumerate(range(0, n, chunk)):
+            s, cx, dc, dcode, dhom, dhet = lanes[k % nstreams]
+            m = min(chunk, n - lo)
+            with torch.cuda.stream(s):
+                dc[:m].copy_(h_counts[lo:lo + m], non_blocking=True)
+                cx.call_local(dc.data_ptr(), m, dcode.data_ptr(), dhom.data_ptr(), dhet.data_ptr(), s.cuda_stream)
+                h_code[lo:lo + m].copy_(dcode[:m], non_blocking=True)
+                h_hom[lo:lo + m].copy_(dhom[:m], non_blocking=True)
+                h_het[lo:lo + m].copy_(dhet[:m], non_blocking=True)
+        torch.cuda.synchronize(dev)
+
+    run()
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        run()
+        times.append(time.perf_counter() - t0)
+    # the same outputs as the resident run (bit patterns, NaN-safe)
+    ok = (torch.equal(h_code, code.cpu()) and torch.equal(h_hom.view(torch.int64), hom.cpu().view(torch.int64))
+          and torch.equal(h_het.view(torch.int64), het.cpu().view(torch.int64)))
+    for _, cx, *_ in lanes:
+        cx.close()
+    dt = min(times)
+    return {"value": n / dt, "unit": "sites/s", "seconds": dt, "runs_s": times, "chunk_sites": chunk,
+            "streams": nstreams, "pcie_GBps": 25 * n / dt / 1e9, "equals_resident_run": ok,
+            "note": "pinned host counts -> H2D -> sid_call_local -> D2H of code + hom + het (25 B/site over PCIe)"}
 
 
 LYNCH_HIST_BYTES = 8         # SURVEY.md §8(d): histogram pass reads the counts
@@ -282,6 +337,8 @@ def bench_lynch(a, torch, dist, rank, world, dev, counts, code, hom, het):
                          "evaluations": est.evaluations, "unique_profiles": u},
             "het_sites_last_step": nhet,
         }
+        if world == 1 and not a.no_e2e:
+            out["pipeline"] = bench_pipeline(a, torch, dev, counts, code, hom, het)
         if world == 1 and a.cpu_sample > 0:
             out["cpu_baseline"], e2e = cpu_and_e2e(a)
             if e2e is not None:
@@ -297,6 +354,45 @@ def method_flags(a):
     if a.method == "local":
         return []
     return (["-R"] if not a.no_R else []) + ["-m", a.method]
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_sharded(a, td, cli):
+    """the CPU path with one process per core on line-aligned
+    shards of the same sample (valid for -m local: sites are independent),
+    P = min(16, cpu_count) -- the GPU box's CPU share is 16 cores."""
+    import sid_amd
+    P = max(1, min(16, os.cpu_count() or 1))
+    m = a.cpu_sample
+    paths = []
+    for k in range(P):
+        lo, hi = m * k // P, m * (k + 1) // P
+        pth = os.path.join(td, f"shard{k}.plp")
+        with open(pth, "wb") as f:
+            f.write(sid_amd.synth_text(a.seed, hi - lo, a.depth, first=lo))
+        with open(pth, "rb") as f:
+            while f.read(1 << 26):
+                pass
+        paths.append(pth)
+    with open(os.devnull, "wb") as dn:
+        t0 = time.perf_counter()
+        procs = [subprocess.Popen([cli] + method_flags(a) + [pth], stdout=dn, stderr=subprocess.DEVNULL)
+                 for pth in paths]
+        rcs = [pr.wait() for pr in procs]
+        dt = time.perf_counter() - t0
+    for pth in paths:
+        os.unlink(pth)
+    return {"value": m / dt if not any(rcs) else None, "unit": "sites/s", "cores": P, "seconds": dt,
+            "note": f"{P} oracle processes on line-aligned shards of the same {m:,}-site sample, wall clock"}
 
 
 def cpu_and_e2e(a):
@@ -331,7 +427,10 @@ def cpu_and_e2e(a):
                 "sample": f"{m:,} sites of the {'C2' if a.method == 'local' else 'C3'} generator "
                           f"{' '.join(method_flags(a))} (seed {a.seed}, {a.depth:g}x, {size / 1e9:.2f} GB text), "
                           f"pileup text -> CSV to /dev/null, oracle/_build/sid_oracle "
-                          f"(call.cpp/lynch.hpp/stats.cpp restated, single thread), {dt:.2f} s"}
+                          f"(call.cpp/lynch.hpp/stats.cpp restated, single thread), {dt:.2f} s",
+                "cpu_model": cpu_model()}
+        if a.method == "local" and r.returncode == 0:
+            base["sharded"] = cpu_sharded(a, td, oracle.CLI)
         if not a.no_e2e and os.path.exists(sid_amd.CLI_PATH):
             e2e = {"unit": "sites/s", "sites": m, "text_bytes": size,
                    "note": "build/sid on the sample file: wall clock of the whole process (start, HIP init, "
