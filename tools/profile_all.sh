@@ -7,8 +7,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-PASSES="trace fetch write" PREFIX=local BENCH_ARGS="--steps 10 --warmup 2 --cpu-sample 0" ./tools/profile_round.sh || exit 1
-PASSES="trace fetch write" PREFIX=c3 BENCH_ARGS="--method likelihood_ratio --steps 5 --warmup 1 --cpu-sample 0" ./tools/profile_round.sh || exit 1
+PASSES="trace fetch write" PREFIX=local BENCH_ARGS="--steps 10 --warmup 2 --cpu-sample 0 --no-e2e" ./tools/profile_round.sh || exit 1
+PASSES="trace fetch write" PREFIX=c3 BENCH_ARGS="--method likelihood_ratio --steps 5 --warmup 1 --cpu-sample 0 --no-e2e" ./tools/profile_round.sh || exit 1
 python3 - <<'PY' || exit 1
 import sys
 sys.path.insert(0, ".")
