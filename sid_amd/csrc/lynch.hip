@@ -19,6 +19,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "sid_math.h"
 
@@ -741,15 +742,26 @@ __device__ __forceinline__ uint32_t sid_class_hash(uint64_t w, const unsigned lo
 // hash-probe and gather loads inside the streaming loop.
 #define SID_LOOKUP_LMISS 2048
 
-__device__ __forceinline__ uint32_t sid_lookup_rec(uint64_t w, const sid_dvec2* R, const uint8_t* C, sid_dvec2& conf)
+// record table (LDS) first; a dense-coded site that is not a record site
+// through the dense table (L2-resident, SID_DENSE_N entries) inline, before
+// the stores (an L2 hit the other waves hide; deferring it meant scattered
+// rewrites of stored lines); 0xFF: deferred to the class hash
+__device__ __forceinline__ uint32_t sid_lookup_rec(uint64_t w, const sid_dvec2* R, const uint8_t* C,
+                                                   const sid_dvec2* __restrict__ D, const uint8_t* __restrict__ DC,
+                                                   sid_dvec2& conf)
 {
-    const uint32_t r = sid_rec_code(sid_dense_code(w));
-    if (r == SID_DENSE_NONE) {
-        conf = sid_dvec2{0.0, 0.0};
-        return 0xFFu;   // deferred
+    const uint32_t d = sid_dense_code(w);
+    const uint32_t r = sid_rec_code(d);
+    if (r != SID_DENSE_NONE) {
+        conf = R[r];
+        return C[r];
     }
-    conf = R[r];
-    return C[r];
+    if (D && d != SID_DENSE_NONE) {
+        conf = D[d];
+        return DC[d];
+    }
+    conf = sid_dvec2{0.0, 0.0};
+    return 0xFFu;   // deferred
 }
 
 template <int U>
@@ -763,8 +775,10 @@ __global__ __launch_bounds__(1024) void sid_lookup_rec_kernel(const ulonglong2* 
                                                               const sid_dvec2* __restrict__ cc,
                                                               uint16_t* __restrict__ code2,
                                                               sid_dvec2* __restrict__ hom,
-                                                              sid_dvec2* __restrict__ het)
+                                                              sid_dvec2* __restrict__ het, bool dense_inline)
 {
+    const sid_dvec2* D = dense_inline ? g_rec + SID_REC_N : nullptr;
+    const uint8_t* DC = g_rcode + SID_REC_N;
     __shared__ sid_dvec2 R[SID_REC_N];
     __shared__ uint8_t C[SID_REC_N];
     __shared__ unsigned long long lmiss[SID_LOOKUP_LMISS];
@@ -806,8 +820,8 @@ __global__ __launch_bounds__(1024) void sid_lookup_rec_kernel(const ulonglong2* 
             const size_t p = base + (size_t)j * blockDim.x + threadIdx.x;
             if (p < npairs) {
                 sid_dvec2 ca, cb;
-                const uint32_t ka = sid_lookup_rec(c[j].x, R, C, ca);
-                const uint32_t kb = sid_lookup_rec(c[j].y, R, C, cb);
+                const uint32_t ka = sid_lookup_rec(c[j].x, R, C, D, DC, ca);
+                const uint32_t kb = sid_lookup_rec(c[j].y, R, C, D, DC, cb);
                 code2[p] = (uint16_t)(ka | (kb << 8));
                 hom[p] = sid_dvec2{ca.x, cb.x};
                 het[p] = sid_dvec2{ca.y, cb.y};
@@ -829,15 +843,16 @@ __global__ __launch_bounds__(1024) void sid_lookup_rec_kernel(const ulonglong2* 
 }
 
 // record tables from the dense class index: rec[r] = {p1, p2}, rcode[r] =
-// code of the class of record code r (0x40 / zeros: no class)
+// code of the class of record code r (0x40 / zeros: no class); then, at
+// SID_REC_N + d, the same for every dense code d
 __global__ __launch_bounds__(256) void sid_rec_build_kernel(const uint32_t* __restrict__ dense_cidx,
                                                             const uint8_t* __restrict__ pcode,
                                                             const sid_dvec2* __restrict__ cc,
                                                             sid_dvec2* __restrict__ rec, uint8_t* __restrict__ rcode)
 {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= SID_REC_N) return;
-    const uint32_t idx = dense_cidx[sid_rec_dense(r)];
+    if (r >= SID_REC_N + SID_DENSE_N) return;
+    const uint32_t idx = dense_cidx[r < SID_REC_N ? sid_rec_dense(r) : r - SID_REC_N];
     rec[r] = idx == SID_DENSE_NONE ? sid_dvec2{0.0, 0.0} : cc[idx];
     rcode[r] = idx == SID_DENSE_NONE ? (uint8_t)0x40 : pcode[idx];
 }
@@ -1240,8 +1255,8 @@ hipError_t sid_launch_bh_label(const double* adj_het, size_t m, double sig, uint
 hipError_t sid_launch_rec_build(const uint32_t* dense_cidx, const uint8_t* pcode, const double* cc, double* rec,
                                 uint8_t* rcode, hipStream_t st)
 {
-    sid_rec_build_kernel<<<SID_REC_N / 256, 256, 0, st>>>(dense_cidx, pcode, (const sid_dvec2*)cc, (sid_dvec2*)rec,
-                                                          rcode);
+    sid_rec_build_kernel<<<(SID_REC_N + SID_DENSE_N) / 256, 256, 0, st>>>(dense_cidx, pcode, (const sid_dvec2*)cc,
+                                                                          (sid_dvec2*)rec, rcode);
     return hipGetLastError();
 }
 
@@ -1311,10 +1326,15 @@ hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned lo
         const int U = 2;
         size_t want = (npairs + (size_t)1024 * U - 1) / ((size_t)1024 * U);
         const unsigned grid = (unsigned)(want < 1024 ? want : 1024);
+        // SID_LOOKUP_INLINE=0: defer every non-record site to the block tail (A/B)
+        static const bool dense_inline = [] {
+            const char* e = std::getenv("SID_LOOKUP_INLINE");
+            return !e || std::atoi(e) != 0;
+        }();
         sid_lookup_rec_kernel<2><<<grid, 1024, 0, st>>>((const ulonglong2*)counts, npairs, (const sid_dvec2*)rec,
                                                         rcode, ckeys, cidx, cmask, special_idx, pcode,
                                                         (const sid_dvec2*)cc, (uint16_t*)code, (sid_dvec2*)hom,
-                                                        (sid_dvec2*)het);
+                                                        (sid_dvec2*)het, dense_inline);
         done = 2 * npairs;
     }
     if (done < n) {

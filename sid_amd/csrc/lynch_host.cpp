@@ -143,8 +143,8 @@ struct sid_lynch_dev {
     double* d_lg = nullptr;                // device copy of lg
     size_t d_lg_n = 0;
     double* d_cc = nullptr;                // {p1, p2} per class, packed for the gather
-    double* d_rec = nullptr;               // {p1, p2} per record code (sid_math.h), SID_REC_N
-    uint8_t* d_rcode = nullptr;            // code per record code
+    double* d_rec = nullptr;               // {p1, p2} per record code (sid_math.h), SID_REC_N, then per dense code
+    uint8_t* d_rcode = nullptr;            // code per record code, then per dense code
     void* d_bhws = nullptr;                // device BH scratch (radix sort)
     size_t bhws_bytes = 0;
     int* d_odd = nullptr;                  // BH saw NaN / -0 p-values: host BH instead
@@ -1098,8 +1098,8 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     HIPCHECK(sid_launch_class_tables(L->d_keys, (uint32_t)U, L->d_dense_cidx, L->d_ckeys, L->d_cidx, L->cmask, 0));
     HIPCHECK(sid_launch_pack_class(L->d_c1, L->d_c2, U, L->d_cc, 0));
     if (!L->d_rec) {
-        HIPCHECK(hipMalloc(&L->d_rec, SID_REC_N * 16));
-        HIPCHECK(hipMalloc(&L->d_rcode, SID_REC_N));
+        HIPCHECK(hipMalloc(&L->d_rec, (SID_REC_N + SID_DENSE_N) * 16));
+        HIPCHECK(hipMalloc(&L->d_rcode, SID_REC_N + SID_DENSE_N));
     }
     HIPCHECK(sid_launch_rec_build(L->d_dense_cidx, L->d_pcode, L->d_cc, L->d_rec, L->d_rcode, 0));
     HIPCHECK(hipStreamSynchronize(0));
