@@ -46,7 +46,7 @@ namespace {
 struct Options {
     std::string method = "local";
     sid_opts o;
-    int devices = 1;
+    int devices = 0;   // 0: every visible device
     int threads = 0;
     bool stats = false;
     bool host_parse = false;   // parse and format on the host (sid_parse_text / sid_format_csv)
@@ -258,7 +258,7 @@ int main(int argc, char** argv)
     }
     // shard d runs on device d % ndev (more shards than devices: a
     // multi-device run's splitting and merging on fewer GPUs)
-    const int D = std::max(1, opt.devices);
+    const int D = opt.devices > 0 ? opt.devices : ndev;
     const bool quality = method == SID_METHOD_QUALITY;
     // the Lynch estimate: LR and bayes always, local and quality with -R
     const bool lynch = method == SID_METHOD_LIKELIHOOD_RATIO || method == SID_METHOD_BAYES || opt.o.estimate_prior;

@@ -13,7 +13,11 @@
 #include "../../include/sid.h"
 #include "../../sid_amd/csrc/sid_math.h"
 
-enum { LOADS = 0, LDS = 1, LDS_RAW = 2, FB = 3, FULL = 4, WAVEAGG = 5 };
+enum { LOADS = 0, LDS = 1, LDS_RAW = 2, FB = 3, FULL = 4, WAVEAGG = 5, LDSROW = 6, LDSLIST = 7 };
+
+extern "C" hipError_t sid_launch_hist_dense(const uint16_t* counts, size_t n, uint32_t* part, unsigned long long* dense,
+                                            unsigned long long* list, uint64_t cap, unsigned long long* ctr,
+                                            int grid_max, hipStream_t st);
 
 __device__ __forceinline__ uint64_t key_of(uint64_t w)
 {
@@ -42,6 +46,9 @@ __global__ __launch_bounds__(1024) void probe(const ulonglong2* __restrict__ pai
                                               uint32_t* sink)
 {
     __shared__ uint32_t H[SID_DENSE_N];
+    __shared__ unsigned long long llist[1024];
+    __shared__ uint32_t lcnt;
+    if (threadIdx.x == 0) lcnt = 0;
     for (uint32_t i = threadIdx.x; i < SID_DENSE_N; i += blockDim.x) H[i] = 0;
     __syncthreads();
     uint32_t acc = 0;
@@ -77,15 +84,20 @@ __global__ __launch_bounds__(1024) void probe(const ulonglong2* __restrict__ pai
             const uint32_t d = sid_dense_code(w[k]);
             const bool fb = v[k] && d == SID_DENSE_NONE;
             if (MODE == LOADS) acc += d;
-            if (MODE == LDS || MODE == FB || MODE == FULL)
+            if (MODE == LDS || MODE == FB || MODE == FULL || MODE == LDSROW || MODE == LDSLIST)
                 if (v[k] && !fb) atomicAdd(&H[sid_dense_slot(d)], 1u);
+            if (MODE == LDSLIST && fb) {
+                const uint32_t slot = atomicAdd(&lcnt, 1u);
+                if (slot < 1024) llist[slot] = key_of(w[k]);
+            }
             if (MODE == LDS_RAW)
                 if (v[k] && !fb) atomicAdd(&H[d], 1u);
             if (MODE == FB || MODE == FULL) fb_append(fb, key_of(w[k]), list, cap, ctr);
         }
     }
     __syncthreads();
-    if (MODE == FULL || MODE == WAVEAGG) {
+    if (MODE == LDSLIST && threadIdx.x < (lcnt < 1024 ? lcnt : 1024)) list[blockIdx.x * 1024 + threadIdx.x] = llist[threadIdx.x];
+    if (MODE == FULL || MODE == WAVEAGG || MODE == LDSROW || MODE == LDSLIST) {
         uint32_t* row = part + (size_t)blockIdx.x * SID_DENSE_N;
         for (uint32_t i = threadIdx.x; i < SID_DENSE_N; i += blockDim.x) row[i] = H[sid_dense_slot(i)];
     } else {
@@ -109,6 +121,9 @@ int main()
     hipMalloc(&list, (1ull << 22) * 8);
     hipMalloc(&ctr, 8);
     hipMalloc(&sink, 4);
+    unsigned long long* dense;
+    hipMalloc(&dense, 16ull * SID_DENSE_N * 8);
+    hipMemset(dense, 0, 16ull * SID_DENSE_N * 8);
     sid_synth_counts(ctx, 3, 30.0, 0, n, counts, nullptr);
     hipDeviceSynchronize();
     hipEvent_t e0, e1;
@@ -139,7 +154,10 @@ int main()
         timeit([&] { probe<LDS_RAW><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "lds_raw", grid);
         timeit([&] { probe<FB><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "fb", grid);
         timeit([&] { probe<FULL><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "full", grid);
-        timeit([&] { probe<WAVEAGG><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "waveagg", grid);
+        timeit([&] { probe<LDSROW><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "lds+row", grid);
+        timeit([&] { probe<LDSLIST><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "lds+row+llist", grid);
+        timeit([&] { (void)sid_launch_hist_dense(counts, n, part, dense, list, 1 << 22, ctr, grid, nullptr); },
+               "product(dense+reduce)", grid);
     }
     sid_destroy(ctx);
     return 0;
