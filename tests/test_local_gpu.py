@@ -98,3 +98,41 @@ def test_unaligned_device_pointers(gpu, oracle, sid):
 def test_empty_input(gpu):
     code, hom, het = gpu.run_local(np.zeros((0, 4), np.uint16))
     assert len(code) == 0
+
+
+def _table_coverage_profiles():
+    """Every (nf, ns, r2) class around the table borders: nf across the LDS
+    (256) and second-level (512) limits, ns across 8 and 128, the minor
+    counts split over two bases across r2 = 4 and 8, the major in every
+    position."""
+    rows = []
+    for nf in (0, 1, 30, 200, 255, 256, 257, 300, 511, 512, 513, 700, 1023):
+        for ns in (0, 1, 7, 8, 9, 63, 64, 100, 127, 128, 129):
+            if ns > nf:
+                continue
+            for r2 in (0, 1, 3, 4, 5, 7, 8, 9, 20):
+                a = min(r2, ns)
+                b = r2 - a
+                if b > ns:
+                    continue
+                for f in range(4):
+                    p = [ns, a, b]
+                    p.insert(f, nf)
+                    rows.append(p)
+    return np.array(rows, np.uint16)
+
+
+@pytest.mark.parametrize("tail", ["1", "0"])
+def test_second_level_table_borders(gpu, oracle, sid, monkeypatch, tail):
+    """Sites the LDS class table misses, resolved inline through the
+    second-level table (SID_TABLE_TAIL=1, the default) or all by the fix-up
+    kernel (0): the same outputs as the oracle either way, at the borders of
+    both tables and mixed into 30x/200x streams."""
+    monkeypatch.setenv("SID_TABLE_TAIL", tail)   # read when the context is created
+    border = _table_coverage_profiles()
+    rng = np.random.default_rng(17)
+    counts = np.concatenate([sid.synth_counts_host(5, 60_000, 200.0), border,
+                             sid.synth_counts_host(2, 60_000, 30.0)])
+    counts = counts[rng.permutation(len(counts))]
+    check(gpu, oracle, counts, f"table borders tail={tail}")
+    check(gpu, oracle, border, f"table borders only tail={tail}", snp_prior=1e-3, site_error_threshold=0.05)

@@ -182,3 +182,25 @@ def test_context_reuse_and_unaligned_lookup(gpu, sid, oracle):
     rc, rcode, rhom, rhet, rest, u = oracle.call_method(counts, "likelihood_ratio", estimate_prior=True)
     for code, hom, het in res:
         assert_parity(code, hom, het, rcode, rhom, rhet, what="reuse/unaligned")
+
+
+@pytest.mark.parametrize("depth,n,seed", [(30.0, 80_000, 3), (200.0, 20_000, 5)])
+def test_prefetch_policy_keeps_trajectory(gpu, sid, oracle, monkeypatch, depth, n, seed):
+    """The Nelder-Mead prefetch (the next iteration's candidates evaluated
+    with the current ones, SID_NM_LOOKAHEAD=1; four points per launch with 0)
+    only changes how many launches the estimate takes: the same (pi, eps),
+    iterations, evaluations and outputs, equal to the oracle's."""
+    counts = sid.synth_counts_host(seed, n, depth)
+    res = {}
+    for la in ("0", "1"):
+        monkeypatch.setenv("SID_NM_LOOKAHEAD", la)   # read when the profiles are set up
+        res[la] = gpu.run_method(counts, "likelihood_ratio", estimate_prior=True)
+    (c0, h0, t0, e0), (c1, h1, t1, e1) = res["0"], res["1"]
+    assert (e0.heterozygosity, e0.error_rate, e0.iterations, e0.evaluations) == \
+        (e1.heterozygosity, e1.error_rate, e1.iterations, e1.evaluations)
+    assert np.array_equal(c0, c1) and np.array_equal(h0.view(np.int64), h1.view(np.int64)) \
+        and np.array_equal(t0.view(np.int64), t1.view(np.int64))
+    rc, rcode, rhom, rhet, rest, u = oracle.call_method(counts, "likelihood_ratio", estimate_prior=True)
+    assert (e1.heterozygosity, e1.error_rate, e1.iterations) == (rest.heterozygosity, rest.error_rate,
+                                                                 rest.iterations)
+    assert_parity(c1, h1, t1, rcode, rhom, rhet, what=f"prefetch {depth}x")

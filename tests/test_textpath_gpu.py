@@ -179,3 +179,24 @@ def test_parse_fd_equals_host(gpu, sid, tmp_path, n, threads, offset_lines):
     assert len(t) == len(s)
     counts = gpu.device_view(t.counts_ptr, (len(t), 4)).cpu().numpy().view(np.uint16)
     assert np.array_equal(counts, s.counts)
+
+
+def test_large_text_multi_block_scans(gpu, sid):
+    """1.2M sites: the line-index scan (4 KiB tiles) and the record-offset scan
+    (256 records per block) both span several 4096-element scan blocks."""
+    import torch
+    n = 1_200_000
+    text = sid.synth_text(29, n, 30.0, sites_per_chrom=400_000)
+    ctx, t, counts = dparse(gpu, sid, text)
+    s = sid.parse_text(text)
+    assert len(t) == len(s) == n
+    assert np.array_equal(counts, s.counts)
+    rng = np.random.default_rng(8)
+    code = (rng.integers(0, 256, n).astype(np.uint8) & 0x8F)
+    hom = rng.random(n) ** 8
+    het = np.where(rng.random(n) < 0.5, 1.0, rng.random(n) * 1e-7)
+    dc = torch.from_numpy(code).cuda()
+    dh = torch.from_numpy(hom).cuda()
+    dt = torch.from_numpy(het).cuda()
+    got = t.format(dc.data_ptr(), dh.data_ptr(), dt.data_ptr(), "p_value")
+    assert got == sid.format_csv(s, code, hom, het, "p_value")
