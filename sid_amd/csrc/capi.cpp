@@ -133,6 +133,7 @@ extern "C" int sid_create(int device, const sid_opts* opts, sid_ctx** out)
     if (const char* g = std::getenv("SID_LOCAL_DIRECT")) c->ws.direct = std::atoi(g) != 0;
     if (const char* g = std::getenv("SID_TABLE_UNROLL")) c->ws.unroll = std::atoi(g);
     if (const char* g = std::getenv("SID_TABLE_NT")) c->ws.nt = std::atoi(g) != 0;
+    if (const char* g = std::getenv("SID_TABLE_CHUNK")) c->ws.chunk = std::atoi(g) != 0;
     if (const char* g = std::getenv("SID_TABLE_TAIL")) c->ws.tail = std::atoi(g) != 0;
 
     std::vector<double> lnt(SID_LUTN);

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __r
                                                            const double* __restrict__ g_table, double sig,
                                                            const double* __restrict__ T2,
                                                            uint32_t* __restrict__ miss, uint32_t cap,
-                                                           uint32_t* __restrict__ ctr)
+                                                           uint32_t* __restrict__ ctr, bool chunk)
 {
     __shared__ double T[SID_TAB_N];
     __shared__ uint32_t lmiss[SID_LMISS];
@@ -303,7 +303,16 @@ __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __r
     if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
     const size_t tile = (size_t)blockDim.x * U;
-    for (size_t base = (size_t)blockIdx.x * tile; base < npairs; base += (size_t)gridDim.x * tile) {
+    // tiles of this block: grid-stride, or (chunk) one contiguous range
+    const size_t ntiles = (npairs + tile - 1) / tile;
+    size_t tb = blockIdx.x, te = ntiles, ts = gridDim.x;
+    if (chunk) {
+        tb = ntiles * blockIdx.x / gridDim.x;
+        te = ntiles * (blockIdx.x + 1) / gridDim.x;
+        ts = 1;
+    }
+    for (size_t t = tb; t < te; t += ts) {
+        const size_t base = t * tile;
         ulonglong2 c[U];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
@@ -471,12 +480,12 @@ extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t
             auto* H = (sid_dvec2*)hom;
             auto* Q = (sid_dvec2*)het;
             const double* T2 = ws->tail ? ws->table2 : nullptr;
-            if (U == 1 && !ws->nt) sid_local_table_p2<1, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
-            else if (U == 1) sid_local_table_p2<1, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
-            else if (U == 4 && !ws->nt) sid_local_table_p2<4, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
-            else if (U == 4) sid_local_table_p2<4, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
-            else if (!ws->nt) sid_local_table_p2<2, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
-            else sid_local_table_p2<2, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr);
+            if (U == 1 && !ws->nt) sid_local_table_p2<1, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
+            else if (U == 1) sid_local_table_p2<1, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
+            else if (U == 4 && !ws->nt) sid_local_table_p2<4, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
+            else if (U == 4) sid_local_table_p2<4, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
+            else if (!ws->nt) sid_local_table_p2<2, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
+            else sid_local_table_p2<2, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
             done = npairs * 2;
         }
         if (done < n) {

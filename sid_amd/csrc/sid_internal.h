@@ -25,10 +25,11 @@ struct sid_local_ws {
     uint32_t cap = 0;            // miss list capacity
     uint32_t* ctr = nullptr;     // [2] miss counters, alternating per call
     int parity = 0;
-    int table_grid = 1024;       // blocks of the table kernel (2 resident per CU)
+    int table_grid = 4096;       // blocks of the table kernel (2 resident per CU; 8 rounds)
     int direct = 0;              // SID_LOCAL_DIRECT=1: bypass the table (A/B)
-    int unroll = 2;              // SID_TABLE_UNROLL: pairs per thread per tile (1, 2, 4)
+    int unroll = 1;              // SID_TABLE_UNROLL: pairs per thread per tile (1, 2, 4)
     int nt = 0;                  // SID_TABLE_NT=1: non-temporal output stores
+    int chunk = 0;               // SID_TABLE_CHUNK=1: one contiguous tile range per block
     int tail = 1;                // SID_TABLE_TAIL=0: no inline second-level lookup, every miss to the fix-up (A/B)
     hipEvent_t ev_mid = nullptr; // set only while timing: recorded between main and fix-up
 };

@@ -27,11 +27,13 @@ def main():
     het = torch.empty(n, dtype=torch.float64, device=dev)
     st = torch.cuda.current_stream(dev)
     variants = [dict(SID_LOCAL_DIRECT="1")]
-    for u, nt, g in itertools.product(["1", "2", "4"], ["0", "1"], ["256", "512", "1024"]):
-        variants.append(dict(SID_TABLE_UNROLL=u, SID_TABLE_NT=nt, SID_TABLE_GRID=g))
+    grids = os.environ.get("SWEEP_GRIDS", "512,1024,2048,4096,8192").split(",")
+    unrolls = os.environ.get("SWEEP_UNROLLS", "1,2").split(",")
+    for u, nt, g, ch in itertools.product(unrolls, ["0", "1"], grids, ["0", "1"]):
+        variants.append(dict(SID_TABLE_UNROLL=u, SID_TABLE_NT=nt, SID_TABLE_GRID=g, SID_TABLE_CHUNK=ch))
     ctxs = []
     for v in variants:
-        for k in ("SID_LOCAL_DIRECT", "SID_TABLE_UNROLL", "SID_TABLE_NT", "SID_TABLE_GRID"):
+        for k in ("SID_LOCAL_DIRECT", "SID_TABLE_UNROLL", "SID_TABLE_NT", "SID_TABLE_GRID", "SID_TABLE_CHUNK"):
             os.environ.pop(k, None)
         os.environ.update(v)
         ctxs.append(sid_amd.Context(0))
