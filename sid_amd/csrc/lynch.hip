@@ -19,9 +19,11 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cfloat>
 #include <cstdlib>
 
 #include "sid_math.h"
+#include "sid_nm.h"
 
 #define SID_EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
 #define SID_LN_LDBL_TRUE_MIN (-SID_LDBL_DENORM_SHIFT)
@@ -404,6 +406,7 @@ struct sid_dense_src {
 
 __device__ __forceinline__ double sid_lse2(double a, double b)
 {
+    if (isnan(a) || isnan(b)) return a + b;   // NaN operands propagate (fmax would drop them)
     double m = fmax(a, b);
     if (m == -__builtin_inf()) return m;
     return m + log1p(exp(fmin(a, b) - m));
@@ -459,7 +462,12 @@ __device__ __forceinline__ void sid_mixture(uint64_t key, const sid_lynch_eval& 
             mu = fmax(mu, u[k]);
             ++k;
         }
-    if (mu != -__builtin_inf()) {
+    if (E.lnorm == __builtin_inf()) {
+        // one base only in the distribution: every d_i d_j is 0 and so is
+        // 1 - sum d^2, so the reference's het likelihood is 0/0 = -nan
+        // (lynch.hpp:70-72), and so is every L that contains it
+        s_het = -__builtin_nan("");
+    } else if (mu != -__builtin_inf()) {
         double a2 = 0.0;
 #pragma unroll
         for (int q = 0; q < 6; ++q) a2 += exp(u[q] - mu);
@@ -483,26 +491,17 @@ __device__ __forceinline__ void sid_two_sum(double a, double b, double& s, doubl
 // same-address atomic: +7 us per launch at 188 blocks) and than block
 // partials written straight to host-mapped memory and folded by the host
 // (+1.7 us per round trip) (tools/debug/obj_probe.hip).
-__global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __restrict__ keys,
-                                                            const uint32_t* __restrict__ cnt,
-                                                            const double* __restrict__ lnM, size_t u,
-                                                            sid_lynch_evals EV, double* __restrict__ partial)
+// sum count * ln L over one slice of the profiles (i = slice*256 + tid +
+// j*nslices*256) reduced over the block in double-double; the result is in
+// thread 0.  blockDim.x == 256.
+__device__ __forceinline__ void sid_objective_slice(const uint64_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ cnt,
+                                                    const double* __restrict__ lnM, size_t u, size_t slice,
+                                                    size_t nslices, const sid_lynch_eval& E, double& H,
+                                                    double& Lo)
 {
-    const int pt = blockIdx.y;
-    sid_lynch_eval E;
-    E.la = EV.p[pt].la;
-    E.lb = EV.p[pt].lb;
-    E.lh = EV.p[pt].lh;
-    E.l1p = EV.p[pt].l1p;
-    E.lp = EV.p[pt].lp;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) E.ld[i] = EV.ld[i];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) E.ldd[i] = EV.ldd[i];
-    E.lnorm = EV.lnorm;
     double hi = 0.0, lo = 0.0;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < u;
-         i += (size_t)gridDim.x * blockDim.x) {
+    for (size_t i = slice * blockDim.x + threadIdx.x; i < u; i += nslices * blockDim.x) {
         double sh, st;
         sid_mixture(keys[i], E, sh, st);
         // L = (1-pi) M S_hom + pi M S_het  (lynch.cpp:46-47); M multiplies last
@@ -535,13 +534,38 @@ __global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __re
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        double H = 0.0, Lo = 0.0;
+        H = 0.0;
+        Lo = 0.0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
             double s, e;
             sid_two_sum(H, sh_hi[w], s, e);
             H = s;
             Lo += sh_lo[w] + e;
         }
+    }
+    __syncthreads();   // sh_hi/sh_lo reusable
+}
+
+__global__ __launch_bounds__(256) void sid_objective_kernel(const uint64_t* __restrict__ keys,
+                                                            const uint32_t* __restrict__ cnt,
+                                                            const double* __restrict__ lnM, size_t u,
+                                                            sid_lynch_evals EV, double* __restrict__ partial)
+{
+    const int pt = blockIdx.y;
+    sid_lynch_eval E;
+    E.la = EV.p[pt].la;
+    E.lb = EV.p[pt].lb;
+    E.lh = EV.p[pt].lh;
+    E.l1p = EV.p[pt].l1p;
+    E.lp = EV.p[pt].lp;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) E.ld[i] = EV.ld[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) E.ldd[i] = EV.ldd[i];
+    E.lnorm = EV.lnorm;
+    double H, Lo;
+    sid_objective_slice(keys, cnt, lnM, u, blockIdx.x, gridDim.x, E, H, Lo);
+    if (threadIdx.x == 0) {
         double* part = partial + ((size_t)pt * gridDim.x + blockIdx.x) * 2;
         part[0] = H;
         part[1] = Lo;
@@ -593,6 +617,444 @@ __global__ __launch_bounds__(256) void sid_objective_fold_kernel(const double* _
     out[2 * pt + 1] = e;
     __threadfence_system();
     seq_out[pt] = seq;
+}
+
+// ------------------------------------------------ device-resident estimate --
+// estimateProfileGenotypeLikelihoods (lynch.cpp:17-35) + FunctionMinimizer
+// (optimization.hpp:50-89) in one cooperative launch: G co-resident blocks
+// evaluate the objective for the points Nelder-Mead asks for (work items =
+// point x 256-profile slice, the slices of sid_objective_kernel), meet at a
+// grid barrier, and every block folds the partials and advances its own copy
+// of the simplex (sid_nm.h arithmetic) — the same values in every block, so
+// they all request the same points next and stop together: one barrier per
+// round and no host round trip.
+//
+// The simplex is advanced by wave 0 of each block with all 64 lanes running
+// the same (uniform) code on register-resident state; the value cache is
+// lane-distributed (lane i holds entry i), so a lookup is one compare and a
+// ballot instead of a serial scan.  An iteration whose candidate values are
+// not all known is undone and its candidates (with lookahead: also the next
+// iteration's) become the next round's points; earlier values stay cached,
+// so the replay after the round takes the exact path the host driver takes.
+// Every wait is bounded by a wall-clock deadline: on expiry the kernel sets
+// an abort flag that every block polls, all blocks leave, and the host falls
+// back to the host driver.
+#define SID_NM_MAX_ROUNDS 4096
+#define SID_NM_ITER_MAX 1000   // optimization.hpp:79 (i < 1000)
+
+// wave-0 controller state: uniform across the wave except the cache
+struct sid_nmw {
+    sid_nm_simplex S;
+    int phase;   // 0: simplex not set, 1: iterating
+    int iter;
+    int state;   // 0 running, else 16 + sid_nm_result.status
+    int converged;
+    unsigned long long evals;
+    double x[2], fval, size;
+    double cx, cy, cv;   // this lane's cache entry
+    int cn, chead;
+    double rx, ry;       // this lane's point of the next round
+    int npts;
+};
+
+// what wave 0 posts for a round (LDS)
+struct sid_nm_round {
+    int go;
+    int npts, ne;
+    double pts[SID_OBJ_PTS][2];
+    double val[SID_OBJ_PTS];
+    int evl[SID_OBJ_PTS];
+    sid_lynch_pt prm[SID_OBJ_PTS];
+};
+
+__device__ __forceinline__ int sid_lane() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ bool sid_nmw_get(const sid_nmw& w, const double* x, double& v)
+{
+    const bool hit = sid_lane() < w.cn && w.cx == x[0] && w.cy == x[1];
+    const unsigned long long m = __ballot(hit);
+    if (!m) return false;
+    v = __shfl(w.cv, __ffsll((unsigned long long)m) - 1, 64);
+    return true;
+}
+
+__device__ __forceinline__ void sid_nmw_put(sid_nmw& w, double x0, double x1, double v)
+{
+    if (sid_lane() == w.chead) {
+        w.cx = x0;
+        w.cy = x1;
+        w.cv = v;
+    }
+    w.chead = (w.chead + 1) & 63;
+    if (w.cn < 64) ++w.cn;
+}
+
+// appends x to the lane-held point list unless present or full
+__device__ __forceinline__ void sid_nmw_add(sid_nmw& w, const double* x)
+{
+    const bool dup = sid_lane() < w.npts && w.rx == x[0] && w.ry == x[1];
+    if (__ballot(dup)) return;
+    if (w.npts >= SID_OBJ_PTS) return;
+    if (sid_lane() == w.npts) {
+        w.rx = x[0];
+        w.ry = x[1];
+    }
+    ++w.npts;
+}
+
+// the points of the next round: the iteration's candidates (+ lookahead, as
+// sid_nm_request) that are not cached
+__device__ __forceinline__ void sid_nmw_request(sid_nmw& w, bool lookahead)
+{
+    w.npts = 0;
+    int hi, s_hi, lo;
+    sid_nm_order(w.S, hi, s_hi, lo);
+    double c1[4][SID_NM_N];
+    sid_nm_candidates(w.S, hi, c1);
+    double t;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (!sid_nmw_get(w, c1[i], t)) sid_nmw_add(w, c1[i]);
+    if (!lookahead) return;
+    for (int o = 0; o < 4; ++o) {
+        sid_nm_simplex s = w.S;
+        if (o == 0) sid_nm_update_point(s, hi, c1[0], 0.0);   // reflection accepted
+        if (o == 1) sid_nm_update_point(s, hi, c1[1], 0.0);   // expansion accepted
+        if (o == 2) {                                         // outside contraction
+            sid_nm_update_point(s, hi, c1[0], 0.0);
+            sid_nm_update_point(s, hi, c1[3], 0.0);
+        }
+        if (o == 3) sid_nm_update_point(s, hi, c1[2], 0.0);   // inside contraction
+        for (int q = 0; q < 2; ++q) {
+            const int h2 = q == 0 ? s_hi : hi;
+            if (h2 == hi && o < 2) continue;
+            double c2[4][SID_NM_N];
+            sid_nm_candidates(s, h2, c2);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (!sid_nmw_get(w, c2[i], t)) sid_nmw_add(w, c2[i]);
+        }
+    }
+}
+
+// nmsimplex2_set with the three start values known; 1: need, -1: non-finite
+__device__ __forceinline__ int sid_nmw_try_set(sid_nmw& w, const double* x, const double* step)
+{
+    const double p0[2] = {x[0], x[1]}, p1[2] = {x[0] + step[0], x[1]}, p2[2] = {x[0], x[1] + step[1]};
+    double v0, v1, v2;
+    const bool h0 = sid_nmw_get(w, p0, v0), h1 = sid_nmw_get(w, p1, v1), h2 = sid_nmw_get(w, p2, v2);
+    if (!(h0 && h1 && h2)) {
+        w.npts = 0;
+        if (!h0) sid_nmw_add(w, p0);
+        if (!h1) sid_nmw_add(w, p1);
+        if (!h2) sid_nmw_add(w, p2);
+        return 1;
+    }
+    // f(x), then f(x + step_i e_i) in order, stopping at the first non-finite
+    ++w.evals;
+    if (!isfinite(v0)) return -1;
+    ++w.evals;
+    if (!isfinite(v1)) return -1;
+    ++w.evals;
+    if (!isfinite(v2)) return -1;
+    w.S.x1[0][0] = p0[0];
+    w.S.x1[0][1] = p0[1];
+    w.S.x1[1][0] = p1[0];
+    w.S.x1[1][1] = p1[1];
+    w.S.x1[2][0] = p2[0];
+    w.S.x1[2][1] = p2[1];
+    w.S.y1[0] = v0;
+    w.S.y1[1] = v1;
+    w.S.y1[2] = v2;
+    sid_nm_compute_center(w.S);
+    w.size = sid_nm_compute_size(w.S);
+    return 0;
+}
+
+// nmsimplex2_iterate on a copy of the simplex, committed only when every value
+// it asks for is known.  0: done, 1: need (points listed), -1: contraction failed
+__device__ __forceinline__ int sid_nmw_try_iterate(sid_nmw& w, bool lookahead)
+{
+    sid_nm_simplex t = w.S;
+    unsigned long long ev = 0;
+    int hi, s_hi, lo;
+    sid_nm_order(t, hi, s_hi, lo);
+    double xc[2], xc2[2], val, val2;
+    bool miss = false;
+    sid_nm_corner_point(t, -1.0, hi, xc);
+    ++ev;
+    if (!sid_nmw_get(w, xc, val)) miss = true;
+    if (!miss) {
+        if (isfinite(val) && val < t.y1[lo]) {
+            sid_nm_corner_point(t, -2.0, hi, xc2);
+            ++ev;
+            if (!sid_nmw_get(w, xc2, val2)) {
+                miss = true;
+            } else if (isfinite(val2) && val2 < t.y1[lo]) {
+                sid_nm_update_point(t, hi, xc2, val2);
+            } else {
+                sid_nm_update_point(t, hi, xc, val);
+            }
+        } else if (!isfinite(val) || val > t.y1[s_hi]) {
+            if (isfinite(val) && val <= t.y1[hi]) sid_nm_update_point(t, hi, xc, val);
+            sid_nm_corner_point(t, 0.5, hi, xc2);
+            ++ev;
+            if (!sid_nmw_get(w, xc2, val2)) {
+                miss = true;
+            } else if (isfinite(val2) && val2 <= t.y1[hi]) {
+                sid_nm_update_point(t, hi, xc2, val2);
+            } else {
+                // contract_by_best(lo): the two other vertices move halfway
+                // to the best one (x1[lo] itself does not move)
+                const int a = lo == 0 ? 1 : 0, b = lo == 2 ? 1 : 2;
+                double pa[2], pb[2], va, vb;
+                for (int j = 0; j < SID_NM_N; ++j) {
+                    pa[j] = 0.5 * (t.x1[a][j] + t.x1[lo][j]);
+                    pb[j] = 0.5 * (t.x1[b][j] + t.x1[lo][j]);
+                }
+                const bool ha = sid_nmw_get(w, pa, va), hb = sid_nmw_get(w, pb, vb);
+                if (!(ha && hb)) {
+                    w.npts = 0;
+                    if (!ha) sid_nmw_add(w, pa);
+                    if (!hb) sid_nmw_add(w, pb);
+                    return 1;
+                }
+                for (int j = 0; j < SID_NM_N; ++j) {
+                    t.x1[a][j] = pa[j];
+                    t.x1[b][j] = pb[j];
+                }
+                ev += 2;
+                t.y1[a] = va;
+                t.y1[b] = vb;
+                const bool ok = isfinite(va) && isfinite(vb);
+                sid_nm_compute_center(t);
+                sid_nm_compute_size(t);
+                if (!ok) return -1;
+            }
+        } else {
+            sid_nm_update_point(t, hi, xc, val);
+        }
+    }
+    if (miss) {
+        sid_nmw_request(w, lookahead);
+        return 1;
+    }
+    w.S = t;
+    w.evals += ev;
+    const int imin = sid_nm_min_index(w.S);
+    w.x[0] = w.S.x1[imin][0];
+    w.x[1] = w.S.x1[imin][1];
+    w.fval = w.S.y1[imin];
+    w.size = w.S.S2 > 0 ? sqrt(w.S.S2) : sid_nm_compute_size(w.S);
+    return 0;
+}
+
+// runs the algorithm as far as the known values allow (wave 0, uniform)
+__device__ __forceinline__ void sid_nmw_advance(sid_nmw& w, const double* x0, const double* step, bool lookahead)
+{
+    w.npts = 0;
+    while (w.state == 0) {
+        if (w.phase == 0) {
+            const int r = sid_nmw_try_set(w, x0, step);
+            if (r == 1) break;
+            if (r < 0) {
+                w.state = 16 + 1;
+                break;
+            }
+            w.phase = 1;
+            continue;
+        }
+        const int r = sid_nmw_try_iterate(w, lookahead);
+        if (r == 1) break;
+        ++w.iter;
+        if (r < 0) {
+            w.state = 16 + 1;   // "contraction failed"
+            break;
+        }
+        if (w.size < 1e-5) {
+            w.state = 16;
+            w.converged = 1;
+        } else if (w.iter >= SID_NM_ITER_MAX) {
+            w.state = 16;
+            w.converged = 0;
+        }
+    }
+    if (w.state == 0 && w.npts == 0) w.state = 16 + 4;   // no progress possible: never expected
+}
+
+// wave 0: the round's points into LDS; out of [0,1]^2 -> DBL_MAX without
+// evaluation (lynch.cpp:40-42), an empty table -> -0.0
+// (static_cast<double>(-0.0L)); lynch.hpp:57-90 constants of the others
+__device__ __forceinline__ void sid_nmw_post(const sid_nmw& w, size_t u, sid_nm_round& R)
+{
+    const int lane = sid_lane();
+    const bool mine = lane < w.npts;
+    const double pi = w.rx, e = w.ry;
+    const bool out = mine && (pi < 0 || pi > 1 || e < 0 || e > 1);
+    const bool ev = mine && !out && u != 0;
+    const unsigned long long em = __ballot(ev);
+    if (mine) {
+        R.pts[lane][0] = pi;
+        R.pts[lane][1] = e;
+        if (!ev) R.val[lane] = out ? DBL_MAX : -0.0;
+    }
+    if (ev) {
+        const int q = __popcll(em & ((1ull << lane) - 1ull));
+        R.evl[q] = lane;
+        R.prm[q] = {log(1 - e), log(e / 3.), log((1 - 2. / 3. * e) / 2.), log(1. - pi), log(pi)};
+    }
+    if (lane == 0) {
+        R.npts = w.npts;
+        R.ne = __popcll(em);
+        R.go = w.state == 0;
+    }
+}
+
+// thread 0: arrive at the round's barrier and wait for every block; false on
+// abort (another block gave up) or when this block's deadline passes
+__device__ bool sid_nm_barrier(unsigned int* bar, unsigned int target, int* abort_flag, long long deadline)
+{
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed polls (an acquire load would invalidate this XCD's L2 on every
+    // poll, under the blocks still evaluating); the caller fences once
+    unsigned int spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 31) == 0) {
+            if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+            if (wall_clock64() > deadline) {
+                __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void sid_nm_kernel(const uint64_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ cnt,
+                                                     const double* __restrict__ lnM, size_t u, int nb,
+                                                     sid_nm_dist D, double x00, double x01, double st0,
+                                                     double st1, int lookahead, double* partial,
+                                                     unsigned int* bar, int* abort_flag, long long timeout,
+                                                     sid_nm_result* res)
+{
+    __shared__ sid_nm_round R;
+    __shared__ int alive;
+    const double x0[2] = {x00, x01}, step[2] = {st0, st1};
+    const long long deadline = wall_clock64() + timeout;
+    const unsigned int G = gridDim.x;
+    const bool w0 = threadIdx.x < 64;
+    sid_nmw w;
+    if (w0) {
+        w.cn = w.chead = 0;
+        w.cx = w.cy = w.cv = 0.0;
+        w.rx = w.ry = 0.0;
+        w.phase = w.iter = w.state = w.converged = 0;
+        w.evals = 0;
+        w.x[0] = x0[0];
+        w.x[1] = x0[1];
+        w.fval = w.size = 0.0;
+        sid_nmw_advance(w, x0, step, lookahead != 0);
+        sid_nmw_post(w, u, R);
+    }
+    if (threadIdx.x == 0) alive = 1;
+    __syncthreads();
+    int round = 0;
+    unsigned long long points = 0;
+    long long tk[4] = {0, 0, 0, 0}, t0 = wall_clock64(), t1;
+    for (;;) {
+        if (!R.go || !alive || round >= SID_NM_MAX_ROUNDS) break;
+        const int ne = R.ne;
+        double* part = partial + (size_t)(round & 1) * SID_OBJ_PTS * nb * 2;
+        for (int it = blockIdx.x; it < ne * nb; it += G) {
+            const int q = it / nb, s = it - q * nb;
+            sid_lynch_eval E;
+            E.la = R.prm[q].la;
+            E.lb = R.prm[q].lb;
+            E.lh = R.prm[q].lh;
+            E.l1p = R.prm[q].l1p;
+            E.lp = R.prm[q].lp;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) E.ld[i] = D.ld[i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) E.ldd[i] = D.ldd[i];
+            E.lnorm = D.lnorm;
+            double H, Lo;
+            sid_objective_slice(keys, cnt, lnM, u, s, nb, E, H, Lo);
+            if (threadIdx.x == 0) {
+                part[((size_t)q * nb + s) * 2] = H;
+                part[((size_t)q * nb + s) * 2 + 1] = Lo;
+            }
+        }
+        t1 = wall_clock64();
+        tk[0] += t1 - t0;
+        t0 = t1;
+        if (threadIdx.x == 0) alive = sid_nm_barrier(bar, G * (unsigned)(round + 1), abort_flag, deadline);
+        __syncthreads();
+        if (!alive) break;
+        t1 = wall_clock64();
+        tk[1] += t1 - t0;
+        t0 = t1;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // fold: one wave per point, lanes over the slices, double-double
+        const int lane = sid_lane(), wid = threadIdx.x >> 6;
+        for (int q = wid; q < ne; q += (int)(blockDim.x >> 6)) {
+            double bh = 0.0, bl = 0.0;
+            for (int b = lane; b < nb; b += 64) {
+                double s, e;
+                sid_two_sum(bh, part[((size_t)q * nb + b) * 2], s, e);
+                bh = s;
+                bl += part[((size_t)q * nb + b) * 2 + 1] + e;
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ohi = __shfl_down(bh, off, 64);
+                const double olo = __shfl_down(bl, off, 64);
+                double s, e;
+                sid_two_sum(bh, ohi, s, e);
+                bh = s;
+                bl += olo + e;
+            }
+            if (lane == 0) {
+                double s, e;
+                sid_two_sum(bh, bl, s, e);
+                R.val[R.evl[q]] = -s;   // -(sum) (lynch.cpp:59-60); an infinite sum stays infinite
+            }
+        }
+        __syncthreads();
+        t1 = wall_clock64();
+        tk[2] += t1 - t0;
+        t0 = t1;
+        if (w0) {
+            points += ne;
+            const int np = R.npts;
+            for (int i = 0; i < np; ++i) sid_nmw_put(w, R.pts[i][0], R.pts[i][1], R.val[i]);
+            sid_nmw_advance(w, x0, step, lookahead != 0);
+        }
+        __syncthreads();   // R read by every wave above
+        if (w0) {
+            if (w.state == 0 && round + 1 >= SID_NM_MAX_ROUNDS) w.state = 16 + 3;
+            sid_nmw_post(w, u, R);
+        }
+        __syncthreads();
+        t1 = wall_clock64();
+        tk[3] += t1 - t0;
+        t0 = t1;
+        ++round;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        res->x[0] = w.x[0];
+        res->x[1] = w.x[1];
+        res->fval = w.fval;
+        res->size = w.size;
+        res->iterations = w.iter;
+        res->converged = w.converged;
+        res->status = !alive ? 2 : (w.state >= 16 ? w.state - 16 : 4);
+        res->rounds = round;
+        res->evals = w.evals;
+        res->points = points;
+        for (int i = 0; i < 4; ++i) res->ticks[i] = tk[i];
+    }
 }
 
 // Per-profile L_hom, L_het at eps-hat as emulated long doubles (ln, sign=+).
@@ -1288,6 +1750,24 @@ hipError_t sid_launch_objective(const uint64_t* keys, const uint32_t* cnt, const
     sid_objective_kernel<<<dim3(grid, npts), 256, 0, st>>>(keys, cnt, lnM, u, *EV, partial);
     sid_objective_fold_kernel<<<npts, 256, 0, st>>>(partial, grid, out, seq_out, seq);
     return hipGetLastError();
+}
+
+hipError_t sid_launch_nm(const uint64_t* keys, const uint32_t* cnt, const double* lnM, size_t u, int nb,
+                         const sid_nm_dist* D, const double* x0, const double* step, int lookahead,
+                         double* partial, unsigned int* bar, int grid, long long timeout, sid_nm_result* res,
+                         hipStream_t st)
+{
+    if (nb < 1 || nb > 1024 || grid < 1) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(bar, 0, 2 * sizeof(unsigned int), st);
+    if (e != hipSuccess) return e;
+    sid_nm_dist d = *D;
+    double x00 = x0[0], x01 = x0[1], st0 = step[0], st1 = step[1];
+    int* abort_flag = (int*)(bar + 1);
+    void* args[] = {(void*)&keys, (void*)&cnt,   (void*)&lnM, (void*)&u,          (void*)&nb,
+                    (void*)&d,    (void*)&x00,   (void*)&x01, (void*)&st0,        (void*)&st1,
+                    (void*)&lookahead, (void*)&partial, (void*)&bar, (void*)&abort_flag, (void*)&timeout,
+                    (void*)&res};
+    return hipLaunchCooperativeKernel((const void*)sid_nm_kernel, dim3(grid), dim3(256), args, 0, st);
 }
 
 hipError_t sid_launch_profile_lik(const uint64_t* keys, const double* lnM, size_t u,

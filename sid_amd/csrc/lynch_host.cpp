@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "sid_internal.h"
+#include "sid_nm.h"
 
 
 
@@ -45,6 +46,10 @@ hipError_t sid_launch_compact(const unsigned long long* gkeys, const unsigned lo
 hipError_t sid_launch_objective(const uint64_t* keys, const uint32_t* cnt, const double* lnM, size_t u,
                                 const sid_lynch_evals* EV, int npts, double* partial, double* out,
                                 unsigned int* seq_out, unsigned int seq, int grid, hipStream_t st);
+hipError_t sid_launch_nm(const uint64_t* keys, const uint32_t* cnt, const double* lnM, size_t u, int nb,
+                         const sid_nm_dist* D, const double* x0, const double* step, int lookahead,
+                         double* partial, unsigned int* bar, int grid, long long timeout, sid_nm_result* res,
+                         hipStream_t st);
 hipError_t sid_launch_profile_lik(const uint64_t* keys, const double* lnM, size_t u,
                                   const sid_lynch_eval* E, double* lhom, double* lhet, hipStream_t st);
 hipError_t sid_launch_classify(const uint64_t* keys, const double* lhom, const double* lhet, size_t u,
@@ -120,6 +125,18 @@ struct sid_lynch_dev {
     double* d_out = nullptr;
     unsigned int* d_seq = nullptr;
     unsigned int seq = 0;
+    // device-resident estimate (sid_nm_kernel), SID_NM_DEVICE=1; off by
+    // default: measured 1.0 ms per estimate vs 0.44 ms host-driven (C3,
+    // U = 12k), its rounds bound by cross-XCD synchronisation (barrier
+    // 8 us, fold after the L2 invalidate 7 us, simplex step 8 us per round)
+    bool nm_device = false;
+    int nm_grid = 0;                       // co-resident blocks (one per CU)
+    long long nm_timeout = 0;              // wall-clock ticks
+    double* d_nmpart = nullptr;            // [2][SID_OBJ_PTS][1024][2]
+    unsigned int* d_nmbar = nullptr;       // barrier counter, abort flag
+    sid_nm_result* d_nmres = nullptr;
+    sid_nm_result* h_nmres = nullptr;      // pinned
+    uint64_t nm_rounds = 0, nm_points = 0, nm_fallbacks = 0;
     // class table
     bool prepared = false;
     double* d_lhom = nullptr;
@@ -178,6 +195,9 @@ static void release_buffers(sid_lynch_dev* L)
     dfree(L->d_pcode);
     dfree(L->d_cc);
     dfree(L->d_partial);
+    dfree(L->d_nmpart);
+    dfree(L->d_nmbar);
+    dfree(L->d_nmres);
     dfree(L->d_ckeys);
     dfree(L->d_cidx);
     dfree(L->d_dense_cidx);
@@ -206,6 +226,7 @@ void sid_lynch_dev_destroy(sid_lynch_dev* L)
     dfree(L->list);
     if (L->h_out) (void)hipHostFree(L->h_out);
     if (L->h_seq) (void)hipHostFree(L->h_seq);
+    if (L->h_nmres) (void)hipHostFree(L->h_nmres);
     release_buffers(L);
     delete L;
 }
@@ -553,6 +574,7 @@ extern "C" int sid_lynch_setup(sid_ctx* c, sid_estimate* est)
         // SID_NM_LOOKAHEAD=0/1 overrides (measurement)
         L->lookahead = U <= 32768;
         if (const char* e = std::getenv("SID_NM_LOOKAHEAD")) L->lookahead = std::atoi(e) != 0;
+        if (const char* e = std::getenv("SID_NM_DEVICE")) L->nm_device = std::atoi(e) != 0;
         if (!L->d_partial) HIPCHECK(hipMalloc(&L->d_partial, SID_OBJ_PTS * 2 * 1024 * sizeof(double)));
         if (!L->h_out) {
             HIPCHECK(hipHostMalloc((void**)&L->h_out, 2 * SID_OBJ_PTS * sizeof(double),
@@ -662,18 +684,14 @@ extern "C" int sid_lynch_objective(sid_ctx* c, double pi, double eps, double* ou
 }
 
 // ---------------------------------------------------------------------------
-// Nelder-Mead: GSL 2.7.1 multimin/nmsimplex2.c for 2 parameters, with the
-// gslcblas kernels it uses (dnrm2 with scale/ssq).  The vertex arithmetic
-// depends only on the sequence of comparisons between objective values, so
-// agreeing comparisons give bit-identical (pi, eps).
+// Nelder-Mead driven from the host: GSL 2.7.1 multimin/nmsimplex2.c for 2
+// parameters, vertex arithmetic from sid_nm.h (shared with the device-resident
+// estimate, sid_nm_kernel), one objective launch per prefetch.
 // ---------------------------------------------------------------------------
 namespace {
 struct Simplex {
-    static const int N = 2, P = 3;
-    double x1[P][N];
-    double y1[P];
-    double center[N];
-    double S2 = 0;
+    static const int N = SID_NM_N, P = SID_NM_P;
+    sid_nm_simplex s;
     sid_ctx* ctx;
     int err = SID_OK;
 
@@ -715,97 +733,10 @@ struct Simplex {
         if (rc && !err) err = rc;
         return v;
     }
-    static double nrm2(const double* x)
-    {
-        double scale = 0.0, ssq = 1.0;
-        for (int i = 0; i < N; ++i) {
-            if (x[i] != 0.0) {
-                double ax = std::fabs(x[i]);
-                if (scale < ax) {
-                    ssq = 1.0 + ssq * (scale / ax) * (scale / ax);
-                    scale = ax;
-                } else {
-                    ssq += (ax / scale) * (ax / scale);
-                }
-            }
-        }
-        return scale * std::sqrt(ssq);
-    }
-    static void axpy(double a, const double* x, double* y)
-    {
-        if (a == 0.0) return;
-        for (int i = 0; i < N; ++i) y[i] += a * x[i];
-    }
-    void compute_center()
-    {
-        for (int j = 0; j < N; ++j) center[j] = 0.0;
-        for (int i = 0; i < P; ++i) axpy(1.0, x1[i], center);
-        for (int j = 0; j < N; ++j) center[j] *= 1.0 / P;
-    }
-    double compute_size()
-    {
-        double ss = 0.0;
-        for (int i = 0; i < P; ++i) {
-            double s[N];
-            for (int j = 0; j < N; ++j) s[j] = x1[i][j];
-            axpy(-1.0, center, s);
-            double t = nrm2(s);
-            ss += t * t;
-        }
-        S2 = ss / P;
-        return std::sqrt(ss / P);
-    }
-    void corner_point(double coeff, int corner, double* xc) const
-    {
-        const size_t p = P;
-        double alpha = (1 - coeff) * p / (p - 1.0);
-        double beta = (p * coeff - 1.0) / (p - 1.0);
-        for (int j = 0; j < N; ++j) xc[j] = center[j] * alpha;
-        axpy(beta, x1[corner], xc);
-    }
-    // candidate points of an iteration whose worst vertex is h: reflection,
-    // expansion, inside contraction, and the contraction after the reflected
-    // point is accepted (optimization.hpp -> nmsimplex2_iterate)
-    void candidates(int h, double (*pts)[N]) const
-    {
-        corner_point(-1.0, h, pts[0]);
-        corner_point(-2.0, h, pts[1]);
-        corner_point(0.5, h, pts[2]);
-        Simplex T = *this;
-        T.update_point(h, pts[0], 0.0);
-        T.corner_point(0.5, h, pts[3]);
-    }
-    static void add_point(double (*pts)[N], int& k, const double* x)
-    {
-        for (int i = 0; i < k; ++i)
-            if (pts[i][0] == x[0] && pts[i][1] == x[1]) return;
-        if (k < SID_OBJ_PTS) {
-            pts[k][0] = x[0];
-            pts[k][1] = x[1];
-            ++k;
-        }
-    }
     double corner_move(double coeff, int corner, double* xc)
     {
-        corner_point(coeff, corner, xc);
+        sid_nm_corner_point(s, coeff, corner, xc);
         return f(xc);
-    }
-    void update_point(int i, const double* x, double val)
-    {
-        const size_t p = P;
-        double delta[N], xmc[N];
-        for (int j = 0; j < N; ++j) delta[j] = x[j];
-        axpy(-1.0, x1[i], delta);
-        for (int j = 0; j < N; ++j) xmc[j] = x1[i][j];
-        axpy(-1.0, center, xmc);
-        double d = nrm2(delta);
-        double xmcd = 0.0;
-        for (int j = 0; j < N; ++j) xmcd += xmc[j] * delta[j];
-        S2 += (2.0 / p) * xmcd + ((p - 1.0) / p) * (d * d / p);
-        axpy(-1.0 / p, x1[i], center);
-        axpy(1.0 / p, x, center);
-        for (int j = 0; j < N; ++j) x1[i][j] = x[j];
-        y1[i] = val;
     }
     bool contract_by_best(int best)
     {
@@ -813,20 +744,20 @@ struct Simplex {
         int k = 0;
         for (int i = 0; i < P; ++i) {
             if (i == best) continue;
-            for (int j = 0; j < N; ++j) pts[k][j] = 0.5 * (x1[i][j] + x1[best][j]);
+            for (int j = 0; j < N; ++j) pts[k][j] = 0.5 * (s.x1[i][j] + s.x1[best][j]);
             ++k;
         }
         prefetch(pts, k);
         bool ok = true;
         for (int i = 0; i < P; ++i) {
             if (i == best) continue;
-            for (int j = 0; j < N; ++j) x1[i][j] = 0.5 * (x1[i][j] + x1[best][j]);
-            double xc[N] = {x1[i][0], x1[i][1]};
-            y1[i] = f(xc);
-            if (!std::isfinite(y1[i])) ok = false;
+            for (int j = 0; j < N; ++j) s.x1[i][j] = 0.5 * (s.x1[i][j] + s.x1[best][j]);
+            double xc[N] = {s.x1[i][0], s.x1[i][1]};
+            s.y1[i] = f(xc);
+            if (!std::isfinite(s.y1[i])) ok = false;
         }
-        compute_center();
-        compute_size();
+        sid_nm_compute_center(s);
+        sid_nm_compute_size(s);
         return ok;
     }
     bool set(const double* x, const double* step, double* size)
@@ -835,111 +766,59 @@ struct Simplex {
         prefetch(pts, P);
         double v = f(x);
         if (!std::isfinite(v)) return false;
-        x1[0][0] = x[0];
-        x1[0][1] = x[1];
-        y1[0] = v;
+        s.x1[0][0] = x[0];
+        s.x1[0][1] = x[1];
+        s.y1[0] = v;
         for (int i = 0; i < N; ++i) {
             double xt[N] = {x[0], x[1]};
             xt[i] = x[i] + step[i];
             v = f(xt);
             if (!std::isfinite(v)) return false;
-            x1[i + 1][0] = xt[0];
-            x1[i + 1][1] = xt[1];
-            y1[i + 1] = v;
+            s.x1[i + 1][0] = xt[0];
+            s.x1[i + 1][1] = xt[1];
+            s.y1[i + 1] = v;
         }
-        compute_center();
-        *size = compute_size();
+        sid_nm_compute_center(s);
+        *size = sid_nm_compute_size(s);
         return true;
     }
     bool iterate(double* x, double* size, double* fval)
     {
         double xc[N], xc2[N];
-        int hi = 0, lo = 0, s_hi = 1;
-        double dhi = y1[0], dlo = y1[0], ds_hi = y1[1];
-        for (int i = 1; i < P; ++i) {
-            double v = y1[i];
-            if (v < dlo) {
-                dlo = v;
-                lo = i;
-            } else if (v > dhi) {
-                ds_hi = dhi;
-                s_hi = hi;
-                dhi = v;
-                hi = i;
-            } else if (v > ds_hi) {
-                ds_hi = v;
-                s_hi = i;
-            }
-        }
+        int hi, s_hi, lo;
+        sid_nm_order(s, hi, s_hi, lo);
         {
             double c1[4][N];
-            candidates(hi, c1);
+            sid_nm_candidates(s, hi, c1);
             if (!(cached(c1[0]) && cached(c1[1]) && cached(c1[2]) && cached(c1[3]))) {
                 double pts[SID_OBJ_PTS][N];
-                int k = 0;
-                for (int i = 0; i < 4; ++i) add_point(pts, k, c1[i]);
-                if (ctx->lynch->lookahead) {
-                    // the next iteration's candidates after each outcome of
-                    // this one (only the worst vertex moves, so the new
-                    // worst is the old second worst, or the moved vertex
-                    // after a contraction); the trajectory does not depend
-                    // on what is prefetched
-                    for (int o = 0; o < 4; ++o) {
-                        Simplex T = *this;
-                        T.cn = 0;
-                        if (o == 0) T.update_point(hi, c1[0], 0.0);   // reflection accepted
-                        if (o == 1) T.update_point(hi, c1[1], 0.0);   // expansion accepted
-                        if (o == 2) {                                 // outside contraction
-                            T.update_point(hi, c1[0], 0.0);
-                            T.update_point(hi, c1[3], 0.0);
-                        }
-                        if (o == 3) T.update_point(hi, c1[2], 0.0);   // inside contraction
-                        for (int h2 : {s_hi, hi}) {
-                            if (h2 == hi && o < 2) continue;
-                            double c2[4][N];
-                            T.candidates(h2, c2);
-                            for (int i = 0; i < 4; ++i) add_point(pts, k, c2[i]);
-                        }
-                    }
-                }
+                int k = sid_nm_request(s, ctx->lynch->lookahead, pts, SID_OBJ_PTS);
                 prefetch(pts, k);
             }
         }
         double val = corner_move(-1.0, hi, xc);
-        if (std::isfinite(val) && val < y1[lo]) {
+        if (std::isfinite(val) && val < s.y1[lo]) {
             double val2 = corner_move(-2.0, hi, xc2);
-            if (std::isfinite(val2) && val2 < y1[lo])
-                update_point(hi, xc2, val2);
+            if (std::isfinite(val2) && val2 < s.y1[lo])
+                sid_nm_update_point(s, hi, xc2, val2);
             else
-                update_point(hi, xc, val);
-        } else if (!std::isfinite(val) || val > y1[s_hi]) {
-            if (std::isfinite(val) && val <= y1[hi]) update_point(hi, xc, val);
+                sid_nm_update_point(s, hi, xc, val);
+        } else if (!std::isfinite(val) || val > s.y1[s_hi]) {
+            if (std::isfinite(val) && val <= s.y1[hi]) sid_nm_update_point(s, hi, xc, val);
             double val2 = corner_move(0.5, hi, xc2);
-            if (std::isfinite(val2) && val2 <= y1[hi]) {
-                update_point(hi, xc2, val2);
+            if (std::isfinite(val2) && val2 <= s.y1[hi]) {
+                sid_nm_update_point(s, hi, xc2, val2);
             } else if (!contract_by_best(lo)) {
                 return false;
             }
         } else {
-            update_point(hi, xc, val);
+            sid_nm_update_point(s, hi, xc, val);
         }
-        // gsl_vector_min_index
-        int imin = 0;
-        double mn = y1[0];
-        for (int i = 0; i < P; ++i) {
-            if (y1[i] < mn) {
-                mn = y1[i];
-                imin = i;
-            }
-            if (std::isnan(y1[i])) {
-                imin = i;
-                break;
-            }
-        }
-        x[0] = x1[imin][0];
-        x[1] = x1[imin][1];
-        *fval = y1[imin];
-        *size = S2 > 0 ? std::sqrt(S2) : compute_size();
+        const int imin = sid_nm_min_index(s);
+        x[0] = s.x1[imin][0];
+        x[1] = s.x1[imin][1];
+        *fval = s.y1[imin];
+        *size = s.S2 > 0 ? std::sqrt(s.S2) : sid_nm_compute_size(s);
         return true;
     }
 };
@@ -983,6 +862,79 @@ static int run_estimate(sid_ctx* c, int verbose, sid_estimate* est)
     return SID_OK;
 }
 
+// lynch.cpp:17-35 + optimization.hpp:50-89 in one cooperative launch
+// (lynch.hip sid_nm_kernel).  Returns SID_OK with *done = false when the
+// device estimate is unavailable (cooperative launch refused, deadline):
+// the caller then runs the host driver.
+static int run_estimate_device(sid_ctx* c, int verbose, sid_estimate* est, bool* done)
+{
+    sid_lynch_dev* L = c->lynch;
+    *done = false;
+    if (!L->d_nmpart) {
+        int ncu = 0, coop = 0, khz = 0;
+        HIPCHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+        HIPCHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device));
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        if (!coop || ncu < 1) {
+            L->nm_device = false;
+            return SID_OK;
+        }
+        L->nm_grid = ncu;
+        L->nm_timeout = (long long)khz * 1000 * 5;   // 5 s: the estimate takes < 1 ms
+        HIPCHECK(hipMalloc(&L->d_nmpart, (size_t)2 * SID_OBJ_PTS * 1024 * 2 * sizeof(double)));
+        HIPCHECK(hipMalloc(&L->d_nmbar, 2 * sizeof(unsigned int)));
+        HIPCHECK(hipMalloc(&L->d_nmres, sizeof(sid_nm_result)));
+        HIPCHECK(hipHostMalloc((void**)&L->h_nmres, sizeof(sid_nm_result), hipHostMallocDefault));
+    }
+    sid_lynch_eval E;
+    make_eval(L->dist, 0.5, 0.5, &E);   // only the dist-only constants are used
+    sid_nm_dist D;
+    std::memcpy(D.ld, E.ld, sizeof(D.ld));
+    std::memcpy(D.ldd, E.ldd, sizeof(D.ldd));
+    D.lnorm = E.lnorm;
+    const double x0[2] = {1e-3, 1e-3};   // DEFAULT_PI, DEFAULT_EPSILON  lynch.cpp:8-10
+    const double step[2] = {1e-4, 1e-4}; // DEFAULT_STEPSIZE
+    hipError_t e = sid_launch_nm(L->d_keys, L->d_cnt, L->d_lnM, L->nU, L->obj_grid, &D, x0, step, L->lookahead ? 1 : 0,
+                                 L->d_nmpart, L->d_nmbar, L->nm_grid, L->nm_timeout, L->d_nmres, 0);
+    if (e == hipErrorCooperativeLaunchTooLarge || e == hipErrorNotSupported) {
+        (void)hipGetLastError();
+        L->nm_device = false;
+        return SID_OK;
+    }
+    HIPCHECK(e);
+    HIPCHECK(hipMemcpyAsync(L->h_nmres, L->d_nmres, sizeof(sid_nm_result), hipMemcpyDeviceToHost, 0));
+    HIPCHECK(hipStreamSynchronize(0));
+    const sid_nm_result r = *L->h_nmres;
+    L->nm_rounds = (uint64_t)r.rounds;
+    L->nm_points = r.points;
+    if (std::getenv("SID_LYNCH_TIMING"))
+        std::fprintf(stderr, "{\"nm_ticks\": [%lld, %lld, %lld, %lld]}\n", r.ticks[0], r.ticks[1], r.ticks[2],
+                     r.ticks[3]);
+    L->launches = 1;
+    if (r.status >= 2) {   // deadline, round cap, internal: the host driver decides
+        L->nm_fallbacks++;
+        return SID_OK;
+    }
+    L->evals = r.evals;
+    if (r.status == 1) return SID_EBADFUNC;   // non-finite at the start, or "contraction failed"
+    *done = true;
+    const int i = r.iterations;
+    if (verbose) {
+        if (r.converged)
+            std::fprintf(stderr, "# GSL function minimization converged in %d iterations.\n", i);
+        else
+            std::fprintf(stderr, "# Error: GSL function minimization did not converge in %d iterations!\n", i);
+    }
+    est->heterozygosity = r.x[0];
+    est->error_rate = r.x[1];
+    est->fval = r.fval;
+    est->iterations = i;
+    est->converged = r.converged;
+    est->evaluations = r.evals;
+    return SID_OK;
+}
+
 extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
 {
     sid_lynch_dev* L;
@@ -1004,8 +956,15 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     // the -R estimate of local and quality prints only the minimiser's line
     const bool local_like = method == SID_METHOD_LOCAL || method == SID_METHOD_QUALITY;
     if (verbose && !local_like) std::fprintf(stderr, "# unique profiles: %zu\n", U);
-    rc = run_estimate(c, verbose, &est);
-    if (rc) return rc;
+    bool done = false;
+    if (L->nm_device && U > 0) {
+        rc = run_estimate_device(c, verbose, &est, &done);
+        if (rc) return rc;
+    }
+    if (!done) {
+        rc = run_estimate(c, verbose, &est);
+        if (rc) return rc;
+    }
     const auto t2 = now();
     if (est_out) *est_out = est;
     if (local_like) return SID_OK;   // -R local / quality: the caller applies the prior
@@ -1107,8 +1066,10 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     if (timing)
         std::fprintf(stderr,
                      "{\"lynch_prepare_ms\": {\"setup\": %.3f, \"estimate\": %.3f, \"evaluations\": %llu, "
-                     "\"launches\": %llu, \"classify_bh\": %.3f, \"class_tables\": %.3f}}\n",
+                     "\"launches\": %llu, \"nm_device\": %d, \"nm_rounds\": %llu, \"nm_points\": %llu, "
+                     "\"classify_bh\": %.3f, \"class_tables\": %.3f}}\n",
                      ms(t0, t1), ms(t1, t2), (unsigned long long)est.evaluations, (unsigned long long)L->launches,
+                     (int)L->nm_device, (unsigned long long)L->nm_rounds, (unsigned long long)L->nm_points,
                      ms(t2, t3), ms(t3, now()));
     return SID_OK;
 }

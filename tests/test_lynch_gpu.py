@@ -184,23 +184,65 @@ def test_context_reuse_and_unaligned_lookup(gpu, sid, oracle):
         assert_parity(code, hom, het, rcode, rhom, rhet, what="reuse/unaligned")
 
 
-@pytest.mark.parametrize("depth,n,seed", [(30.0, 80_000, 3), (200.0, 20_000, 5)])
+@pytest.mark.parametrize("depth,n,seed", [(30.0, 80_000, 3), (200.0, 20_000, 5), (8.0, 50_000, 7)])
 def test_prefetch_policy_keeps_trajectory(gpu, sid, oracle, monkeypatch, depth, n, seed):
-    """The Nelder-Mead prefetch (the next iteration's candidates evaluated
-    with the current ones, SID_NM_LOOKAHEAD=1; four points per launch with 0)
-    only changes how many launches the estimate takes: the same (pi, eps),
-    iterations, evaluations and outputs, equal to the oracle's."""
+    """The Nelder-Mead estimate on the device (one cooperative launch,
+    SID_NM_DEVICE=1) and driven from the host (0, the default), each with and without the
+    next iteration's candidates evaluated ahead (SID_NM_LOOKAHEAD): the same
+    (pi, eps), iterations, evaluations and outputs, equal to the oracle's."""
     counts = sid.synth_counts_host(seed, n, depth)
     res = {}
-    for la in ("0", "1"):
-        monkeypatch.setenv("SID_NM_LOOKAHEAD", la)   # read when the profiles are set up
-        res[la] = gpu.run_method(counts, "likelihood_ratio", estimate_prior=True)
-    (c0, h0, t0, e0), (c1, h1, t1, e1) = res["0"], res["1"]
-    assert (e0.heterozygosity, e0.error_rate, e0.iterations, e0.evaluations) == \
-        (e1.heterozygosity, e1.error_rate, e1.iterations, e1.evaluations)
-    assert np.array_equal(c0, c1) and np.array_equal(h0.view(np.int64), h1.view(np.int64)) \
-        and np.array_equal(t0.view(np.int64), t1.view(np.int64))
+    for dev in ("0", "1"):
+        for la in ("0", "1"):
+            monkeypatch.setenv("SID_NM_DEVICE", dev)     # read when the profiles are set up
+            monkeypatch.setenv("SID_NM_LOOKAHEAD", la)
+            res[dev + la] = gpu.run_method(counts, "likelihood_ratio", estimate_prior=True)
+    c1, h1, t1, e1 = res["01"]
+    for key, (c0, h0, t0, e0) in res.items():
+        assert (e0.heterozygosity, e0.error_rate, e0.iterations, e0.evaluations, e0.converged) == \
+            (e1.heterozygosity, e1.error_rate, e1.iterations, e1.evaluations, e1.converged), key
+        assert np.array_equal(c0, c1) and np.array_equal(h0.view(np.int64), h1.view(np.int64)) \
+            and np.array_equal(t0.view(np.int64), t1.view(np.int64)), key
     rc, rcode, rhom, rhet, rest, u = oracle.call_method(counts, "likelihood_ratio", estimate_prior=True)
     assert (e1.heterozygosity, e1.error_rate, e1.iterations) == (rest.heterozygosity, rest.error_rate,
                                                                  rest.iterations)
     assert_parity(c1, h1, t1, rcode, rhom, rhet, what=f"prefetch {depth}x")
+
+
+@pytest.mark.parametrize("method,o", [("likelihood_ratio", dict(estimate_prior=True)), ("bayes", dict()),
+                                      ("local", dict(estimate_prior=True))], ids=lambda x: str(x))
+def test_device_estimate_edge_tables(gpu, sid, oracle, monkeypatch, method, o):
+    """Small and degenerate profile tables through the device estimate: a
+    single profile with one base only (the het mixture is 0/0, every L is
+    NaN, the objective is -0.0 everywhere and the simplex runs its 1000
+    iterations), one base plus a rare second, a handful of profiles, and a
+    table whose slices exceed one block per CU — the same estimate as the
+    host driver and the oracle, and the oracle's outputs."""
+    rng = np.random.default_rng(17)
+    tables = [
+        np.array([[10, 0, 0, 0]] * 50, np.uint16),
+        np.array([[0, 0, 7, 0]] * 20 + [[0, 0, 9, 1]] * 3, np.uint16),
+        np.array([[5, 5, 0, 0], [9, 0, 1, 0], [0, 12, 0, 0], [3, 3, 3, 3], [40, 2, 0, 1]] * 40, np.uint16),
+        rng.integers(0, 30, (70_000, 4)).astype(np.uint16),   # U ~ 67k: more slices than blocks
+    ]
+    for ti, t in enumerate(tables):
+        out = {}
+        for dev in ("0", "1"):
+            monkeypatch.setenv("SID_NM_DEVICE", dev)
+            try:
+                out[dev] = gpu.run_method(t, method, **o)
+            except sid.SidError as e:
+                out[dev] = e.status
+        if isinstance(out["0"], int):
+            assert out["1"] == out["0"]
+            continue
+        (c0, h0, t0, e0), (c1, h1, t1, e1) = out["0"], out["1"]
+        assert (e0.heterozygosity, e0.error_rate, e0.iterations, e0.evaluations) == \
+            (e1.heterozygosity, e1.error_rate, e1.iterations, e1.evaluations)
+        assert np.array_equal(c0, c1) and np.array_equal(h0.view(np.int64), h1.view(np.int64))
+        if ti == len(tables) - 1:
+            continue   # the oracle needs ~80 s for 67k profiles; the host driver is pinned to it above
+        rc, rcode, rhom, rhet, rest, u = oracle.call_method(t, method, **o)
+        assert rc == 0 and (e1.heterozygosity, e1.error_rate, e1.iterations) == \
+            (rest.heterozygosity, rest.error_rate, rest.iterations)
+        assert_parity(c1, h1, t1, rcode, rhom, rhet, what=f"device estimate edge table {method}")
