@@ -97,7 +97,7 @@ struct sid_lynch_dev {
     // profiles' keys go through the fallback list into the hash
     unsigned long long* dense = nullptr;   // [SID_DENSE_ROWS][SID_DENSE_N]
     uint32_t* part = nullptr;              // per-block rows of the dense pass
-    int hist_grid = 512;                   // SID_HIST_GRID (measurement knob)
+    int hist_grid = 256;                   // SID_HIST_GRID (measurement knob); 256: 89 us vs 95 us at 512 (hist_probe)
     unsigned long long* list = nullptr;
     uint64_t list_cap = 0;
     hipStream_t acc_stream = nullptr;      // stream of the last accumulate

@@ -40,7 +40,7 @@ __device__ __forceinline__ void fb_append(bool fb, uint64_t key, unsigned long l
     }
 }
 
-template <int MODE>
+template <int MODE, int U = 2>
 __global__ __launch_bounds__(1024) void probe(const ulonglong2* __restrict__ pairs, size_t npairs, uint32_t* part,
                                               unsigned long long* list, uint64_t cap, unsigned long long* ctr,
                                               uint32_t* sink)
@@ -53,18 +53,27 @@ __global__ __launch_bounds__(1024) void probe(const ulonglong2* __restrict__ pai
     __syncthreads();
     uint32_t acc = 0;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < npairs; base += 2 * stride) {
-        const size_t p0 = base + threadIdx.x, p1 = p0 + stride;
-        ulonglong2 c0 = {0, 0}, c1 = {0, 0};
-        const bool v0 = p0 < npairs, v1 = p1 < npairs;
-        if (v0) c0 = pairs[p0];
-        if (v1) c1 = pairs[p1];
-        const uint64_t w[4] = {c0.x, c0.y, c1.x, c1.y};
-        const bool v[4] = {v0, v0, v1, v1};
+    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < npairs; base += U * stride) {
+        ulonglong2 c[U];
+        bool vv[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const size_t pj = base + threadIdx.x + j * stride;
+            vv[j] = pj < npairs;
+            c[j] = vv[j] ? pairs[pj] : ulonglong2{0, 0};
+        }
+        uint64_t w[2 * U];
+        bool v[2 * U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            w[2 * j] = c[j].x;
+            w[2 * j + 1] = c[j].y;
+            v[2 * j] = v[2 * j + 1] = vv[j];
+        }
         if (MODE == WAVEAGG) {
             // one LDS add per distinct code of the wave's 64 lanes (leader loop)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 2 * U; ++k) {
                 const uint32_t d = sid_dense_code(w[k]);
                 bool pending = v[k] && d != SID_DENSE_NONE;
                 unsigned long long rem = __ballot(pending);
@@ -80,7 +89,7 @@ __global__ __launch_bounds__(1024) void probe(const ulonglong2* __restrict__ pai
             continue;
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 2 * U; ++k) {
             const uint32_t d = sid_dense_code(w[k]);
             const bool fb = v[k] && d == SID_DENSE_NONE;
             if (MODE == LOADS) acc += d;
@@ -156,6 +165,13 @@ int main()
         timeit([&] { probe<FULL><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "full", grid);
         timeit([&] { probe<LDSROW><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "lds+row", grid);
         timeit([&] { probe<LDSLIST><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "lds+row+llist", grid);
+        timeit([&] { probe<LOADS, 4><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "loads_u4", grid);
+        timeit([&] { probe<LOADS, 8><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "loads_u8", grid);
+        timeit([&] { probe<LOADS, 1><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "loads_u1", grid);
+        timeit([&] { probe<LDS, 4><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "lds_u4", grid);
+        timeit([&] { probe<LDSLIST, 4><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "lds+row+llist_u4", grid);
+        timeit([&] { probe<LDSLIST, 8><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "lds+row+llist_u8", grid);
+        timeit([&] { probe<WAVEAGG, 2><<<grid, 1024>>>(P, npairs, part, list, 1 << 22, ctr, sink); }, "waveagg", grid);
         timeit([&] { (void)sid_launch_hist_dense(counts, n, part, dense, list, 1 << 22, ctr, grid, nullptr); },
                "product(dense+reduce)", grid);
     }
