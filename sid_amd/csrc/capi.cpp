@@ -175,7 +175,7 @@ extern "C" int sid_destroy(sid_ctx* c)
     }
     for (char* p : c->in_h)
         if (p) (void)hipHostFree(p);
-    for (void* p : {(void*)c->d_qtab, (void*)c->d_lg, (void*)c->d_scratch})
+    for (void* p : {(void*)c->d_qtab, (void*)c->d_lg, (void*)c->d_scratch, (void*)c->d_qlo})
         if (p) (void)hipFree(p);
     for (auto& v : {c->ev_pool, c->ev_pending})
         for (auto& ev : v) {

@@ -85,6 +85,8 @@ struct sid_ctx {
     double* d_lg = nullptr;     // log_gamma(x), x < lg_n
     size_t lg_n = 0;
     uint32_t* d_scratch = nullptr;
+    double* d_qlo = nullptr;    // -m quality phase 1 -> 2: lo parts of the two sums, 16 B per site
+    size_t qlo_n = 0;
 };
 
 // host helpers (capi.cpp)

@@ -272,9 +272,12 @@ struct Reader {
             wpos = w;
             win = *(const uint4*)(text + w);   // text is padded to a 16-B multiple
         }
+        // byte k of the window by a select of the 8-byte half and a 64-bit
+        // shift: a word select on k was turned into a dynamically indexed
+        // stack array (scratch store + load per byte) in the quality kernel
         const uint32_t k = (uint32_t)(i & 15);
-        const uint32_t word = k < 8 ? (k < 4 ? win.x : win.y) : (k < 12 ? win.z : win.w);
-        return (word >> (8 * (k & 3))) & 0xffu;
+        const uint64_t half = (k & 8) ? (((uint64_t)win.w << 32) | win.z) : (((uint64_t)win.y << 32) | win.x);
+        return (uint32_t)(half >> (8 * (k & 7))) & 0xffu;
     }
 };
 
@@ -644,48 +647,55 @@ __device__ __forceinline__ void dd_acc(sid_dd& a, double t)
     a.lo += e;
 }
 
-__global__ __launch_bounds__(TB) void sid_quality_kernel(const char* __restrict__ text, uint64_t len,
-                                                         const uint64_t* __restrict__ starts,
-                                                         const uint64_t* __restrict__ counts, uint64_t n,
-                                                         const double* __restrict__ g_qtab,
-                                                         const double* __restrict__ lg, QParams P,
-                                                         uint8_t* __restrict__ code, double* __restrict__ hom,
-                                                         double* __restrict__ het)
+// Two kernels: the walk over the text (phase 1) and the per-site tail
+// (phase 2).  In one kernel the tail's double-double, erfc and emulated
+// long-double code set the register count for the walk too (203 VGPRs, 2
+// waves per SIMD) and the latency-bound walk ran at that occupancy.
+// Phase 1 stores the two per-read sums as double-double: the hi parts in
+// hom/het (phase 2 overwrites them), the lo parts in lo2.
+__global__ __launch_bounds__(TB) void sid_quality_sum_kernel(const char* __restrict__ text, uint64_t len,
+                                                             const uint64_t* __restrict__ starts,
+                                                             const uint64_t* __restrict__ counts, uint64_t n,
+                                                             const double* __restrict__ g_qtab,
+                                                             double* __restrict__ hom, double* __restrict__ het,
+                                                             double2* __restrict__ lo2)
 {
     __shared__ double T[4 * 256];
     __shared__ uint8_t cls[256];
     for (uint32_t i = threadIdx.x; i < 4 * 256; i += blockDim.x) T[i] = g_qtab[i];
     if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
     __syncthreads();
-    const sid_dd LN2_LD = {0.6931471805599453, 2.3201926491189795e-17};   // x87 logl(2), exactly
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t w = counts[i];
         uint32_t f, s2, nf, ns, cov;
         sid_major(w, f, s2, nf, ns, cov);   // getMajorAlleleIndices (same std::sort)
         Reader R{text, len};
-        // tokens 4, 5, 6 (the line parsed with 7 fields)
-        uint64_t tb[7], te[7];
+        // tokens 2 (ref), 4, 5, 6 of the line (parsed with 7 fields)
+        uint64_t b2 = 0, b4 = 0, e4 = 0, b5 = 0, e5 = 0, b6 = 0, e6 = 0;
         {
             uint64_t q = starts[i];
             for (int t = 0; t < 7; ++t) {
                 while (is_sep(R.at(q))) ++q;
-                tb[t] = q;
+                const uint64_t tb = q;
                 uint32_t c;
                 while ((c = R.at(q)) != ' ' && c != '\t' && c != '\n' && c != 0 && q < len) ++q;
-                te[t] = q;
+                if (t == 2) b2 = tb;
+                else if (t == 4) b4 = tb, e4 = q;
+                else if (t == 5) b5 = tb, e5 = q;
+                else if (t == 6) b6 = tb, e6 = q;
             }
         }
-        const uint32_t ref = R.at(tb[2]);
+        const uint32_t ref = R.at(b2);
         const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
         const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
         const uint32_t cdot = cls[up], ccomma = cls[lw];
         Reader RB{text, len}, RM{text, len};
-        const uint64_t nbq = te[5] - tb[5], nmq = te[6] - tb[6];
+        const uint64_t nbq = e5 - b5, nmq = e6 - b6;
         sid_dd lph = {0.0, 0.0}, lpt = {0.0, 0.0};
         uint64_t j = 0, skip = 0, num = 0;
         int ind = 0;
         bool ovf = false;
-        for (uint64_t q = tb[4]; q < te[4]; ++q) {
+        for (uint64_t q = b4; q < e4; ++q) {
             const uint32_t c = R.at(q);
             if (ind == 1) {
                 ind = 0;
@@ -716,11 +726,11 @@ __global__ __launch_bounds__(TB) void sid_quality_kernel(const char* __restrict_
                 // parseQualities: uint8_t(c - 33), at least 1
                 uint32_t bq = 1, mq = 1;
                 if (j < nbq) {
-                    bq = (RB.at(tb[5] + j) - 33u) & 0xffu;
+                    bq = (RB.at(b5 + j) - 33u) & 0xffu;
                     bq = bq < 1 ? 1 : bq;
                 }
                 if (j < nmq) {
-                    mq = (RM.at(tb[6] + j) - 33u) & 0xffu;
+                    mq = (RM.at(b6 + j) - 33u) & 0xffu;
                     mq = mq < 1 ? 1 : mq;
                 }
                 const uint32_t qv = bq < mq ? bq : mq;
@@ -735,6 +745,24 @@ __global__ __launch_bounds__(TB) void sid_quality_kernel(const char* __restrict_
             }
         }
         lph = dd_norm(lph.hi, lph.lo);
+        hom[i] = lph.hi;
+        het[i] = lpt.hi;
+        lo2[i] = make_double2(lph.lo, lpt.lo);
+    }
+}
+
+__global__ __launch_bounds__(TB) void sid_quality_finish_kernel(const uint64_t* __restrict__ counts, uint64_t n,
+                                                                const double* __restrict__ lg, QParams P,
+                                                                uint8_t* __restrict__ code, double* __restrict__ hom,
+                                                                double* __restrict__ het,
+                                                                const double2* __restrict__ lo2)
+{
+    const sid_dd LN2_LD = {0.6931471805599453, 2.3201926491189795e-17};   // x87 logl(2), exactly
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t f, s2, nf, ns, cov;
+        sid_major(counts[i], f, s2, nf, ns, cov);
+        const double2 lo = lo2[i];
+        sid_dd lph = {hom[i], lo.x}, lpt = {het[i], lo.y};
         // log_probability_heterozygous += logbinom(n, k) - n * logl(2)
         const uint32_t nn = nf + ns, kk = ns;
         const double lb = lg[nn + 1] - lg[nn - kk + 1] - lg[kk + 1];
@@ -1235,9 +1263,18 @@ extern "C" int sid_call_quality(sid_ctx* ctx, const sid_dtext* T, uint8_t* code,
         P.lp2 = {(double)b, (double)(b - (long double)(double)b)};
     }
     P.lg15 = ctx->K.lg15;
+    if (n > ctx->qlo_n) {   // phase 1's lo parts, grow-only
+        if (ctx->d_qlo) (void)hipFree(ctx->d_qlo);
+        ctx->d_qlo = nullptr;
+        ctx->qlo_n = 0;
+        TCHECK(hipMalloc(&ctx->d_qlo, n * 16));
+        ctx->qlo_n = n;
+    }
     const unsigned grid = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, 16384);
-    sid_quality_kernel<<<grid, TB, 0, st>>>(T->d_text, T->len, T->d_starts, T->d_counts, n, ctx->d_qtab, ctx->d_lg,
-                                            P, code, hom_conf, het_conf);
+    sid_quality_sum_kernel<<<grid, TB, 0, st>>>(T->d_text, T->len, T->d_starts, T->d_counts, n, ctx->d_qtab,
+                                                hom_conf, het_conf, (double2*)ctx->d_qlo);
+    sid_quality_finish_kernel<<<grid, TB, 0, st>>>(T->d_counts, n, ctx->d_lg, P, code, hom_conf, het_conf,
+                                                   (const double2*)ctx->d_qlo);
     TCHECK(hipGetLastError());
     return SID_OK;
 }
