@@ -24,7 +24,7 @@ run() {   # tag, env...
     echo "{\"tag\": \"$tag\", \"rep\": $rep, \"wall_s\": $(python3 -c "print('%.4f' % ($b - $a))"), \"lines\": [$(paste -sd, $O/probe_$tag.err)]}" | tee -a $O/e2e_probe.jsonl
   done
 }
-for v in ${VARIANTS:-default fd nosdma}; do
+for v in ${VARIANTS:-default default}; do
   case $v in
     default) run default ;;
     fd) run fd SID_READ_FD=1 ;;
