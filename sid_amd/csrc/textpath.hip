@@ -1063,7 +1063,14 @@ extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, 
     TCHECK(hipSetDevice(T->device));
     hipStream_t st = (hipStream_t)stream;
     const size_t n = end - begin;
-    const size_t PB = 4096;                          // blocks (of TB sites) per piece: 1 Mi sites
+    // blocks (of TB sites) per piece: 256 Ki sites, ~17 MB of records.  The
+    // two pinned staging buffers are allocated while the lengths are computed
+    // and the allocation holds up the device work: 1 Mi-site pieces cost
+    // 33-41 ms before the first write at 50M sites, 256 Ki-site pieces 14-16
+    // ms with the same D2H rate; 64 Ki-site pieces D2H slower
+    // (tools/e2e_probe.sh; SID_FMT_PIECE_BLOCKS overrides, measurement)
+    size_t PB = 1024;
+    if (const char* e = std::getenv("SID_FMT_PIECE_BLOCKS")) PB = std::max(1, std::atoi(e));
     const size_t nb = (n + TB - 1) / TB;
     uint32_t* d_bsum = nullptr;
     uint64_t* d_boff = nullptr;

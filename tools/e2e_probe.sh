@@ -29,5 +29,7 @@ for v in ${VARIANTS:-default default}; do
     default) run default ;;
     fd) run fd SID_READ_FD=1 ;;
     nosdma) run nosdma HSA_ENABLE_SDMA=0 ;;
+    piece1k) run piece1k SID_FMT_PIECE_BLOCKS=1024 ;;
+    piece256) run piece256 SID_FMT_PIECE_BLOCKS=256 ;;
   esac
 done
