@@ -81,10 +81,13 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
     import sid_amd
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one rank per GPU; more ranks than GPUs share them round-robin (a
+    # rehearsal of the N>1 path on a smaller box)
+    gpu = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     n = a.sites
-    ctx = sid_amd.Context(local_rank)
+    ctx = sid_amd.Context(gpu)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     counts = torch.empty((n, 4), dtype=torch.int16, device=dev)
