@@ -10,7 +10,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall 
 HOSTFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Iinclude
 
 KERNELS := local synth lynch textpath
-HOSTSRC := capi lynch_host parse emit
+HOSTSRC := capi lynch_host parse emit run
 OBJS := $(KERNELS:%=$(BUILD)/%.o) $(HOSTSRC:%=$(BUILD)/%.o)
 HDRS := include/sid.h $(wildcard $(SRC)/*.h)
 

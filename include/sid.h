@@ -66,6 +66,10 @@ int sid_last_hip_error(void);
 const char* sid_version(void);
 
 /* --------------------------------------------------------------- options -- */
+/* per-site result code bits (see Conventions) */
+#define SID_CODE_HET 0x80
+#define SID_CODE_DROPPED 0x40
+
 enum { SID_METHOD_LOCAL = 0, SID_METHOD_LIKELIHOOD_RATIO = 1, SID_METHOD_BAYES = 2, SID_METHOD_QUALITY = 3 };
 
 /* GlobalOptions, sid.cpp:11-17 */
@@ -107,8 +111,10 @@ int sid_timing_read(sid_ctx* ctx, uint64_t* calls, double* main_ms, double* fixu
  *    device hash histogram of the site profiles (countUniqueProfiles,
  *    pileup.cpp:169-196).
  * 2. optional multi-device / multi-rank merge: sid_profile_table exports the
- *    sorted unique profiles, sid_profile_load replaces the context's table by
- *    a merged one (counts are summed by the caller).
+ *    sorted unique profiles (cached until the histogram changes),
+ *    sid_profile_load replaces the context's table by a merged one: the
+ *    concatenated per-device tables may repeat keys, it sorts them and sums
+ *    the counts of equal keys itself.
  * 3. sid_lynch_prepare: coverage >= 4 filter (call.cpp:66-70), nucleotide
  *    distribution (pileup.cpp:198-217), Nelder-Mead estimate of (pi, eps)
  *    with the objective evaluated on the GPU (lynch.cpp:17-61,
@@ -141,8 +147,15 @@ int sid_profile_load(sid_ctx* ctx, const uint64_t* keys, const uint64_t* counts6
  * sid_lynch_setup).  Synchronises. */
 int sid_lynch_setup(sid_ctx* ctx, sid_estimate* est /* dist, n_unique filled */);
 int sid_lynch_objective(sid_ctx* ctx, double pi, double eps, double* out);
-/* verbose != 0 prints the reference's "# ..." stderr lines. Synchronises. */
+/* verbose != 0 prints the reference's "# ..." stderr lines. Synchronises.
+ * -m bayes with no profile of coverage >= 4 succeeds and drops every site
+ * (callBayes prints the header only); likelihood_ratio returns SID_EEMPTY. */
 int sid_lynch_prepare(sid_ctx* ctx, int verbose, sid_estimate* est);
+/* The same with (pi-hat, eps-hat) taken from `given` (an estimate another
+ * device or rank computed on the same merged table, SURVEY.md §8(e) steps
+ * 3-4): no Nelder-Mead here, only the per-profile classification.  Prints
+ * only the "# unique profiles" line when verbose. */
+int sid_lynch_prepare_given(sid_ctx* ctx, int verbose, const sid_estimate* given, sid_estimate* est);
 int sid_lookup_sites(sid_ctx* ctx, const uint16_t* counts, size_t n, uint8_t* code,
                      double* hom_conf, double* het_conf, void* stream);
 
@@ -232,6 +245,92 @@ int sid_call_quality(sid_ctx* ctx, const sid_dtext* t, uint8_t* code, double* ho
  * 16 bytes per value, NUL-padded. */
 int sid_format_g6(double v, char* buf, size_t cap);
 int sid_format_g6_device(sid_ctx* ctx, const double* values, size_t n, char* out, void* stream);
+
+
+/* ------------------------------------------------ streaming engine -------
+ * The whole path of one sid run -- pileup text in, CSV records out, in file
+ * order -- replacing readFile + callX + the output loop (call.cpp:11-20,
+ * call.cpp:62-289, sid.cpp:92-105) with a bounded-memory pipeline over
+ * line-aligned chunks of the input:
+ *
+ *   host text --H2D (ring of device buffers)--> line index + parse
+ *     [-m local / quality: call + CSV format, held in HBM]
+ *     [Lynch (likelihood_ratio, bayes, -R): profile histogram]
+ *   (the whole input validated; Lynch: merge + one estimate + class tables)
+ *   [second pass over the chunks not formatted yet: parse, call / lookup,
+ *    format] --D2H (pinned ring)--> write() in file order
+ *
+ * Chunk j runs on device j % devices; every device formats and copies back
+ * concurrently and one writer keeps file order.  As in the reference, no
+ * record is written before the whole input has parsed: the first malformed
+ * line in file order is reported (its input byte offset in err_offset) and
+ * nothing is written.  Host memory stays bounded (pinned rings); device
+ * memory holds the formatted records of the chunks processed before the input
+ * was validated, up to hold_bytes per device, beyond which chunks are
+ * formatted in the second pass (their text kept in HBM up to retain_bytes,
+ * else read again from the source).
+ *
+ * Usage: sid_engine_create, one sid_engine_source_*, then sid_engine_run --
+ * or the three phases separately (multi-rank runs exchange the Lynch
+ * histogram between ingest and estimate: sid_engine_context + the
+ * sid_profile_* calls).  An engine is reusable: set a new source and run
+ * again.  Not thread-safe. */
+typedef struct sid_engine sid_engine;
+typedef struct {
+    int devices;            /* GPUs used (0 = every visible one); chunk j runs on
+                               device (first_device + j % devices) % visible       */
+    int first_device;
+    uint64_t chunk_bytes;   /* input text per chunk (0 = 128 MiB)                  */
+    int slots;              /* device text buffers per device (0 = 3)              */
+    uint64_t hold_bytes;    /* per device, HBM for records held until the input is
+                               validated (0 = 40% of free HBM)                     */
+    uint64_t retain_bytes;  /* per device, HBM for text kept for the second pass
+                               (0 = 40% of free HBM)                               */
+    int host_threads;       /* host threads generating / prefetching input (0 = 8) */
+    int verbose;            /* the reference's "# ..." lines on stderr             */
+    int device_sink;        /* 1: records stay in HBM (measurement), nothing is
+                               written; 0: write() in file order                   */
+} sid_engine_cfg;
+typedef struct {
+    uint64_t sites;              /* non-empty lines parsed                           */
+    uint64_t chunks;
+    uint64_t bytes_in;           /* input text bytes                                 */
+    uint64_t bytes_out;          /* CSV bytes (header excluded)                      */
+    uint64_t chunks_held;        /* formatted in the first pass                      */
+    uint64_t chunks_retained;    /* text kept in HBM for the second pass             */
+    uint64_t chunks_reloaded;    /* text read from the source a second time          */
+    int devices;
+    int status_kind;             /* parse error status of the first bad line, or 0   */
+    uint64_t err_offset;         /* its input byte offset                            */
+    double ingest_s, estimate_s, emit_s;
+    sid_estimate estimate;       /* Lynch paths                                      */
+} sid_run_stats;
+void sid_engine_cfg_default(sid_engine_cfg* cfg);
+int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg, sid_engine** out);
+int sid_engine_destroy(sid_engine* e);
+int sid_engine_devices(const sid_engine* e);
+sid_ctx* sid_engine_context(sid_engine* e, int i);
+/* Sources.  The engine keeps the pointer / descriptor until the next source. */
+int sid_engine_source_text(sid_engine* e, const char* text, uint64_t len);          /* host memory */
+int sid_engine_source_file(sid_engine* e, int fd, uint64_t offset, uint64_t len);   /* regular file */
+/* Text already in HBM on the engine's first device (measurement): d_text must
+ * be readable for 256 bytes past len. */
+int sid_engine_source_device_text(sid_engine* e, const char* d_text, uint64_t len);
+/* The synthetic generator (sid_synth_text) streamed, never stored: sites
+ * [first_site, first_site + n), sites_per_chunk per chunk (0 = about
+ * chunk_bytes of text), generated by host threads into pinned buffers
+ * (on_device = 0) or by a kernel straight into the device buffer (1). */
+int sid_engine_source_synth(sid_engine* e, uint64_t seed, double mean_depth, uint64_t first_site, uint64_t n,
+                            uint64_t sites_per_chrom, uint64_t sites_per_chunk, int on_device);
+/* Phases.  ingest returns the parse status of the first malformed line
+ * (stats->err_offset); estimate runs the Lynch estimate when the method needs
+ * it (given != NULL: skip the Nelder-Mead, use given's pi/eps) and returns its
+ * status (SID_EEMPTY, SID_EBADFUNC); emit writes `header` (unless NULL) and
+ * the records through write(). */
+int sid_engine_ingest(sid_engine* e, sid_run_stats* stats);
+int sid_engine_estimate(sid_engine* e, const sid_estimate* given, sid_estimate* out);
+int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn write, void* user, sid_run_stats* stats);
+int sid_engine_run(sid_engine* e, const char* header, sid_write_fn write, void* user, sid_run_stats* stats);
 
 #ifdef __cplusplus
 }

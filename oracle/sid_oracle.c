@@ -930,15 +930,18 @@ int oracle_call_method(int method, int estimate_prior, double snp_prior, double 
             fprintf(stderr, "# heterozygosity: %e\n", est.heterozygosity);
             fprintf(stderr, "# error: %e\n", est.error_rate);
         }
-        if (u == 0) { /* reference: adjustBenjaminiHochberg reads sorted[0] of an empty vector */
+        if (u == 0 && method == ORACLE_LIKELIHOOD_RATIO) {
+            /* reference: adjustBenjaminiHochberg reads sorted[0] of an empty
+               vector (stats.cpp:73); callBayes (call.cpp:145-211) never calls
+               it and prints no record */
             free(lhom);
             free(lhet);
             rc = 2;
             goto done;
         }
-        uint8_t* pc = (uint8_t*)malloc(u);
-        double* c1 = (double*)malloc(u * sizeof(double));
-        double* c2 = (double*)malloc(u * sizeof(double));
+        uint8_t* pc = (uint8_t*)malloc(u ? u : 1);
+        double* c1 = (double*)malloc((u ? u : 1) * sizeof(double));
+        double* c2 = (double*)malloc((u ? u : 1) * sizeof(double));
         if (method == ORACLE_LIKELIHOOD_RATIO) {
             double* ph = (double*)malloc(u * sizeof(double));
             double* pt = (double*)malloc(u * sizeof(double));

@@ -56,6 +56,21 @@ class Estimate(C.Structure):
                 ("evaluations", C.c_uint64), ("n_unique", C.c_uint64)]
 
 
+class EngineCfg(C.Structure):
+    """sid_engine_cfg (include/sid.h, streaming engine)."""
+    _fields_ = [("devices", C.c_int), ("first_device", C.c_int), ("chunk_bytes", C.c_uint64),
+                ("slots", C.c_int), ("hold_bytes", C.c_uint64), ("retain_bytes", C.c_uint64),
+                ("host_threads", C.c_int), ("verbose", C.c_int), ("device_sink", C.c_int)]
+
+
+class RunStats(C.Structure):
+    _fields_ = [("sites", C.c_uint64), ("chunks", C.c_uint64), ("bytes_in", C.c_uint64),
+                ("bytes_out", C.c_uint64), ("chunks_held", C.c_uint64), ("chunks_retained", C.c_uint64),
+                ("chunks_reloaded", C.c_uint64), ("devices", C.c_int), ("status_kind", C.c_int),
+                ("err_offset", C.c_uint64), ("ingest_s", C.c_double), ("estimate_s", C.c_double),
+                ("emit_s", C.c_double), ("estimate", Estimate)]
+
+
 _LIB = None
 
 # (name, restype, argtypes) for every entry point of include/sid.h
@@ -80,6 +95,7 @@ SIGNATURES = [
     ("sid_lynch_setup", _I, [_P, C.POINTER(Estimate)]),
     ("sid_lynch_objective", _I, [_P, _D, _D, C.POINTER(C.c_double)]),
     ("sid_lynch_prepare", _I, [_P, _I, C.POINTER(Estimate)]),
+    ("sid_lynch_prepare_given", _I, [_P, _I, C.POINTER(Estimate), C.POINTER(Estimate)]),
     ("sid_lookup_sites", _I, [_P, _P, _SZ, _P, _P, _P, _P]),
     ("sid_synth_counts", _I, [_P, _U64, _D, _U64, _SZ, _P, _P]),
     ("sid_synth_text", _I, [_U64, _D, _U64, _SZ, _U64, _P, _SZ, C.POINTER(C.c_size_t)]),
@@ -103,6 +119,19 @@ SIGNATURES = [
     ("sid_call_quality", _I, [_P, _P, _P, _P, _P, _P]),
     ("sid_format_g6", _I, [_D, C.c_char_p, _SZ]),
     ("sid_format_g6_device", _I, [_P, _P, _SZ, _P, _P]),
+    ("sid_engine_cfg_default", None, [C.POINTER(EngineCfg)]),
+    ("sid_engine_create", _I, [C.POINTER(Opts), C.POINTER(EngineCfg), C.POINTER(_P)]),
+    ("sid_engine_destroy", _I, [_P]),
+    ("sid_engine_devices", _I, [_P]),
+    ("sid_engine_context", _P, [_P, _I]),
+    ("sid_engine_source_text", _I, [_P, _P, _U64]),
+    ("sid_engine_source_file", _I, [_P, _I, _U64, _U64]),
+    ("sid_engine_source_device_text", _I, [_P, _P, _U64]),
+    ("sid_engine_source_synth", _I, [_P, _U64, _D, _U64, _U64, _U64, _U64, _I]),
+    ("sid_engine_ingest", _I, [_P, C.POINTER(RunStats)]),
+    ("sid_engine_estimate", _I, [_P, C.POINTER(Estimate), C.POINTER(Estimate)]),
+    ("sid_engine_emit", _I, [_P, C.c_char_p, WRITE_FN, _P, C.POINTER(RunStats)]),
+    ("sid_engine_run", _I, [_P, C.c_char_p, WRITE_FN, _P, C.POINTER(RunStats)]),
 ]
 
 
@@ -377,6 +406,104 @@ class Context:
     def synth_counts(self, seed, depth, first, n, counts_ptr, stream=None):
         check(lib().sid_synth_counts(self.h, seed, depth, first, n, counts_ptr, stream),
               "sid_synth_counts")
+
+
+HEADER = b"chrom,pos,label,gt,hom_conf,het_conf,conf_type\n"
+
+
+class Engine:
+    """The streaming engine (sid_engine_*): pileup text in, CSV out, in
+    line-aligned chunks over one or more devices."""
+
+    def __init__(self, method="local", devices=1, first_device=0, chunk_bytes=0, slots=0, hold_bytes=0,
+                 retain_bytes=0, host_threads=0, verbose=False, device_sink=False, **opts):
+        self.opts = make_opts(method=method, **opts)
+        cfg = EngineCfg()
+        lib().sid_engine_cfg_default(C.byref(cfg))
+        cfg.devices, cfg.first_device, cfg.chunk_bytes, cfg.slots = devices, first_device, chunk_bytes, slots
+        cfg.hold_bytes, cfg.retain_bytes, cfg.host_threads = hold_bytes, retain_bytes, host_threads
+        cfg.verbose, cfg.device_sink = int(bool(verbose)), int(bool(device_sink))
+        self.cfg = cfg
+        h = C.c_void_p()
+        check(lib().sid_engine_create(C.byref(self.opts), C.byref(cfg), C.byref(h)), "sid_engine_create")
+        self.h = h
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sid_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def context(self, i=0):
+        return lib().sid_engine_context(self.h, i)
+
+    def source_text(self, text: bytes):
+        self._keep = C.create_string_buffer(text, len(text)) if text else None
+        check(lib().sid_engine_source_text(self.h, C.cast(self._keep, C.c_void_p) if text else None, len(text)),
+              "source_text")
+
+    def source_host_ptr(self, ptr: int, n: int, keep=None):
+        self._keep = keep
+        check(lib().sid_engine_source_text(self.h, ptr, n), "source_text")
+
+    def source_file(self, fd: int, offset: int = 0, length: int = None):
+        if length is None:
+            length = os.fstat(fd).st_size - offset
+        check(lib().sid_engine_source_file(self.h, fd, offset, length), "source_file")
+
+    def source_device_text(self, ptr: int, n: int, keep=None):
+        self._keep = keep
+        check(lib().sid_engine_source_device_text(self.h, ptr, n), "source_device_text")
+
+    def source_synth(self, seed, n, depth=30.0, first=0, sites_per_chrom=0, sites_per_chunk=0, on_device=True):
+        check(lib().sid_engine_source_synth(self.h, seed, depth, first, n, sites_per_chrom, sites_per_chunk,
+                                            int(bool(on_device))), "source_synth")
+
+    def ingest(self) -> RunStats:
+        st = RunStats()
+        rc = lib().sid_engine_ingest(self.h, C.byref(st))
+        if rc != 0:
+            err = SidError(rc, "sid_engine_ingest")
+            err.offset = st.err_offset
+            err.stats = st
+            raise err
+        return st
+
+    def estimate(self, given: Estimate = None) -> Estimate:
+        out = Estimate()
+        check(lib().sid_engine_estimate(self.h, C.byref(given) if given is not None else None, C.byref(out)),
+              "sid_engine_estimate")
+        return out
+
+    def emit(self, header=HEADER, sink=None, stats: RunStats = None):
+        """Records in file order: returned as bytes (sink None), written to a
+        file descriptor (sink int), or dropped (the device-sink engine)."""
+        parts = []
+
+        def w(_user, data, n):
+            if isinstance(sink, int):
+                os.write(sink, C.string_at(data, n))
+            else:
+                parts.append(C.string_at(data, n))
+            return 0
+        cb = WRITE_FN(w)
+        st = stats if stats is not None else RunStats()
+        check(lib().sid_engine_emit(self.h, header, cb, None, C.byref(st)), "sid_engine_emit")
+        return b"".join(parts), st
+
+    def run(self, header=HEADER, sink=None):
+        st = self.ingest()
+        est = self.estimate()
+        out, st2 = self.emit(header, sink)
+        st.bytes_out, st.emit_s, st.chunks_reloaded = st2.bytes_out, st2.emit_s, st2.chunks_reloaded
+        st.estimate = est
+        return out, st
 
 
 def profile_key(counts: np.ndarray) -> np.ndarray:

@@ -3,6 +3,7 @@
 // parser in parse.cpp, the CSV emitter in emit.cpp.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -15,15 +16,16 @@
 #include "sid_internal.h"
 #include "synth.h"
 
-static thread_local int g_last_hip_error = 0;
+// process-wide: the streaming engine's worker threads report through it
+static std::atomic<int> g_last_hip_error{0};
 
 int sid_set_hip_error(hipError_t e)
 {
-    g_last_hip_error = (int)e;
+    g_last_hip_error.store((int)e);
     return e == hipErrorOutOfMemory ? SID_ENOMEM : SID_EHIP;
 }
 
-extern "C" int sid_last_hip_error(void) { return g_last_hip_error; }
+extern "C" int sid_last_hip_error(void) { return g_last_hip_error.load(); }
 
 extern "C" const char* sid_strerror(int status)
 {

@@ -105,6 +105,13 @@ struct sid_lynch_dev {
     // explicit (merged) table
     bool loaded = false;
     std::vector<uint64_t> tkeys, tcnt;
+    // exported table of the current histogram (sid_profile_table), valid until
+    // the next reset / accumulate / load
+    bool export_valid = false;
+    std::vector<uint64_t> ekeys, ecnt;
+    // no profile survived the coverage filter under -m bayes: every site is
+    // dropped (callBayes prints the header only, call.cpp:145-211)
+    bool empty_classes = false;
     // filtered profiles (device): U of them, sorted by key
     bool setup = false;
     size_t nU = 0;
@@ -234,6 +241,9 @@ void sid_lynch_dev_destroy(sid_lynch_dev* L)
 static int lynch_of(sid_ctx* c, sid_lynch_dev** out)
 {
     if (!c) return SID_EINVAL;
+    // every Lynch entry point works on the context's device, whichever
+    // device the calling thread had current
+    if (hipSetDevice(c->device) != hipSuccess) return SID_EHIP;
     if (!c->lynch) {
         int err;
         c->lynch = sid_lynch_dev_create(&err);
@@ -286,6 +296,7 @@ extern "C" int sid_profile_reset(sid_ctx* c, void* stream)
     L->loaded = false;
     L->tkeys.clear();
     L->tcnt.clear();
+    L->export_valid = false;
     free_setup(L);
     return SID_OK;
 }
@@ -355,8 +366,8 @@ extern "C" int sid_profile_accumulate(sid_ctx* c, const uint16_t* counts, size_t
         }
         L->distinct += F;   // upper bound until the next read of stats[0]
     }
-    L->setup = false;
-    free_class(L);
+    L->export_valid = false;
+    free_setup(L);
     return SID_OK;
 }
 
@@ -446,18 +457,23 @@ static int current_table(sid_lynch_dev* L, std::vector<uint64_t>& keys, std::vec
         return SID_OK;
     }
     if (!L->have_hist) return SID_OK;
-    size_t n;
-    const unsigned long long *k, *v;
-    uint32_t ns, mc;
-    int rc = device_table(L, &n, &k, &v, &ns, &mc);
-    if (rc) return rc;
-    keys.resize(n);
-    cnt.resize(n);
-    if (n) {
-        HIPCHECK(hipMemcpyAsync(keys.data(), k, n * 8, hipMemcpyDeviceToHost, 0));
-        HIPCHECK(hipMemcpyAsync(cnt.data(), v, n * 8, hipMemcpyDeviceToHost, 0));
-        HIPCHECK(hipStreamSynchronize(0));
+    if (!L->export_valid) {   // one export per histogram (compaction, sort, syncs)
+        size_t n;
+        const unsigned long long *k, *v;
+        uint32_t ns, mc;
+        int rc = device_table(L, &n, &k, &v, &ns, &mc);
+        if (rc) return rc;
+        L->ekeys.resize(n);
+        L->ecnt.resize(n);
+        if (n) {
+            HIPCHECK(hipMemcpyAsync(L->ekeys.data(), k, n * 8, hipMemcpyDeviceToHost, 0));
+            HIPCHECK(hipMemcpyAsync(L->ecnt.data(), v, n * 8, hipMemcpyDeviceToHost, 0));
+            HIPCHECK(hipStreamSynchronize(0));
+        }
+        L->export_valid = true;   // until the histogram changes
     }
+    keys = L->ekeys;
+    cnt = L->ecnt;
     return SID_OK;
 }
 
@@ -498,6 +514,7 @@ extern "C" int sid_profile_load(sid_ctx* c, const uint64_t* keys, const uint64_t
         }
     }
     L->loaded = true;
+    L->export_valid = false;
     free_setup(L);
     return SID_OK;
 }
@@ -937,6 +954,14 @@ static int run_estimate_device(sid_ctx* c, int verbose, sid_estimate* est, bool*
 
 extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
 {
+    return sid_lynch_prepare_given(c, verbose, nullptr, est_out);
+}
+
+// The estimate (pi-hat, eps-hat) may come from another device or rank that ran
+// the Nelder-Mead on the same merged table (one
+// estimate, broadcast): then only the per-profile classification runs here.
+extern "C" int sid_lynch_prepare_given(sid_ctx* c, int verbose, const sid_estimate* given, sid_estimate* est_out)
+{
     sid_lynch_dev* L;
     int rc = lynch_of(c, &L);
     if (rc) return rc;
@@ -957,7 +982,16 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
     const bool local_like = method == SID_METHOD_LOCAL || method == SID_METHOD_QUALITY;
     if (verbose && !local_like) std::fprintf(stderr, "# unique profiles: %zu\n", U);
     bool done = false;
-    if (L->nm_device && U > 0) {
+    if (given) {
+        const uint64_t nu = est.n_unique;
+        double dist[4];
+        std::memcpy(dist, est.dist, sizeof dist);
+        est = *given;
+        est.n_unique = nu;
+        std::memcpy(est.dist, dist, sizeof dist);
+        done = true;
+    }
+    if (!done && L->nm_device && U > 0) {
         rc = run_estimate_device(c, verbose, &est, &done);
         if (rc) return rc;
     }
@@ -972,9 +1006,17 @@ extern "C" int sid_lynch_prepare(sid_ctx* c, int verbose, sid_estimate* est_out)
         std::fprintf(stderr, "# heterozygosity: %e\n", est.heterozygosity);
         std::fprintf(stderr, "# error: %e\n", est.error_rate);
     }
-    if (U == 0) return SID_EEMPTY;
-
     free_class(L);
+    L->empty_classes = false;
+    if (U == 0) {
+        // likelihood_ratio: adjustBenjaminiHochberg reads sorted[0] of an
+        // empty vector (stats.cpp:73) and the reference crashes; bayes never
+        // adjusts and prints no record at all (call.cpp:145-211)
+        if (method == SID_METHOD_LIKELIHOOD_RATIO) return SID_EEMPTY;
+        L->empty_classes = true;
+        L->prepared = true;
+        return SID_OK;
+    }
     sid_lynch_eval E;
     make_eval(L->dist, est.heterozygosity, est.error_rate, &E);
     HIPCHECK(sid_launch_profile_lik(L->d_keys, L->d_lnM, U, &E, L->d_lhom, L->d_lhet, 0));
@@ -1082,6 +1124,11 @@ extern "C" int sid_lookup_sites(sid_ctx* c, const uint16_t* counts, size_t n, ui
     if (!L || !L->prepared) return SID_ESTATE;
     if (n == 0) return SID_OK;
     if (!counts || !code || !hom_conf || !het_conf || ((uintptr_t)counts & 7u)) return SID_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return SID_EHIP;
+    if (L->empty_classes) {   // no class: every site dropped (code bit 6)
+        HIPCHECK(hipMemsetAsync(code, SID_CODE_DROPPED, n, (hipStream_t)stream));
+        return SID_OK;
+    }
     HIPCHECK(sid_launch_lookup(counts, n, L->d_ckeys, L->d_cidx, L->cmask, L->special_idx, L->d_pcode,
                                L->d_c1, L->d_c2, L->d_rec, L->d_rcode, L->d_cc, code, hom_conf, het_conf, c->grid_cap,
                                (hipStream_t)stream));

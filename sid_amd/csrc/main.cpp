@@ -2,20 +2,19 @@
 //
 // Same surface as sid.cpp:1-110: getopt flags -h -m -r -R -p -E with the
 // reference's defaults, help text, error messages and exit codes; CSV on
-// stdout, "# ..." diagnostics on stderr.  Behind it:
-//
-//   mmap(file) -> text to HBM, parsed there (sid_dtext_parse; one line-aligned
-//   shard per GPU) -> sid_call_local | sid_profile_* + sid_lynch_prepare +
-//   sid_lookup_sites -> records formatted on the device (sid_dtext_format) ->
-//   stdout in input order.
+// stdout, "# ..." diagnostics on stderr.  Behind it, by default, the
+// streaming engine (run.cpp, sid_engine_*): the input file in line-aligned
+// chunks -> device text buffers -> parse -> call / Lynch -> records formatted
+// on the device -> stdout in file order, every visible GPU taking chunks in
+// turn, with bounded host memory (C4's 3G sites stream through).
 //
 // Extra long options (no short letter, so they cannot collide with the
-// reference's flags): --devices N, --threads N, --stats, --host-parse.
+// reference's flags): --devices N, --threads N, --stats, --host-parse,
+// --chunk-bytes N, --hold-bytes N, --retain-bytes N.
 //
-// Default path: the text itself goes to each device (sid_dtext_parse: a
-// line-aligned byte range per device, parsed in HBM), and the CSV records
-// come back formatted by the device (sid_dtext_format).  --host-parse keeps
-// the host parser and emitter (sid_parse_text / sid_format_csv) instead.
+// --host-parse keeps the round-1 path instead: the whole input parsed on the
+// host (sid_parse_text), counts to the devices, records formatted on the host
+// (sid_format_csv).
 //
 // As in the reference, the whole input is parsed before anything is written
 // to stdout, so a malformed line aborts with no CSV output (call.cpp:11-20
@@ -50,6 +49,9 @@ struct Options {
     int threads = 0;
     bool stats = false;
     bool host_parse = false;   // parse and format on the host (sid_parse_text / sid_format_csv)
+    uint64_t chunk_bytes = 0;  // engine knobs (0 = defaults)
+    uint64_t hold_bytes = 0;
+    uint64_t retain_bytes = 0;
 };
 
 // sid.cpp:26-58; std::map<char,...> iterates E R h m p r
@@ -109,7 +111,7 @@ struct Input {
     size_t len = 0;
     void* map = nullptr;
     std::string owned;
-    int fd = -1;                  // regular file: read by the device path with pread()
+    int fd = -1;                  // regular file: mapped by the engine (sid_engine_source_file)
 };
 
 void map_input(Input& in, bool populate)
@@ -159,30 +161,11 @@ bool open_input(const char* path, Input& in)
     return true;
 }
 
-// first line start at or after c: one past the next '\n' (pread in windows)
-size_t next_line_start(const Input& in, size_t c)
-{
-    if (c == 0 || c >= in.len) return std::min(c, in.len);
-    if (in.data) {
-        const char* nl = (const char*)std::memchr(in.data + c - 1, '\n', in.len - c + 1);
-        return nl ? (size_t)(nl - in.data) + 1 : in.len;
-    }
-    std::vector<char> w(1 << 20);
-    for (size_t at = c - 1; at < in.len; at += w.size()) {
-        const ssize_t r = ::pread(in.fd, w.data(), std::min(w.size(), in.len - at), (off_t)at);
-        if (r <= 0) break;
-        const char* nl = (const char*)std::memchr(w.data(), '\n', (size_t)r);
-        if (nl) return at + (size_t)(nl - w.data()) + 1;
-    }
-    return in.len;
-}
-
 struct Shard {
     size_t begin = 0, end = 0;            // global site range
     sid_ctx* ctx = nullptr;
-    const uint16_t* d_counts = nullptr;   // the shard's counts (owned below or by `text`)
+    const uint16_t* d_counts = nullptr;   // the shard's counts
     uint16_t* d_own_counts = nullptr;     // host-parse path: uploaded counts
-    sid_dtext* text = nullptr;            // device-parse path: resident text + counts
     uint8_t* d_code = nullptr;
     double* d_hom = nullptr;
     double* d_het = nullptr;
@@ -199,6 +182,9 @@ int main(int argc, char** argv)
                                          {"threads", required_argument, nullptr, 2},
                                          {"stats", no_argument, nullptr, 3},
                                          {"host-parse", no_argument, nullptr, 4},
+                                         {"chunk-bytes", required_argument, nullptr, 5},
+                                         {"hold-bytes", required_argument, nullptr, 6},
+                                         {"retain-bytes", required_argument, nullptr, 7},
                                          {nullptr, 0, nullptr, 0}};
     int flag;
     while ((flag = getopt_long(argc, argv, "E:Rhm:p:r:", LONG, nullptr)) != -1) {
@@ -220,6 +206,9 @@ int main(int argc, char** argv)
         case 2: opt.threads = std::max(1, std::atoi(optarg)); break;
         case 3: opt.stats = true; break;
         case 4: opt.host_parse = true; break;
+        case 5: opt.chunk_bytes = std::strtoull(optarg, nullptr, 10); break;
+        case 6: opt.hold_bytes = std::strtoull(optarg, nullptr, 10); break;
+        case 7: opt.retain_bytes = std::strtoull(optarg, nullptr, 10); break;
         default: std::exit(EXIT_FAILURE);
         }
     }
@@ -298,11 +287,77 @@ int main(int argc, char** argv)
         for (auto& x : th) x.join();
     };
 
-    // ---------------------------------------------------------------- parse --
+    auto write_all = [](void*, const char* p, size_t len) -> int {
+        size_t off = 0;
+        while (off < len) {
+            ssize_t w = ::write(1, p + off, len - off);
+            if (w <= 0) return -1;
+            off += (size_t)w;
+        }
+        return 0;
+    };
+    const char* HEADER = "chrom,pos,label,gt,hom_conf,het_conf,conf_type\n";
+
+    // ------------------------------------------------ streaming engine path --
+    if (!opt.host_parse) {
+        const double t0 = now();
+        sid_engine_cfg cfg;
+        sid_engine_cfg_default(&cfg);
+        cfg.devices = D;
+        cfg.chunk_bytes = opt.chunk_bytes;
+        cfg.hold_bytes = opt.hold_bytes;
+        cfg.retain_bytes = opt.retain_bytes;
+        cfg.host_threads = T;
+        cfg.verbose = 1;
+        sid_engine* eng = nullptr;
+        CHECK(sid_engine_create(&opt.o, &cfg, &eng), "engine");
+        if (in.fd >= 0 && !in.data) CHECK(sid_engine_source_file(eng, in.fd, 0, in.len), "input");
+        else CHECK(sid_engine_source_text(eng, in.data, in.len), "input");
+        sid_run_stats st;
+        std::memset(&st, 0, sizeof st);
+        int rc = sid_engine_ingest(eng, &st);
+        if (rc != SID_OK) on_parse_error(rc);
+        const double t1 = now();
+        rc = sid_engine_estimate(eng, nullptr, &st.estimate);
+        if (rc == SID_EEMPTY) {
+            std::fflush(stdout);
+            std::fputs("sid: no profile with coverage >= 4 (the reference crashes here)\n", stderr);
+            std::exit(139);
+        }
+        if (rc == SID_EBADFUNC) {
+            std::fflush(stdout);
+            std::fputs("gsl: nmsimplex2.c: ERROR: non-finite function value encountered\n"
+                       "Default GSL error handler invoked.\n", stderr);
+            std::abort();
+        }
+        CHECK(rc, "estimate");
+        const double t2 = now();
+        std::fflush(stdout);
+        rc = sid_engine_emit(eng, HEADER, write_all, nullptr, &st);
+        if (rc == SID_EIO) std::exit(EXIT_FAILURE);
+        CHECK(rc, "emit");
+        const double t3 = now();
+        if (opt.stats)
+            std::fprintf(stderr,
+                         "{\"sites\": %llu, \"devices\": %d, \"threads\": %d, \"path\": \"stream\", "
+                         "\"parse_s\": %.6f, \"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, "
+                         "\"sites_per_s\": %.1f, \"chunks\": %llu, \"chunks_held\": %llu, "
+                         "\"chunks_retained\": %llu, \"chunks_reloaded\": %llu, \"bytes_in\": %llu, "
+                         "\"bytes_out\": %llu}\n",
+                         (unsigned long long)st.sites, D, T, t1 - t0, t2 - t1, t3 - t2, t3 - t0,
+                         st.sites / std::max(1e-9, t3 - t0), (unsigned long long)st.chunks,
+                         (unsigned long long)st.chunks_held, (unsigned long long)st.chunks_retained,
+                         (unsigned long long)st.chunks_reloaded, (unsigned long long)st.bytes_in,
+                         (unsigned long long)st.bytes_out);
+        // device memory, pinned staging and the mapping go with the process
+        return 0;
+    }
+
+    // ------------------------------------------------------ host-parse path --
     double t0 = now();
-    sid_sites* sites = nullptr;   // host path only
+    sid_sites* sites = nullptr;
     size_t n = 0;
-    if (opt.host_parse) {
+    {
         uint64_t bad = 0;
         map_input(in, true);
         int prc = sid_parse_text(in.data, in.len, T, &sites, &bad);
@@ -327,55 +382,6 @@ int main(int argc, char** argv)
             alloc_out(s);
             HCHECK(hipStreamSynchronize(s.stream), "H2D");
         });
-    } else {
-        // one line-aligned byte range of the text per device, parsed there
-        // a populated mapping, copied by one stream per device, measured
-        // fastest end to end (SID_READ_FD=1: pread into pinned staging instead)
-        const bool use_fd = std::getenv("SID_READ_FD") != nullptr;
-        if (!use_fd) map_input(in, true);
-        std::vector<size_t> cut(D + 1, 0);
-        cut[D] = in.len;
-        for (int d = 1; d < D; ++d) cut[d] = next_line_start(in, std::max(cut[d - 1], in.len / D * d));
-        std::vector<int> rcs(D, SID_OK);
-        std::vector<uint64_t> eoff(D, 0);
-        parallel([&](int d) {
-            make_ctx(d);
-            Shard& s = sh[d];
-            if (in.fd >= 0 && !in.data)
-                rcs[d] = sid_dtext_parse_fd(s.ctx, in.fd, cut[d], cut[d + 1] - cut[d], std::max(1, std::min(8, T / D)),
-                                            &s.text, &eoff[d], s.stream);
-            else
-                rcs[d] = sid_dtext_parse(s.ctx, in.data + cut[d], cut[d + 1] - cut[d], 0, &s.text, &eoff[d],
-                                         s.stream);
-            if (rcs[d] == SID_OK) {
-                s.d_counts = sid_dtext_counts(s.text);
-                s.end = sid_dtext_count(s.text);
-                alloc_out(s);
-            }
-        });
-        // the first malformed line in file order decides
-        int prc = SID_OK;
-        uint64_t first = UINT64_MAX;
-        for (int d = 0; d < D; ++d) {
-            if (rcs[d] == SID_EMALFORMED || rcs[d] == SID_ENULLCHROM || rcs[d] == SID_EMISSING_MQ ||
-                rcs[d] == SID_ENOBQ) {
-                if (cut[d] + eoff[d] < first) {
-                    first = cut[d] + eoff[d];
-                    prc = rcs[d];
-                }
-            } else if (rcs[d] != SID_OK && prc == SID_OK) {
-                prc = rcs[d];
-            }
-        }
-        on_parse_error(prc);
-        size_t off = 0;
-        for (int d = 0; d < D; ++d) {   // global site index ranges
-            const size_t m = sh[d].end;
-            sh[d].begin = off;
-            sh[d].end = off + m;
-            off += m;
-        }
-        n = off;
     }
     double t1 = now();
 
@@ -410,7 +416,7 @@ int main(int argc, char** argv)
                 }
             }
             rcs[d] = sid_lynch_prepare(sh[d].ctx, d == 0, &est[d]);
-            if (rcs[d] == SID_OK && (method == SID_METHOD_LOCAL || quality))
+            if (rcs[d] == SID_OK && method == SID_METHOD_LOCAL)
                 rcs[d] = sid_set_prior(sh[d].ctx, est[d].heterozygosity);   // call.cpp:233, :305
         };
         // device 0 prints the reference's diagnostics; the others run the same
@@ -437,9 +443,7 @@ int main(int argc, char** argv)
         Shard& s = sh[d];
         (void)hipSetDevice(d % ndev);
         const size_t m = s.end - s.begin;
-        if (quality)
-            CHECK(sid_call_quality(s.ctx, s.text, s.d_code, s.d_hom, s.d_het, s.stream), "quality");
-        else if (method == SID_METHOD_LOCAL)
+        if (method == SID_METHOD_LOCAL)
             CHECK(sid_call_local(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "local");
         else
             CHECK(sid_lookup_sites(s.ctx, s.d_counts, m, s.d_code, s.d_hom, s.d_het, s.stream), "lookup");
@@ -448,28 +452,9 @@ int main(int argc, char** argv)
     double t2 = now();
 
     // ----------------------------------------------------------------- emit --
-    std::fputs("chrom,pos,label,gt,hom_conf,het_conf,conf_type\n", stdout);
+    std::fputs(HEADER, stdout);
     std::fflush(stdout);
-    if (!opt.host_parse) {
-        // records formatted on each device, written in device (= file) order
-        auto write_all = [](void*, const char* p, size_t len) -> int {
-            size_t off = 0;
-            while (off < len) {
-                ssize_t w = ::write(1, p + off, len - off);
-                if (w <= 0) return -1;
-                off += (size_t)w;
-            }
-            return 0;
-        };
-        for (int d = 0; d < D; ++d) {
-            Shard& s = sh[d];
-            (void)hipSetDevice(d % ndev);
-            int rc = sid_dtext_format(s.ctx, s.text, 0, s.end - s.begin, s.d_code, s.d_hom, s.d_het, conf_type,
-                                      write_all, nullptr, s.stream);
-            if (rc == SID_EIO) std::exit(EXIT_FAILURE);
-            CHECK(rc, "format");
-        }
-    } else {
+    {
         uint8_t* h_code = nullptr;
         double *h_hom = nullptr, *h_het = nullptr;
         const size_t nn = std::max<size_t>(n, 1);
@@ -527,7 +512,7 @@ int main(int argc, char** argv)
         std::fprintf(stderr,
                      "{\"sites\": %zu, \"devices\": %d, \"threads\": %d, \"path\": \"%s\", \"parse_s\": %.6f, "
                      "\"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, \"sites_per_s\": %.1f}\n",
-                     n, D, T, opt.host_parse ? "host" : "device", t1 - t0, t2 - t1, t3 - t2, t3 - t0,
+                     n, D, T, "host", t1 - t0, t2 - t1, t3 - t2, t3 - t0,
                      n / std::max(1e-9, t3 - t0));
     }
     // device memory, pinned staging and mappings go with the process: freeing

@@ -1,0 +1,1288 @@
+// run.cpp — the streaming engine: one sid run, pileup text in, CSV out, over
+// line-aligned chunks with bounded host memory (include/sid.h "streaming
+// engine").
+//
+// It replaces the reference's whole-input flow -- readFile materialising
+// every site (call.cpp:11-20), callX over the vector (call.cpp:62-289), the
+// output loop (sid.cpp:102-105) -- by a pipeline per device:
+//
+//   uploader   source chunk -> device text buffer (ring of `slots`, or a
+//              retained buffer); H2D on its own stream
+//   compute    line index -> (sync: sites) -> parse -> call -> record lengths
+//              -> (sync: bytes) -> records into a device CSV buffer
+//   drain      CSV buffer -> pinned ring -> writer (D2H on its own stream)
+//   writer     one for all devices: write() in chunk = file order
+//
+// Two passes keep the reference's all-or-nothing output (a malformed line
+// aborts before anything is printed):
+//   pass 1  every chunk is indexed and parsed (validation); -m local / quality
+//           also call and format it, the records held in HBM (hold budget);
+//           the Lynch methods accumulate the profile histogram instead.
+//   (first error in file order -> return it, nothing written)
+//   (Lynch: merge the device histograms, one estimate, class tables)
+//   pass 2  header, then every chunk in file order: held records are copied
+//           back as they are; the others are processed again from their text
+//           (kept in HBM within the retain budget, else read again).
+#include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "sid_internal.h"
+#include "synth.h"
+
+namespace {
+
+constexpr uint64_t PAD = 256;   // readable bytes past every chunk's end (16-B windows, zeroed)
+
+double wall()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// bounded blocking queue; close() wakes every waiter (push fails, pop drains)
+template <class T>
+class Chan {
+public:
+    bool push(T v)
+    {
+        std::unique_lock<std::mutex> l(m_);
+        if (closed_) return false;
+        q_.push_back(std::move(v));
+        cv_.notify_one();
+        return true;
+    }
+    bool pop(T& v)
+    {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return !q_.empty() || closed_; });
+        if (q_.empty()) return false;
+        v = std::move(q_.front());
+        q_.pop_front();
+        return true;
+    }
+    void close()
+    {
+        std::lock_guard<std::mutex> l(m_);
+        closed_ = true;
+        cv_.notify_all();
+    }
+    void reset()
+    {
+        std::lock_guard<std::mutex> l(m_);
+        q_.clear();
+        closed_ = false;
+    }
+
+private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<T> q_;
+    bool closed_ = false;
+};
+
+// Device buffers reused across chunks and runs (hipMalloc/hipFree are slow and
+// hipFree waits for the device).  A buffer returned with an event is reused
+// on another stream only after that event.
+class DevPool {
+public:
+    int device = 0;
+    ~DevPool() { release(); }
+    char* get(uint64_t need, uint64_t* cap, hipStream_t st)
+    {
+        std::lock_guard<std::mutex> l(m_);
+        auto it = free_.lower_bound(need);
+        if (it != free_.end() && it->first <= 2 * need + (64u << 20)) {
+            Entry en = it->second;
+            *cap = it->first;
+            free_.erase(it);
+            if (en.ev) {
+                (void)hipStreamWaitEvent(st, en.ev, 0);
+                evs_.push_back(en.ev);
+            }
+            return en.p;
+        }
+        const uint64_t c = (need + PAD + (4u << 20) - 1) & ~(uint64_t)((4u << 20) - 1);
+        char* p = nullptr;
+        if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+        all_.push_back(p);
+        bytes_ += c;
+        *cap = c;
+        return p;
+    }
+    // `after` (may be null): the buffer is free once the work before it on
+    // its stream has run
+    void put(char* p, uint64_t cap, hipStream_t after)
+    {
+        if (!p) return;
+        std::lock_guard<std::mutex> l(m_);
+        Entry en{p, nullptr};
+        if (after) {
+            if (evs_.empty()) {
+                hipEvent_t ev;
+                if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) evs_.push_back(ev);
+            }
+            if (!evs_.empty()) {
+                en.ev = evs_.back();
+                evs_.pop_back();
+                (void)hipEventRecord(en.ev, after);
+            }
+        }
+        free_.emplace(cap, en);
+    }
+    uint64_t bytes() const { return bytes_; }
+    void release()
+    {
+        (void)hipSetDevice(device);
+        for (char* p : all_) (void)hipFree(p);
+        for (auto& kv : free_)
+            if (kv.second.ev) (void)hipEventDestroy(kv.second.ev);
+        for (hipEvent_t ev : evs_) (void)hipEventDestroy(ev);
+        all_.clear();
+        free_.clear();
+        evs_.clear();
+        bytes_ = 0;
+    }
+
+private:
+    struct Entry {
+        char* p;
+        hipEvent_t ev;
+    };
+    std::mutex m_;
+    std::multimap<uint64_t, Entry> free_;
+    std::vector<char*> all_;
+    std::vector<hipEvent_t> evs_;
+    uint64_t bytes_ = 0;
+};
+
+struct ChunkRec {
+    uint64_t off = 0, len = 0;       // input bytes (host / file / device text sources)
+    uint64_t site0 = 0, nsites = 0;  // synthetic sources: sites [site0, site0 + nsites)
+    int dev = 0;
+    uint64_t parsed = 0;             // sites found by the index
+    char* held = nullptr;            // CSV records formatted in pass 1 (device)
+    uint64_t held_cap = 0, held_len = 0;
+    char* kept = nullptr;            // text kept for pass 2 (device)
+    uint64_t kept_cap = 0, kept_len = 0;
+    uint64_t err = ~0ull;            // min(offset * 8 + kind) of the chunk's malformed lines
+};
+
+enum SrcKind { SRC_NONE, SRC_HOST, SRC_FILE, SRC_DEVICE, SRC_SYNTH_HOST, SRC_SYNTH_DEVICE };
+
+struct Loaded {
+    uint64_t j = 0;
+    int kind = 0;            // 0 = text in a ring slot / kept buffer / device source, 1 = held records
+    int slot = -1;           // ring slot, or -1
+    const char* base = nullptr;
+    uint64_t c0 = 0, c1 = 0;
+    hipEvent_t ev = nullptr; // upload done (slot only)
+};
+
+struct OutItem {
+    uint64_t j = 0;
+    char* buf = nullptr;
+    uint64_t cap = 0, len = 0;
+    hipEvent_t ev = nullptr;  // records written (null: already complete)
+    bool pooled = true;
+};
+
+struct Piece {
+    uint64_t j = 0;
+    int ps = -1;              // pinned slot, -1: no bytes
+    uint64_t len = 0;
+    bool last = false;
+    char* buf = nullptr;      // the chunk's device CSV buffer, returned after the last piece
+    uint64_t cap = 0;
+};
+
+struct Slot {
+    char* text = nullptr;
+    uint64_t cap = 0;
+    hipEvent_t ev_up = nullptr;    // upload done
+    hipEvent_t ev_free = nullptr;  // last read of the text done
+    bool used = false;
+};
+
+struct Dev {
+    int index = 0, device = 0;
+    sid_ctx* ctx = nullptr;
+    hipStream_t s_up = nullptr, s_comp = nullptr, s_d2h = nullptr;
+    std::vector<Slot> slots;
+    Chan<int> free_slots;
+    Chan<Loaded> loaded;
+    Chan<OutItem> drain_q;
+    Chan<Piece> out_q;
+    Chan<int> free_pinned;
+    std::vector<char*> pinned;
+    std::vector<hipEvent_t> pinned_ev;
+    uint64_t pinned_cap = 0;
+    sid_chunk_ws ws;
+    uint64_t* h_small = nullptr;   // pinned: state[0..5] read back
+    DevPool pool;
+    uint64_t hold_budget = 0, retain_budget = 0;
+    std::atomic<uint64_t> hold_used{0}, retain_used{0};
+    std::atomic<bool> hold_full{false};
+    std::mutex ev_m;
+    std::vector<hipEvent_t> ev_cache;   // events marking a chunk's records written (compute -> drain)
+    hipEvent_t take_event()
+    {
+        std::lock_guard<std::mutex> l(ev_m);
+        hipEvent_t ev = nullptr;
+        if (!ev_cache.empty()) {
+            ev = ev_cache.back();
+            ev_cache.pop_back();
+        } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            ev = nullptr;
+        }
+        return ev;
+    }
+    void give_event(hipEvent_t ev)
+    {
+        std::lock_guard<std::mutex> l(ev_m);
+        ev_cache.push_back(ev);
+    }
+};
+
+}  // namespace
+
+struct sid_engine {
+    sid_opts opts{};
+    sid_engine_cfg cfg{};
+    std::vector<std::unique_ptr<Dev>> devs;
+    // source
+    int src = SRC_NONE;
+    const char* text = nullptr;     // SRC_HOST / SRC_FILE (mapping) / SRC_DEVICE
+    uint64_t text_len = 0;
+    void* map = nullptr;
+    uint64_t map_len = 0, map_skew = 0;
+    uint64_t synth_seed = 0, synth_first = 0, synth_n = 0, synth_spc = 0, synth_per = 0;
+    double synth_depth = 30.0;
+    std::vector<uint64_t> synth_cdf;
+    uint64_t* d_cdf = nullptr;       // on the first device (SRC_SYNTH_DEVICE)
+    std::vector<uint64_t*> d_cdf_dev;
+    std::vector<sid_synth_gen_ws> gen_ws;
+    std::vector<ChunkRec> recs;
+    // run state
+    bool lynch = false, quality = false, ingested = false, estimated = false;
+    const char* conf_type = "p_value";
+    std::atomic<int> rc{SID_OK};
+    std::atomic<uint64_t> first_err{UINT64_MAX};
+    std::atomic<uint64_t> reloaded{0};
+    // host-generated input: pinned buffers
+    std::vector<char*> gen_buf;
+    std::vector<uint64_t> gen_cap;
+    std::vector<hipEvent_t> gen_ev;   // H2D of the buffer done (recorded by the uploader)
+    std::vector<int> gen_dev;         // device whose stream recorded gen_ev
+    uint64_t per_chunk_cap = 0;
+    sid_estimate est{};
+};
+
+namespace {
+
+void close_all(sid_engine* e)
+{
+    for (auto& d : e->devs) {
+        d->free_slots.close();
+        d->loaded.close();
+        d->drain_q.close();
+        d->out_q.close();
+        d->free_pinned.close();
+    }
+}
+
+// the first failure wins; every queue closes so no thread waits on a peer
+// that has stopped
+void fail(sid_engine* e, int rc)
+{
+    int ok = SID_OK;
+    e->rc.compare_exchange_strong(ok, rc);
+    close_all(e);
+}
+
+int hipfail(sid_engine* e, hipError_t x)
+{
+    if (x == hipSuccess) return SID_OK;
+    const int rc = sid_set_hip_error(x);
+    fail(e, rc);
+    return rc;
+}
+
+const uint64_t CHUNK_DEFAULT = 128ull << 20;
+
+uint64_t chunk_bytes(const sid_engine* e) { return e->cfg.chunk_bytes ? e->cfg.chunk_bytes : CHUNK_DEFAULT; }
+
+// first line start at or after c (one past the next '\n')
+uint64_t next_line_start(const char* t, uint64_t len, uint64_t c)
+{
+    if (c == 0 || c >= len) return std::min(c, len);
+    const char* nl = (const char*)std::memchr(t + c - 1, '\n', len - c + 1);
+    return nl ? (uint64_t)(nl - t) + 1 : len;
+}
+
+void split_host_text(sid_engine* e, const char* t, uint64_t len)
+{
+    const uint64_t C = chunk_bytes(e);
+    e->recs.clear();
+    uint64_t at = 0;
+    while (at < len) {
+        uint64_t end = next_line_start(t, len, std::max(at + 1, std::min(len, at + C)));
+        if (end <= at) end = len;
+        ChunkRec r;
+        r.off = at;
+        r.len = end - at;
+        e->recs.push_back(r);
+        at = end;
+    }
+}
+
+// ------------------------------------------------------------- generator --
+// the synthetic text of sites [first, first + n) into dst (cap bytes); the
+// same bytes as sid_synth_text (capi.cpp), without intermediate strings.
+// Returns the length, or UINT64_MAX when it does not fit.
+uint64_t synth_host(const std::vector<uint64_t>& cdf, uint64_t seed, uint64_t first, uint64_t n, uint64_t spc,
+                    char* dst, uint64_t cap)
+{
+    static const char UP[] = "ACGT", LO[] = "acgt";
+    const uint32_t k = (uint32_t)cdf.size();
+    char* o = dst;
+    char* const end = dst + cap;
+    auto put_u = [&](uint64_t v) {
+        char tmp[24];
+        int m = 0;
+        do {
+            tmp[m++] = (char)('0' + v % 10);
+            v /= 10;
+        } while (v);
+        while (m) *o++ = tmp[--m];
+    };
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t site = first + i;
+        const uint64_t chrom = spc ? site / spc + 1 : 1;
+        const uint64_t pos = spc ? site % spc + 1 : site + 1;
+        sid_synth_site s = sid_synth_site_header(seed, site, cdf.data(), k);
+        // worst case of this line: names and numbers (64) + 4 bytes per read
+        if ((uint64_t)(end - o) < 64 + 5ull * s.depth) return UINT64_MAX;
+        *o++ = 'c';
+        *o++ = 'h';
+        *o++ = 'r';
+        put_u(chrom);
+        *o++ = '\t';
+        put_u(pos);
+        *o++ = '\t';
+        *o++ = UP[s.ref];
+        *o++ = '\t';
+        put_u(s.depth);
+        *o++ = '\t';
+        if (s.depth == 0) {
+            *o++ = '*';
+            *o++ = '\t';
+            *o++ = '*';
+            *o++ = '\n';
+            continue;
+        }
+        char* q = o + 4 * s.depth;   // qualities after the bases: written in one walk
+        char* qs = q;
+        for (uint32_t r = 0; r < s.depth; ++r) {
+            uint32_t strand;
+            const uint32_t b = sid_synth_read_base(&s, r, &strand);
+            int st, en;
+            uint32_t ql;
+            sid_synth_read_marks(&s, r, &st, &en, &ql);
+            if (st) {
+                *o++ = '^';
+                *o++ = ']';
+            }
+            *o++ = b == s.ref ? (strand ? '.' : ',') : (strand ? UP[b] : LO[b]);
+            if (en) *o++ = '$';
+            *q++ = (char)('!' + ql);
+        }
+        *o++ = '\t';
+        std::memmove(o, qs, s.depth);
+        o += s.depth;
+        *o++ = '\n';
+    }
+    return (uint64_t)(o - dst);
+}
+
+}  // namespace
+
+// ================================================================= C ABI ==
+extern "C" void sid_engine_cfg_default(sid_engine_cfg* c)
+{
+    if (!c) return;
+    std::memset(c, 0, sizeof *c);
+}
+
+extern "C" int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg, sid_engine** out)
+{
+    if (!out) return SID_EINVAL;
+    *out = nullptr;
+    int nvis = 0;
+    if (hipGetDeviceCount(&nvis) != hipSuccess || nvis <= 0) return SID_EHIP;
+    sid_engine* e = new sid_engine();
+    if (opts) e->opts = *opts; else sid_opts_default(&e->opts);
+    if (cfg) e->cfg = *cfg; else sid_engine_cfg_default(&e->cfg);
+    const int D = e->cfg.devices > 0 ? e->cfg.devices : nvis;
+    const int R = e->cfg.slots > 0 ? e->cfg.slots : 3;
+    for (int i = 0; i < D; ++i) {
+        auto d = std::make_unique<Dev>();
+        d->index = i;
+        d->device = (e->cfg.first_device + i) % nvis;
+        d->pool.device = d->device;
+        int rc = sid_create(d->device, &e->opts, &d->ctx);
+        hipError_t x = hipSuccess;
+        if (rc == SID_OK) {
+            x = hipStreamCreateWithFlags(&d->s_up, hipStreamNonBlocking);
+            if (x == hipSuccess) x = hipStreamCreateWithFlags(&d->s_comp, hipStreamNonBlocking);
+            if (x == hipSuccess) x = hipStreamCreateWithFlags(&d->s_d2h, hipStreamNonBlocking);
+            if (x == hipSuccess) x = hipHostMalloc((void**)&d->h_small, 64, hipHostMallocDefault);
+            d->slots.resize(R);
+            for (auto& s : d->slots) {
+                if (x == hipSuccess) x = hipEventCreateWithFlags(&s.ev_up, hipEventDisableTiming);
+                if (x == hipSuccess) x = hipEventCreateWithFlags(&s.ev_free, hipEventDisableTiming);
+            }
+            if (x != hipSuccess) rc = sid_set_hip_error(x);
+        }
+        e->devs.push_back(std::move(d));
+        if (rc != SID_OK) {
+            sid_engine_destroy(e);
+            return rc;
+        }
+    }
+    *out = e;
+    return SID_OK;
+}
+
+static void drop_source(sid_engine* e)
+{
+    if (e->map) munmap(e->map, e->map_len);
+    e->map = nullptr;
+    for (auto& r : e->recs) {
+        Dev& d = *e->devs[r.dev];
+        if (r.held) d.pool.put(r.held, r.held_cap, nullptr);
+        if (r.kept) d.pool.put(r.kept, r.kept_cap, nullptr);
+        r.held = r.kept = nullptr;
+    }
+    e->recs.clear();
+    e->src = SRC_NONE;
+    e->text = nullptr;
+    e->text_len = 0;
+    e->ingested = e->estimated = false;
+}
+
+extern "C" int sid_engine_destroy(sid_engine* e)
+{
+    if (!e) return SID_OK;
+    for (auto& d : e->devs) (void)hipSetDevice(d->device), (void)hipDeviceSynchronize();
+    drop_source(e);
+    for (auto& d : e->devs) {
+        (void)hipSetDevice(d->device);
+        for (auto& s : d->slots) {
+            if (s.text) (void)hipFree(s.text);
+            if (s.ev_up) (void)hipEventDestroy(s.ev_up);
+            if (s.ev_free) (void)hipEventDestroy(s.ev_free);
+        }
+        for (char* p : d->pinned) (void)hipHostFree(p);
+        for (hipEvent_t ev : d->pinned_ev) (void)hipEventDestroy(ev);
+        for (hipEvent_t ev : d->ev_cache) (void)hipEventDestroy(ev);
+        sid_chunk_release(&d->ws);
+        if (d->h_small) (void)hipHostFree(d->h_small);
+        for (hipStream_t s : {d->s_up, d->s_comp, d->s_d2h})
+            if (s) (void)hipStreamDestroy(s);
+        d->pool.release();
+        sid_destroy(d->ctx);
+    }
+    for (size_t i = 0; i < e->d_cdf_dev.size(); ++i)
+        if (e->d_cdf_dev[i]) (void)hipSetDevice(e->devs[i]->device), (void)hipFree(e->d_cdf_dev[i]);
+    for (size_t i = 0; i < e->gen_ws.size(); ++i) {
+        (void)hipSetDevice(e->devs[i]->device);
+        sid_synth_gen_release(&e->gen_ws[i]);
+    }
+    for (char* p : e->gen_buf) (void)hipHostFree(p);
+    for (hipEvent_t ev : e->gen_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    delete e;
+    return SID_OK;
+}
+
+extern "C" int sid_engine_devices(const sid_engine* e) { return e ? (int)e->devs.size() : 0; }
+
+extern "C" sid_ctx* sid_engine_context(sid_engine* e, int i)
+{
+    if (!e || i < 0 || i >= (int)e->devs.size()) return nullptr;
+    return e->devs[i]->ctx;
+}
+
+static void assign_devices(sid_engine* e)
+{
+    const int D = (int)e->devs.size();
+    for (size_t j = 0; j < e->recs.size(); ++j) e->recs[j].dev = (int)(j % D);
+}
+
+extern "C" int sid_engine_source_text(sid_engine* e, const char* text, uint64_t len)
+{
+    if (!e || (!text && len)) return SID_EINVAL;
+    drop_source(e);
+    e->src = SRC_HOST;
+    e->text = text;
+    e->text_len = len;
+    split_host_text(e, text, len);
+    assign_devices(e);
+    return SID_OK;
+}
+
+extern "C" int sid_engine_source_file(sid_engine* e, int fd, uint64_t offset, uint64_t len)
+{
+    if (!e || fd < 0) return SID_EINVAL;
+    drop_source(e);
+    if (len == 0) {
+        e->src = SRC_HOST;
+        return SID_OK;
+    }
+    const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+    const uint64_t a = offset & ~(pg - 1);
+    e->map_skew = offset - a;
+    e->map_len = len + e->map_skew;
+    // populated up front below 8 GiB (one kernel pass over the page tables was
+    // measured fastest); larger inputs are populated chunk by chunk
+    // ahead of the uploads and released behind them
+    const bool populate = len <= (8ull << 30);
+    void* m = mmap(nullptr, e->map_len, PROT_READ, MAP_PRIVATE | (populate ? MAP_POPULATE : 0), fd, (off_t)a);
+    if (m == MAP_FAILED) return SID_EIO;
+    (void)madvise(m, e->map_len, MADV_SEQUENTIAL);
+    e->map = m;
+    e->src = SRC_FILE;
+    e->text = (const char*)m + e->map_skew;
+    e->text_len = len;
+    split_host_text(e, e->text, len);
+    assign_devices(e);
+    return SID_OK;
+}
+
+extern "C" int sid_engine_source_device_text(sid_engine* e, const char* d_text, uint64_t len)
+{
+    if (!e || (!d_text && len)) return SID_EINVAL;
+    drop_source(e);
+    e->src = SRC_DEVICE;
+    e->text = d_text;
+    e->text_len = len;
+    // line-aligned cuts: a window around each nominal cut is read back
+    Dev& d0 = *e->devs[0];
+    if (hipSetDevice(d0.device) != hipSuccess) return SID_EHIP;
+    const uint64_t C = chunk_bytes(e);
+    std::vector<char> w(1 << 16);
+    uint64_t at = 0;
+    while (at < len) {
+        uint64_t c = std::min(len, at + C);
+        while (c < len) {   // the next '\n' at or after c - 1
+            const uint64_t m = std::min<uint64_t>(w.size(), len - (c - 1));
+            if (hipMemcpy(w.data(), d_text + c - 1, m, hipMemcpyDeviceToHost) != hipSuccess) return SID_EHIP;
+            const char* nl = (const char*)std::memchr(w.data(), '\n', m);
+            if (nl) {
+                c = c - 1 + (uint64_t)(nl - w.data()) + 1;
+                break;
+            }
+            c += m;
+        }
+        c = std::min(c, len);
+        ChunkRec r;
+        r.off = at;
+        r.len = c - at;
+        e->recs.push_back(r);
+        at = c;
+    }
+    for (auto& r : e->recs) r.dev = 0;   // the text lives on the first device
+    return SID_OK;
+}
+
+extern "C" int sid_engine_source_synth(sid_engine* e, uint64_t seed, double mean_depth, uint64_t first_site,
+                                       uint64_t n, uint64_t sites_per_chrom, uint64_t sites_per_chunk, int on_device)
+{
+    if (!e || !(mean_depth >= 0) || mean_depth > 600) return SID_EINVAL;
+    drop_source(e);
+    e->src = on_device ? SRC_SYNTH_DEVICE : SRC_SYNTH_HOST;
+    e->synth_seed = seed;
+    e->synth_depth = mean_depth;
+    e->synth_first = first_site;
+    e->synth_n = n;
+    e->synth_spc = sites_per_chrom;
+    sid_poisson_cdf(mean_depth, e->synth_cdf);
+    // about 2.7 B per read (base, quality, marks) + 20 B of fields per site
+    const double per_site = 20.0 + 2.75 * mean_depth;
+    uint64_t per = sites_per_chunk ? sites_per_chunk : (uint64_t)(chunk_bytes(e) / per_site);
+    per = std::max<uint64_t>(per, 1);
+    e->synth_per = per;
+    // capacity: the mean plus a wide margin (the generator reports overflow)
+    e->per_chunk_cap = (uint64_t)(per * per_site * 1.25) + (64ull + 5ull * e->synth_cdf.size()) + (1u << 20);
+    for (uint64_t s = 0; s < n; s += per) {
+        ChunkRec r;
+        r.site0 = first_site + s;
+        r.nsites = std::min(per, n - s);
+        e->recs.push_back(r);
+    }
+    assign_devices(e);
+    if (on_device) {
+        const size_t D = e->devs.size();
+        e->d_cdf_dev.resize(D, nullptr);
+        e->gen_ws.resize(D);
+        for (size_t i = 0; i < D; ++i) {
+            if (hipSetDevice(e->devs[i]->device) != hipSuccess) return SID_EHIP;
+            if (e->d_cdf_dev[i]) (void)hipFree(e->d_cdf_dev[i]);
+            e->d_cdf_dev[i] = nullptr;
+            if (hipMalloc(&e->d_cdf_dev[i], e->synth_cdf.size() * 8) != hipSuccess ||
+                hipMemcpy(e->d_cdf_dev[i], e->synth_cdf.data(), e->synth_cdf.size() * 8, hipMemcpyHostToDevice) !=
+                    hipSuccess)
+                return SID_EHIP;
+        }
+    }
+    return SID_OK;
+}
+
+// --------------------------------------------------------------- threads --
+namespace {
+
+bool needs_format_pass1(const sid_engine* e) { return !e->lynch; }
+
+// the uploader of device d: the chunks of `list` into device buffers, in order
+void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass)
+{
+    if (hipSetDevice(d.device) != hipSuccess) return (void)fail(e, SID_EHIP);
+    for (uint64_t j : list) {
+        if (e->rc.load() != SID_OK) break;
+        if (pass == 1 && j > e->first_err.load()) break;
+        ChunkRec& r = e->recs[j];
+        Loaded L;
+        L.j = j;
+        if (pass == 2 && r.held) {
+            L.kind = 1;
+            if (!d.loaded.push(L)) break;
+            continue;
+        }
+        if (e->src == SRC_DEVICE) {   // resident text: a view, 16-B aligned base
+            const uint64_t a = (uint64_t)(uintptr_t)(e->text + r.off);
+            L.base = (const char*)(uintptr_t)(a & ~(uint64_t)15);
+            L.c0 = a & 15;
+            L.c1 = L.c0 + r.len;
+            if (!d.loaded.push(L)) break;
+            continue;
+        }
+        if (pass == 2 && r.kept) {
+            L.base = r.kept;
+            L.c0 = 0;
+            L.c1 = r.kept_len;
+            if (!d.loaded.push(L)) break;
+            continue;
+        }
+        // text length (synthetic sources: a bound until generated)
+        uint64_t need = e->src == SRC_SYNTH_HOST || e->src == SRC_SYNTH_DEVICE ? e->per_chunk_cap : r.len;
+        // keep it for pass 2?  Lynch always needs a second pass; local and
+        // quality only once the hold budget ran out
+        const bool want_keep = pass == 1 && (e->lynch || d.hold_full.load()) &&
+                               d.retain_used.load() + need + PAD <= d.retain_budget;
+        char* dst = nullptr;
+        uint64_t dcap = 0;
+        int slot = -1;
+        hipError_t x = hipSuccess;
+        if (want_keep) {
+            dst = d.pool.get(need + PAD, &dcap, d.s_up);
+            if (!dst) return (void)fail(e, SID_ENOMEM);
+            d.retain_used += dcap;
+        } else {
+            if (!d.free_slots.pop(slot)) break;
+            Slot& s = d.slots[slot];
+            if (s.cap < need) {   // grow: wait for the slot's last reader first
+                if (s.used) x = hipEventSynchronize(s.ev_free);
+                if (s.text) (void)hipFree(s.text);
+                s.text = nullptr;
+                s.cap = 0;
+                const uint64_t c = std::max<uint64_t>(need, chunk_bytes(e) + (chunk_bytes(e) >> 3));
+                if (x == hipSuccess) x = hipMalloc(&s.text, c + PAD);
+                if (x == hipSuccess) s.cap = c;
+                s.used = false;
+            } else if (s.used) {
+                x = hipStreamWaitEvent(d.s_up, s.ev_free, 0);
+            }
+            if (x != hipSuccess) return (void)hipfail(e, x);
+            dst = s.text;
+            dcap = s.cap + PAD;
+            s.used = true;
+        }
+        uint64_t len = r.len;
+        if (e->src == SRC_HOST || e->src == SRC_FILE) {
+            if (len) x = hipMemcpyAsync(dst, e->text + r.off, len, hipMemcpyHostToDevice, d.s_up);
+            if (e->src == SRC_FILE && x == hipSuccess && e->text_len > (8ull << 30)) {
+                // large mapped inputs: drop the chunk's page-table entries once
+                // copied (the page cache keeps the data; RSS stays bounded)
+                x = hipStreamSynchronize(d.s_up);
+                const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+                const uint64_t a = (e->map_skew + r.off + pg - 1) & ~(pg - 1);
+                const uint64_t b = (e->map_skew + r.off + len) & ~(pg - 1);
+                if (b > a) (void)madvise((char*)e->map + a, b - a, MADV_DONTNEED);
+            }
+        } else if (e->src == SRC_SYNTH_HOST) {
+            // generated by host threads into this device's pinned staging,
+            // one region per thread, each region DMA'd to its place
+            const size_t gi = (size_t)d.index;
+            const int T = std::max(1, e->cfg.host_threads > 0 ? e->cfg.host_threads : 8);
+            const uint64_t region = e->per_chunk_cap / T + e->per_chunk_cap / (4 * T) + 64 + 5 * e->synth_cdf.size();
+            x = hipEventSynchronize(e->gen_ev[gi]);   // the previous chunk's copies are done
+            if (x == hipSuccess && e->gen_cap[gi] < region * T) {
+                if (e->gen_buf[gi]) (void)hipHostFree(e->gen_buf[gi]);
+                e->gen_buf[gi] = nullptr;
+                e->gen_cap[gi] = 0;
+                x = hipHostMalloc((void**)&e->gen_buf[gi], region * T, hipHostMallocDefault);
+                if (x == hipSuccess) e->gen_cap[gi] = region * T;
+            }
+            std::vector<uint64_t> plen(T, 0);
+            if (x == hipSuccess) {
+                std::vector<std::thread> th;
+                for (int t = 0; t < T; ++t)
+                    th.emplace_back([&, t] {
+                        const uint64_t a = r.nsites * t / T, b = r.nsites * (t + 1) / T;
+                        plen[t] = synth_host(e->synth_cdf, e->synth_seed, r.site0 + a, b - a, e->synth_spc,
+                                             e->gen_buf[gi] + region * t, region);
+                    });
+                for (auto& t : th) t.join();
+            }
+            len = 0;
+            for (int t = 0; t < T && x == hipSuccess; ++t) {
+                if (plen[t] == UINT64_MAX || len + plen[t] > dcap - PAD) return (void)fail(e, SID_ENOMEM);
+                if (plen[t])
+                    x = hipMemcpyAsync(dst + len, e->gen_buf[gi] + region * t, plen[t], hipMemcpyHostToDevice,
+                                       d.s_up);
+                len += plen[t];
+            }
+            if (x == hipSuccess) x = hipEventRecord(e->gen_ev[gi], d.s_up);
+        } else if (e->src == SRC_SYNTH_DEVICE) {
+            sid_synth_gen_ws& G = e->gen_ws[d.index];
+            x = sid_launch_synth_text(e->synth_seed, e->d_cdf_dev[d.index], (uint32_t)e->synth_cdf.size(), r.site0,
+                                      r.nsites, e->synth_spc, &G, dst, dcap - PAD, d.s_up);
+            if (x == hipSuccess) x = hipMemcpyAsync(d.h_small + 6, G.res, 16, hipMemcpyDeviceToHost, d.s_up);
+            if (x == hipSuccess) x = hipStreamSynchronize(d.s_up);
+            if (x == hipSuccess) {
+                if (d.h_small[7]) return (void)fail(e, SID_ENOMEM);   // beyond the generator's margin
+                len = d.h_small[6];
+            }
+        }
+        if (x == hipSuccess) x = hipMemsetAsync(dst + len, 0, PAD, d.s_up);
+        hipEvent_t ev = nullptr;
+        if (slot >= 0) {
+            ev = d.slots[slot].ev_up;
+            if (x == hipSuccess) x = hipEventRecord(ev, d.s_up);
+        } else if (x == hipSuccess) {
+            x = hipStreamSynchronize(d.s_up);   // kept buffers: no per-buffer event
+        }
+        if (x != hipSuccess) return (void)hipfail(e, x);
+        if (want_keep) {
+            r.kept = dst;
+            r.kept_cap = dcap;
+            r.kept_len = len;
+        }
+        L.slot = slot;
+        L.base = dst;
+        L.c0 = 0;
+        L.c1 = len;
+        L.ev = ev;
+        if (pass == 2) e->reloaded++;
+        if (!d.loaded.push(L)) break;
+    }
+    d.loaded.close();
+}
+
+int call_sites(sid_engine* e, Dev& d, const Loaded& L, uint64_t n)
+{
+    sid_chunk_ws& W = d.ws;
+    if (n == 0) return SID_OK;
+    const int m = e->opts.method;
+    if (m == SID_METHOD_QUALITY) return sid_chunk_quality(d.ctx, &W, L.base, L.c1, n, d.s_comp);
+    if (m == SID_METHOD_LOCAL)
+        return sid_call_local(d.ctx, (const uint16_t*)W.counts, n, W.code, W.hom, W.het, d.s_comp);
+    return sid_lookup_sites(d.ctx, (const uint16_t*)W.counts, n, W.code, W.hom, W.het, d.s_comp);
+}
+
+// the compute thread of device d, for one pass
+void compute(sid_engine* e, Dev& d, int pass)
+{
+    if (hipSetDevice(d.device) != hipSuccess) return (void)fail(e, SID_EHIP);
+    sid_chunk_ws& W = d.ws;
+    uint64_t* hs = d.h_small;
+    const int qmode = e->quality ? 1 : 0;
+    auto sync = [&]() { return hipStreamSynchronize(d.s_comp); };
+    Loaded L;
+    while (d.loaded.pop(L)) {
+        if (e->rc.load() != SID_OK) break;
+        ChunkRec& r = e->recs[L.j];
+        auto release_slot = [&]() {
+            if (L.slot < 0) return;
+            (void)hipEventRecord(d.slots[L.slot].ev_free, d.s_comp);
+            d.free_slots.push(L.slot);
+        };
+        if (L.kind == 1) {   // pass 2: records held since pass 1
+            OutItem it;
+            it.j = L.j;
+            it.buf = r.held;
+            it.cap = r.held_cap;
+            it.len = r.held_len;
+            r.held = nullptr;
+            if (e->cfg.device_sink) d.pool.put(it.buf, it.cap, nullptr);
+            else if (!d.drain_q.push(it)) break;
+            continue;
+        }
+        if (pass == 1 && L.j > e->first_err.load()) {
+            release_slot();
+            continue;
+        }
+        int rc = SID_OK;
+        hipError_t x = hipSuccess;
+        if (L.ev) x = hipStreamWaitEvent(d.s_comp, L.ev, 0);
+        if (x == hipSuccess) rc = sid_chunk_reserve(&W, L.c1 - (L.c0 & ~(uint64_t)15), 0);
+        if (rc == SID_OK && x == hipSuccess) rc = sid_chunk_index(&W, L.base, L.c0, L.c1, d.s_comp);
+        if (rc == SID_OK && x == hipSuccess) x = hipMemcpyAsync(hs, W.state, 8, hipMemcpyDeviceToHost, d.s_comp);
+        if (rc == SID_OK && x == hipSuccess) x = sync();
+        if (x != hipSuccess) return (void)hipfail(e, x);
+        if (rc != SID_OK) return (void)fail(e, rc);
+        const uint64_t n = hs[0];
+        r.parsed = n;
+        rc = sid_chunk_reserve(&W, 0, n);
+        if (rc == SID_OK) rc = sid_chunk_parse(&W, L.base, L.c0, L.c1, n, qmode, d.s_comp);
+        if (rc != SID_OK) return (void)fail(e, rc);
+        const bool lynch_hist = pass == 1 && e->lynch;
+        const bool format = pass == 2 || (needs_format_pass1(e) && !d.hold_full.load());
+        if (lynch_hist) {
+            x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
+            if (x != hipSuccess) return (void)hipfail(e, x);
+            rc = sid_profile_accumulate(d.ctx, (const uint16_t*)W.counts, n, d.s_comp);   // synchronises
+            if (rc == SID_OK && n == 0) x = sync();
+            if (rc != SID_OK) return (void)fail(e, rc);
+            if (x != hipSuccess) return (void)hipfail(e, x);
+        } else if (format) {
+            rc = call_sites(e, d, L, n);
+            if (rc == SID_OK) rc = sid_chunk_fmt_len(&W, L.base, L.c1, n, e->conf_type, d.s_comp);
+            if (rc != SID_OK) return (void)fail(e, rc);
+            x = hipMemcpyAsync(hs + 3, W.state + 3, 24, hipMemcpyDeviceToHost, d.s_comp);
+            if (x == hipSuccess) x = sync();
+            if (x != hipSuccess) return (void)hipfail(e, x);
+        } else {
+            x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
+            if (x == hipSuccess) x = sync();
+            if (x != hipSuccess) return (void)hipfail(e, x);
+        }
+        const uint64_t err = hs[4];
+        if (err != ~0ull) {   // a malformed line: the rest of the input is moot
+            r.err = err - 8 * L.c0;
+            uint64_t cur = e->first_err.load();
+            while (L.j < cur && !e->first_err.compare_exchange_weak(cur, L.j)) {
+            }
+            release_slot();
+            if (pass == 2) return (void)fail(e, SID_EMALFORMED);   // cannot happen: pass 1 validated
+            continue;
+        }
+        if (!format || lynch_hist) {
+            release_slot();
+            continue;
+        }
+        if (hs[5]) return (void)fail(e, SID_ERANGE);
+        const uint64_t bytes = hs[3];
+        if (pass == 1 && d.hold_used.load() + bytes > d.hold_budget) {
+            d.hold_full = true;   // this chunk and the rest: formatted in pass 2
+            release_slot();
+            continue;
+        }
+        uint64_t cap = 0;
+        char* out = d.pool.get(bytes + 16, &cap, d.s_comp);
+        if (!out) return (void)fail(e, SID_ENOMEM);
+        rc = sid_chunk_fmt_write(&W, L.base, L.c1, n, e->conf_type, out, d.s_comp);
+        if (rc != SID_OK) return (void)fail(e, rc);
+        release_slot();
+        if (pass == 2 && r.kept) {   // kept text done with: back to the pool after this stream's work
+            d.pool.put(r.kept, r.kept_cap, d.s_comp);
+            r.kept = nullptr;
+        }
+        if (pass == 1) {
+            r.held = out;
+            r.held_cap = cap;
+            r.held_len = bytes;
+            d.hold_used += cap;
+            continue;
+        }
+        if (e->cfg.device_sink) {
+            d.pool.put(out, cap, nullptr);   // reused on this stream only: ordered
+            continue;
+        }
+        OutItem it;
+        it.j = L.j;
+        it.buf = out;
+        it.cap = cap;
+        it.len = bytes;
+        hipEvent_t ev = d.take_event();
+        if (!ev) return (void)fail(e, SID_EHIP);
+        (void)hipEventRecord(ev, d.s_comp);
+        it.ev = ev;
+        if (!d.drain_q.push(it)) break;
+    }
+    if (pass == 2) d.drain_q.close();
+}
+
+// the drain of device d: CSV buffers through the pinned ring to the writer
+void drain(sid_engine* e, Dev& d)
+{
+    if (hipSetDevice(d.device) != hipSuccess) return (void)fail(e, SID_EHIP);
+    OutItem it;
+    while (d.drain_q.pop(it)) {
+        if (e->rc.load() != SID_OK) break;
+        hipError_t x = hipSuccess;
+        if (it.ev) {
+            x = hipStreamWaitEvent(d.s_d2h, it.ev, 0);
+            // free again once the wait is enqueued: the wait is on the record
+            // made before it, a later record does not affect it
+            d.give_event(it.ev);
+        }
+        if (x != hipSuccess) return (void)hipfail(e, x);
+        if (it.len == 0) {
+            Piece p;
+            p.j = it.j;
+            p.last = true;
+            p.buf = it.buf;
+            p.cap = it.cap;
+            if (!d.out_q.push(p)) break;
+            continue;
+        }
+        for (uint64_t o = 0; o < it.len;) {
+            int ps;
+            if (!d.free_pinned.pop(ps)) return;
+            const uint64_t m = std::min<uint64_t>(d.pinned_cap, it.len - o);
+            x = hipMemcpyAsync(d.pinned[ps], it.buf + o, m, hipMemcpyDeviceToHost, d.s_d2h);
+            if (x == hipSuccess) x = hipEventRecord(d.pinned_ev[ps], d.s_d2h);
+            if (x != hipSuccess) return (void)hipfail(e, x);
+            o += m;
+            Piece p;
+            p.j = it.j;
+            p.ps = ps;
+            p.len = m;
+            p.last = o == it.len;
+            if (p.last) {
+                p.buf = it.buf;
+                p.cap = it.cap;
+            }
+            if (!d.out_q.push(p)) return;
+        }
+    }
+    d.out_q.close();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ phases --
+static void reset_run(sid_engine* e)
+{
+    e->rc = SID_OK;
+    e->first_err = UINT64_MAX;
+    const int m = e->opts.method;
+    e->quality = m == SID_METHOD_QUALITY;
+    e->lynch = m == SID_METHOD_LIKELIHOOD_RATIO || m == SID_METHOD_BAYES || e->opts.estimate_prior;
+    e->conf_type = m == SID_METHOD_BAYES ? "probability" : "p_value";
+    for (auto& r : e->recs) {
+        Dev& d = *e->devs[r.dev];
+        if (r.held) d.pool.put(r.held, r.held_cap, nullptr);
+        if (r.kept) d.pool.put(r.kept, r.kept_cap, nullptr);
+        r.held = r.kept = nullptr;
+        r.held_len = r.kept_len = 0;
+        r.err = ~0ull;
+        r.parsed = 0;
+    }
+    for (auto& dp : e->devs) {
+        Dev& d = *dp;
+        d.hold_used = 0;
+        d.retain_used = 0;
+        d.hold_full = false;
+    }
+}
+
+static void start_queues(sid_engine* e)
+{
+    for (auto& dp : e->devs) {
+        Dev& d = *dp;
+        d.free_slots.reset();
+        d.loaded.reset();
+        d.drain_q.reset();
+        d.out_q.reset();
+        d.free_pinned.reset();
+        for (int s = 0; s < (int)d.slots.size(); ++s) d.free_slots.push(s);
+    }
+}
+
+static int setup_budgets(sid_engine* e)
+{
+    for (auto& dp : e->devs) {
+        Dev& d = *dp;
+        if (hipSetDevice(d.device) != hipSuccess) return SID_EHIP;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) return SID_EHIP;
+        const uint64_t avail = fr + d.pool.bytes();   // pooled buffers are reusable
+        d.hold_budget = e->cfg.hold_bytes ? e->cfg.hold_bytes : (uint64_t)(avail * 0.40);
+        d.retain_budget = e->cfg.retain_bytes ? e->cfg.retain_bytes : (uint64_t)(avail * 0.40);
+    }
+    return SID_OK;
+}
+
+static int setup_generator(sid_engine* e)
+{
+    const size_t D = e->devs.size();
+    if (e->src == SRC_SYNTH_HOST && e->gen_buf.size() != D) {
+        e->gen_buf.assign(D, nullptr);
+        e->gen_cap.assign(D, 0);
+        e->gen_ev.assign(D, nullptr);
+        for (size_t i = 0; i < D; ++i) {
+            if (hipSetDevice(e->devs[i]->device) != hipSuccess) return SID_EHIP;
+            if (hipEventCreateWithFlags(&e->gen_ev[i], hipEventDisableTiming) != hipSuccess) return SID_EHIP;
+            if (hipEventRecord(e->gen_ev[i], e->devs[i]->s_up) != hipSuccess) return SID_EHIP;
+        }
+    }
+    return SID_OK;
+}
+
+extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
+{
+    if (!e || e->src == SRC_NONE) return SID_EINVAL;
+    const double t0 = wall();
+    reset_run(e);
+    int rc = setup_budgets(e);
+    if (rc == SID_OK) rc = setup_generator(e);
+    if (rc != SID_OK) return rc;
+    start_queues(e);
+    const int D = (int)e->devs.size();
+    if (e->lynch)
+        for (auto& dp : e->devs)
+            if ((rc = sid_profile_reset(dp->ctx, dp->s_comp)) != SID_OK) return rc;
+    std::vector<std::vector<uint64_t>> lists(D);
+    for (uint64_t j = 0; j < e->recs.size(); ++j) lists[e->recs[j].dev].push_back(j);
+    std::vector<std::thread> th;
+    for (int i = 0; i < D; ++i) {
+        th.emplace_back(uploader, e, std::ref(*e->devs[i]), std::cref(lists[i]), 1);
+        th.emplace_back(compute, e, std::ref(*e->devs[i]), 1);
+    }
+    for (auto& t : th) t.join();
+    if (e->rc.load() != SID_OK) {
+        close_all(e);
+        for (auto& dp : e->devs) (void)hipSetDevice(dp->device), (void)hipDeviceSynchronize();
+        return e->rc.load();
+    }
+    for (auto& dp : e->devs) {
+        (void)hipSetDevice(dp->device);
+        if (hipStreamSynchronize(dp->s_comp) != hipSuccess || hipStreamSynchronize(dp->s_up) != hipSuccess)
+            return SID_EHIP;
+    }
+    uint64_t sites = 0, bytes = 0, held = 0, kept = 0;
+    for (auto& r : e->recs) {
+        sites += r.parsed;
+        bytes += r.len;
+        held += r.held != nullptr;
+        kept += r.kept != nullptr;
+    }
+    if (st) {
+        st->sites = sites;
+        st->chunks = e->recs.size();
+        st->bytes_in = e->src == SRC_SYNTH_HOST || e->src == SRC_SYNTH_DEVICE ? 0 : bytes;
+        st->chunks_held = held;
+        st->chunks_retained = kept;
+        st->devices = D;
+        st->status_kind = 0;
+        st->err_offset = 0;
+        st->ingest_s = wall() - t0;
+    }
+    const uint64_t fe = e->first_err.load();
+    if (fe != UINT64_MAX) {
+        const ChunkRec& r = e->recs[fe];
+        const unsigned kind = (unsigned)(r.err & 7);
+        const int prc = kind == 1 ? SID_EMALFORMED : kind == 2 ? SID_ENULLCHROM : kind == 3 ? SID_EMISSING_MQ
+                                                                                             : SID_ENOBQ;
+        if (st) {
+            st->status_kind = prc;
+            st->err_offset = r.off + (r.err >> 3);
+        }
+        return prc;
+    }
+    e->ingested = true;
+    e->estimated = !e->lynch;
+    return SID_OK;
+}
+
+extern "C" int sid_engine_estimate(sid_engine* e, const sid_estimate* given, sid_estimate* out)
+{
+    if (!e || !e->ingested) return SID_ESTATE;
+    if (!e->lynch) {
+        e->estimated = true;
+        return SID_OK;
+    }
+    const int D = (int)e->devs.size();
+    const int verbose = e->cfg.verbose;
+    int rc = SID_OK;
+    if (D > 1) {   // merge the device histograms (KB-sized tables)
+        std::vector<std::vector<uint64_t>> k(D), v(D);
+        std::vector<int> rcs(D, SID_OK);
+        std::vector<std::thread> th;
+        for (int i = 0; i < D; ++i)
+            th.emplace_back([&, i] {
+                size_t u = 0;
+                sid_ctx* c = e->devs[i]->ctx;
+                rcs[i] = sid_profile_table(c, nullptr, nullptr, 0, &u);
+                if (rcs[i]) return;
+                k[i].resize(u);
+                v[i].resize(u);
+                rcs[i] = sid_profile_table(c, k[i].data(), v[i].data(), u, &u);
+            });
+        for (auto& t : th) t.join();
+        for (int r : rcs)
+            if (r) return r;
+        std::vector<uint64_t> K, V;
+        for (int i = 0; i < D; ++i) {
+            K.insert(K.end(), k[i].begin(), k[i].end());
+            V.insert(V.end(), v[i].begin(), v[i].end());
+        }
+        for (int i = 0; i < D; ++i)
+            if ((rc = sid_profile_load(e->devs[i]->ctx, K.data(), V.data(), K.size())) != SID_OK) return rc;
+    }
+    // one estimate (device 0, prints the reference's lines), the others
+    // classify with its (pi, eps)
+    sid_estimate est{};
+    rc = sid_lynch_prepare_given(e->devs[0]->ctx, verbose, given, &est);
+    if (rc != SID_OK) return rc;
+    if (D > 1) {
+        std::vector<int> rcs(D, SID_OK);
+        std::vector<std::thread> th;
+        for (int i = 1; i < D; ++i)
+            th.emplace_back([&, i] { rcs[i] = sid_lynch_prepare_given(e->devs[i]->ctx, 0, &est, nullptr); });
+        for (auto& t : th) t.join();
+        for (int r : rcs)
+            if (r) return r;
+    }
+    const int m = e->opts.method;
+    if (m == SID_METHOD_LOCAL || m == SID_METHOD_QUALITY)   // -R: call.cpp:223-234, :305
+        for (auto& dp : e->devs)
+            if ((rc = sid_set_prior(dp->ctx, est.heterozygosity)) != SID_OK) return rc;
+    e->est = est;
+    if (out) *out = est;
+    e->estimated = true;
+    return SID_OK;
+}
+
+extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn write, void* user,
+                               sid_run_stats* st)
+{
+    if (!e || !e->ingested || !e->estimated) return SID_ESTATE;
+    if (!e->cfg.device_sink && !write) return SID_EINVAL;
+    const double t0 = wall();
+    e->rc = SID_OK;
+    e->reloaded = 0;
+    start_queues(e);
+    const int D = (int)e->devs.size();
+    // pinned ring per device: 4 x 16 MiB (pinned once, reused by every run)
+    const uint64_t PC = 16ull << 20;
+    const int NP = 4;
+    if (!e->cfg.device_sink)
+        for (auto& dp : e->devs) {
+            Dev& d = *dp;
+            if (hipSetDevice(d.device) != hipSuccess) return SID_EHIP;
+            while ((int)d.pinned.size() < NP) {
+                char* p = nullptr;
+                hipEvent_t ev;
+                if (hipHostMalloc((void**)&p, PC, hipHostMallocDefault) != hipSuccess) return SID_ENOMEM;
+                if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return SID_EHIP;
+                d.pinned.push_back(p);
+                d.pinned_ev.push_back(ev);
+            }
+            d.pinned_cap = PC;
+            for (int i = 0; i < NP; ++i) d.free_pinned.push(i);
+        }
+    std::vector<std::vector<uint64_t>> lists(D);
+    for (uint64_t j = 0; j < e->recs.size(); ++j) lists[e->recs[j].dev].push_back(j);
+    std::atomic<uint64_t> out_bytes{0};
+    std::vector<std::thread> th;
+    for (int i = 0; i < D; ++i) {
+        th.emplace_back(uploader, e, std::ref(*e->devs[i]), std::cref(lists[i]), 2);
+        th.emplace_back(compute, e, std::ref(*e->devs[i]), 2);
+        if (!e->cfg.device_sink) th.emplace_back(drain, e, std::ref(*e->devs[i]));
+    }
+    // the writer: header, then every chunk's pieces in file order
+    if (!e->cfg.device_sink) {
+        bool ok = true;
+        if (header && write(user, header, std::strlen(header)) != 0) ok = false;
+        for (uint64_t j = 0; j < e->recs.size() && e->rc.load() == SID_OK; ++j) {
+            Dev& d = *e->devs[e->recs[j].dev];
+            Piece p;
+            bool got_last = false;
+            while (d.out_q.pop(p)) {
+                if (p.ps >= 0) {
+                    if (hipEventSynchronize(d.pinned_ev[p.ps]) != hipSuccess) {
+                        fail(e, SID_EHIP);
+                        break;
+                    }
+                    if (ok && write(user, d.pinned[p.ps], p.len) != 0) ok = false;
+                    out_bytes += p.len;
+                    d.free_pinned.push(p.ps);
+                }
+                if (p.last) {
+                    d.pool.put(p.buf, p.cap, nullptr);   // its D2H completed (event above)
+                    got_last = true;
+                    break;
+                }
+            }
+            if (!ok) fail(e, SID_EIO);
+            if (!got_last) break;
+        }
+        if (!ok) fail(e, SID_EIO);
+        if (e->rc.load() != SID_OK) close_all(e);
+    }
+    for (auto& t : th) t.join();
+    for (auto& dp : e->devs) {
+        (void)hipSetDevice(dp->device);
+        if (hipDeviceSynchronize() != hipSuccess) fail(e, SID_EHIP);
+    }
+    if (st) {
+        st->chunks_reloaded = e->reloaded.load();
+        st->bytes_out = out_bytes.load();
+        st->emit_s = wall() - t0;
+    }
+    // every held / kept buffer went back to the pools
+    for (auto& r : e->recs) {
+        Dev& d = *e->devs[r.dev];
+        if (r.held) d.pool.put(r.held, r.held_cap, nullptr);
+        if (r.kept) d.pool.put(r.kept, r.kept_cap, nullptr);
+        r.held = r.kept = nullptr;
+    }
+    e->ingested = false;
+    return e->rc.load();
+}
+
+extern "C" int sid_engine_run(sid_engine* e, const char* header, sid_write_fn write, void* user,
+                              sid_run_stats* st)
+{
+    if (!e) return SID_EINVAL;
+    sid_run_stats local{};
+    sid_run_stats* s = st ? st : &local;
+    std::memset(s, 0, sizeof *s);
+    int rc = sid_engine_ingest(e, s);
+    if (rc != SID_OK) return rc;
+    const double t0 = wall();
+    rc = sid_engine_estimate(e, nullptr, &s->estimate);
+    s->estimate_s = wall() - t0;
+    if (rc != SID_OK) return rc;
+    return sid_engine_emit(e, header, write, user, s);
+}

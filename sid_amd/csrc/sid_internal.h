@@ -89,6 +89,50 @@ struct sid_ctx {
     size_t qlo_n = 0;
 };
 
+// ----------------------------------------------------- chunk pipeline ----
+// textpath.hip: one line-aligned chunk of text resident on the device,
+// processed in place by the streaming engine (run.cpp).  Grow-only device
+// workspace; every function is asynchronous on `st`.
+struct sid_chunk_ws {
+    uint64_t site_cap = 0, tile_cap = 0;
+    uint64_t* starts = nullptr;   // line start offsets (relative to the chunk's base)
+    uint64_t* counts = nullptr;   // profile_t per site
+    uint8_t* code = nullptr;
+    double* hom = nullptr;
+    double* het = nullptr;
+    uint32_t* tcnt = nullptr;     // per 4 KiB tile line counts (+ scan workspace)
+    uint64_t* toff = nullptr;
+    uint32_t* bsum = nullptr;     // per 256-site block record bytes (+ scan workspace)
+    uint64_t* boff = nullptr;
+    uint64_t* state = nullptr;    // [0] sites [1..2] parse range [3] CSV bytes [4] first error key [5] range flag
+};
+int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites);
+void sid_chunk_release(sid_chunk_ws* W);
+int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, hipStream_t st);
+int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint64_t n, int qmode,
+                    hipStream_t st);
+int sid_chunk_fmt_len(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type,
+                      hipStream_t st);
+int sid_chunk_fmt_write(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
+                        hipStream_t st);
+int sid_chunk_quality(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st);
+// synth.hip: the synthetic text of sites [first, first + n) (the bytes of
+// sid_synth_text) generated on the device into out (cap bytes): res[0] =
+// bytes, res[1] != 0 when they did not fit (nothing usable written then)
+struct sid_synth_gen_ws {
+    uint32_t* len = nullptr;      // per site line length (+ scan workspace)
+    uint64_t* off = nullptr;      // per site line offset
+    uint64_t* res = nullptr;      // [0] bytes, [1] overflow
+    uint64_t cap = 0;             // sites
+};
+hipError_t sid_launch_synth_text(uint64_t seed, const uint64_t* d_cdf, uint32_t kmax, uint64_t first, uint64_t n,
+                                 uint64_t sites_per_chrom, sid_synth_gen_ws* ws, char* out, uint64_t cap,
+                                 hipStream_t st);
+void sid_synth_gen_release(sid_synth_gen_ws* ws);
+// textpath.hip: exclusive u32 -> u64 scan (three kernels) from *base
+size_t sid_scan_ws_bytes(uint64_t m);
+hipError_t sid_scan_u32(const uint32_t* in, uint64_t m, uint64_t* out, uint64_t* base, uint64_t* ws, hipStream_t st);
+
 // host helpers (capi.cpp)
 int sid_set_hip_error(hipError_t e);
 double sid_gsl_lngamma(double x);   // GSL 2.7.1 gsl_sf_lngamma restated (x >= 0.5)

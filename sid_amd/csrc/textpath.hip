@@ -499,14 +499,18 @@ __device__ __forceinline__ int record(Reader& R, uint64_t start, uint8_t c, doub
                                       const char* ctype, int tlen, char* out)
 {
     if (c & 0x40) return 0;   // filtered profile: no record (call.cpp:131-140)
-    // the line parsed (>= 5 tokens before any NUL or newline), so its first
-    // two tokens are plain separator-delimited runs
+    // a parsed line has >= 5 tokens before any NUL or newline, so its first
+    // two tokens are plain separator-delimited runs.  The scan also stops at a
+    // newline or NUL: the streaming engine formats a chunk before it knows
+    // whether one of its lines is malformed (it then discards the records),
+    // and such a line must not send the scan past its end
     uint64_t tb[2], te[2];
     uint64_t q = start;
     for (int k = 0; k < 2; ++k) {
         while (is_sep(R.at(q))) ++q;
         tb[k] = q;
-        while (!is_sep(R.at(q))) ++q;
+        for (uint32_t ch = R.at(q); !is_sep(ch) && ch != '\n' && ch != 0; ch = R.at(++q)) {
+        }
         te[k] = q;
     }
     const int32_t pos = atoi_like(R, tb[1], te[1]);
@@ -1211,20 +1215,16 @@ extern "C" int sid_format_g6_device(sid_ctx* ctx, const double* d_v, size_t n, c
     return SID_OK;
 }
 
-// call.cpp:291-372 over a shard parsed with the context's method = quality.
+// call.cpp:291-372 over n sites parsed with the context's method = quality
+// (7 fields per line): starts/counts of the sites, text [0, len) resident.
 // Host tables: the four per-quality terms (glibc pow/log through volatile
 // pointers, so no compiler rewrite of pow(10, x)) and log_gamma up to the
-// largest n = count[ref0] + count[ref1] of the shard.
-extern "C" int sid_call_quality(sid_ctx* ctx, const sid_dtext* T, uint8_t* code, double* hom_conf,
-                                double* het_conf, void* stream)
+// largest n = count[ref0] + count[ref1] of the sites.
+static int quality_run(sid_ctx* ctx, const char* text, uint64_t len, const uint64_t* starts, const uint64_t* counts,
+                       uint64_t n, uint8_t* code, double* hom_conf, double* het_conf, hipStream_t st)
 {
-    if (!ctx || !T) return SID_EINVAL;
-    if (!T->quality || ctx->opts.method != SID_METHOD_QUALITY) return SID_ESTATE;
-    const uint64_t n = T->nsites;
     if (n == 0) return SID_OK;
     if (!code || !hom_conf || !het_conf) return SID_EINVAL;
-    TCHECK(hipSetDevice(T->device));
-    hipStream_t st = (hipStream_t)stream;
     if (!ctx->d_qtab) {
         double (*volatile powp)(double, double) = pow;
         double (*volatile logp)(double) = log;
@@ -1241,7 +1241,7 @@ extern "C" int sid_call_quality(sid_ctx* ctx, const sid_dtext* T, uint8_t* code,
     }
     if (!ctx->d_scratch) TCHECK(hipMalloc(&ctx->d_scratch, 16));
     TCHECK(hipMemsetAsync(ctx->d_scratch, 0, 4, st));
-    sid_max_major_kernel<<<(unsigned)std::min<uint64_t>((n + TB - 1) / TB, 2048), TB, 0, st>>>(T->d_counts, n,
+    sid_max_major_kernel<<<(unsigned)std::min<uint64_t>((n + TB - 1) / TB, 2048), TB, 0, st>>>(counts, n,
                                                                                              ctx->d_scratch);
     uint32_t mx = 0;
     TCHECK(hipMemcpyAsync(&mx, ctx->d_scratch, 4, hipMemcpyDeviceToHost, st));
@@ -1278,10 +1278,180 @@ extern "C" int sid_call_quality(sid_ctx* ctx, const sid_dtext* T, uint8_t* code,
         ctx->qlo_n = n;
     }
     const unsigned grid = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, 16384);
-    sid_quality_sum_kernel<<<grid, TB, 0, st>>>(T->d_text, T->len, T->d_starts, T->d_counts, n, ctx->d_qtab,
-                                                hom_conf, het_conf, (double2*)ctx->d_qlo);
-    sid_quality_finish_kernel<<<grid, TB, 0, st>>>(T->d_counts, n, ctx->d_lg, P, code, hom_conf, het_conf,
+    sid_quality_sum_kernel<<<grid, TB, 0, st>>>(text, len, starts, counts, n, ctx->d_qtab, hom_conf, het_conf,
+                                                (double2*)ctx->d_qlo);
+    sid_quality_finish_kernel<<<grid, TB, 0, st>>>(counts, n, ctx->d_lg, P, code, hom_conf, het_conf,
                                                    (const double2*)ctx->d_qlo);
     TCHECK(hipGetLastError());
     return SID_OK;
+}
+
+extern "C" int sid_call_quality(sid_ctx* ctx, const sid_dtext* T, uint8_t* code, double* hom_conf,
+                                double* het_conf, void* stream)
+{
+    if (!ctx || !T) return SID_EINVAL;
+    if (!T->quality || ctx->opts.method != SID_METHOD_QUALITY) return SID_ESTATE;
+    TCHECK(hipSetDevice(T->device));
+    return quality_run(ctx, T->d_text, T->len, T->d_starts, T->d_counts, T->nsites, code, hom_conf, het_conf,
+                       (hipStream_t)stream);
+}
+
+// exclusive scan of m u32 into u64 offsets from *base (*base advances by the
+// sum); ws = sid_scan_ws_bytes(m) bytes (synth.hip's text generator)
+size_t sid_scan_ws_bytes(uint64_t m) { return scan_ws_bytes(m); }
+hipError_t sid_scan_u32(const uint32_t* in, uint64_t m, uint64_t* out, uint64_t* base, uint64_t* ws, hipStream_t st)
+{
+    launch_scan(in, m, out, base, nullptr, ws, st);
+    return hipGetLastError();
+}
+
+// ======================================================= chunk pipeline ====
+// One line-aligned chunk of text resident on the device (a ring slot, a
+// retained buffer or a slice of a resident text), processed in place by the
+// streaming engine (run.cpp).  `base` is 16-B aligned; the chunk is bytes
+// [c0, c1) of it; every byte past c1 that a 16-B window may touch is readable
+// (a zero pad, or the next chunk's text).  Offsets (line starts, the error
+// key) are relative to `base`.
+#define WCHECK(x)                                                   \
+    do {                                                            \
+        hipError_t e_ = (x);                                        \
+        if (e_ != hipSuccess) return sid_set_hip_error(e_);         \
+    } while (0)
+
+static uint64_t chunk_tiles(uint64_t c0, uint64_t c1)
+{
+    const uint64_t t0 = c0 & ~(uint64_t)15;
+    return std::max<uint64_t>((c1 - t0 + TILE - 1) / TILE, 1);
+}
+
+int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
+{
+    // grow-only; hipFree waits for the device, so buffers still in use by
+    // queued work are not released under it (growth is rare: the first
+    // chunks, or a chunk far above the usual lines per byte)
+    if (!W->state) WCHECK(hipMalloc(&W->state, 8 * sizeof(uint64_t)));
+    const uint64_t tiles = (bytes + 16 + TILE - 1) / TILE + 1;
+    if (tiles > W->tile_cap) {
+        const uint64_t t = std::max<uint64_t>(tiles, W->tile_cap + W->tile_cap / 2);
+        if (W->tcnt) (void)hipFree(W->tcnt);
+        if (W->toff) (void)hipFree(W->toff);
+        W->tcnt = nullptr;
+        W->toff = nullptr;
+        W->tile_cap = 0;
+        WCHECK(hipMalloc(&W->tcnt, ((t * 4 + 7) & ~(size_t)7) + scan_ws_bytes(t)));
+        WCHECK(hipMalloc(&W->toff, t * 8));
+        W->tile_cap = t;
+    }
+    if (sites > W->site_cap) {
+        const uint64_t m = std::max<uint64_t>(sites, W->site_cap + W->site_cap / 2);
+        for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
+                        (void*)W->bsum, (void*)W->boff})
+            if (p) (void)hipFree(p);
+        W->starts = W->counts = nullptr;
+        W->code = nullptr;
+        W->hom = W->het = nullptr;
+        W->bsum = nullptr;
+        W->boff = nullptr;
+        W->site_cap = 0;
+        const uint64_t nb = (m + TB - 1) / TB + 1;
+        WCHECK(hipMalloc(&W->starts, m * 8));
+        WCHECK(hipMalloc(&W->counts, m * 8));
+        WCHECK(hipMalloc(&W->code, m));
+        WCHECK(hipMalloc(&W->hom, m * 8));
+        WCHECK(hipMalloc(&W->het, m * 8));
+        WCHECK(hipMalloc(&W->bsum, ((nb * 4 + 7) & ~(size_t)7) + scan_ws_bytes(nb)));
+        WCHECK(hipMalloc(&W->boff, (nb + 1) * 8));
+        W->site_cap = m;
+    }
+    return SID_OK;
+}
+
+void sid_chunk_release(sid_chunk_ws* W)
+{
+    for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
+                    (void*)W->bsum, (void*)W->boff, (void*)W->tcnt, (void*)W->toff, (void*)W->state})
+        if (p) (void)hipFree(p);
+    *W = sid_chunk_ws{};
+}
+
+// line starts of [c0, c1): per-tile counts, scan; state[0] = sites (the
+// caller reads it back), state[1..2] = [0, sites), state[4] = no error yet
+int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, hipStream_t st)
+{
+    const uint64_t tiles = chunk_tiles(c0, c1);
+    if (tiles > W->tile_cap) return SID_EINVAL;
+    WCHECK(hipMemsetAsync(W->state, 0, 4 * sizeof(uint64_t), st));
+    WCHECK(hipMemsetAsync(W->state + 4, 0xFF, sizeof(uint64_t), st));
+    if (c1 <= c0) return SID_OK;
+    const uint64_t t0 = c0 & ~(uint64_t)15;
+    sid_lines_count_kernel<<<(unsigned)tiles, TB, 0, st>>>(base, t0, c0, c1, W->tcnt);
+    launch_scan(W->tcnt, tiles, W->toff, W->state, W->state + 1,
+                (uint64_t*)((char*)W->tcnt + ((tiles * 4 + 7) & ~(size_t)7)), st);
+    WCHECK(hipGetLastError());
+    return SID_OK;
+}
+
+// line offsets + one-pass parse of the n sites found by sid_chunk_index;
+// state[4] = min(offset * 8 + kind) over the malformed lines (all ones: none)
+int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint64_t n, int qmode,
+                    hipStream_t st)
+{
+    if (n > W->site_cap) return SID_EINVAL;
+    if (n == 0) return SID_OK;
+    const uint64_t tiles = chunk_tiles(c0, c1);
+    const uint64_t t0 = c0 & ~(uint64_t)15;
+    sid_lines_emit_kernel<<<(unsigned)tiles, TB, 0, st>>>(base, t0, c0, c1, W->toff, W->starts);
+    const unsigned pg = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, 16384);
+    sid_parse_kernel<<<pg, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts,
+                                        (unsigned long long*)(W->state + 4), qmode);
+    WCHECK(hipGetLastError());
+    return SID_OK;
+}
+
+static int chunk_ctype(const char* conf_type, CType* ct)
+{
+    *ct = CType{};
+    ct->len = (int)std::strlen(conf_type);
+    if (ct->len >= (int)sizeof ct->s) return SID_EINVAL;
+    std::memcpy(ct->s, conf_type, ct->len);
+    return SID_OK;
+}
+
+// record lengths of the n sites (code/hom/het in the workspace) and their
+// block offsets; state[3] = CSV bytes of the chunk, state[5] != 0: a
+// confidence outside the formatter's range
+int sid_chunk_fmt_len(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type,
+                      hipStream_t st)
+{
+    CType ct;
+    if (chunk_ctype(conf_type, &ct)) return SID_EINVAL;
+    WCHECK(hipMemsetAsync(W->state + 3, 0, sizeof(uint64_t), st));   // ([4] holds the error key)
+    WCHECK(hipMemsetAsync(W->state + 5, 0, sizeof(uint64_t), st));
+    if (n == 0) return SID_OK;
+    const uint64_t nb = (n + TB - 1) / TB;
+    sid_fmt_len_kernel<<<(unsigned)nb, TB, 0, st>>>(base, c1, W->starts, 0, n, W->code, W->hom, W->het, ct, W->bsum,
+                                                    (int*)(W->state + 5));
+    launch_scan(W->bsum, nb, W->boff, W->state + 3, nullptr,
+                (uint64_t*)((char*)W->bsum + ((nb * 4 + 7) & ~(size_t)7)), st);
+    WCHECK(hipGetLastError());
+    return SID_OK;
+}
+
+// the chunk's records into out (state[3] bytes, 16-B aligned buffer)
+int sid_chunk_fmt_write(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
+                        hipStream_t st)
+{
+    CType ct;
+    if (chunk_ctype(conf_type, &ct)) return SID_EINVAL;
+    if (n == 0) return SID_OK;
+    const uint64_t nb = (n + TB - 1) / TB;
+    sid_fmt_write_kernel<<<(unsigned)nb, TB, 0, st>>>(base, c1, W->starts, 0, n, W->code, W->hom, W->het, ct, W->boff,
+                                                      0, out);
+    WCHECK(hipGetLastError());
+    return SID_OK;
+}
+
+int sid_chunk_quality(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st)
+{
+    return quality_run(ctx, base, c1, W->starts, W->counts, n, W->code, W->hom, W->het, st);
 }

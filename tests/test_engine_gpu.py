@@ -1,0 +1,227 @@
+"""The streaming engine (run.cpp, sid_engine_*) against the oracle CLI (the
+reference's sid.cpp/call.cpp restated): many small chunks over several
+devices, the hold / retain fallbacks of the two-pass flow, first-error
+semantics across chunks, every kind of source, and a slice of the C4 layout
+(seed 4, 24 x 125M-site chromosomes) spanning a chromosome boundary."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+def run(exe, args, **kw):
+    return subprocess.run([exe] + list(args), capture_output=True, timeout=600, **kw)
+
+
+@pytest.fixture(scope="module")
+def inputs(sid, tmp_path_factory):
+    d = tmp_path_factory.mktemp("engine")
+    paths = {"c1": os.path.join(GOLD, "c1_10k.plp"), "edge": os.path.join(GOLD, "edge.plp")}
+    p = d / "deep.plp"
+    p.write_bytes(sid.synth_text(5, 3000, 200.0, sites_per_chrom=1000))
+    paths["deep"] = str(p)
+    q = d / "q30.plp"
+    q.write_bytes(sid.synth_text(7, 20_000, 30.0, sites_per_chrom=7000, mapq=True))
+    paths["quality"] = str(q)
+    return paths
+
+
+FLAGS = [[], ["-R", "-m", "likelihood_ratio"], ["-m", "bayes"], ["-R", "-m", "local"],
+         ["-E", "0.05", "-p", "0.01", "-r", "0.001"]]
+
+
+@pytest.mark.parametrize("extra", [["--chunk-bytes", "4096"], ["--chunk-bytes", "65536", "--devices", "3"],
+                                   ["--chunk-bytes", "3000", "--devices", "2"]], ids=lambda e: " ".join(e))
+@pytest.mark.parametrize("flags", FLAGS, ids=lambda f: " ".join(f) or "default")
+@pytest.mark.parametrize("name", ["c1", "edge", "deep"])
+def test_chunked_cli_matches_oracle(sid, oracle, inputs, name, flags, extra):
+    a = run(sid.CLI_PATH, extra + flags + [inputs[name]])
+    b = oracle.run_cli(flags + [inputs[name]])
+    assert a.returncode == b.returncode == 0, a.stderr
+    assert a.stdout == b.stdout
+    assert a.stderr == b.stderr
+
+
+@pytest.mark.parametrize("extra", [["--hold-bytes", "1"], ["--hold-bytes", "1", "--retain-bytes", "1"],
+                                   ["--hold-bytes", "200000", "--retain-bytes", "150000"]],
+                         ids=["all-in-pass-2-kept", "all-reloaded", "mixed"])
+@pytest.mark.parametrize("flags", [[], ["-R", "-m", "likelihood_ratio"], ["-m", "quality"],
+                                   ["-R", "-m", "quality"]], ids=lambda f: " ".join(f) or "default")
+def test_hold_and_retain_fallbacks(sid, oracle, inputs, flags, extra):
+    """Records that do not fit the hold budget are formatted in the second
+    pass, from text kept in HBM or read again from the file."""
+    name = "quality" if "quality" in flags else "c1"
+    args = ["--chunk-bytes", "32768", "--devices", "2"] + extra + flags + [inputs[name]]
+    a = run(sid.CLI_PATH, ["--stats"] + args)
+    b = oracle.run_cli(flags + [inputs[name]])
+    assert a.returncode == b.returncode == 0, a.stderr
+    assert a.stdout == b.stdout
+    lines = a.stderr.splitlines(keepends=True)   # --stats: the last stderr line
+    assert b"".join(lines[:-1]) == b.stderr
+    st = json.loads(lines[-1])
+    assert st["chunks"] > 4
+    lynch = "-R" in flags or "likelihood_ratio" in flags
+    if lynch or extra[1] == "1":
+        assert st["chunks_held"] == 0
+    if extra == ["--hold-bytes", "1", "--retain-bytes", "1"]:
+        assert st["chunks_retained"] == 0 and st["chunks_reloaded"] == st["chunks"]
+    if extra == ["--hold-bytes", "1"]:
+        # text is kept once the hold budget is seen to be spent; the chunks
+        # already uploaded by then are read again
+        assert st["chunks_retained"] > 0
+        assert st["chunks_retained"] + st["chunks_reloaded"] == st["chunks"]
+
+
+def test_quality_chunked(sid, oracle, inputs):
+    for extra in (["--chunk-bytes", "8192"], ["--chunk-bytes", "50000", "--devices", "3"]):
+        for flags in ([ "-m", "quality"], ["-m", "quality", "-r", "0.01", "-p", "0.2"]):
+            a = run(sid.CLI_PATH, extra + flags + [inputs["quality"]])
+            b = oracle.run_cli(flags + [inputs["quality"]])
+            assert a.returncode == b.returncode == 0, a.stderr
+            assert a.stdout == b.stdout, (extra, flags)
+
+
+def test_first_error_in_a_late_chunk(sid, oracle, tmp_path):
+    good = b"".join(b"chr1\t%d\tA\t3\t.,.\tIII\n" % i for i in range(1, 3000))
+    cases = {
+        "malformed_late": good * 3 + b"chr1\t1\tAC\t3\t...\tIII\n" + good + b" \t\n" + good,
+        "blank_first": good + b" \t\n" + good * 2 + b"chr1\t1\tAC\t3\t...\tIII\n" + good,
+        "last_line": good * 4 + b"chr1\t9\tA",
+    }
+    for tag, text in cases.items():
+        p = tmp_path / f"{tag}.plp"
+        p.write_bytes(text)
+        b = oracle.run_cli([str(p)])
+        for extra, flags in ((["--chunk-bytes", "4096"], []), (["--chunk-bytes", "10000", "--devices", "4"], []),
+                             (["--chunk-bytes", "4096"], ["-R", "-m", "likelihood_ratio"]),
+                             (["--chunk-bytes", "4096", "--devices", "3"], ["-m", "quality"])):
+            bb = oracle.run_cli(flags + [str(p)]) if flags else b
+            a = run(sid.CLI_PATH, extra + flags + [str(p)])
+            assert a.returncode == bb.returncode, (tag, extra, a.returncode, bb.returncode)
+            assert a.stdout == bb.stdout, (tag, extra)
+            assert a.stderr == bb.stderr, (tag, extra)
+
+
+def test_bayes_without_coverage_prints_the_header(sid, oracle, tmp_path):
+    """callBayes on a file where no profile reaches coverage 4: the estimate
+    runs on an empty table, no record survives, exit 0 (call.cpp:145-211)."""
+    p = tmp_path / "low.plp"
+    p.write_bytes(b"chr1\t1\tA\t2\t..\tII\nchr1\t2\tC\t3\t,,G\tIII\n")
+    for extra in ([], ["--devices", "2"], ["--host-parse"]):
+        a = run(sid.CLI_PATH, extra + ["-m", "bayes", str(p)])
+        b = oracle.run_cli(["-m", "bayes", str(p)])
+        assert b.returncode == 0, b.stderr
+        assert a.returncode == 0, (extra, a.stderr)
+        assert a.stdout == b.stdout == b"chrom,pos,label,gt,hom_conf,het_conf,conf_type\n"
+        assert a.stderr == b.stderr
+
+
+def test_stdin_pipe(sid, oracle, inputs):
+    data = open(inputs["c1"], "rb").read()
+    a = subprocess.run([sid.CLI_PATH, "--chunk-bytes", "5000", "/dev/stdin"], input=data, capture_output=True,
+                       timeout=120)
+    b = oracle.run_cli([inputs["c1"]])
+    assert a.returncode == 0, a.stderr
+    assert a.stdout == b.stdout
+
+
+def engine_csv(sid, method, source, text, n=None, seed=None, depth=30.0, first=0, spc=0, **kw):
+    eng = sid.Engine(method=method, **kw)
+    if source == "text":
+        eng.source_text(text)
+    elif source == "device":
+        import torch
+        buf = torch.zeros(len(text) + 512, dtype=torch.uint8, device="cuda")
+        buf[: len(text)] = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
+        torch.cuda.synchronize()
+        eng.source_device_text(buf.data_ptr(), len(text), keep=buf)
+    elif source in ("synth_host", "synth_device"):
+        eng.source_synth(seed, n, depth, first=first, sites_per_chrom=spc, sites_per_chunk=kw.get("per", 0),
+                         on_device=source == "synth_device")
+    out, st = eng.run()
+    eng.close()
+    return out, st
+
+
+@pytest.mark.parametrize("source", ["text", "device", "synth_host", "synth_device"])
+@pytest.mark.parametrize("method", ["local", "likelihood_ratio"])
+def test_engine_sources_agree_with_oracle(sid, oracle, tmp_path, source, method):
+    n, seed, depth, spc = 60_000, 11, 30.0, 25_000
+    text = sid.synth_text(seed, n, depth, first=5, sites_per_chrom=spc)
+    p = tmp_path / "s.plp"
+    p.write_bytes(text)
+    flags = [] if method == "local" else ["-R", "-m", method]
+    ref = oracle.run_cli(flags + [str(p)])
+    assert ref.returncode == 0
+    out, st = engine_csv(sid, method, source, text, n=n, seed=seed, depth=depth, first=5, spc=spc,
+                         chunk_bytes=1 << 20, estimate_prior=method != "local")
+    assert st.sites == n
+    assert st.chunks >= 4
+    assert out == ref.stdout
+
+
+def test_engine_file_source_and_reuse(sid, oracle, tmp_path):
+    text = sid.synth_text(12, 40_000, 30.0, sites_per_chrom=15_000)
+    p = tmp_path / "f.plp"
+    p.write_bytes(text)
+    ref = oracle.run_cli([str(p)]).stdout
+    eng = sid.Engine(chunk_bytes=300_000)
+    with open(p, "rb") as f:
+        for _ in range(2):   # an engine is reusable
+            eng.source_file(f.fileno())
+            out, st = eng.run()
+            assert out == ref
+            assert st.chunks > 5
+    eng.source_text(text)
+    assert eng.run()[0] == ref
+    eng.close()
+
+
+def test_engine_device_sink_counts_the_same_records(sid, oracle):
+    text = sid.synth_text(13, 30_000, 30.0)
+    eng = sid.Engine(chunk_bytes=1 << 18, device_sink=True)
+    eng.source_text(text)
+    st = eng.ingest()
+    eng.estimate()
+    out, st2 = eng.emit()
+    assert out == b"" and st.sites == 30_000 and st.chunks_held == st.chunks
+    eng.close()
+
+
+@pytest.mark.parametrize("depth,n", [(200.0, 4000), (30.0, 1)])
+def test_device_generator_equals_host_text(sid, depth, n):
+    """The device text generator writes the bytes of sid_synth_text."""
+    import torch
+    text = sid.synth_text(5, n, depth, first=777, sites_per_chrom=1000)
+    eng = sid.Engine(device_sink=False, chunk_bytes=1 << 20)
+    eng.source_synth(5, n, depth, first=777, sites_per_chrom=1000, on_device=True)
+    out_dev, _ = eng.run()
+    eng.source_text(text)
+    out_txt, _ = eng.run()
+    assert out_dev == out_txt
+    eng.close()
+
+
+def test_c4_layout_slice_across_devices(sid, oracle, tmp_path):
+    """C4 (seed 4, 24 chromosomes x 125,000,000 sites): a 2M-site slice that
+    spans the chr1/chr2 boundary, through the CLI on 8 (logical) devices in
+    4 MiB chunks, byte for byte against the oracle CLI."""
+    spc = 125_000_000
+    first, n = spc - 1_000_000, 2_000_000
+    p = tmp_path / "c4_slice.plp"
+    with open(p, "wb") as f:
+        for lo in range(0, n, 500_000):
+            f.write(sid.synth_text(4, min(500_000, n - lo), 30.0, first=first + lo, sites_per_chrom=spc))
+    ref = oracle.run_cli([str(p)])
+    assert ref.returncode == 0
+    assert b"\nchr1,125000000," in ref.stdout and b"\nchr2,1," in ref.stdout
+    a = run(sid.CLI_PATH, ["--devices", "8", "--chunk-bytes", str(4 << 20), str(p)])
+    assert a.returncode == 0, a.stderr
+    assert a.stdout == ref.stdout
