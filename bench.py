@@ -1,38 +1,53 @@
 #!/usr/bin/env python3
-"""bench.py — genome sites/s of the sid hot path on MI355X.
+"""bench.py — genome sites/s of sid's pileup -> CSV path on MI355X.
 
-Workload (BASELINE.json configs[1], "C2"): 50,000,000 synthetic 30x diploid
-sites per GPU, `-m local`.  A step is one pass of the hot path
-(sid_call_local: counts -> code + hom_conf + het_conf) over one batch of 50M
-sites already resident in HBM.  N GPUs = N ranks (torchrun), each with its own
-50M-site range of the counter-based generator (weak scaling, no data-path
-collective; gloo only for the barrier and the max over ranks).
+Headline (BASELINE.json metric, configs[1] = "C2"): 50,000,000 synthetic 30x
+diploid sites per GPU, `-m local`.  A step is one whole sid run over the rank's
+pileup text, already resident in HBM when the timed region starts:
 
-With --method likelihood_ratio (BASELINE configs[2], "C3": the reference has
-no `-m lynch`; SURVEY.md §8(d) runs C3 as `-R -m likelihood_ratio`), a step is
-the whole Lynch path over the resident 50M sites: profile histogram (device
-hash), [N>1: one all-gather of the histograms], Nelder-Mead on the GPU
-objective, classification + Benjamini-Hochberg, and the per-site lookup.
-`--method bayes` runs the same with the posterior classification.
+    line index -> parse (counts) -> per-site call -> CSV records formatted
 
-Prints ONE JSON line on rank 0 (contract in the task statement), including
-  roofline      25 algorithmic bytes/site (8 B counts in, 1 B code + 2 x 8 B
-                confs out) / average kernel duration from HIP events on the
-                launch stream, against 8 TB/s HBM3E;
-  cpu_baseline  the oracle's end-to-end CLI (reference sid.cpp/call.cpp
-                restated in C, single thread, text -> CSV) on a bounded sample
-                of the same workload, rank 0 at N=1 only;
-  e2e           the product CLI (build/sid) on the same sample file, text
-                in -> CSV out, device text path and --host-parse (wall clock
-                of the whole process and the CLI's own clock), informational;
-  pipeline      SURVEY.md §8(d) throughput 2: counts in pinned host memory ->
-                H2D -> sid_call_local -> D2H of code + confs, in chunks over
-                three streams (PCIe-bound, 25 B/site cross the link),
-                informational.
+i.e. readFile + callSiteMLError + the output loop (call.cpp:11-20, :213-289,
+sid.cpp:102-105) through the streaming engine (include/sid.h sid_engine_*,
+device-text source, 128 MiB chunks); the CSV records are left in HBM.  The
+PCIe-inclusive rate (text in host memory -> CSV copied back to host memory) is
+reported beside it as `e2e`, and the CLI (build/sid, file -> /dev/null) as
+`e2e.cli`; they are never `value`.
+
+Configs (--config):
+  C2  -m local, seed 2, 50M sites per GPU (weak scaling)           [default]
+  C3  -R -m likelihood_ratio, seed 3, 50M sites per GPU (weak): ingest builds
+      the profile histogram; N>1 all-gathers it over RCCL (device tensors,
+      backend "nccl"), rank 0 runs the one Nelder-Mead estimate and broadcasts
+      (pi, eps) over RCCL; then every rank formats its records
+  C4  -m local, seed 4, 3G sites in total = 24 chromosomes x 125M (strong
+      scaling: rank r takes sites [r*3G/N, (r+1)*3G/N)); the text is generated
+      on the device chunk by chunk inside the step (never stored: 244 GB)
+  C5  -m local, seed 5, 200x, 500M sites in total (strong), generated as C4
+
+Multi-GPU: one rank per GPU (torchrun).  -m local has no data-path exchange;
+the Lynch path exchanges only the O(U) profile histogram.  Ranks beyond the
+visible GPUs are refused unless --allow-shared-gpu (a rehearsal: n_gpus then
+counts distinct devices and "oversubscribed" is set).
+
+The JSON line also carries
+  roofline      the dominant kernel stage of the step (device time from HIP
+                events on the engine's compute stream over the timed region),
+                its algorithmic bytes per launch / average launch duration vs
+                8 TB/s, and the PMC-measured HBM bytes per launch
+                (profiles/pmc_<stage>_r02.json) when present
+  stages_ms     device time per stage per step
+  kernel_local  sid_call_local alone over resident counts (25 B/site)
+  e2e           host-memory text -> CSV in host memory (PCIe both ways),
+                engine clock; and the CLI on a 50M-site file
+  cpu_baseline  the oracle CLI (the reference's path restated in C) on the
+                same 50M-site text, 16 line-aligned shard processes, plus a
+                1-core figure on a 4M-site sample (rank 0, N=1 only)
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import tempfile
@@ -41,8 +56,19 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-BYTES_PER_SITE = 25          # 8 in + 17 out
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+LOCAL_BYTES_PER_SITE = 25    # sid_call_local: 8 B counts in, 1 B code + 2 x 8 B confs out
+
+CONFIGS = {
+    "C2": dict(method="local", R=False, seed=2, depth=30.0, per_gpu=50_000_000, total=None, spc=0,
+               resident=True, desc="-m local, 50M-site 30x synthetic pileup per GPU"),
+    "C3": dict(method="likelihood_ratio", R=True, seed=3, depth=30.0, per_gpu=50_000_000, total=None, spc=0,
+               resident=True, desc="-R -m likelihood_ratio, 50M-site 30x synthetic pileup per GPU"),
+    "C4": dict(method="local", R=False, seed=4, depth=30.0, per_gpu=None, total=3_000_000_000, spc=125_000_000,
+               resident=False, desc="-m local, 3G-site whole-genome 30x pileup (24 x 125M), site-range shards"),
+    "C5": dict(method="local", R=False, seed=5, depth=200.0, per_gpu=None, total=500_000_000, spc=125_000_000,
+               resident=False, desc="-m local, 500M-site 200x pileup, site-range shards"),
+}
 
 
 def parse_args():
@@ -50,313 +76,350 @@ def parse_args():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--sites", type=int, default=50_000_000, help="sites per GPU")
-    p.add_argument("--depth", type=float, default=30.0)
-    p.add_argument("--seed", type=int, default=None, help="default: 2 (C2) / 3 (C3)")
-    p.add_argument("--cpu-sample", type=int, default=16_000_000,
-                   help="sites in the CPU-baseline / e2e sample (0 = skip); ~10 s of oracle CPU time at C2")
-    p.add_argument("--no-e2e", action="store_true")
-    p.add_argument("--method", default="local", choices=["local", "likelihood_ratio", "bayes"],
-                   help="local = C2 (default); likelihood_ratio = C3 (with -R, as SURVEY.md §8(d)); bayes")
-    p.add_argument("--no-R", action="store_true", help="C3 without -R (estimate_prior off)")
-    p.add_argument("--direct", action="store_true",
-                   help="A/B: bypass the class-table kernel (SID_LOCAL_DIRECT=1)")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_local_r01.json"),
-                   help="per-launch HBM traffic from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
-    return p.parse_args()
+    p.add_argument("--config", default=None, choices=sorted(CONFIGS))
+    p.add_argument("--method", default=None, choices=["local", "likelihood_ratio"],
+                   help="alias: local = C2, likelihood_ratio = C3")
+    p.add_argument("--sites", type=int, default=None, help="override: sites per GPU (C2/C3) or in total (C4/C5)")
+    p.add_argument("--chunk-mib", type=int, default=0, help="engine chunk size (0 = 128 MiB)")
+    p.add_argument("--no-extras", action="store_true", help="skip kernel_local, e2e and cpu_baseline")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--allow-shared-gpu", action="store_true",
+                   help="rehearsal: more ranks than GPUs share them round-robin")
+    p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
+    a = p.parse_args()
+    if a.config is None:
+        a.config = "C3" if a.method == "likelihood_ratio" else "C2"
+    return a
+
+
+def stage_bytes(stage, text_per_site, csv_per_site):
+    """Algorithmic HBM bytes per site of each engine stage."""
+    return {
+        "index": text_per_site,                        # text read once (line starts per tile)
+        "parse": text_per_site + 8 + 8,                # text read, line offsets + counts written
+        "call": LOCAL_BYTES_PER_SITE,                  # counts in, code + confs out
+        "hist": 8,                                     # counts read
+        "fmt_len": 17 + 8,                             # code + confs + line offset read (chrom/pos: L2)
+        "fmt_write": 17 + 8 + csv_per_site,            # the same + the records written
+    }[stage]
 
 
 def main():
     a = parse_args()
-    if a.seed is None:
-        a.seed = 2 if a.method == "local" else 3
-    if a.direct:
-        os.environ["SID_LOCAL_DIRECT"] = "1"
+    cfg = CONFIGS[a.config]
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
-    import torch  # plumbing: device memory, streams, events, process group
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    import sid_amd
-    # one rank per GPU; more ranks than GPUs share them round-robin (a
-    # rehearsal of the N>1 path on a smaller box)
-    gpu = local_rank % max(1, torch.cuda.device_count())
+    import torch  # plumbing: device memory, events, process group
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    if local_rank >= ndev and not a.allow_shared_gpu:
+        raise SystemExit(f"bench.py: rank {rank} (local {local_rank}) has no GPU of its own ({ndev} visible); "
+                         "pass --allow-shared-gpu for a rehearsal")
+    gpu = local_rank % ndev
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    n = a.sites
-    ctx = sid_amd.Context(gpu)
-    stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
+    dist = None
+    n_gpus, oversub = 1, False
+    if world > 1:
+        import torch.distributed as dist
+        backend = a.backend or "nccl"
+        dist.init_process_group(backend, rank=rank, world_size=world, device_id=dev if backend == "nccl" else None)
+        ids = [None] * world
+        dist.all_gather_object(ids, (socket.gethostname(), gpu))
+        n_gpus = len(set(ids))
+        oversub = n_gpus < world
+    import sid_amd
+
+    # ---------------------------------------------------------------- input --
+    if cfg["resident"]:
+        n = a.sites or cfg["per_gpu"]
+        first = rank * n
+        total = n * world
+    else:
+        total = a.sites or cfg["total"]
+        first, hi = total * rank // world, total * (rank + 1) // world
+        n = hi - first
+    text = None
+    if cfg["resident"]:
+        ctx = sid_amd.Context(gpu)
+        cap = int(n * (24 + 2.9 * cfg["depth"])) + (64 << 20)
+        text = torch.empty(cap + 512, dtype=torch.uint8, device=dev)
+        ln = ctx.synth_text_device(cfg["seed"], cfg["depth"], first, n, text.data_ptr(), cap,
+                                   sites_per_chrom=cfg["spc"])
+        text[ln:ln + 512].zero_()
+        torch.cuda.synchronize(dev)
+        ctx.close()
+    eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=gpu,
+                         chunk_bytes=a.chunk_mib << 20, device_sink=1)
+    if cfg["resident"]:
+        eng.source_device_text(text.data_ptr(), ln, keep=text)
+    else:
+        eng.source_synth(cfg["seed"], n, cfg["depth"], first=first, sites_per_chrom=cfg["spc"], on_device=True)
+    lynch = cfg["method"] != "local" or cfg["R"]
+    est_box = {}
+
+    def step():
+        st = eng.ingest()
+        if lynch and dist is not None:
+            exchange_histogram(torch, dist, eng, dev, rank)
+        if lynch and dist is not None and world > 1:
+            est = broadcast_estimate(torch, dist, eng, dev, rank)
+        else:
+            est = eng.estimate()
+        _, st2 = eng.emit()
+        est_box["est"] = est
+        return st, st2
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    eng.profile(True)   # HIP event pairs around every stage on the compute stream
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        st, st2 = step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    prof = eng.profile_read()
+    eng.profile(False)
+    sites_rank = st.sites
+    stages = {k[:-3]: v / a.steps for k, v in prof.items() if k.endswith("_ms")}
+    if dist:
+        vec = torch.tensor([elapsed] + [stages[k] for k in sorted(stages)], dtype=torch.float64, device=dev)
+        dist.all_reduce(vec, op=dist.ReduceOp.MAX)
+        elapsed = float(vec[0])
+        stages = {k: float(v) for k, v in zip(sorted(stages), vec[1:].tolist())}
+        tot = torch.tensor([float(sites_rank)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        sites_all = int(tot.item())
+    else:
+        sites_all = sites_rank
+
+    if rank == 0:
+        text_bytes = st.bytes_in if cfg["resident"] else None
+        tps = (text_bytes / sites_rank) if text_bytes else (24 + 2.7 * cfg["depth"])
+        cps = st2.bytes_out / sites_rank if sites_rank else 0.0
+        dom = max(stages, key=lambda k: stages[k])
+        bps = stage_bytes(dom, tps, cps)
+        per_launch_sites = sites_rank / max(1, prof["chunks"] / a.steps)
+        launch_ms = stages[dom] / max(1, prof["chunks"] / a.steps)
+        achieved = bps * per_launch_sites / (launch_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(dom, per_launch_sites)
+        step_bytes = (text_bytes or 0) + st2.bytes_out
+        out = {
+            "metric": "genome sites/sec (whole node) on 30x synthetic pileup; 1/2/4/8 GPU scaling",
+            "value": sites_all * a.steps / elapsed,
+            "unit": "sites/s",
+            "n_gpus": n_gpus,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak" if cfg["resident"] else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": ("synthetic (counter-based pileup generator, BASELINE.md): pileup text "
+                     + ("resident in HBM before the timed region" if cfg["resident"] else
+                        "generated on the device chunk by chunk inside the step (never stored)")
+                     + "; CSV records formatted into HBM"),
+            "config": {"workload": f"{a.config}: {cfg['desc']}", "method": cfg["method"],
+                       "estimate_prior": cfg["R"], "seed": cfg["seed"], "depth": cfg["depth"],
+                       "sites_per_gpu": n, "sites_total": sites_all,
+                       "sites_per_chrom": cfg["spc"] or None, "chunks_per_step_rank0": prof["chunks"] / a.steps,
+                       "text_bytes_rank0": text_bytes, "csv_bytes_rank0": st2.bytes_out,
+                       "parallelism": f"site-range shards x{world}" + (" + RCCL histogram all-gather"
+                                                                       if lynch and world > 1 else ""),
+                       "ranks": world, "oversubscribed": oversub},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": f"engine stage '{dom}'", "stage_kernels": STAGE_KERNELS[dom],
+                         "launch_ms": launch_ms, "sites_per_launch": per_launch_sites,
+                         "bytes_per_site": bps},
+            "stages_ms": stages,
+            "path": {"bytes_per_site": tps + cps, "text_per_site": tps, "csv_per_site": cps,
+                     "GBps": step_bytes / (elapsed / a.steps) / 1e9 if text_bytes else None,
+                     "note": "text in + CSV out per step (the path's minimum HBM traffic) / ms_per_step"},
+        }
+        if lynch:
+            e = est_box["est"]
+            out["estimate"] = {"pi": e.heterozygosity, "eps": e.error_rate, "iterations": e.iterations,
+                               "n_unique": e.n_unique}
+        if world == 1 and cfg["resident"] and not a.no_extras:
+            out["kernel_local"] = bench_kernel_local(torch, dev, cfg, n)
+            out["e2e"] = bench_e2e(torch, sid_amd, cfg, text, ln, n, a)
+            if not a.no_cpu:
+                out["cpu_baseline"] = bench_cpu(cfg, text, ln, n)
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+STAGE_KERNELS = {
+    "index": ["sid_lines_count_kernel", "sid_scan_*"],
+    "parse": ["sid_lines_emit_kernel", "sid_parse_kernel"],
+    "call": ["sid_local_table_p2", "sid_local_fixup"],
+    "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
+    "fmt_len": ["sid_fmt_len_kernel", "sid_scan_*"],
+    "fmt_write": ["sid_fmt_write_kernel"],
+}
+
+
+def pmc_traffic(stage, sites):
+    """HBM bytes per launch of the stage from the committed PMC summary
+    (tools/pmc_traffic.py over separate FETCH_SIZE / WRITE_SIZE passes), scaled
+    to this launch's sites; None when absent."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{stage}_r02.json")
+    try:
+        pm = json.load(open(p))
+        return pm["hbm_bytes_per_site"] * sites
+    except Exception:
+        return None
+
+
+def exchange_histogram(torch, dist, eng, dev, rank):
+    """The one exchange of the Lynch path: every rank's unique-profile table
+    (O(U) x 16 B) all-gathered as device tensors over RCCL, merged, loaded."""
+    from sid_amd import dist as sdist
+    ctx = sid_amd_ctx(eng)
+    keys, cnts = ctx.profile_table()
+    keys, cnts = sdist.allgather_profile_table(keys, cnts, device=dev)
+    ctx.profile_load(keys, cnts)
+
+
+def broadcast_estimate(torch, dist, eng, dev, rank):
+    """Rank 0 runs the one Nelder-Mead estimate on the merged table; (pi, eps)
+    go to the other ranks over RCCL, which classify with them."""
+    import sid_amd
+    if rank == 0:
+        est = eng.estimate()
+        vec = torch.tensor([est.heterozygosity, est.error_rate, float(est.iterations)], dtype=torch.float64,
+                           device=dev)
+    else:
+        vec = torch.zeros(3, dtype=torch.float64, device=dev)
+    dist.broadcast(vec, 0)
+    if rank != 0:
+        g = sid_amd.Estimate()
+        g.heterozygosity, g.error_rate, g.iterations = float(vec[0]), float(vec[1]), int(vec[2])
+        est = eng.estimate(given=g)
+    return est
+
+
+def sid_amd_ctx(eng):
+    import sid_amd
+    return sid_amd.Context.wrap(eng.context(0))
+
+
+def bench_kernel_local(torch, dev, cfg, n):
+    """sid_call_local alone over the counts of the same sites resident in HBM
+    (the per-site arithmetic kernel: 25 B/site), HIP events on its stream."""
+    import sid_amd
+    ctx = sid_amd.Context(dev.index)
+    st = torch.cuda.current_stream(dev)
     counts = torch.empty((n, 4), dtype=torch.int16, device=dev)
     code = torch.empty(n, dtype=torch.uint8, device=dev)
     hom = torch.empty(n, dtype=torch.float64, device=dev)
     het = torch.empty(n, dtype=torch.float64, device=dev)
-    # inputs resident in HBM before the timed region: this rank's site range
-    ctx.synth_counts(a.seed, a.depth, rank * n, n, counts.data_ptr(), sh)
+    ctx.synth_counts(cfg["seed"], cfg["depth"], 0, n, counts.data_ptr(), st.cuda_stream)
+    args = (counts.data_ptr(), n, code.data_ptr(), hom.data_ptr(), het.data_ptr(), st.cuda_stream)
+    for _ in range(3):
+        ctx.call_local(*args)
     torch.cuda.synchronize(dev)
-    if a.method != "local":
-        ctx.close()
-        return bench_lynch(a, torch, dist, rank, world, dev, counts, code, hom, het)
-
-    def step():
-        ctx.call_local(counts.data_ptr(), n, code.data_ptr(), hom.data_ptr(), het.data_ptr(), sh)
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    # HIP events on the launch stream bracket every step of the timed region;
-    # a step is one sid_call_local = class-table kernel + fix-up kernel
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(a.steps)]
-    t0 = time.perf_counter()
+    K = 20
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     for s, e in ev:
-        s.record(stream)
-        step()
-        e.record(stream)
+        s.record(st)
+        ctx.call_local(*args)
+        e.record(st)
     torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    elapsed = t1 - t0
-    step_ms = sum(s.elapsed_time(e) for s, e in ev) / a.steps
-    # split of a step into its two kernels, from libsid's own events in a
-    # separate untimed pass (events between the kernels would perturb the
-    # timed region)
+    ms = sum(s.elapsed_time(e) for s, e in ev) / K
     ctx.timing_enable(True)
-    for _ in range(min(a.steps, 10)):
-        step()
+    for _ in range(10):
+        ctx.call_local(*args)
     torch.cuda.synchronize(dev)
     ctx.timing_enable(False)
-    ncalls, main_ms, fixup_ms = ctx.timing_read()
-    if dist:
-        t = torch.tensor([elapsed, step_ms, main_ms, fixup_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, step_ms, main_ms, fixup_ms = (float(x) for x in t)
-
-    # a cheap on-device sanity check of this rank's last step (host oracle
-    # parity is covered by tests/ and smoke())
-    nhet = int((code >= 0x80).sum().item())
-
-    if rank == 0:
-        value = world * n * a.steps / elapsed
-        # the unit priced against the roofline is the whole sid_call_local
-        # (class-table kernel + fix-up), timed over the timed region
-        kern_ms = step_ms
-        achieved = BYTES_PER_SITE * n / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        if a.pmc_json and os.path.exists(a.pmc_json):
-            try:
-                pm = json.load(open(a.pmc_json))
-                if int(pm.get("sites", -1)) == n:
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        out = {
-            "metric": "genome sites/sec (whole node) on 30x synthetic pileup; 1/2/4/8 GPU scaling",
-            "value": value,
-            "unit": "sites/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (counter-based 30x diploid pileup generator, BASELINE.md), counts resident in HBM",
-            "config": {"workload": "C2: -m local, 50M-site 30x synthetic pileup per GPU",
-                       "sites_per_gpu": n, "depth": a.depth, "seed": a.seed, "method": "local",
-                       "parallelism": f"site-range shards x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": ("sid_call_local = sid_local_table_p2 + sid_local_fixup" if not a.direct
-                                    else "sid_local_kernel_x4"),
-                         "kernel_ms": kern_ms, "bytes_per_site": BYTES_PER_SITE,
-                         "split_ms": {"sid_local_table_p2": main_ms, "sid_local_fixup": fixup_ms},
-                         "achieved_main_kernel": (BYTES_PER_SITE * n / (main_ms * 1e-3) / 1e9
-                                                  if main_ms > 0 else None)},
-            "het_sites_last_step": nhet,
-            "kernel_path": "direct" if a.direct else "class-table + fix-up",
-        }
-        if world == 1 and not a.no_e2e:
-            out["pipeline"] = bench_pipeline(a, torch, dev, counts, code, hom, het)
-        if world == 1 and a.cpu_sample > 0:
-            out["cpu_baseline"], e2e = cpu_and_e2e(a)
-            if e2e is not None:
-                out["e2e"] = e2e
-        print(json.dumps(out), flush=True)
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
-
-
-def bench_pipeline(a, torch, dev, counts, code, hom, het):
-    """Pinned host counts -> H2D -> sid_call_local -> D2H (code, hom, het) for
-    the whole shard, 4M-site chunks round-robin over three streams, one
-    context per stream (a context's miss list is per call)."""
-    import sid_amd
-    n = a.sites
-    chunk = 1 << 22
-    nstreams = 3
-    h_counts = counts.cpu().pin_memory()
-    h_code = torch.empty(n, dtype=torch.uint8).pin_memory()
-    h_hom = torch.empty(n, dtype=torch.float64).pin_memory()
-    h_het = torch.empty(n, dtype=torch.float64).pin_memory()
-    lanes = []
-    for _ in range(nstreams):
-        lanes.append((torch.cuda.Stream(dev), sid_amd.Context(dev.index),
-                      torch.empty((chunk, 4), dtype=torch.int16, device=dev),
-                      torch.empty(chunk, dtype=torch.uint8, device=dev),
-                      torch.empty(chunk, dtype=torch.float64, device=dev),
-                      torch.empty(chunk, dtype=torch.float64, device=dev)))
-
-    def run():
-        for k, lo in enumerate(range(0, n, chunk)):
-            s, cx, dc, dcode, dhom, dhet = lanes[k % nstreams]
-            m = min(chunk, n - lo)
-            with torch.cuda.stream(s):
-                dc[:m].copy_(h_counts[lo:lo + m], non_blocking=True)
-                cx.call_local(dc.data_ptr(), m, dcode.data_ptr(), dhom.data_ptr(), dhet.data_ptr(), s.cuda_stream)
-                h_code[lo:lo + m].copy_(dcode[:m], non_blocking=True)
-                h_hom[lo:lo + m].copy_(dhom[:m], non_blocking=True)
-                h_het[lo:lo + m].copy_(dhet[:m], non_blocking=True)
-        torch.cuda.synchronize(dev)
-
-    run()
-    times = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        run()
-        times.append(time.perf_counter() - t0)
-    # the same outputs as the resident run (bit patterns, NaN-safe)
-    ok = (torch.equal(h_code, code.cpu()) and torch.equal(h_hom.view(torch.int64), hom.cpu().view(torch.int64))
-          and torch.equal(h_het.view(torch.int64), het.cpu().view(torch.int64)))
-    for _, cx, *_ in lanes:
-        cx.close()
-    dt = min(times)
-    return {"value": n / dt, "unit": "sites/s", "seconds": dt, "runs_s": times, "chunk_sites": chunk,
-            "streams": nstreams, "pcie_GBps": 25 * n / dt / 1e9, "equals_resident_run": ok,
-            "note": "pinned host counts -> H2D -> sid_call_local -> D2H of code + hom + het (25 B/site over PCIe)"}
-
-
-LYNCH_HIST_BYTES = 8         # SURVEY.md §8(d): histogram pass reads the counts
-LYNCH_LOOKUP_BYTES = 25      # lookup pass: 8 in + 17 out
-
-
-def bench_lynch(a, torch, dist, rank, world, dev, counts, code, hom, het):
-    """C3: the whole -R -m likelihood_ratio (or bayes) path per step."""
-    import sid_amd
-    from sid_amd import dist as sdist
-    n = a.sites
-    R = not a.no_R
-    ctx = sid_amd.Context(dev.index, method=a.method, estimate_prior=R)
-    stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
-    cp = counts.data_ptr()
-    ev = []
-
-    def step(record):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
-        t0 = time.perf_counter()
-        if e:
-            e[0].record(stream)
-        ctx.profile_reset(sh)
-        ctx.profile_accumulate(cp, n, sh)
-        if e:
-            e[1].record(stream)
-        if world > 1:   # the one exchange of the Lynch path: O(U) histogram
-            keys, cnts = ctx.profile_table()
-            keys, cnts = sdist.allgather_profile_table(keys, cnts)
-            ctx.profile_load(keys, cnts)
-        t1 = time.perf_counter()
-        est = ctx.lynch_prepare(False)
-        t2 = time.perf_counter()
-        if e:
-            e[2].record(stream)
-        ctx.lookup_sites(cp, n, code.data_ptr(), hom.data_ptr(), het.data_ptr(), sh)
-        if e:
-            e[3].record(stream)
-            ev.append((e, t1 - t0, t2 - t1))
-        return est
-
-    for _ in range(a.warmup):
-        step(False)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        est = step(True)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    elapsed = t1 - t0
-    hist_ms = sum(e[0].elapsed_time(e[1]) for e, _, _ in ev) / a.steps
-    look_ms = sum(e[2].elapsed_time(e[3]) for e, _, _ in ev) / a.steps
-    prep_ms = sum(p for _, _, p in ev) / a.steps * 1e3
-    if dist:
-        t = torch.tensor([elapsed, hist_ms, look_ms, prep_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, hist_ms, look_ms, prep_ms = (float(x) for x in t)
-    nhet = int((code >= 0x80).sum().item())
-    u = len(ctx.profile_table()[0])
-    if rank == 0:
-        hist_gbs = LYNCH_HIST_BYTES * n / (hist_ms * 1e-3) / 1e9
-        look_gbs = LYNCH_LOOKUP_BYTES * n / (look_ms * 1e-3) / 1e9
-        dom = ("sid_lookup_sites", look_gbs, look_ms) if look_ms >= hist_ms else \
-              ("sid_profile_accumulate", hist_gbs, hist_ms)
-        out = {
-            "metric": "genome sites/sec (whole node) on 30x synthetic pileup; 1/2/4/8 GPU scaling",
-            "value": world * n * a.steps / elapsed,
-            "unit": "sites/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (counter-based 30x diploid pileup generator, BASELINE.md), counts resident in HBM",
-            "config": {"workload": f"C3: {'-R ' if R else ''}-m {a.method}, 50M-site 30x synthetic pileup per GPU",
-                       "sites_per_gpu": n, "depth": a.depth, "seed": a.seed, "method": a.method,
-                       "estimate_prior": R, "parallelism": f"site-range shards x{world} + histogram all-gather"},
-            "roofline": {"bound": "hbm", "achieved": dom[1], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": dom[1] / HBM_PEAK_GBS, "traffic": None, "kernel": dom[0], "kernel_ms": dom[2],
-                         "kernels": {"sid_profile_accumulate": {"ms": hist_ms, "bytes_per_site": LYNCH_HIST_BYTES,
-                                                                "GBps": hist_gbs},
-                                     "sid_lookup_sites": {"ms": look_ms, "bytes_per_site": LYNCH_LOOKUP_BYTES,
-                                                          "GBps": look_gbs}}},
-            "phases_ms": {"histogram": hist_ms, "estimate_classify_host": prep_ms, "lookup": look_ms},
-            "estimate": {"pi": est.heterozygosity, "eps": est.error_rate, "iterations": est.iterations,
-                         "evaluations": est.evaluations, "unique_profiles": u},
-            "het_sites_last_step": nhet,
-        }
-        if world == 1 and not a.no_e2e:
-            out["pipeline"] = bench_pipeline(a, torch, dev, counts, code, hom, het)
-        if world == 1 and a.cpu_sample > 0:
-            out["cpu_baseline"], e2e = cpu_and_e2e(a)
-            if e2e is not None:
-                out["e2e"] = e2e
-        print(json.dumps(out), flush=True)
+    _, main_ms, fix_ms = ctx.timing_read()
     ctx.close()
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+    gbs = LOCAL_BYTES_PER_SITE * n / (ms * 1e-3) / 1e9
+    pm = None
+    try:
+        pm = json.load(open(os.path.join(ROOT, "profiles", "pmc_local_r01.json"))).get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return {"sites_per_s": n / (ms * 1e-3), "ms": ms, "GBps": gbs, "frac": gbs / HBM_PEAK_GBS,
+            "split_ms": {"sid_local_table_p2": main_ms, "sid_local_fixup": fix_ms}, "bytes_per_site": 25,
+            "traffic": pm, "note": "counts resident in HBM -> code + confs (the round-1 headline kernel)"}
 
 
-def method_flags(a):
-    if a.method == "local":
-        return []
-    return (["-R"] if not a.no_R else []) + ["-m", a.method]
+def bench_e2e(torch, sid_amd, cfg, text, ln, n, a):
+    """PCIe-inclusive: (1) the engine over the text in pinned host memory, CSV
+    copied back into pinned host memory (engine clock); (2) the CLI on the same
+    text as a file in the page cache, CSV to /dev/null (wall clock and the
+    CLI's own clock)."""
+    res = {"sites": n, "text_bytes": ln}
+    host = text[:ln].cpu().pin_memory()
+    eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], device_sink=2,
+                         chunk_bytes=a.chunk_mib << 20)
+    eng.source_host_ptr(host.data_ptr(), ln, keep=host)
+    runs = []
+    for r in range(3):
+        t0 = time.perf_counter()
+        st = eng.ingest()
+        eng.estimate()
+        _, st2 = eng.emit()
+        runs.append(time.perf_counter() - t0)
+    eng.close()
+    dt = min(runs[1:])
+    res["host_memory"] = {"sites_per_s": n / dt, "s": dt, "runs_s": runs, "csv_bytes": st2.bytes_out,
+                          "note": "pinned host text -> H2D -> index/parse/call/format -> D2H into pinned host "
+                                  "memory (records dropped there), one GPU, engine clock"}
+    del host
+    cli = os.path.join(ROOT, "build", "sid")
+    if not os.path.exists(cli):
+        return res
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "c.plp")
+        write_text_file(text, ln, path)
+        flags = [] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) + ["-m", cfg["method"]]
+        cli_runs = []
+        for _ in range(3):
+            with open(os.devnull, "wb") as dn:
+                t0 = time.perf_counter()
+                r = subprocess.run([cli, "--stats"] + flags + [path], stdout=dn, stderr=subprocess.PIPE)
+                dt = time.perf_counter() - t0
+            if r.returncode != 0:
+                res["cli"] = {"error": r.returncode, "stderr": r.stderr.decode()[-400:]}
+                return res
+            try:
+                stt = json.loads(r.stderr.decode().strip().splitlines()[-1])
+            except Exception:
+                stt = {}
+            cli_runs.append((dt, stt))
+        dt, stt = min(cli_runs[1:], key=lambda x: x[0])
+        res["cli"] = {"wall_s": dt, "sites_per_s_wall": n / dt, "sites_per_s_cli_clock": stt.get("sites_per_s"),
+                      "wall_s_runs": [x[0] for x in cli_runs], "cli_stats": stt,
+                      "note": "build/sid FILE > /dev/null, one GPU: wall = process start + HIP init + mmap + "
+                              "H2D + parse/call/format + D2H + write; cli_clock = input mapping to last write"}
+    return res
+
+
+def write_text_file(text, ln, path):
+    """The resident text, copied back in 256 MiB pieces, as a file."""
+    step = 256 << 20
+    with open(path, "wb") as f:
+        for lo in range(0, ln, step):
+            f.write(text[lo:min(ln, lo + step)].cpu().numpy().tobytes())
+    with open(path, "rb") as f:   # into the page cache
+        while f.read(1 << 26):
+            pass
 
 
 def cpu_model():
@@ -369,99 +432,73 @@ def cpu_model():
     return None
 
 
-def cpu_sharded(a, td, cli):
-    """the CPU path with one process per core on line-aligned
-    shards of the same sample (valid for -m local: sites are independent),
-    P = min(16, cpu_count) -- the GPU box's CPU share is 16 cores."""
-    import sid_amd
-    P = max(1, min(16, os.cpu_count() or 1))
-    m = a.cpu_sample
-    paths = []
-    for k in range(P):
-        lo, hi = m * k // P, m * (k + 1) // P
-        pth = os.path.join(td, f"shard{k}.plp")
-        with open(pth, "wb") as f:
-            f.write(sid_amd.synth_text(a.seed, hi - lo, a.depth, first=lo))
-        with open(pth, "rb") as f:
-            while f.read(1 << 26):
-                pass
-        paths.append(pth)
-    with open(os.devnull, "wb") as dn:
-        t0 = time.perf_counter()
-        procs = [subprocess.Popen([cli] + method_flags(a) + [pth], stdout=dn, stderr=subprocess.DEVNULL)
-                 for pth in paths]
-        rcs = [pr.wait() for pr in procs]
-        dt = time.perf_counter() - t0
-    for pth in paths:
-        os.unlink(pth)
-    return {"value": m / dt if not any(rcs) else None, "unit": "sites/s", "cores": P, "seconds": dt,
-            "note": f"{P} oracle processes on line-aligned shards of the same {m:,}-site sample, wall clock"}
-
-
-def cpu_and_e2e(a):
-    """Oracle CLI (reference path restated, 1 thread) and the product CLI on the
-    same bounded sample text of the workload (file in page cache, CSV to
-    /dev/null).  The product runs twice: the device text path (text to HBM,
-    parsed and formatted on the GPU) and --host-parse."""
-    import sid_amd
+def bench_cpu(cfg, text, ln, n):
+    """The oracle CLI (reference sid.cpp/call.cpp/lynch/stats restated in C,
+    single-threaded) on the same text: 16 line-aligned shard processes over
+    all n sites (-m local: sites are independent; the GPU box's CPU share is
+    16 cores), and one process on the first 4M sites."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    m = a.cpu_sample
-    base = None
-    e2e = None
+    if not os.path.exists(oracle.CLI):
+        oracle.build()
+    flags = [] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) + ["-m", cfg["method"]]
+    P = 16
+    host = text[:ln].cpu().numpy()
     with tempfile.TemporaryDirectory() as td:
-        path = os.path.join(td, "sample.plp")
-        with open(path, "wb") as f:
-            step = 2_000_000
-            for lo in range(0, m, step):
-                f.write(sid_amd.synth_text(a.seed, min(step, m - lo), a.depth, first=lo))
-        size = os.path.getsize(path)
-        if not os.path.exists(oracle.CLI):
-            oracle.build()
-        with open(path, "rb") as f:   # page cache
-            while f.read(1 << 26):
-                pass
-        t0 = time.perf_counter()
+        cuts = [0]
+        for k in range(1, P):
+            c = ln * k // P
+            nl = host[c:c + (1 << 20)].tobytes().find(b"\n")
+            cuts.append(c + nl + 1)
+        cuts.append(ln)
+        paths = []
+        for k in range(P):
+            pth = os.path.join(td, f"s{k}.plp")
+            with open(pth, "wb") as f:
+                f.write(host[cuts[k]:cuts[k + 1]].tobytes())
+            paths.append(pth)
+        res = {"unit": "sites/s", "kind": "port", "cpu_model": cpu_model()}
+        if cfg["method"] == "local":
+            with open(os.devnull, "wb") as dn:
+                t0 = time.perf_counter()
+                procs = [subprocess.Popen([oracle.CLI] + flags + [p], stdout=dn, stderr=subprocess.DEVNULL)
+                         for p in paths]
+                rcs = [p.wait() for p in procs]
+                dt = time.perf_counter() - t0
+            res.update({"value": n / dt if not any(rcs) else None, "cores": P, "seconds": dt,
+                        "sample": f"the same {n:,}-site {cfg['desc']} text ({ln / 1e9:.2f} GB), {P} line-aligned "
+                                  f"shards, one oracle/_build/sid_oracle process each, CSV to /dev/null, wall"})
+        # one core on the first 4M sites
+        m = min(n, 4_000_000)
+        cut = 0
+        need = m
+        while need > 0:
+            nl = host[cut:cut + (64 << 20)].tobytes().count(b"\n")
+            if nl <= need:
+                cut += 64 << 20
+                need -= nl
+            else:
+                seg = host[cut:cut + (64 << 20)].tobytes()
+                idx = -1
+                for _ in range(need):
+                    idx = seg.find(b"\n", idx + 1)
+                cut += idx + 1
+                need = 0
+        one = os.path.join(td, "one.plp")
+        with open(one, "wb") as f:
+            f.write(host[:cut].tobytes())
         with open(os.devnull, "wb") as dn:
-            r = subprocess.run([oracle.CLI] + method_flags(a) + [path], stdout=dn, stderr=subprocess.PIPE)
-        dt = time.perf_counter() - t0
-        base = {"value": m / dt if r.returncode == 0 else None, "unit": "sites/s", "cores": 1,
-                "kind": "port",
-                "sample": f"{m:,} sites of the {'C2' if a.method == 'local' else 'C3'} generator "
-                          f"{' '.join(method_flags(a))} (seed {a.seed}, {a.depth:g}x, {size / 1e9:.2f} GB text), "
-                          f"pileup text -> CSV to /dev/null, oracle/_build/sid_oracle "
-                          f"(call.cpp/lynch.hpp/stats.cpp restated, single thread), {dt:.2f} s",
-                "cpu_model": cpu_model()}
-        if a.method == "local" and r.returncode == 0:
-            base["sharded"] = cpu_sharded(a, td, oracle.CLI)
-        if not a.no_e2e and os.path.exists(sid_amd.CLI_PATH):
-            e2e = {"unit": "sites/s", "sites": m, "text_bytes": size,
-                   "note": "build/sid on the sample file: wall clock of the whole process (start, HIP init, "
-                           "mmap, text -> HBM over PCIe, parse, call, CSV formatting, D2H, write to /dev/null); "
-                           "in_process = the CLI's own clock from input mapping to the last byte written"}
-            for tag, extra in (("device_text_path", []), ("host_parse", ["--host-parse"])):
-                runs = []
-                for _ in range(2):   # the first run of a fresh process on the box also loads code objects
-                    with open(os.devnull, "wb") as dn:
-                        t0 = time.perf_counter()
-                        r = subprocess.run([sid_amd.CLI_PATH, "--stats"] + extra + method_flags(a) + [path],
-                                           stdout=dn, stderr=subprocess.PIPE)
-                        dt = time.perf_counter() - t0
-                    if r.returncode != 0:
-                        runs = None
-                        e2e[tag] = {"error": r.returncode}
-                        break
-                    try:
-                        st = json.loads(r.stderr.decode().strip().splitlines()[-1])
-                    except Exception:
-                        st = {}
-                    runs.append((dt, st))
-                if not runs:
-                    continue
-                dt, st = min(runs, key=lambda x: x[0])
-                e2e[tag] = {"wall_s": dt, "value_wall": m / dt, "value_in_process": st.get("sites_per_s"),
-                            "wall_s_runs": [x[0] for x in runs], "cli_stats": st}
-    return base, e2e
+            t0 = time.perf_counter()
+            r = subprocess.run([oracle.CLI] + flags + [one], stdout=dn, stderr=subprocess.DEVNULL)
+            dt = time.perf_counter() - t0
+        single = {"value": m / dt if r.returncode == 0 else None, "cores": 1, "seconds": dt,
+                  "sample": f"the first {m:,} sites of the same text, one process"}
+        if "value" not in res:
+            res.update(single)
+            res["sample"] = single["sample"]
+        else:
+            res["single_core"] = single
+    return res
 
 
 if __name__ == "__main__":

@@ -166,6 +166,11 @@ int sid_lookup_sites(sid_ctx* ctx, const uint16_t* counts, size_t n, uint8_t* co
  * (positions restart at 1; keeps positions < 2^31). */
 int sid_synth_counts(sid_ctx* ctx, uint64_t seed, double mean_depth, uint64_t first_site,
                      size_t n, uint16_t* counts /* device */, void* stream);
+/* The same text generated on the device into out (cap bytes, device memory),
+ * stream-ordered, then synchronised: *len = its bytes; SID_ERANGE when they
+ * exceed cap (then out holds no usable text). */
+int sid_synth_text_device(sid_ctx* ctx, uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
+                          uint64_t sites_per_chrom, char* out /* device */, size_t cap, size_t* len, void* stream);
 /* Host text of sites [first_site, first_site+n).  Returns the bytes needed in
  * *len; writes at most cap bytes (call with buf == NULL to size). */
 int sid_synth_text(uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
@@ -288,8 +293,10 @@ typedef struct {
                                (0 = 40% of free HBM)                               */
     int host_threads;       /* host threads generating / prefetching input (0 = 8) */
     int verbose;            /* the reference's "# ..." lines on stderr             */
-    int device_sink;        /* 1: records stay in HBM (measurement), nothing is
-                               written; 0: write() in file order                   */
+    int device_sink;        /* 0: write() in file order; 1: records stay in HBM,
+                               nothing is copied back (measurement); 2: records
+                               copied back to pinned host memory and dropped
+                               (measurement of the PCIe path, no write)          */
 } sid_engine_cfg;
 typedef struct {
     uint64_t sites;              /* non-empty lines parsed                           */
@@ -331,6 +338,20 @@ int sid_engine_ingest(sid_engine* e, sid_run_stats* stats);
 int sid_engine_estimate(sid_engine* e, const sid_estimate* given, sid_estimate* out);
 int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn write, void* user, sid_run_stats* stats);
 int sid_engine_run(sid_engine* e, const char* header, sid_write_fn write, void* user, sid_run_stats* stats);
+/* Measurement: with profiling on, every stage of every chunk is bracketed by
+ * a pair of HIP events on its device's compute stream; _read sums the stages'
+ * device time over the chunks and devices since the last read (synchronises). */
+typedef struct {
+    uint64_t chunks;        /* chunks processed (either pass)                      */
+    double index_ms;        /* line index: line starts per tile + scan             */
+    double parse_ms;        /* line offsets + parse to counts                      */
+    double call_ms;         /* sid_call_local / sid_lookup_sites / quality kernels */
+    double hist_ms;         /* Lynch profile histogram                             */
+    double fmt_len_ms;      /* record lengths + scan                               */
+    double fmt_write_ms;    /* records written                                     */
+} sid_engine_prof;
+int sid_engine_profile(sid_engine* e, int enable);
+int sid_engine_profile_read(sid_engine* e, sid_engine_prof* out);
 
 #ifdef __cplusplus
 }

@@ -71,6 +71,11 @@ class RunStats(C.Structure):
                 ("emit_s", C.c_double), ("estimate", Estimate)]
 
 
+class EngineProf(C.Structure):
+    _fields_ = [("chunks", C.c_uint64), ("index_ms", C.c_double), ("parse_ms", C.c_double), ("call_ms", C.c_double),
+                ("hist_ms", C.c_double), ("fmt_len_ms", C.c_double), ("fmt_write_ms", C.c_double)]
+
+
 _LIB = None
 
 # (name, restype, argtypes) for every entry point of include/sid.h
@@ -100,6 +105,7 @@ SIGNATURES = [
     ("sid_synth_counts", _I, [_P, _U64, _D, _U64, _SZ, _P, _P]),
     ("sid_synth_text", _I, [_U64, _D, _U64, _SZ, _U64, _P, _SZ, C.POINTER(C.c_size_t)]),
     ("sid_synth_counts_host", _I, [_U64, _D, _U64, _SZ, _P]),
+    ("sid_synth_text_device", _I, [_P, _U64, _D, _U64, _SZ, _U64, _P, _SZ, C.POINTER(C.c_size_t), _P]),
     ("sid_synth_text_mq", _I, [_U64, _D, _U64, _SZ, _U64, _P, _SZ, C.POINTER(C.c_size_t)]),
     ("sid_parse_text", _I, [C.c_char_p, _SZ, _I, C.POINTER(_P), C.POINTER(C.c_uint64)]),
     ("sid_sites_free", None, [_P]),
@@ -132,6 +138,8 @@ SIGNATURES = [
     ("sid_engine_estimate", _I, [_P, C.POINTER(Estimate), C.POINTER(Estimate)]),
     ("sid_engine_emit", _I, [_P, C.c_char_p, WRITE_FN, _P, C.POINTER(RunStats)]),
     ("sid_engine_run", _I, [_P, C.c_char_p, WRITE_FN, _P, C.POINTER(RunStats)]),
+    ("sid_engine_profile", _I, [_P, _I]),
+    ("sid_engine_profile_read", _I, [_P, C.POINTER(EngineProf)]),
 ]
 
 
@@ -335,10 +343,17 @@ class Context:
         check(lib().sid_create(device, C.byref(self.opts), C.byref(h)), "sid_create")
         self.h = h
 
+    @classmethod
+    def wrap(cls, handle, device: int = 0):
+        """A non-owning view of a context another object owns (e.g. an engine's)."""
+        c = cls.__new__(cls)
+        c.opts, c.device, c.h, c._borrowed = None, device, C.c_void_p(handle), True
+        return c
+
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and not getattr(self, "_borrowed", False):
             lib().sid_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -407,6 +422,13 @@ class Context:
         check(lib().sid_synth_counts(self.h, seed, depth, first, n, counts_ptr, stream),
               "sid_synth_counts")
 
+    def synth_text_device(self, seed, depth, first, n, out_ptr, cap, sites_per_chrom=0, stream=None) -> int:
+        """The generator's text written on the device (sid_synth_text_device); returns its bytes."""
+        ln = C.c_size_t(0)
+        check(lib().sid_synth_text_device(self.h, seed, depth, first, n, sites_per_chrom, out_ptr, cap,
+                                          C.byref(ln), stream), "sid_synth_text_device")
+        return ln.value
+
 
 HEADER = b"chrom,pos,label,gt,hom_conf,het_conf,conf_type\n"
 
@@ -422,7 +444,7 @@ class Engine:
         lib().sid_engine_cfg_default(C.byref(cfg))
         cfg.devices, cfg.first_device, cfg.chunk_bytes, cfg.slots = devices, first_device, chunk_bytes, slots
         cfg.hold_bytes, cfg.retain_bytes, cfg.host_threads = hold_bytes, retain_bytes, host_threads
-        cfg.verbose, cfg.device_sink = int(bool(verbose)), int(bool(device_sink))
+        cfg.verbose, cfg.device_sink = int(bool(verbose)), int(device_sink)
         self.cfg = cfg
         h = C.c_void_p()
         check(lib().sid_engine_create(C.byref(self.opts), C.byref(cfg), C.byref(h)), "sid_engine_create")
@@ -496,6 +518,14 @@ class Engine:
         st = stats if stats is not None else RunStats()
         check(lib().sid_engine_emit(self.h, header, cb, None, C.byref(st)), "sid_engine_emit")
         return b"".join(parts), st
+
+    def profile(self, enable=True):
+        check(lib().sid_engine_profile(self.h, int(bool(enable))), "sid_engine_profile")
+
+    def profile_read(self) -> dict:
+        p = EngineProf()
+        check(lib().sid_engine_profile_read(self.h, C.byref(p)), "sid_engine_profile_read")
+        return {f: getattr(p, f) for f, _ in EngineProf._fields_}
 
     def run(self, header=HEADER, sink=None):
         st = self.ingest()

@@ -285,12 +285,9 @@ uint32_t sid_poisson_cdf(double mean, std::vector<uint64_t>& cdf)
     return (uint32_t)cdf.size();
 }
 
-extern "C" int sid_synth_counts(sid_ctx* c, uint64_t seed, double mean_depth, uint64_t first_site,
-                                size_t n, uint16_t* counts, void* stream)
+// the context's device copy of the Poisson CDF for mean_depth
+static int ctx_cdf(sid_ctx* c, double mean_depth)
 {
-    if (!c || (!counts && n) || !(mean_depth >= 0) || mean_depth > 600) return SID_EINVAL;
-    if (n == 0) return SID_OK;
-    if ((uintptr_t)counts & 7u) return SID_EINVAL;
     if (mean_depth != c->cdf_mean) {
         std::vector<uint64_t> cdf;
         uint32_t k = sid_poisson_cdf(mean_depth, cdf);
@@ -302,8 +299,39 @@ extern "C" int sid_synth_counts(sid_ctx* c, uint64_t seed, double mean_depth, ui
         c->cdf_k = k;
         c->cdf_mean = mean_depth;
     }
+    return SID_OK;
+}
+
+extern "C" int sid_synth_counts(sid_ctx* c, uint64_t seed, double mean_depth, uint64_t first_site,
+                                size_t n, uint16_t* counts, void* stream)
+{
+    if (!c || (!counts && n) || !(mean_depth >= 0) || mean_depth > 600) return SID_EINVAL;
+    if (n == 0) return SID_OK;
+    if ((uintptr_t)counts & 7u) return SID_EINVAL;
+    (void)hipSetDevice(c->device);
+    int rc = ctx_cdf(c, mean_depth);
+    if (rc != SID_OK) return rc;
     hipError_t e = sid_launch_synth(seed, first_site, n, c->d_cdf, c->cdf_k, counts, (hipStream_t)stream);
     return e == hipSuccess ? SID_OK : sid_set_hip_error(e);
+}
+
+extern "C" int sid_synth_text_device(sid_ctx* c, uint64_t seed, double mean_depth, uint64_t first_site, size_t n,
+                                     uint64_t sites_per_chrom, char* out, size_t cap, size_t* len, void* stream)
+{
+    if (!c || !len || (!out && cap) || !(mean_depth >= 0) || mean_depth > 600) return SID_EINVAL;
+    (void)hipSetDevice(c->device);
+    int rc = ctx_cdf(c, mean_depth);
+    if (rc != SID_OK) return rc;
+    sid_synth_gen_ws ws;
+    const hipStream_t st = (hipStream_t)stream;
+    uint64_t res[2] = {0, 0};
+    hipError_t e = sid_launch_synth_text(seed, c->d_cdf, c->cdf_k, first_site, n, sites_per_chrom, &ws, out, cap, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(res, ws.res, sizeof res, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    sid_synth_gen_release(&ws);
+    if (e != hipSuccess) return sid_set_hip_error(e);
+    *len = res[0];
+    return res[1] ? SID_ERANGE : SID_OK;
 }
 
 extern "C" int sid_synth_counts_host(uint64_t seed, double mean_depth, uint64_t first_site,

@@ -241,6 +241,29 @@ struct Dev {
     std::atomic<bool> hold_full{false};
     std::mutex ev_m;
     std::vector<hipEvent_t> ev_cache;   // events marking a chunk's records written (compute -> drain)
+    // sid_engine_profile: (stage, start, end) per stage and chunk, read after a sync
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
+    std::vector<hipEvent_t> prof_free;
+    uint64_t prof_chunks = 0;
+    hipEvent_t prof_begin(bool on)
+    {
+        if (!on) return nullptr;
+        hipEvent_t ev = nullptr;
+        if (!prof_free.empty()) {
+            ev = prof_free.back();
+            prof_free.pop_back();
+        } else if (hipEventCreate(&ev) != hipSuccess) {
+            return nullptr;
+        }
+        (void)hipEventRecord(ev, s_comp);
+        return ev;
+    }
+    void prof_end(int stage, hipEvent_t start)
+    {
+        if (!start) return;
+        hipEvent_t ev = prof_begin(true);
+        if (ev) prof_pending.push_back({stage, {start, ev}});
+    }
     hipEvent_t take_event()
     {
         std::lock_guard<std::mutex> l(ev_m);
@@ -285,6 +308,7 @@ struct sid_engine {
     std::atomic<int> rc{SID_OK};
     std::atomic<uint64_t> first_err{UINT64_MAX};
     std::atomic<uint64_t> reloaded{0};
+    std::atomic<uint64_t> sink_bytes{0};   // device sink: CSV bytes formatted and dropped
     // host-generated input: pinned buffers
     std::vector<char*> gen_buf;
     std::vector<uint64_t> gen_cap;
@@ -292,6 +316,9 @@ struct sid_engine {
     std::vector<int> gen_dev;         // device whose stream recorded gen_ev
     uint64_t per_chunk_cap = 0;
     sid_estimate est{};
+    bool prof = false;
+    double prof_ms[6] = {0, 0, 0, 0, 0, 0};   // sid_engine_prof order: index parse call hist fmt_len fmt_write
+    uint64_t prof_chunks = 0;
 };
 
 namespace {
@@ -502,6 +529,8 @@ extern "C" int sid_engine_destroy(sid_engine* e)
         for (char* p : d->pinned) (void)hipHostFree(p);
         for (hipEvent_t ev : d->pinned_ev) (void)hipEventDestroy(ev);
         for (hipEvent_t ev : d->ev_cache) (void)hipEventDestroy(ev);
+        for (auto& pr : d->prof_pending) (void)hipEventDestroy(pr.second.first), (void)hipEventDestroy(pr.second.second);
+        for (hipEvent_t ev : d->prof_free) (void)hipEventDestroy(ev);
         sid_chunk_release(&d->ws);
         if (d->h_small) (void)hipHostFree(d->h_small);
         for (hipStream_t s : {d->s_up, d->s_comp, d->s_d2h})
@@ -841,7 +870,7 @@ void compute(sid_engine* e, Dev& d, int pass)
             it.cap = r.held_cap;
             it.len = r.held_len;
             r.held = nullptr;
-            if (e->cfg.device_sink) d.pool.put(it.buf, it.cap, nullptr);
+            if (e->cfg.device_sink == 1) e->sink_bytes += it.len, d.pool.put(it.buf, it.cap, nullptr);
             else if (!d.drain_q.push(it)) break;
             continue;
         }
@@ -852,8 +881,12 @@ void compute(sid_engine* e, Dev& d, int pass)
         int rc = SID_OK;
         hipError_t x = hipSuccess;
         if (L.ev) x = hipStreamWaitEvent(d.s_comp, L.ev, 0);
+        const bool P = e->prof;
+        if (P) d.prof_chunks++;
         if (x == hipSuccess) rc = sid_chunk_reserve(&W, L.c1 - (L.c0 & ~(uint64_t)15), 0);
+        hipEvent_t pe = d.prof_begin(P);
         if (rc == SID_OK && x == hipSuccess) rc = sid_chunk_index(&W, L.base, L.c0, L.c1, d.s_comp);
+        d.prof_end(0, pe);
         if (rc == SID_OK && x == hipSuccess) x = hipMemcpyAsync(hs, W.state, 8, hipMemcpyDeviceToHost, d.s_comp);
         if (rc == SID_OK && x == hipSuccess) x = sync();
         if (x != hipSuccess) return (void)hipfail(e, x);
@@ -861,20 +894,28 @@ void compute(sid_engine* e, Dev& d, int pass)
         const uint64_t n = hs[0];
         r.parsed = n;
         rc = sid_chunk_reserve(&W, 0, n);
+        pe = d.prof_begin(P);
         if (rc == SID_OK) rc = sid_chunk_parse(&W, L.base, L.c0, L.c1, n, qmode, d.s_comp);
+        d.prof_end(1, pe);
         if (rc != SID_OK) return (void)fail(e, rc);
         const bool lynch_hist = pass == 1 && e->lynch;
         const bool format = pass == 2 || (needs_format_pass1(e) && !d.hold_full.load());
         if (lynch_hist) {
             x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
             if (x != hipSuccess) return (void)hipfail(e, x);
+            pe = d.prof_begin(P);
             rc = sid_profile_accumulate(d.ctx, (const uint16_t*)W.counts, n, d.s_comp);   // synchronises
+            d.prof_end(3, pe);
             if (rc == SID_OK && n == 0) x = sync();
             if (rc != SID_OK) return (void)fail(e, rc);
             if (x != hipSuccess) return (void)hipfail(e, x);
         } else if (format) {
+            pe = d.prof_begin(P);
             rc = call_sites(e, d, L, n);
+            d.prof_end(2, pe);
+            pe = d.prof_begin(P);
             if (rc == SID_OK) rc = sid_chunk_fmt_len(&W, L.base, L.c1, n, e->conf_type, d.s_comp);
+            d.prof_end(4, pe);
             if (rc != SID_OK) return (void)fail(e, rc);
             x = hipMemcpyAsync(hs + 3, W.state + 3, 24, hipMemcpyDeviceToHost, d.s_comp);
             if (x == hipSuccess) x = sync();
@@ -908,7 +949,9 @@ void compute(sid_engine* e, Dev& d, int pass)
         uint64_t cap = 0;
         char* out = d.pool.get(bytes + 16, &cap, d.s_comp);
         if (!out) return (void)fail(e, SID_ENOMEM);
+        pe = d.prof_begin(P);
         rc = sid_chunk_fmt_write(&W, L.base, L.c1, n, e->conf_type, out, d.s_comp);
+        d.prof_end(5, pe);
         if (rc != SID_OK) return (void)fail(e, rc);
         release_slot();
         if (pass == 2 && r.kept) {   // kept text done with: back to the pool after this stream's work
@@ -922,7 +965,8 @@ void compute(sid_engine* e, Dev& d, int pass)
             d.hold_used += cap;
             continue;
         }
-        if (e->cfg.device_sink) {
+        if (e->cfg.device_sink == 1) {
+            e->sink_bytes += bytes;
             d.pool.put(out, cap, nullptr);   // reused on this stream only: ordered
             continue;
         }
@@ -1187,16 +1231,18 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
                                sid_run_stats* st)
 {
     if (!e || !e->ingested || !e->estimated) return SID_ESTATE;
-    if (!e->cfg.device_sink && !write) return SID_EINVAL;
+    const int sink = e->cfg.device_sink;   // 0 write, 1 HBM only, 2 D2H only
+    if (sink == 0 && !write) return SID_EINVAL;
     const double t0 = wall();
     e->rc = SID_OK;
     e->reloaded = 0;
+    e->sink_bytes = 0;
     start_queues(e);
     const int D = (int)e->devs.size();
     // pinned ring per device: 4 x 16 MiB (pinned once, reused by every run)
     const uint64_t PC = 16ull << 20;
     const int NP = 4;
-    if (!e->cfg.device_sink)
+    if (sink != 1)
         for (auto& dp : e->devs) {
             Dev& d = *dp;
             if (hipSetDevice(d.device) != hipSuccess) return SID_EHIP;
@@ -1218,12 +1264,12 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
     for (int i = 0; i < D; ++i) {
         th.emplace_back(uploader, e, std::ref(*e->devs[i]), std::cref(lists[i]), 2);
         th.emplace_back(compute, e, std::ref(*e->devs[i]), 2);
-        if (!e->cfg.device_sink) th.emplace_back(drain, e, std::ref(*e->devs[i]));
+        if (sink != 1) th.emplace_back(drain, e, std::ref(*e->devs[i]));
     }
     // the writer: header, then every chunk's pieces in file order
-    if (!e->cfg.device_sink) {
+    if (sink != 1) {
         bool ok = true;
-        if (header && write(user, header, std::strlen(header)) != 0) ok = false;
+        if (sink == 0 && header && write(user, header, std::strlen(header)) != 0) ok = false;
         for (uint64_t j = 0; j < e->recs.size() && e->rc.load() == SID_OK; ++j) {
             Dev& d = *e->devs[e->recs[j].dev];
             Piece p;
@@ -1234,7 +1280,7 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
                         fail(e, SID_EHIP);
                         break;
                     }
-                    if (ok && write(user, d.pinned[p.ps], p.len) != 0) ok = false;
+                    if (ok && sink == 0 && write(user, d.pinned[p.ps], p.len) != 0) ok = false;
                     out_bytes += p.len;
                     d.free_pinned.push(p.ps);
                 }
@@ -1257,7 +1303,7 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
     }
     if (st) {
         st->chunks_reloaded = e->reloaded.load();
-        st->bytes_out = out_bytes.load();
+        st->bytes_out = sink == 1 ? e->sink_bytes.load() : out_bytes.load();
         st->emit_s = wall() - t0;
     }
     // every held / kept buffer went back to the pools
@@ -1285,4 +1331,41 @@ extern "C" int sid_engine_run(sid_engine* e, const char* header, sid_write_fn wr
     s->estimate_s = wall() - t0;
     if (rc != SID_OK) return rc;
     return sid_engine_emit(e, header, write, user, s);
+}
+
+extern "C" int sid_engine_profile(sid_engine* e, int enable)
+{
+    if (!e) return SID_EINVAL;
+    e->prof = enable != 0;
+    return SID_OK;
+}
+
+// sums the pending event pairs of every device (after their streams drained)
+extern "C" int sid_engine_profile_read(sid_engine* e, sid_engine_prof* out)
+{
+    if (!e || !out) return SID_EINVAL;
+    for (auto& dp : e->devs) {
+        Dev& d = *dp;
+        if (hipSetDevice(d.device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return SID_EHIP;
+        for (auto& pr : d.prof_pending) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, pr.second.first, pr.second.second) == hipSuccess) e->prof_ms[pr.first] += ms;
+            d.prof_free.push_back(pr.second.first);
+            d.prof_free.push_back(pr.second.second);
+        }
+        d.prof_pending.clear();
+        e->prof_chunks += d.prof_chunks;
+        d.prof_chunks = 0;
+    }
+    std::memset(out, 0, sizeof *out);
+    out->chunks = e->prof_chunks;
+    out->index_ms = e->prof_ms[0];
+    out->parse_ms = e->prof_ms[1];
+    out->call_ms = e->prof_ms[2];
+    out->hist_ms = e->prof_ms[3];
+    out->fmt_len_ms = e->prof_ms[4];
+    out->fmt_write_ms = e->prof_ms[5];
+    for (double& v : e->prof_ms) v = 0;
+    e->prof_chunks = 0;
+    return SID_OK;
 }
