@@ -13,8 +13,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sid_pow10.h"
 #include "sid_pow5.h"
 
+static __device__ const double sid_p10_d[SID_P10_MAX - SID_P10_MIN + 1] = SID_P10_INIT;
+static const double sid_p10_h[SID_P10_MAX - SID_P10_MIN + 1] = SID_P10_INIT;
 static __device__ const uint16_t sid_pow5_off_d[SID_POW5_MAX + 2] = SID_POW5_OFF_INIT;
 static __device__ const uint64_t sid_pow5_limb_d[SID_POW5_NLIMBS] = SID_POW5_LIMB_INIT;
 static const uint16_t sid_pow5_off_h[SID_POW5_MAX + 2] = SID_POW5_OFF_INIT;
@@ -68,10 +71,57 @@ __host__ __device__ inline uint64_t sid_scale10(uint64_t M, int E, int k, int& c
     return Q;
 }
 
+// Fast path of sid_dec6 for normal v: y = fl(v * fl(10^k)) is within
+// 2 * 2^-53 * y < 2.3e-10 of the exact v * 10^k (two roundings), so its
+// integer part and the side of one half its fraction lies on are exact unless
+// the fraction is within 2^-20 of one half, or y within 1e-3 of the 10^5 /
+// 10^6 ends of the 6-digit range -- those (a few in 10^6 values) and
+// denormals / k outside the table go to the exact multi-limb path.
+__host__ __device__ inline bool sid_dec6_fast(double v, int be, uint32_t& D, int& X)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double* p10 = sid_p10_d;
+#else
+    const double* p10 = sid_p10_h;
+#endif
+    if (be == 0) return false;
+    int x = ((be - 1023) * 78913) >> 18;   // floor(e2 * log10(2)): the exponent x or x - 1
+    int k = 5 - x;
+    if (k - 1 < SID_P10_MIN || k > SID_P10_MAX) return false;
+    double y = v * p10[k - SID_P10_MIN];
+    if (y >= 1e6) {
+        --k;
+        ++x;
+        y = v * p10[k - SID_P10_MIN];
+    }
+    if (!(y >= 100000.001) || !(y < 999999.999)) return false;
+    const uint32_t Q = (uint32_t)y;
+    const double f = y - (double)Q;   // exact (y < 2^20)
+    if (f > 0.5 - 0x1p-20 && f < 0.5 + 0x1p-20) return false;
+    D = Q + (f > 0.5 ? 1u : 0u);
+    X = x;
+    if (D == 1000000u) {
+        D = 100000u;
+        ++X;
+    }
+    return true;
+}
+
 // Six significant digits of v > 0 (finite): D in [100000, 999999], decimal
 // exponent X of the leading digit, rounded half-to-even.  false if v is out of
 // the supported range (v >= 2^63).
+__host__ __device__ __noinline__ bool sid_dec6_exact(double v, uint32_t& D, int& X);
+
 __host__ __device__ inline bool sid_dec6(double v, uint32_t& D, int& X)
+{
+    const uint64_t bits = __builtin_bit_cast(uint64_t, v);
+    const int be = (int)((bits >> 52) & 0x7ff);
+    if (be < 1023 + 63 && sid_dec6_fast(v, be, D, X)) return true;
+    return sid_dec6_exact(v, D, X);
+}
+
+// the exact multi-limb path (kept out of line: its limb array lives in scratch)
+__host__ __device__ __noinline__ bool sid_dec6_exact(double v, uint32_t& D, int& X)
 {
     const uint64_t bits = __builtin_bit_cast(uint64_t, v);
     const int be = (int)((bits >> 52) & 0x7ff);
@@ -130,50 +180,86 @@ __host__ __device__ inline bool sid_dec6(double v, uint32_t& D, int& X)
     return false;
 }
 
-// "%g" of v (precision 6) into p (>= SID_FMT_MAX bytes); returns the length,
-// or -1 if v is outside the supported range (|v| >= 2^63, never a confidence).
-__host__ __device__ inline int sid_fmt_g6(double v, char* p)
+// "%g" of v decomposed: the six digits D, the exponent X, the digits kept
+// after trailing zeros are stripped (nd), or a special form.
+enum { SID_G6_NUM = 0, SID_G6_NAN, SID_G6_INF, SID_G6_ZERO, SID_G6_ONE, SID_G6_RANGE };
+struct sid_g6 {
+    uint32_t D;
+    int X, nd, kind, neg;
+};
+
+__host__ __device__ inline sid_g6 sid_g6_prep(double v)
 {
     const uint64_t bits = __builtin_bit_cast(uint64_t, v);
     const uint64_t mag = bits & 0x7fffffffffffffffull;
-    int n = 0;
-    if (bits >> 63) p[n++] = '-';
-    if (mag > 0x7ff0000000000000ull) {
-        p[n++] = 'n';
-        p[n++] = 'a';
-        p[n++] = 'n';
-        return n;
-    }
-    if (mag == 0x7ff0000000000000ull) {
-        p[n++] = 'i';
-        p[n++] = 'n';
-        p[n++] = 'f';
-        return n;
-    }
-    if (mag == 0) {
-        p[n++] = '0';
-        return n;
-    }
-    if (mag == 0x3ff0000000000000ull) {   // 1: the most frequent confidence
-        p[n++] = '1';
-        return n;
-    }
-    uint32_t D;
-    int X;
-    if (!sid_dec6(__builtin_bit_cast(double, mag), D, X)) return -1;
-    char d[6];
-    for (int i = 5; i >= 0; --i) {
-        d[i] = (char)('0' + D % 10u);
-        D /= 10u;
-    }
-    int nd = 6;
-    while (nd > 1 && d[nd - 1] == '0') --nd;
-    if (X < -4 || X >= 6) {
-        p[n++] = d[0];
-        if (nd > 1) {
-            p[n++] = '.';
-            for (int i = 1; i < nd; ++i) p[n++] = d[i];
+    sid_g6 g{0, 0, 0, SID_G6_NUM, (int)(bits >> 63)};
+    if (mag > 0x7ff0000000000000ull) g.kind = SID_G6_NAN;
+    else if (mag == 0x7ff0000000000000ull) g.kind = SID_G6_INF;
+    else if (mag == 0) g.kind = SID_G6_ZERO;
+    else if (mag == 0x3ff0000000000000ull) g.kind = SID_G6_ONE;   // 1: the most frequent confidence
+    else if (!sid_dec6(__builtin_bit_cast(double, mag), g.D, g.X)) g.kind = SID_G6_RANGE;
+    else {
+        int nd = 6;
+        uint32_t d = g.D;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const bool z = nd > 1 && d % 10u == 0u && nd == 6 - i;
+            nd -= z ? 1 : 0;
+            d = z ? d / 10u : d;
         }
+        g.nd = nd;
+    }
+    return g;
+}
+
+// length of the "%g" text, -1 out of range
+__host__ __device__ inline int sid_g6_len(const sid_g6& g)
+{
+    switch (g.kind) {
+    case SID_G6_NAN:
+    case SID_G6_INF: return g.neg + 3;
+    case SID_G6_ZERO:
+    case SID_G6_ONE: return g.neg + 1;
+    case SID_G6_RANGE: return -1;
+    default: break;
+    }
+    const int X = g.X, nd = g.nd;
+    int n = g.neg;
+    if (X < -4 || X >= 6) n += (nd > 1 ? nd + 1 : 1) + 2 + ((X <= -100 || X >= 100) ? 3 : 2);
+    else if (X >= 0) n += X + 1 + (nd > X + 1 ? nd - X : 0);
+    else n += 2 + (-X - 1) + nd;
+    return n;
+}
+
+// digit i (0 = leading) of the six-digit D
+__host__ __device__ inline char sid_g6_digit(uint32_t D, int i)
+{
+    const uint32_t P[6] = {100000u, 10000u, 1000u, 100u, 10u, 1u};
+    return (char)('0' + (D / P[i]) % 10u);
+}
+
+// the text into p (any address space; no private arrays: every loop below is
+// unrolled with constant digit indices); returns the length, -1 out of range
+__host__ __device__ inline int sid_g6_put(const sid_g6& g, char* p)
+{
+    int n = 0;
+    if (g.neg) p[n++] = '-';
+    switch (g.kind) {
+    case SID_G6_NAN: p[n] = 'n', p[n + 1] = 'a', p[n + 2] = 'n'; return n + 3;
+    case SID_G6_INF: p[n] = 'i', p[n + 1] = 'n', p[n + 2] = 'f'; return n + 3;
+    case SID_G6_ZERO: p[n] = '0'; return n + 1;
+    case SID_G6_ONE: p[n] = '1'; return n + 1;
+    case SID_G6_RANGE: return -1;
+    default: break;
+    }
+    const int X = g.X, nd = g.nd;
+    const uint32_t D = g.D;
+    if (X < -4 || X >= 6) {
+        p[n++] = sid_g6_digit(D, 0);
+        if (nd > 1) p[n++] = '.';
+#pragma unroll
+        for (int i = 1; i < 6; ++i)
+            if (i < nd) p[n++] = sid_g6_digit(D, i);
         p[n++] = 'e';
         p[n++] = X < 0 ? '-' : '+';
         int ax = X < 0 ? -X : X;
@@ -184,35 +270,53 @@ __host__ __device__ inline int sid_fmt_g6(double v, char* p)
         p[n++] = (char)('0' + ax / 10);
         p[n++] = (char)('0' + ax % 10);
     } else if (X >= 0) {
-        for (int i = 0; i <= X; ++i) p[n++] = d[i];
-        if (nd > X + 1) {
-            p[n++] = '.';
-            for (int i = X + 1; i < nd; ++i) p[n++] = d[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (i <= X || i < nd) {
+                if (i == X + 1) p[n++] = '.';
+                p[n++] = sid_g6_digit(D, i);
+            }
         }
     } else {
         p[n++] = '0';
         p[n++] = '.';
-        for (int i = 0; i < -X - 1; ++i) p[n++] = '0';
-        for (int i = 0; i < nd; ++i) p[n++] = d[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (i < -X - 1) p[n++] = '0';
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+            if (i < nd) p[n++] = sid_g6_digit(D, i);
     }
     return n;
 }
 
-// decimal of an int32 (std::to_chars / operator<<(int)); returns the length
+// "%g" of v (precision 6) into p (>= SID_FMT_MAX bytes); returns the length,
+// or -1 if v is outside the supported range (|v| >= 2^63, never a confidence).
+__host__ __device__ inline int sid_fmt_g6(double v, char* p) { return sid_g6_put(sid_g6_prep(v), p); }
+
+// decimal of an int32 (std::to_chars / operator<<(int)): its length, and the
+// text into p (any address space, no private arrays)
+__host__ __device__ inline int sid_i32_len(int32_t v)
+{
+    uint32_t u = v < 0 ? 0u - (uint32_t)v : (uint32_t)v;
+    int n = v < 0 ? 2 : 1;
+    const uint32_t P[9] = {10u, 100u, 1000u, 10000u, 100000u, 1000000u, 10000000u, 100000000u, 1000000000u};
+#pragma unroll
+    for (int i = 0; i < 9; ++i) n += u >= P[i] ? 1 : 0;
+    return n;
+}
+
 __host__ __device__ inline int sid_fmt_i32(int32_t v, char* p)
 {
-    int n = 0;
-    uint32_t u = (uint32_t)v;
-    if (v < 0) {
-        p[n++] = '-';
-        u = 0u - u;
+    const int n = sid_i32_len(v);
+    uint32_t u = v < 0 ? 0u - (uint32_t)v : (uint32_t)v;
+    if (v < 0) p[0] = '-';
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        if (k < n - (v < 0 ? 1 : 0)) {
+            p[n - 1 - k] = (char)('0' + u % 10u);
+            u /= 10u;
+        }
     }
-    char t[10];
-    int m = 0;
-    do {
-        t[m++] = (char)('0' + u % 10u);
-        u /= 10u;
-    } while (u);
-    while (m) p[n++] = t[--m];
     return n;
 }

@@ -97,6 +97,8 @@ struct sid_chunk_ws {
     uint64_t site_cap = 0, tile_cap = 0;
     uint64_t* starts = nullptr;   // line start offsets (relative to the chunk's base)
     uint64_t* counts = nullptr;   // profile_t per site
+    uint64_t* hdr = nullptr;      // chrom / position per site for the formatter
+    uint32_t* fb = nullptr;       // lines for the general parse routine (count in state[6])
     uint8_t* code = nullptr;
     double* hom = nullptr;
     double* het = nullptr;

@@ -372,11 +372,241 @@ __device__ int atoi_like(Reader& R, uint64_t b, uint64_t e)
 // branches on the class.
 enum : uint32_t { K_IGN = 0, K_A = 1, K_C = 2, K_G = 3, K_T = 4, K_CARET = 5, K_INDEL = 6 };
 
+// The per-byte walk: the general routine, for every line the fast path below
+// does not take (indels, '^' runs, a '\n'/NUL or an over-long header before
+// token 4, a ref whose '.'/',' class is '^'/'+'/'-', malformed lines) and for
+// the quality-mode validation of tokens 5 and 6.
+__device__ __noinline__ void parse_line_serial(const char* __restrict__ text, uint64_t len, uint64_t s0,
+                                               const uint8_t* cls, uint64_t* out,
+                                               unsigned long long* __restrict__ err, int qmode)
+{
+    Reader R{text, len};
+    int nt = 0;              // tokens started
+    bool in_tok = false;
+    uint64_t tb2 = 0, te2 = 0;
+    uint32_t cdot = 0, ccomma = 0;
+    uint32_t nA = 0, nC = 0, nG = 0, nT = 0;
+    uint64_t skip = 0;       // bytes of token 4 still to skip
+    int ind = 0;             // 1: after '+'/'-'; 2: in its number
+    uint64_t num = 0;
+    bool ovf = false;
+    for (uint64_t q = s0; q < len; ++q) {
+        const uint32_t c = R.at(q);
+        if (c == '\n' || c == 0) break;   // end of the line / of the C string
+        const bool sep = c == ' ' || c == '\t';
+        if (!in_tok) {
+            if (sep) continue;
+            in_tok = true;
+            ++nt;
+            if (nt == 7) break;                // quality mode: both quality fields exist
+            if (nt == 3) tb2 = q;
+            if (nt == 5) {   // token 2 is complete: the '.'/',' classes
+                const uint32_t ref = R.at(tb2);
+                const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
+                const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
+                cdot = cls[up];
+                ccomma = cls[lw];
+            }
+        } else if (sep) {
+            in_tok = false;
+            if (nt == 3) te2 = q;
+            if (nt == 5 && !qmode) break;  // token 4 done: the rest is never read
+            continue;
+        }
+        if (nt != 5) continue;
+        // ---- a byte of the read-bases token
+        if (ind == 1) {   // byte after '+'/'-'
+            ind = 0;
+            if (c >= '0' && c <= '9') {
+                ind = 2;
+                num = c - '0';
+                ovf = false;
+                continue;
+            }
+        } else if (ind == 2) {
+            if (c >= '0' && c <= '9') {
+                const unsigned d = c - '0';
+                if (!ovf) {
+                    if (num > ((unsigned long long)LONG_MAX - d) / 10) ovf = true;
+                    else num = num * 10 + d;
+                }
+                continue;
+            }
+            ind = 0;
+            skip = ovf ? (uint64_t)LONG_MAX : num;   // this byte is the first skipped
+        }
+        if (skip) {
+            --skip;
+            continue;
+        }
+        const uint32_t k = c == '.' ? cdot : (c == ',' ? ccomma : cls[c]);
+        nA += k == K_A;
+        nC += k == K_C;
+        nG += k == K_G;
+        nT += k == K_T;
+        if (k == K_CARET) skip = 1;
+        else if (k == K_INDEL) ind = 1;
+    }
+    if (in_tok && nt == 3) te2 = ~0ull;   // token 2 ran to the end: length checked below
+    int code = SID_OK;
+    if (nt < 1) code = SID_ENULLCHROM;
+    else if (nt < 3) code = SID_EMALFORMED;
+    else {
+        // token 2 length: its end is te2, or (if the line ended inside it) the
+        // first '\n'/NUL/end after tb2
+        uint64_t e2 = te2;
+        if (e2 == 0 || e2 == ~0ull) {
+            e2 = tb2;
+            while (e2 < len) {
+                const uint32_t c = R.at(e2);
+                if (c == '\n' || c == 0 || c == ' ' || c == '\t') break;
+                ++e2;
+            }
+        }
+        if (e2 - tb2 != 1 || nt < 5) code = SID_EMALFORMED;
+        // readFile(in, true, true) (call.cpp:292): parseQualities(NULL) on a
+        // missing 6th field (SIGSEGV), then the mapping-quality check
+        else if (qmode && nt == 5) code = SID_ENOBQ;
+        else if (qmode && nt == 6) code = SID_EMISSING_MQ;
+    }
+    if (code != SID_OK) {   // first in file order: min(offset * 8 + kind)
+        const uint32_t kind = code == SID_EMALFORMED ? 1u : code == SID_ENULLCHROM ? 2u
+                            : code == SID_EMISSING_MQ ? 3u : 4u;
+        atomicMin(err, (unsigned long long)(s0 * 8 + kind));
+        *out = 0;
+        return;
+    }
+    *out = (uint64_t)(uint16_t)nA | ((uint64_t)(uint16_t)nC << 16) | ((uint64_t)(uint16_t)nG << 32) |
+                ((uint64_t)(uint16_t)nT << 48);
+}
+
+// ---- SWAR helpers: bit 7 of each byte of the result flags a byte of w
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x)
+{
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t k4) { return zero_bytes(w ^ k4); }
+// bytes < 0x21: the separators, '\n', NUL (and other control bytes)
+__device__ __forceinline__ uint32_t low_bytes(uint32_t w)
+{
+    return ~(((w & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | w) & 0x80808080u;
+}
+
+// The fast path of one line (pileup.cpp:13-46 + :70-153 for the lines that
+// need none of the general routine's cases): the header (tokens 0-3) byte by
+// byte, then the read-bases token 4 bytes at a time with SWAR byte tests:
+//   A/C/G/T either case     -> their counters (w | 0x20 folds the case)
+//   '.' / ','               -> one "matches ref" counter, added to the ref's
+//                              class at the end (toupper/tolower(ref) have the
+//                              same class for a base)
+//   '^'                     -> the next byte is skipped; a '^' that is itself
+//                              skipped (a '^' run) sends the line to the
+//                              general routine, as does a counted '+'/'-'
+//   ' ', '\t', '\n', NUL  -> end of the token (the rest of the line is never
+//                              read, as in the per-byte walk)
+// Returns false when the line needs the general routine.
+__device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, uint64_t len, uint64_t s0,
+                                                const uint8_t* cls, uint64_t* out, uint64_t* hdr)
+{
+    Reader R{text, len};
+    uint64_t q = s0, t2 = 0, tb0 = 0;
+    int nt = 0;
+    uint32_t l2 = 0, l0 = 0, pos = 0, pdig = 0;
+    bool in = false, pos_ok = true;
+    for (;;) {   // tokens 0-3 and the first byte of token 4
+        if (q >= len || q - s0 > 255) return false;
+        const uint32_t c = R.at(q);
+        if (c == '\n' || c == 0) return false;
+        const bool sep = c == ' ' || c == '\t';
+        if (!sep && !in) {
+            ++nt;
+            if (nt == 1) tb0 = q;
+            if (nt == 3) t2 = q;
+            if (nt == 5) break;
+        }
+        if (!sep) {
+            const uint32_t d = c - '0';
+            l0 += nt == 1;
+            l2 += nt == 3;
+            if (nt == 2) {   // the position: plain decimal digits are atoi's value
+                pos_ok = pos_ok && d < 10u;
+                pos = pos * 10u + d;
+                ++pdig;
+            }
+        }
+        in = !sep;
+        ++q;
+    }
+    // chrom (offset, length) and position for the formatter (bit 63: valid)
+    *hdr = (pos_ok && pdig <= 9) ? (1ull << 63) | ((tb0 - s0) << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
+    if (l2 != 1) return false;   // malformed: the general routine reports it
+    const uint32_t ref = R.at(t2);
+    const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
+    const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
+    const uint32_t kd = cls[up], kc = cls[lw];
+    if (kd >= K_CARET || kc >= K_CARET || kd != kc) return false;
+    // token 4 from q, in aligned 16-B windows
+    uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
+    uint64_t a = q & ~(uint64_t)15;
+    uint32_t lead = (uint32_t)(q & 15);   // bytes of the first window before the token
+    uint32_t carry = 0;                   // bit 7: byte 0 of the next word is skipped
+    bool done = false;
+    while (!done) {
+        const uint4 v = *(const uint4*)(text + a);
+        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+        const uint64_t room = len > a ? len - a : 0;   // bytes of this window inside the text
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w = ws[k];
+            // bytes of this word inside [q, len) and not after the token's end
+            uint32_t vm = 0x80808080u;
+            const int b0 = 4 * k;
+            if ((int)lead > b0) vm &= lead - b0 >= 4 ? 0u : (0x80808080u << (8 * (lead - b0)));
+            if (room < (uint64_t)(b0 + 4)) vm &= room <= (uint64_t)b0 ? 0u : (0x80808080u >> (8 * (b0 + 4 - room)));
+            if (done) vm = 0;
+            const uint32_t lo = low_bytes(w) & vm;
+            if (lo) {
+                const uint32_t term = (eq_bytes(w, 0x20202020u) | eq_bytes(w, 0x09090909u) |
+                                       eq_bytes(w, 0x0A0A0A0Au) | zero_bytes(w)) & vm;
+                if (term) {
+                    vm &= (term & (0u - term)) - 1u;   // bytes before the first terminator
+                    done = true;
+                }
+            }
+            if (room < (uint64_t)(b0 + 4)) done = true;   // end of the text
+            const uint32_t caret = eq_bytes(w, 0x5E5E5E5Eu) & vm;
+            const uint32_t skip = ((caret << 8) | carry) & vm;
+            if (caret & skip) return false;   // '^' run
+            carry = caret >> 24;              // bit 31 -> bit 7
+            const uint32_t cm = vm & ~skip;
+            if ((eq_bytes(w, 0x2B2B2B2Bu) | eq_bytes(w, 0x2D2D2D2Du)) & cm) return false;   // indel
+            const uint32_t f = w | 0x20202020u;
+            nA += __popc(eq_bytes(f, 0x61616161u) & cm);
+            nC += __popc(eq_bytes(f, 0x63636363u) & cm);
+            nG += __popc(eq_bytes(f, 0x67676767u) & cm);
+            nT += __popc(eq_bytes(f, 0x74747474u) & cm);
+            nM += __popc(eq_bytes(w | 0x02020202u, 0x2E2E2E2Eu) & cm);
+        }
+        lead = 0;
+        a += 16;
+    }
+    nA += kd == K_A ? nM : 0;
+    nC += kd == K_C ? nM : 0;
+    nG += kd == K_G ? nM : 0;
+    nT += kd == K_T ? nM : 0;
+    *out = (uint64_t)(uint16_t)nA | ((uint64_t)(uint16_t)nC << 16) | ((uint64_t)(uint16_t)nG << 32) |
+           ((uint64_t)(uint16_t)nT << 48);
+    return true;
+}
+
+// Pass 1: the fast path over every line; a line it cannot take is appended to
+// the fallback list fb (count in *fbn).  Pass 2 (sid_parse_serial_kernel):
+// the general routine over that list -- or over every line, for -m quality.
 __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ text, uint64_t len,
                                                        const uint64_t* __restrict__ starts,
                                                        const uint64_t* __restrict__ range,   // [lo, hi)
-                                                       uint64_t* __restrict__ counts,
-                                                       unsigned long long* __restrict__ err, int qmode)
+                                                       uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
+                                                       uint32_t* __restrict__ fb, unsigned long long* fbn)
 {
     __shared__ uint8_t cls[256];
     if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
@@ -384,178 +614,136 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
     const uint64_t lo = range[0], hi = range[1];
     for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        Reader R{text, len};
-        const uint64_t s0 = starts[i];
-        int nt = 0;              // tokens started
-        bool in_tok = false;
-        uint64_t tb2 = 0, te2 = 0;
-        uint32_t cdot = 0, ccomma = 0;
-        uint32_t nA = 0, nC = 0, nG = 0, nT = 0;
-        uint64_t skip = 0;       // bytes of token 4 still to skip
-        int ind = 0;             // 1: after '+'/'-'; 2: in its number
-        uint64_t num = 0;
-        bool ovf = false;
-        for (uint64_t q = s0; q < len; ++q) {
-            const uint32_t c = R.at(q);
-            if (c == '\n' || c == 0) break;   // end of the line / of the C string
-            const bool sep = c == ' ' || c == '\t';
-            if (!in_tok) {
-                if (sep) continue;
-                in_tok = true;
-                ++nt;
-                if (nt == 7) break;                // quality mode: both quality fields exist
-                if (nt == 3) tb2 = q;
-                if (nt == 5) {   // token 2 is complete: the '.'/',' classes
-                    const uint32_t ref = R.at(tb2);
-                    const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
-                    const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
-                    cdot = cls[up];
-                    ccomma = cls[lw];
-                }
-            } else if (sep) {
-                in_tok = false;
-                if (nt == 3) te2 = q;
-                if (nt == 5 && !qmode) break;  // token 4 done: the rest is never read
-                continue;
-            }
-            if (nt != 5) continue;
-            // ---- a byte of the read-bases token
-            if (ind == 1) {   // byte after '+'/'-'
-                ind = 0;
-                if (c >= '0' && c <= '9') {
-                    ind = 2;
-                    num = c - '0';
-                    ovf = false;
-                    continue;
-                }
-            } else if (ind == 2) {
-                if (c >= '0' && c <= '9') {
-                    const unsigned d = c - '0';
-                    if (!ovf) {
-                        if (num > ((unsigned long long)LONG_MAX - d) / 10) ovf = true;
-                        else num = num * 10 + d;
-                    }
-                    continue;
-                }
-                ind = 0;
-                skip = ovf ? (uint64_t)LONG_MAX : num;   // this byte is the first skipped
-            }
-            if (skip) {
-                --skip;
-                continue;
-            }
-            const uint32_t k = c == '.' ? cdot : (c == ',' ? ccomma : cls[c]);
-            nA += k == K_A;
-            nC += k == K_C;
-            nG += k == K_G;
-            nT += k == K_T;
-            if (k == K_CARET) skip = 1;
-            else if (k == K_INDEL) ind = 1;
+        uint64_t c = 0, h = 0;
+        if (parse_line_fast(text, len, starts[i], cls, &c, &h)) {
+            counts[i] = c;
+            hdr[i] = h;
+        } else {
+            fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
         }
-        if (in_tok && nt == 3) te2 = ~0ull;   // token 2 ran to the end: length checked below
-        int code = SID_OK;
-        if (nt < 1) code = SID_ENULLCHROM;
-        else if (nt < 3) code = SID_EMALFORMED;
-        else {
-            // token 2 length: its end is te2, or (if the line ended inside it) the
-            // first '\n'/NUL/end after tb2
-            uint64_t e2 = te2;
-            if (e2 == 0 || e2 == ~0ull) {
-                e2 = tb2;
-                while (e2 < len) {
-                    const uint32_t c = R.at(e2);
-                    if (c == '\n' || c == 0 || c == ' ' || c == '\t') break;
-                    ++e2;
-                }
-            }
-            if (e2 - tb2 != 1 || nt < 5) code = SID_EMALFORMED;
-            // readFile(in, true, true) (call.cpp:292): parseQualities(NULL) on a
-            // missing 6th field (SIGSEGV), then the mapping-quality check
-            else if (qmode && nt == 5) code = SID_ENOBQ;
-            else if (qmode && nt == 6) code = SID_EMISSING_MQ;
-        }
-        if (code != SID_OK) {   // first in file order: min(offset * 8 + kind)
-            const uint32_t kind = code == SID_EMALFORMED ? 1u : code == SID_ENULLCHROM ? 2u
-                                : code == SID_EMISSING_MQ ? 3u : 4u;
-            atomicMin(err, (unsigned long long)(s0 * 8 + kind));
-            counts[i] = 0;
-            continue;
-        }
-        counts[i] = (uint64_t)(uint16_t)nA | ((uint64_t)(uint16_t)nC << 16) | ((uint64_t)(uint16_t)nG << 32) |
-                    ((uint64_t)(uint16_t)nT << 48);
     }
+}
+
+__global__ __launch_bounds__(TB) void sid_parse_serial_kernel(const char* __restrict__ text, uint64_t len,
+                                                              const uint64_t* __restrict__ starts,
+                                                              const uint64_t* __restrict__ range,
+                                                              uint64_t* __restrict__ counts,
+                                                              uint64_t* __restrict__ hdr,
+                                                              const uint32_t* __restrict__ fb,
+                                                              const unsigned long long* fbn,
+                                                              unsigned long long* __restrict__ err, int qmode)
+{
+    __shared__ uint8_t cls[256];
+    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    __syncthreads();
+    const uint64_t lo = range[0];
+    const uint64_t m = fb ? *fbn : range[1] - lo;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = lo + (fb ? fb[k] : k);
+        uint64_t c = 0;
+        parse_line_serial(text, len, starts[i], cls, &c, err, qmode);
+        counts[i] = c;
+        hdr[i] = 0;   // the formatter tokenises these lines itself
+    }
+}
+
+// the two passes over sites [range[0], range[1]) (the range lives on the device)
+static void launch_parse(const char* text, uint64_t len, const uint64_t* starts, const uint64_t* range, uint64_t n,
+                         uint64_t* counts, uint64_t* hdr, uint32_t* fb, unsigned long long* fbn,
+                         unsigned long long* err, int qmode, hipStream_t st)
+{
+    const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + TB - 1) / TB, 1), 16384);
+    if (qmode) {
+        sid_parse_serial_kernel<<<pg, TB, 0, st>>>(text, len, starts, range, counts, hdr, nullptr, nullptr, err, 1);
+        return;
+    }
+    (void)hipMemsetAsync(fbn, 0, sizeof *fbn, st);
+    sid_parse_kernel<<<pg, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn);
+    sid_parse_serial_kernel<<<256, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, err, 0);
 }
 
 // ---------------------------------------------------------------- format --
-struct Rec {
-    uint64_t cb, ce;   // chrom token
-    int32_t pos;
-    bool skip;
-    int len;
-};
-
-// the record of site i (call.hpp:29-38); writes it to out when out != null
-__device__ __forceinline__ int record(Reader& R, uint64_t start, uint8_t c, double h, double t,
-                                      const char* ctype, int tlen, char* out)
-{
-    if (c & 0x40) return 0;   // filtered profile: no record (call.cpp:131-140)
-    // a parsed line has >= 5 tokens before any NUL or newline, so its first
-    // two tokens are plain separator-delimited runs.  The scan also stops at a
-    // newline or NUL: the streaming engine formats a chunk before it knows
-    // whether one of its lines is malformed (it then discards the records),
-    // and such a line must not send the scan past its end
-    uint64_t tb[2], te[2];
-    uint64_t q = start;
-    for (int k = 0; k < 2; ++k) {
-        while (is_sep(R.at(q))) ++q;
-        tb[k] = q;
-        for (uint32_t ch = R.at(q); !is_sep(ch) && ch != '\n' && ch != 0; ch = R.at(++q)) {
-        }
-        te[k] = q;
-    }
-    const int32_t pos = atoi_like(R, tb[1], te[1]);
-    char buf[64];
-    int n = 0;
-    const int clen = (int)(te[0] - tb[0]);
-    if (out) {
-        for (int k = 0; k < clen; ++k) out[k] = (char)R.at(tb[0] + k);
-        out += clen;
-    }
-    n += clen;
-    buf[0] = ',';
-    int m = 1;
-    m += sid_fmt_i32(pos, buf + m);
-    buf[m++] = ',';
-    const bool het = c & 0x80;
-    buf[m++] = 'h';
-    buf[m++] = het ? 'e' : 'o';
-    buf[m++] = het ? 't' : 'm';
-    buf[m++] = ',';
-    buf[m++] = "ACGT"[c & 3];
-    buf[m++] = "ACGT"[(c >> 2) & 3];
-    buf[m++] = ',';
-    const int a = sid_fmt_g6(h, buf + m);
-    m += a < 0 ? 0 : a;
-    buf[m++] = ',';
-    const int b = sid_fmt_g6(t, buf + m);
-    m += b < 0 ? 0 : b;
-    buf[m++] = ',';
-    if (out) {
-        for (int k = 0; k < m; ++k) out[k] = buf[k];
-        out += m;
-        for (int k = 0; k < tlen; ++k) out[k] = ctype[k];
-        out[tlen] = '\n';
-    }
-    return (a < 0 || b < 0) ? -1 : n + m + tlen + 1;
-}
-
 struct CType {
     char s[16];
     int len;
 };
 
+// chrom token [cb, cb + clen) and position of the site whose line starts at
+// `start`: from the parse's header word when it is valid, else tokenised here
+// (a parsed line has >= 5 tokens before any NUL or newline, so its first two
+// tokens are plain separator-delimited runs; the scan also stops at a newline
+// or NUL: the streaming engine formats a chunk before it knows whether one of
+// its lines is malformed -- it then discards the records -- and such a line
+// must not send the scan past its end)
+struct Head {
+    uint64_t cb;
+    uint32_t clen;
+    int32_t pos;
+};
+
+__device__ __forceinline__ Head site_head(Reader& R, uint64_t start, uint64_t hdr)
+{
+    Head h;
+    if (hdr >> 63) {
+        h.cb = start + ((hdr >> 44) & 0x7FFFFull);
+        h.clen = (uint32_t)(hdr >> 32) & 0xFFFu;
+        h.pos = (int32_t)(uint32_t)hdr;
+        return h;
+    }
+    uint64_t q = start;
+    while (is_sep(R.at(q))) ++q;
+    h.cb = q;
+    for (uint32_t ch = R.at(q); !is_sep(ch) && ch != '\n' && ch != 0; ch = R.at(++q)) {
+    }
+    h.clen = (uint32_t)(q - h.cb);
+    while (is_sep(R.at(q))) ++q;
+    const uint64_t pb = q;
+    for (uint32_t ch = R.at(q); !is_sep(ch) && ch != '\n' && ch != 0; ch = R.at(++q)) {
+    }
+    h.pos = atoi_like(R, pb, q);
+    return h;
+}
+
+// record length of a site (call.hpp:29-38): 0 for a filtered profile (no
+// record, call.cpp:131-140), -1 for a confidence outside the formatter's range
+__device__ __forceinline__ int record_len(const Head& h, uint8_t c, const sid_g6& gh, const sid_g6& gt, int tlen)
+{
+    if (c & 0x40) return 0;
+    const int a = sid_g6_len(gh), b = sid_g6_len(gt);
+    if (a < 0 || b < 0) return -1;
+    // chrom , pos , hom|het , XY , hom_conf , het_conf , conf_type \n
+    return (int)h.clen + 1 + sid_i32_len(h.pos) + 1 + 3 + 1 + 2 + 1 + a + 1 + b + 1 + tlen + 1;
+}
+
+__device__ __forceinline__ void record_put(Reader& R, const Head& h, uint8_t c, const sid_g6& gh, const sid_g6& gt,
+                                           const CType& ct, char* out)
+{
+    for (uint32_t k = 0; k < h.clen; ++k) out[k] = (char)R.at(h.cb + k);
+    int n = (int)h.clen;
+    out[n++] = ',';
+    n += sid_fmt_i32(h.pos, out + n);
+    out[n++] = ',';
+    const bool het = c & 0x80;
+    out[n++] = 'h';
+    out[n++] = het ? 'e' : 'o';
+    out[n++] = het ? 't' : 'm';
+    out[n++] = ',';
+    out[n++] = "ACGT"[c & 3];
+    out[n++] = "ACGT"[(c >> 2) & 3];
+    out[n++] = ',';
+    n += sid_g6_put(gh, out + n);
+    out[n++] = ',';
+    n += sid_g6_put(gt, out + n);
+    out[n++] = ',';
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < ct.len) out[n + k] = ct.s[k];
+    out[n + ct.len] = '\n';
+}
+
 __global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict__ text, uint64_t len,
-                                                         const uint64_t* __restrict__ starts, uint64_t s0,
+                                                         const uint64_t* __restrict__ starts,
+                                                         const uint64_t* __restrict__ hdr, uint64_t s0,
                                                          uint64_t s1, const uint8_t* __restrict__ code,
                                                          const double* __restrict__ hom,
                                                          const double* __restrict__ het, CType ct,
@@ -564,11 +752,15 @@ __global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict_
     const uint64_t i = s0 + (uint64_t)blockIdx.x * TB + threadIdx.x;
     int l = 0;
     if (i < s1) {
-        Reader R{text, len};
-        l = record(R, starts[i], code[i], hom[i], het[i], ct.s, ct.len, nullptr);
-        if (l < 0) {
-            atomicExch(bad, 1);
-            l = 0;
+        const uint8_t c = code[i];
+        if (!(c & 0x40)) {
+            Reader R{text, len};
+            const Head h = site_head(R, starts[i], hdr ? hdr[i] : 0);
+            l = record_len(h, c, sid_g6_prep(hom[i]), sid_g6_prep(het[i]), ct.len);
+            if (l < 0) {
+                atomicExch(bad, 1);
+                l = 0;
+            }
         }
     }
     uint32_t tot;
@@ -579,7 +771,8 @@ __global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict_
 constexpr int FMT_LDS = 24 * 1024;
 
 __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restrict__ text, uint64_t len,
-                                                           const uint64_t* __restrict__ starts, uint64_t s0,
+                                                           const uint64_t* __restrict__ starts,
+                                                           const uint64_t* __restrict__ hdr, uint64_t s0,
                                                            uint64_t s1, const uint8_t* __restrict__ code,
                                                            const double* __restrict__ hom,
                                                            const double* __restrict__ het, CType ct,
@@ -591,26 +784,28 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
     Reader R{text, len};
     int l = 0;
     uint8_t c = 0x40;
-    double h = 0, t = 0;
-    uint64_t st = 0;
+    Head h{0, 0, 0};
+    sid_g6 gh{}, gt{};
     if (i < s1) {
-        st = starts[i];
         c = code[i];
-        h = hom[i];
-        t = het[i];
-        l = record(R, st, c, h, t, ct.s, ct.len, nullptr);
-        if (l < 0) l = 0;
+        if (!(c & 0x40)) {
+            h = site_head(R, starts[i], hdr ? hdr[i] : 0);
+            gh = sid_g6_prep(hom[i]);
+            gt = sid_g6_prep(het[i]);
+            l = record_len(h, c, gh, gt, ct.len);
+            if (l < 0) l = 0;
+        }
     }
     uint32_t tot;
     const uint32_t my = block_exscan((uint32_t)l, &tot);
     const uint64_t base = boff[blockIdx.x] - out0;   // offset of this block in `out`
     if (tot > FMT_LDS) {   // long records (long chromosome names): straight to global
-        if (l) record(R, st, c, h, t, ct.s, ct.len, out + base + my);
+        if (l) record_put(R, h, c, gh, gt, ct, out + base + my);
         return;
     }
     // assemble in LDS at the same 16-B phase as the destination, then 16-B stores
     const uint32_t phase = (uint32_t)((uintptr_t)(out + base) & 15u);
-    if (l) record(R, st, c, h, t, ct.s, ct.len, buf + phase + my);
+    if (l) record_put(R, h, c, gh, gt, ct, buf + phase + my);
     __syncthreads();
     char* dst = out + base - phase;   // 16-B aligned
     const uint32_t span = phase + tot;
@@ -846,8 +1041,10 @@ struct sid_dtext {
     uint64_t len = 0;
     uint64_t* d_starts = nullptr;
     uint64_t* d_counts = nullptr;
+    uint64_t* d_hdr = nullptr;     // chrom / position per site for the formatter (sid_parse_kernel)
+    uint32_t* d_fb = nullptr;      // lines for the general parse routine
     uint64_t nsites = 0;
-    uint64_t* d_state = nullptr;   // [0] running site count, [1..2] chunk range
+    uint64_t* d_state = nullptr;   // [0] running site count, [1..2] chunk range, [3] fallback lines
     unsigned long long* d_err = nullptr;
     uint32_t* d_tcnt = nullptr;
     uint64_t* d_toff = nullptr;
@@ -864,6 +1061,8 @@ extern "C" int sid_dtext_free(sid_dtext* t)
 {
     if (!t) return SID_OK;
     (void)hipSetDevice(t->device);
+    for (void* p : {(void*)t->d_hdr, (void*)t->d_fb})
+        if (p) (void)hipFree(p);
     for (void* p : {(void*)t->d_text, (void*)t->d_starts, (void*)t->d_counts, (void*)t->d_state, (void*)t->d_err,
                     (void*)t->d_tcnt, (void*)t->d_toff})
         if (p) (void)hipFree(p);
@@ -917,12 +1116,12 @@ static int dtext_index_parse(sid_dtext* T, hipStream_t st, uint64_t* err_offset)
         return sid_set_hip_error(e);
     T->nsites = total;
     const size_t m = std::max<uint64_t>(total, 1);
-    if ((e = hipMalloc(&T->d_starts, m * 8)) != hipSuccess || (e = hipMalloc(&T->d_counts, m * 8)) != hipSuccess)
+    if ((e = hipMalloc(&T->d_starts, m * 8)) != hipSuccess || (e = hipMalloc(&T->d_counts, m * 8)) != hipSuccess ||
+        (e = hipMalloc(&T->d_hdr, m * 8)) != hipSuccess || (e = hipMalloc(&T->d_fb, m * 4)) != hipSuccess)
         return sid_set_hip_error(e);
     sid_lines_emit_kernel<<<(unsigned)tiles, TB, 0, st>>>(T->d_text, 0, 0, len, T->d_toff, T->d_starts);
-    const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((total + TB - 1) / TB, 1), 16384);
-    sid_parse_kernel<<<pg, TB, 0, st>>>(T->d_text, len, T->d_starts, T->d_state + 1, T->d_counts, T->d_err,
-                                        T->quality);
+    launch_parse(T->d_text, len, T->d_starts, T->d_state + 1, total, T->d_counts, T->d_hdr, T->d_fb,
+                 (unsigned long long*)(T->d_state + 3), T->d_err, T->quality, st);
     if ((e = hipGetLastError()) != hipSuccess) return sid_set_hip_error(e);
     unsigned long long ek = ~0ull;
     if ((e = hipMemcpyAsync(&ek, T->d_err, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
@@ -1128,7 +1327,7 @@ extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, 
     if (rc == SID_OK && nb) {
         hip(hipMemsetAsync(d_bad, 0, 4, st));
         hip(hipMemsetAsync(d_base, 0, 8, st));
-        sid_fmt_len_kernel<<<(unsigned)nb, TB, 0, st>>>(T->d_text, T->len, T->d_starts, begin, end, d_code, d_hom,
+        sid_fmt_len_kernel<<<(unsigned)nb, TB, 0, st>>>(T->d_text, T->len, T->d_starts, T->d_hdr, begin, end, d_code, d_hom,
                                                         d_het, ct, d_bsum, d_bad);
         launch_scan(d_bsum, nb, d_boff, d_base, nullptr,
                     (uint64_t*)((char*)d_bsum + ((std::max<size_t>(nb, 1) * 4 + 7) & ~(size_t)7)), st);
@@ -1165,7 +1364,7 @@ extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, 
         const uint64_t bytes = boff[b1] - boff[b0];
         flush(k);   // buffer k is about to be reused
         if (rc != SID_OK) break;
-        sid_fmt_write_kernel<<<(unsigned)(b1 - b0), TB, 0, st>>>(T->d_text, T->len, T->d_starts, s0, s1, d_code, d_hom,
+        sid_fmt_write_kernel<<<(unsigned)(b1 - b0), TB, 0, st>>>(T->d_text, T->len, T->d_starts, T->d_hdr, s0, s1, d_code, d_hom,
                                                                  d_het, ct, d_boff + b0, boff[b0], d_out[k]);
         if (!hip(hipGetLastError())) break;
         hip(hipEventRecord(written, st));
@@ -1197,8 +1396,10 @@ extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, 
 extern "C" int sid_format_g6(double v, char* buf, size_t cap)
 {
     char tmp[SID_FMT_MAX];
-    const int n = sid_fmt_g6(v, tmp);
+    const sid_g6 g = sid_g6_prep(v);
+    const int n = sid_g6_put(g, tmp);
     if (n < 0) return -SID_ERANGE;
+    if (sid_g6_len(g) != n) return -SID_EINVAL;   // the length pass must agree with the writer
     if (!buf || cap < (size_t)n + 1) return -(n + 1);
     std::memcpy(buf, tmp, n);
     buf[n] = '\0';
@@ -1345,9 +1546,10 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
     if (sites > W->site_cap) {
         const uint64_t m = std::max<uint64_t>(sites, W->site_cap + W->site_cap / 2);
         for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
-                        (void*)W->bsum, (void*)W->boff})
+                        (void*)W->bsum, (void*)W->boff, (void*)W->hdr, (void*)W->fb})
             if (p) (void)hipFree(p);
-        W->starts = W->counts = nullptr;
+        W->starts = W->counts = W->hdr = nullptr;
+        W->fb = nullptr;
         W->code = nullptr;
         W->hom = W->het = nullptr;
         W->bsum = nullptr;
@@ -1356,6 +1558,8 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         const uint64_t nb = (m + TB - 1) / TB + 1;
         WCHECK(hipMalloc(&W->starts, m * 8));
         WCHECK(hipMalloc(&W->counts, m * 8));
+        WCHECK(hipMalloc(&W->hdr, m * 8));
+        WCHECK(hipMalloc(&W->fb, m * 4));
         WCHECK(hipMalloc(&W->code, m));
         WCHECK(hipMalloc(&W->hom, m * 8));
         WCHECK(hipMalloc(&W->het, m * 8));
@@ -1369,7 +1573,8 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
 void sid_chunk_release(sid_chunk_ws* W)
 {
     for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
-                    (void*)W->bsum, (void*)W->boff, (void*)W->tcnt, (void*)W->toff, (void*)W->state})
+                    (void*)W->bsum, (void*)W->boff, (void*)W->tcnt, (void*)W->toff, (void*)W->state,
+                    (void*)W->hdr, (void*)W->fb})
         if (p) (void)hipFree(p);
     *W = sid_chunk_ws{};
 }
@@ -1401,9 +1606,8 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     const uint64_t tiles = chunk_tiles(c0, c1);
     const uint64_t t0 = c0 & ~(uint64_t)15;
     sid_lines_emit_kernel<<<(unsigned)tiles, TB, 0, st>>>(base, t0, c0, c1, W->toff, W->starts);
-    const unsigned pg = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, 16384);
-    sid_parse_kernel<<<pg, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts,
-                                        (unsigned long long*)(W->state + 4), qmode);
+    launch_parse(base, c1, W->starts, W->state + 1, n, W->counts, W->hdr, W->fb,
+                 (unsigned long long*)(W->state + 6), (unsigned long long*)(W->state + 4), qmode, st);
     WCHECK(hipGetLastError());
     return SID_OK;
 }
@@ -1429,7 +1633,7 @@ int sid_chunk_fmt_len(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n
     WCHECK(hipMemsetAsync(W->state + 5, 0, sizeof(uint64_t), st));
     if (n == 0) return SID_OK;
     const uint64_t nb = (n + TB - 1) / TB;
-    sid_fmt_len_kernel<<<(unsigned)nb, TB, 0, st>>>(base, c1, W->starts, 0, n, W->code, W->hom, W->het, ct, W->bsum,
+    sid_fmt_len_kernel<<<(unsigned)nb, TB, 0, st>>>(base, c1, W->starts, W->hdr, 0, n, W->code, W->hom, W->het, ct, W->bsum,
                                                     (int*)(W->state + 5));
     launch_scan(W->bsum, nb, W->boff, W->state + 3, nullptr,
                 (uint64_t*)((char*)W->bsum + ((nb * 4 + 7) & ~(size_t)7)), st);
@@ -1445,7 +1649,7 @@ int sid_chunk_fmt_write(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t
     if (chunk_ctype(conf_type, &ct)) return SID_EINVAL;
     if (n == 0) return SID_OK;
     const uint64_t nb = (n + TB - 1) / TB;
-    sid_fmt_write_kernel<<<(unsigned)nb, TB, 0, st>>>(base, c1, W->starts, 0, n, W->code, W->hom, W->het, ct, W->boff,
+    sid_fmt_write_kernel<<<(unsigned)nb, TB, 0, st>>>(base, c1, W->starts, W->hdr, 0, n, W->code, W->hom, W->het, ct, W->boff,
                                                       0, out);
     WCHECK(hipGetLastError());
     return SID_OK;

@@ -59,3 +59,26 @@ def test_format_g6_range_error(sid):
         sid.format_g6(1e300)
     assert e.value.status == 11
     assert sid.format_g6(2.0 ** 62) == printf_g(2.0 ** 62)
+
+
+def test_format_g6_fast_path_bulk(sid):
+    """The double-arithmetic fast path (fmt.h sid_dec6_fast) on 400k values of
+    the confidences' range (p-values down to 1e-300, and 6-digit mantissas
+    around each 7th-digit half), against printf."""
+    rng = np.random.default_rng(11)
+    a = np.exp(-rng.random(200_000) * 690.0)
+    d = rng.integers(100_000, 1_000_000, size=200_000)
+    e = rng.integers(-300, 12, size=200_000)
+    half = (d + 0.5) * 10.0 ** (e.astype(np.float64) - 5)
+    b = half * (1.0 + rng.integers(-8, 9, size=200_000) * 2.0 ** -52)
+    bad = []
+    for v in np.concatenate([a, b]):
+        v = float(v)
+        if not (0 < v < 2.0 ** 63):
+            continue
+        got, want = sid.format_g6(v), printf_g(v)
+        if got != want:
+            bad.append((v, got, want))
+            if len(bad) > 5:
+                break
+    assert not bad, bad
