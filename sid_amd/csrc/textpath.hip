@@ -492,104 +492,134 @@ __device__ __forceinline__ uint32_t low_bytes(uint32_t w)
     return ~(((w & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | w) & 0x80808080u;
 }
 
+// bit 7 of each byte of m -> 4 bits
+__device__ __forceinline__ uint32_t compress4(uint32_t m)
+{
+    uint32_t t = m >> 7;
+    t |= t >> 7;
+    t |= t >> 14;
+    return t & 0xFu;
+}
+__device__ __forceinline__ int ctz64(uint64_t x) { return x ? __builtin_ctzll(x) : 64; }
+
+constexpr int HDR_BYTES = 48;   // bytes staged per lane for the header (3 aligned windows)
+
 // The fast path of one line (pileup.cpp:13-46 + :70-153 for the lines that
-// need none of the general routine's cases): the header (tokens 0-3) byte by
-// byte, then the read-bases token 4 bytes at a time with SWAR byte tests:
-//   A/C/G/T either case     -> their counters (w | 0x20 folds the case)
-//   '.' / ','               -> one "matches ref" counter, added to the ref's
-//                              class at the end (toupper/tolower(ref) have the
-//                              same class for a base)
-//   '^'                     -> the next byte is skipped; a '^' that is itself
-//                              skipped (a '^' run) sends the line to the
-//                              general routine, as does a counted '+'/'-'
-//   ' ', '\t', '\n', NUL  -> end of the token (the rest of the line is never
-//                              read, as in the per-byte walk)
+// need none of the general routine's cases), branch-free over SWAR byte masks:
+//   header   the 48 bytes from the line's 16-B window: separator (' ', '\t')
+//            and low-byte (< 0x21) masks -> token starts 0-4 by bit tricks;
+//            tokens 0-3 must be free of '\n', NUL and other control bytes;
+//            ref and the position digits read from the lane's LDS copy
+//   token 4  16 bytes per step, per 4-byte word:
+//            A/C/G/T either case     -> their counters (w | 0x20 folds the case)
+//            '.' / ','               -> one "matches ref" counter, added to the
+//                                       ref's class at the end
+//            '^'                     -> the next byte is skipped; a '^' that is
+//                                       itself skipped (a '^' run) fails
+//            '+'/'-' (and ')'/'/')   -> fail (indel: the general routine)
+//            first byte < 0x21       -> end of the token, which must be ' ',
+//                                       '\t', '\n' or NUL, else fail
 // Returns false when the line needs the general routine.
 __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, uint64_t len, uint64_t s0,
-                                                const uint8_t* cls, uint64_t* out, uint64_t* hdr)
+                                                const uint8_t* cls, char* stage, uint64_t* out, uint64_t* hdr)
 {
-    Reader R{text, len};
-    uint64_t q = s0, t2 = 0, tb0 = 0;
-    int nt = 0;
-    uint32_t l2 = 0, l0 = 0, pos = 0, pdig = 0;
-    bool in = false, pos_ok = true;
-    for (;;) {   // tokens 0-3 and the first byte of token 4
-        if (q >= len || q - s0 > 255) return false;
-        const uint32_t c = R.at(q);
-        if (c == '\n' || c == 0) return false;
-        const bool sep = c == ' ' || c == '\t';
-        if (!sep && !in) {
-            ++nt;
-            if (nt == 1) tb0 = q;
-            if (nt == 3) t2 = q;
-            if (nt == 5) break;
-        }
-        if (!sep) {
-            const uint32_t d = c - '0';
-            l0 += nt == 1;
-            l2 += nt == 3;
-            if (nt == 2) {   // the position: plain decimal digits are atoi's value
-                pos_ok = pos_ok && d < 10u;
-                pos = pos * 10u + d;
-                ++pdig;
-            }
-        }
-        in = !sep;
-        ++q;
+    const uint64_t a0 = s0 & ~(uint64_t)15;
+    const uint32_t sh = (uint32_t)(s0 & 15);
+    const uint4 v0 = *(const uint4*)(text + a0);
+    const uint4 v1 = *(const uint4*)(text + a0 + 16);
+    const uint4 v2 = *(const uint4*)(text + a0 + 32);
+    *(uint4*)(stage) = v0;
+    *(uint4*)(stage + 16) = v1;
+    *(uint4*)(stage + 32) = v2;
+    const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
+    uint64_t S = 0, L = 0;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        S |= (uint64_t)compress4(eq_bytes(w[k], 0x20202020u) | eq_bytes(w[k], 0x09090909u)) << (4 * k);
+        L |= (uint64_t)compress4(low_bytes(w[k])) << (4 * k);
+    }
+    // bit j = byte s0 + j, for the bytes inside the text and the 48 staged
+    const uint64_t avail = len > s0 ? len - s0 : 0;
+    const uint32_t nb = (uint32_t)min((uint64_t)(HDR_BYTES - sh), avail);
+    const uint64_t valid = nb >= 64 ? ~0ull : ((1ull << nb) - 1);
+    S = (S >> sh) & valid;
+    L = (L >> sh) & valid;
+    const uint64_t N = ~S & valid;
+    uint64_t T = N & ~(N << 1);   // token starts
+    const int t0 = ctz64(T);
+    T &= T - 1;
+    const int t1 = ctz64(T);
+    T &= T - 1;
+    const int t2 = ctz64(T);
+    T &= T - 1;
+    T &= T - 1;
+    const int t4 = ctz64(T);
+    bool ok = t4 < (int)nb;                                          // token 4 starts inside the staged bytes
+    ok = ok && ((L & ~S) & ((1ull << (t4 & 63)) - 1)) == 0;          // no '\n', NUL, control byte before it
+    ok = ok && ((S >> ((t2 + 1) & 63)) & 1);                         // token 2 is one byte
+    if (!ok) return false;
+    const int l0 = ctz64(S >> t0);
+    const int lp = ctz64(S >> t1);
+    const uint32_t ref = (uint8_t)stage[sh + t2];
+    uint32_t pos = 0;
+    bool pos_ok = lp <= 9;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const uint32_t d = (uint32_t)(uint8_t)stage[sh + t1 + k] - '0';
+        const bool in = k < lp;
+        pos_ok = pos_ok && (!in || d < 10u);
+        pos = in ? pos * 10u + d : pos;
     }
     // chrom (offset, length) and position for the formatter (bit 63: valid)
-    *hdr = (pos_ok && pdig <= 9) ? (1ull << 63) | ((tb0 - s0) << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
-    if (l2 != 1) return false;   // malformed: the general routine reports it
-    const uint32_t ref = R.at(t2);
+    *hdr = pos_ok ? (1ull << 63) | ((uint64_t)t0 << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
     const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
     const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
     const uint32_t kd = cls[up], kc = cls[lw];
     if (kd >= K_CARET || kc >= K_CARET || kd != kc) return false;
     // token 4 from q, in aligned 16-B windows
+    const uint64_t q = s0 + (uint64_t)t4;
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
     uint64_t a = q & ~(uint64_t)15;
     uint32_t lead = (uint32_t)(q & 15);   // bytes of the first window before the token
     uint32_t carry = 0;                   // bit 7: byte 0 of the next word is skipped
-    bool done = false;
-    while (!done) {
+    bool done = false, bad = false;
+    do {
         const uint4 v = *(const uint4*)(text + a);
         const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
         const uint64_t room = len > a ? len - a : 0;   // bytes of this window inside the text
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t w = ws[k];
-            // bytes of this word inside [q, len) and not after the token's end
-            uint32_t vm = 0x80808080u;
+            const uint32_t x = ws[k];
             const int b0 = 4 * k;
-            if ((int)lead > b0) vm &= lead - b0 >= 4 ? 0u : (0x80808080u << (8 * (lead - b0)));
-            if (room < (uint64_t)(b0 + 4)) vm &= room <= (uint64_t)b0 ? 0u : (0x80808080u >> (8 * (b0 + 4 - room)));
-            if (done) vm = 0;
-            const uint32_t lo = low_bytes(w) & vm;
-            if (lo) {
-                const uint32_t term = (eq_bytes(w, 0x20202020u) | eq_bytes(w, 0x09090909u) |
-                                       eq_bytes(w, 0x0A0A0A0Au) | zero_bytes(w)) & vm;
-                if (term) {
-                    vm &= (term & (0u - term)) - 1u;   // bytes before the first terminator
-                    done = true;
-                }
-            }
-            if (room < (uint64_t)(b0 + 4)) done = true;   // end of the text
-            const uint32_t caret = eq_bytes(w, 0x5E5E5E5Eu) & vm;
+            // bytes of this word inside [q, len) and not after the token's end
+            const int lo_b = (int)lead - b0;                                    // first byte from the lead
+            const int hi_b = room >= (uint64_t)(b0 + 4) ? 4 : (int)room - b0;   // bytes before the end
+            uint32_t vm = lo_b <= 0 ? 0x80808080u : (lo_b >= 4 ? 0u : (0x80808080u << (8 * lo_b)));
+            vm &= hi_b >= 4 ? 0xFFFFFFFFu : (hi_b <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - hi_b))));
+            vm = done ? 0u : vm;
+            const uint32_t lo = low_bytes(x) & vm;
+            const uint32_t first = lo & (0u - lo);                  // the token's end, if in this word
+            const uint32_t tb = (x >> (first ? (__builtin_ctz(first) - 7) : 0)) & 0xFFu;
+            bad = bad || (first && tb != ' ' && tb != '\t' && tb != '\n' && tb != 0);
+            vm &= first - 1u;                                       // bytes before it (all if none)
+            done = done || first != 0 || hi_b < 4;
+            const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
             const uint32_t skip = ((caret << 8) | carry) & vm;
-            if (caret & skip) return false;   // '^' run
-            carry = caret >> 24;              // bit 31 -> bit 7
+            bad = bad || (caret & skip) != 0;                        // '^' run
+            carry = caret >> 24;                                     // bit 31 -> bit 7
             const uint32_t cm = vm & ~skip;
-            if ((eq_bytes(w, 0x2B2B2B2Bu) | eq_bytes(w, 0x2D2D2D2Du)) & cm) return false;   // indel
-            const uint32_t f = w | 0x20202020u;
+            bad = bad || (eq_bytes(x | 0x06060606u, 0x2F2F2F2Fu) & cm) != 0;   // '+' '-' (')' '/')
+            const uint32_t f = x | 0x20202020u;
             nA += __popc(eq_bytes(f, 0x61616161u) & cm);
             nC += __popc(eq_bytes(f, 0x63636363u) & cm);
             nG += __popc(eq_bytes(f, 0x67676767u) & cm);
             nT += __popc(eq_bytes(f, 0x74747474u) & cm);
-            nM += __popc(eq_bytes(w | 0x02020202u, 0x2E2E2E2Eu) & cm);
+            nM += __popc(eq_bytes(x | 0x02020202u, 0x2E2E2E2Eu) & cm);
         }
         lead = 0;
         a += 16;
-    }
+    } while (!done);
+    if (bad) return false;
     nA += kd == K_A ? nM : 0;
     nC += kd == K_C ? nM : 0;
     nG += kd == K_G ? nM : 0;
@@ -609,13 +639,14 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
                                                        uint32_t* __restrict__ fb, unsigned long long* fbn)
 {
     __shared__ uint8_t cls[256];
+    __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
     if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
     __syncthreads();
     const uint64_t lo = range[0], hi = range[1];
     for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
          i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t c = 0, h = 0;
-        if (parse_line_fast(text, len, starts[i], cls, &c, &h)) {
+        if (parse_line_fast(text, len, starts[i], cls, stage + threadIdx.x * HDR_BYTES, &c, &h)) {
             counts[i] = c;
             hdr[i] = h;
         } else {
