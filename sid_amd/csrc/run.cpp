@@ -351,9 +351,19 @@ int hipfail(sid_engine* e, hipError_t x)
     return rc;
 }
 
-const uint64_t CHUNK_DEFAULT = 128ull << 20;
+// default chunk sizes: input that crosses PCIe in 128 MiB pieces (the pipeline
+// fills and drains in a few ms); text already in HBM, or generated there, in
+// larger ones (every chunk costs a few fixed launches and two host round
+// trips; the workspace is a few hundred MB per GiB of text)
+const uint64_t CHUNK_HOST = 128ull << 20;
+const uint64_t CHUNK_DEVICE = 1ull << 30;
+const uint64_t CHUNK_SYNTH = 512ull << 20;
 
-uint64_t chunk_bytes(const sid_engine* e) { return e->cfg.chunk_bytes ? e->cfg.chunk_bytes : CHUNK_DEFAULT; }
+uint64_t chunk_bytes(const sid_engine* e)
+{
+    if (e->cfg.chunk_bytes) return e->cfg.chunk_bytes;
+    return e->src == SRC_DEVICE ? CHUNK_DEVICE : e->src == SRC_SYNTH_DEVICE ? CHUNK_SYNTH : CHUNK_HOST;
+}
 
 // first line start at or after c (one past the next '\n')
 uint64_t next_line_start(const char* t, uint64_t len, uint64_t c)
@@ -883,7 +893,8 @@ void compute(sid_engine* e, Dev& d, int pass)
         if (L.ev) x = hipStreamWaitEvent(d.s_comp, L.ev, 0);
         const bool P = e->prof;
         if (P) d.prof_chunks++;
-        if (x == hipSuccess) rc = sid_chunk_reserve(&W, L.c1 - (L.c0 & ~(uint64_t)15), 0);
+        const uint64_t tbytes = L.c1 - (L.c0 & ~(uint64_t)15);
+        if (x == hipSuccess) rc = sid_chunk_reserve(&W, tbytes, 0);
         hipEvent_t pe = d.prof_begin(P);
         if (rc == SID_OK && x == hipSuccess) rc = sid_chunk_index(&W, L.base, L.c0, L.c1, d.s_comp);
         d.prof_end(0, pe);
@@ -892,8 +903,9 @@ void compute(sid_engine* e, Dev& d, int pass)
         if (x != hipSuccess) return (void)hipfail(e, x);
         if (rc != SID_OK) return (void)fail(e, rc);
         const uint64_t n = hs[0];
-        r.parsed = n;
         rc = sid_chunk_reserve(&W, 0, n);
+        if (rc != SID_OK) return (void)fail(e, rc);
+        r.parsed = n;
         pe = d.prof_begin(P);
         if (rc == SID_OK) rc = sid_chunk_parse(&W, L.base, L.c0, L.c1, n, qmode, d.s_comp);
         d.prof_end(1, pe);

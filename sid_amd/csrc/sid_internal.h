@@ -102,11 +102,13 @@ struct sid_chunk_ws {
     uint8_t* code = nullptr;
     double* hom = nullptr;
     double* het = nullptr;
-    uint32_t* tcnt = nullptr;     // per 4 KiB tile line counts (+ scan workspace)
+    uint32_t* tcnt = nullptr;     // per 16 KiB tile line counts (+ scan workspace)
     uint64_t* toff = nullptr;
     uint32_t* bsum = nullptr;     // per 256-site block record bytes (+ scan workspace)
     uint64_t* boff = nullptr;
+    uint16_t* masks = nullptr;    // line-start masks of the index, a u16 per lane per 4 KiB tile
     uint64_t* state = nullptr;    // [0] sites [1..2] parse range [3] CSV bytes [4] first error key [5] range flag
+                                  // [6] fallback lines
 };
 int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites);
 void sid_chunk_release(sid_chunk_ws* W);
