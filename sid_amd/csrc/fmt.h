@@ -23,7 +23,8 @@ static __device__ const uint64_t sid_pow5_limb_d[SID_POW5_NLIMBS] = SID_POW5_LIM
 static const uint16_t sid_pow5_off_h[SID_POW5_MAX + 2] = SID_POW5_OFF_INIT;
 static const uint64_t sid_pow5_limb_h[SID_POW5_NLIMBS] = SID_POW5_LIMB_INIT;
 
-#define SID_FMT_MAX 16   // longest output: "-4.94066e-324" (13 bytes)
+#define SID_FMT_MAX 16
+#define SID_P10_N (SID_P10_MAX - SID_P10_MIN + 1)   // longest output: "-4.94066e-324" (13 bytes)
 
 // floor(M * 2^E * 10^k) for 0 <= k <= SID_POW5_MAX and where the remainder
 // lies against one half: cmp = -1 below (or no remainder), 0 exactly half,
@@ -77,12 +78,13 @@ __host__ __device__ inline uint64_t sid_scale10(uint64_t M, int E, int k, int& c
 // the fraction is within 2^-20 of one half, or y within 1e-3 of the 10^5 /
 // 10^6 ends of the 6-digit range -- those (a few in 10^6 values) and
 // denormals / k outside the table go to the exact multi-limb path.
-__host__ __device__ inline bool sid_dec6_fast(double v, int be, uint32_t& D, int& X)
+// p10: the 10^k table (a kernel may pass its LDS copy), null = the global one
+__host__ __device__ inline bool sid_dec6_fast(double v, int be, uint32_t& D, int& X, const double* p10)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const double* p10 = sid_p10_d;
+    if (!p10) p10 = sid_p10_d;
 #else
-    const double* p10 = sid_p10_h;
+    if (!p10) p10 = sid_p10_h;
 #endif
     if (be == 0) return false;
     int x = ((be - 1023) * 78913) >> 18;   // floor(e2 * log10(2)): the exponent x or x - 1
@@ -110,18 +112,32 @@ __host__ __device__ inline bool sid_dec6_fast(double v, int be, uint32_t& D, int
 // Six significant digits of v > 0 (finite): D in [100000, 999999], decimal
 // exponent X of the leading digit, rounded half-to-even.  false if v is out of
 // the supported range (v >= 2^63).
-__host__ __device__ __noinline__ bool sid_dec6_exact(double v, uint32_t& D, int& X);
+__host__ __device__ inline bool sid_dec6_exact(double v, uint32_t& D, int& X);
 
-__host__ __device__ inline bool sid_dec6(double v, uint32_t& D, int& X)
+// the exact path out of line (its limb array lives in scratch), its results
+// returned by value -- (ok << 63) | (X + 1024) << 32 | D -- so that the
+// caller's locals never have their address taken (they would live in scratch)
+__host__ __device__ __noinline__ uint64_t sid_dec6_exact_packed(double v)
+{
+    uint32_t D = 0;
+    int X = 0;
+    const bool ok = sid_dec6_exact(v, D, X);
+    return ((uint64_t)ok << 63) | ((uint64_t)(uint32_t)(X + 1024) << 32) | D;
+}
+
+__host__ __device__ inline bool sid_dec6(double v, uint32_t& D, int& X, const double* p10 = nullptr)
 {
     const uint64_t bits = __builtin_bit_cast(uint64_t, v);
     const int be = (int)((bits >> 52) & 0x7ff);
-    if (be < 1023 + 63 && sid_dec6_fast(v, be, D, X)) return true;
-    return sid_dec6_exact(v, D, X);
+    if (be < 1023 + 63 && sid_dec6_fast(v, be, D, X, p10)) return true;
+    const uint64_t r = sid_dec6_exact_packed(v);
+    D = (uint32_t)r;
+    X = (int)((r >> 32) & 0x7FFFFFFFu) - 1024;
+    return r >> 63;
 }
 
-// the exact multi-limb path (kept out of line: its limb array lives in scratch)
-__host__ __device__ __noinline__ bool sid_dec6_exact(double v, uint32_t& D, int& X)
+// the exact multi-limb path
+__host__ __device__ inline bool sid_dec6_exact(double v, uint32_t& D, int& X)
 {
     const uint64_t bits = __builtin_bit_cast(uint64_t, v);
     const int be = (int)((bits >> 52) & 0x7ff);
@@ -188,7 +204,7 @@ struct sid_g6 {
     int X, nd, kind, neg;
 };
 
-__host__ __device__ inline sid_g6 sid_g6_prep(double v)
+__host__ __device__ inline sid_g6 sid_g6_prep(double v, const double* p10 = nullptr)
 {
     const uint64_t bits = __builtin_bit_cast(uint64_t, v);
     const uint64_t mag = bits & 0x7fffffffffffffffull;
@@ -197,7 +213,7 @@ __host__ __device__ inline sid_g6 sid_g6_prep(double v)
     else if (mag == 0x7ff0000000000000ull) g.kind = SID_G6_INF;
     else if (mag == 0) g.kind = SID_G6_ZERO;
     else if (mag == 0x3ff0000000000000ull) g.kind = SID_G6_ONE;   // 1: the most frequent confidence
-    else if (!sid_dec6(__builtin_bit_cast(double, mag), g.D, g.X)) g.kind = SID_G6_RANGE;
+    else if (!sid_dec6(__builtin_bit_cast(double, mag), g.D, g.X, p10)) g.kind = SID_G6_RANGE;
     else {
         int nd = 6;
         uint32_t d = g.D;

@@ -840,6 +840,14 @@ __device__ __forceinline__ void record_put(Reader& R, const Head& h, uint8_t c, 
     out[n + ct.len] = '\n';
 }
 
+// the block's LDS copy of the 10^k table of the %g fast path (a dependent
+// global load per confidence otherwise); synchronises the block
+__device__ __forceinline__ void load_p10(double* p10)
+{
+    for (int k = threadIdx.x; k < SID_P10_N; k += TB) p10[k] = sid_p10_d[k];
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict__ text, uint64_t len,
                                                          const uint64_t* __restrict__ starts,
                                                          const uint64_t* __restrict__ hdr, uint64_t s0,
@@ -848,6 +856,8 @@ __global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict_
                                                          const double* __restrict__ het, CType ct,
                                                          uint32_t* __restrict__ bsum, int* __restrict__ bad)
 {
+    __shared__ double p10[SID_P10_N];
+    load_p10(p10);
     const uint64_t i = s0 + (uint64_t)blockIdx.x * TB + threadIdx.x;
     int l = 0;
     if (i < s1) {
@@ -855,7 +865,7 @@ __global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict_
         if (!(c & 0x40)) {
             Reader R{text, len};
             const Head h = site_head(R, starts[i], hdr ? hdr[i] : 0);
-            l = record_len(h, c, sid_g6_prep(hom[i]), sid_g6_prep(het[i]), ct.len);
+            l = record_len(h, c, sid_g6_prep(hom[i], p10), sid_g6_prep(het[i], p10), ct.len);
             if (l < 0) {
                 atomicExch(bad, 1);
                 l = 0;
@@ -867,7 +877,7 @@ __global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict_
     if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
-constexpr int FMT_LDS = 24 * 1024;
+constexpr int FMT_LDS = 16 * 1024;   // 64 B per record: 8 blocks (32 waves) per CU
 
 __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restrict__ text, uint64_t len,
                                                            const uint64_t* __restrict__ starts,
@@ -879,6 +889,8 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
                                                            char* __restrict__ out)
 {
     __shared__ __attribute__((aligned(16))) char buf[FMT_LDS + 32];
+    __shared__ double p10[SID_P10_N];
+    load_p10(p10);
     const uint64_t i = s0 + (uint64_t)blockIdx.x * TB + threadIdx.x;
     Reader R{text, len};
     int l = 0;
@@ -889,8 +901,8 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
         c = code[i];
         if (!(c & 0x40)) {
             h = site_head(R, starts[i], hdr ? hdr[i] : 0);
-            gh = sid_g6_prep(hom[i]);
-            gt = sid_g6_prep(het[i]);
+            gh = sid_g6_prep(hom[i], p10);
+            gt = sid_g6_prep(het[i], p10);
             l = record_len(h, c, gh, gt, ct.len);
             if (l < 0) l = 0;
         }
