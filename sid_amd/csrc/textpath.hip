@@ -204,31 +204,50 @@ static void launch_scan(const uint32_t* in, uint64_t m, uint64_t* out, uint64_t*
     if (nb) sid_scan_down_kernel<<<(unsigned)nb, TB, 0, st>>>(in, m, ws, out);
 }
 
+// ---- SWAR helpers: bit 7 of each byte of the result flags a byte of w
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x)
+{
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t k4) { return zero_bytes(w ^ k4); }
+// bytes < 0x21: the separators, '\n', NUL (and other control bytes)
+__device__ __forceinline__ uint32_t low_bytes(uint32_t w)
+{
+    return ~(((w & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | w) & 0x80808080u;
+}
+
+// bit 7 of each byte of m -> 4 bits
+__device__ __forceinline__ uint32_t compress4(uint32_t m)
+{
+    uint32_t t = m >> 7;
+    t |= t >> 7;
+    t |= t >> 14;
+    return t & 0xFu;
+}
 // ------------------------------------------------------------ line index --
 // 16 bytes per lane; bit j of the result = byte j starts a non-empty line.
-// Bytes outside [c0, c1) never start a line; c0 is a line start.
+// Bytes outside [c0, c1) never start a line; c0 is a line start.  SWAR: the
+// '\n' bytes of the four words as a 16-bit mask, the previous byte's from the
+// neighbouring lane (a load at a wave's first lane).
 __device__ __forceinline__ uint32_t line_start_mask(const char* __restrict__ text, uint64_t tile0, uint64_t c0,
                                                     uint64_t c1)
 {
     const uint64_t at = tile0 + (uint64_t)threadIdx.x * 16;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (at < c1 && at + 16 > c0) v = *(const uint4*)(text + at);
-    // previous byte: the neighbour lane's last byte, or a load at a wave start
-    uint32_t last = (v.w >> 24) & 0xffu;
-    uint32_t prev = (uint32_t)__shfl_up((int)last, 1, 64);
-    if ((threadIdx.x & 63) == 0) prev = (at > c0 && at - 1 < c1) ? (uint8_t)text[at - 1] : (uint32_t)'\n';
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t mask = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
-        const uint64_t pos = at + j;
-        const bool in = pos >= c0 && pos < c1;
-        const uint32_t p = pos == c0 ? (uint32_t)'\n' : prev;
-        if (in && b != '\n' && p == '\n') mask |= 1u << j;
-        prev = b;
+    uint32_t nl = compress4(eq_bytes(v.x, 0x0A0A0A0Au)) | (compress4(eq_bytes(v.y, 0x0A0A0A0Au)) << 4) |
+                  (compress4(eq_bytes(v.z, 0x0A0A0A0Au)) << 8) | (compress4(eq_bytes(v.w, 0x0A0A0A0Au)) << 12);
+    // is the byte before `at` a '\n': the neighbour lane's bit 15, or a load at a wave start
+    uint32_t prev = (uint32_t)__shfl_up((int)(nl >> 15), 1, 64);
+    if ((threadIdx.x & 63) == 0) prev = (at > c0 && at - 1 < c1) ? (text[at - 1] == '\n') : 1u;
+    uint32_t m = ((nl << 1) | prev) & ~nl & 0xFFFFu;
+    if (at + 16 > c0 && at <= c0) {   // c0 in this lane: it starts a line (unless a '\n'), nothing before it does
+        const uint32_t j = (uint32_t)(c0 - at);
+        m = (m | ((1u << j) & ~nl)) & ~((1u << j) - 1u);
     }
-    return mask;
+    if (at + 16 > c1) m &= c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
+    if (at + 16 <= c0) m = 0;
+    return m;
 }
 
 __global__ __launch_bounds__(TB) void sid_lines_count_kernel(const char* __restrict__ text, uint64_t tile_base,
@@ -261,8 +280,9 @@ __global__ __launch_bounds__(TB) void sid_lines_emit_kernel(const char* __restri
 // Line index of a chunk (the engine's path), two passes over 16 KiB tiles:
 //   sid_index_count_kernel  4 lane-contiguous 4 KiB sub-tiles per block, one
 //                           16-B load per lane each (4 loads in flight per
-//                           lane): line-start masks (u16 per lane and
-//                           sub-tile, 1/8 of the text) and the tile's count
+//                           lane; 8 measured slower): line-start masks (u16
+//                           per lane and sub-tile, 1/8 of the text) and the
+//                           tile's count
 //   (scan of the tile counts -> tile offsets, state[0] = sites)
 //   sid_index_emit_kernel   the offsets of every line start, from the masks
 // (A single pass with a decoupled look-back was measured 25x slower: the
@@ -302,27 +322,29 @@ __global__ __launch_bounds__(TB) void sid_index_emit_kernel(const uint16_t* __re
 {
     const uint16_t* mi = masks + (uint64_t)blockIdx.x * (IX_SUB * TB) + threadIdx.x;
     uint32_t m[IX_SUB];
-    uint64_t packed = 0;   // 16-bit line counts of the 4 sub-tiles
 #pragma unroll
-    for (int k = 0; k < IX_SUB; ++k) {
-        m[k] = mi[k * TB];
-        packed |= (uint64_t)__popc(m[k]) << (16 * k);
-    }
-    uint64_t tot;
-    const uint64_t pre = block_exscan64(packed, &tot);   // per-field prefixes (fields stay < 2^16)
+    for (int k = 0; k < IX_SUB; ++k) m[k] = mi[k * TB];
     uint64_t o = toff[blockIdx.x];
     const uint64_t t0 = tile_base + (uint64_t)blockIdx.x * IX_TILE;
 #pragma unroll
-    for (int k = 0; k < IX_SUB; ++k) {
-        uint64_t q = o + ((pre >> (16 * k)) & 0xFFFF);
-        const uint64_t at = t0 + (uint64_t)k * TILE + (uint64_t)threadIdx.x * 16;
-        uint32_t mk = m[k];
-        while (mk) {
-            const int j = __ffs(mk) - 1;
-            starts[q++] = at + j;
-            mk &= mk - 1;
+    for (int g = 0; g < IX_SUB; g += 4) {   // four sub-tiles per block scan: 16-bit fields stay < 2^16
+        uint64_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) packed |= (uint64_t)__popc(m[g + k]) << (16 * k);
+        uint64_t tot;
+        const uint64_t pre = block_exscan64(packed, &tot);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint64_t q = o + ((pre >> (16 * k)) & 0xFFFF);
+            const uint64_t at = t0 + (uint64_t)(g + k) * TILE + (uint64_t)threadIdx.x * 16;
+            uint32_t mk = m[g + k];
+            while (mk) {
+                const int j = __ffs(mk) - 1;
+                starts[q++] = at + j;
+                mk &= mk - 1;
+            }
+            o += (tot >> (16 * k)) & 0xFFFF;
         }
-        o += (tot >> (16 * k)) & 0xFFFF;
     }
 }
 
@@ -548,26 +570,6 @@ __device__ __noinline__ void parse_line_serial(const char* __restrict__ text, ui
                 ((uint64_t)(uint16_t)nT << 48);
 }
 
-// ---- SWAR helpers: bit 7 of each byte of the result flags a byte of w
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t x)
-{
-    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-}
-__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t k4) { return zero_bytes(w ^ k4); }
-// bytes < 0x21: the separators, '\n', NUL (and other control bytes)
-__device__ __forceinline__ uint32_t low_bytes(uint32_t w)
-{
-    return ~(((w & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | w) & 0x80808080u;
-}
-
-// bit 7 of each byte of m -> 4 bits
-__device__ __forceinline__ uint32_t compress4(uint32_t m)
-{
-    uint32_t t = m >> 7;
-    t |= t >> 7;
-    t |= t >> 14;
-    return t & 0xFu;
-}
 __device__ __forceinline__ int ctz64(uint64_t x) { return x ? __builtin_ctzll(x) : 64; }
 
 constexpr int HDR_BYTES = 48;   // bytes staged per lane for the header (3 aligned windows)
@@ -651,8 +653,10 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     uint32_t lead = (uint32_t)(q & 15);   // bytes of the first window before the token
     uint32_t carry = 0;                   // bit 7: byte 0 of the next word is skipped
     bool done = false, bad = false;
+    uint4 vn = *(const uint4*)(text + a);
     do {
-        const uint4 v = *(const uint4*)(text + a);
+        const uint4 v = vn;
+        vn = *(const uint4*)(text + a + 16);   // the next window in flight while this one is processed
         const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
         const uint64_t room = len > a ? len - a : 0;   // bytes of this window inside the text
 #pragma unroll
@@ -711,10 +715,14 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
     if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
     __syncthreads();
     const uint64_t lo = range[0], hi = range[1];
-    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
-         i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t s_next = i < hi ? starts[i] : 0;
+    for (; i < hi; i += stride) {
+        const uint64_t s0 = s_next;
+        if (i + stride < hi) s_next = starts[i + stride];   // the next line's offset in flight
         uint64_t c = 0, h = 0;
-        if (parse_line_fast(text, len, starts[i], cls, stage + threadIdx.x * HDR_BYTES, &c, &h)) {
+        if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, &h)) {
             counts[i] = c;
             hdr[i] = h;
         } else {
@@ -1642,7 +1650,7 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
     // queued work are not released under it (growth is rare: the first
     // chunks, or a chunk far above the usual lines per byte)
     if (!W->state) WCHECK(hipMalloc(&W->state, 8 * sizeof(uint64_t)));
-    const uint64_t tiles = ((bytes + 16 + IX_TILE - 1) / IX_TILE + 1) * IX_SUB;   // 4 KiB tiles, whole 16 KiB ones
+    const uint64_t tiles = ((bytes + 16 + IX_TILE - 1) / IX_TILE + 1) * IX_SUB;   // 4 KiB tiles, in whole index tiles
     if (tiles > W->tile_cap) {
         const uint64_t t = std::max<uint64_t>(tiles, W->tile_cap + W->tile_cap / 2);
         if (W->tcnt) (void)hipFree(W->tcnt);
