@@ -95,12 +95,14 @@ def parse_args():
 def stage_bytes(stage, text_per_site, csv_per_site):
     """Algorithmic HBM bytes per site of each engine stage."""
     return {
-        "index": text_per_site,                        # text read once (line starts per tile)
-        "parse": text_per_site + 8 + 8,                # text read, line offsets + counts written
+        "index": text_per_site + text_per_site / 8,    # text read once, line-start masks written
+        # text read; line-start masks (1/8 of the text) and offsets read back;
+        # counts (8) and the formatter's header pair (16) written
+        "parse": text_per_site + text_per_site / 8 + 8 + 8 + 16,
         "call": LOCAL_BYTES_PER_SITE,                  # counts in, code + confs out
         "hist": 8,                                     # counts read
-        "fmt_len": 17 + 8,                             # code + confs + line offset read (chrom/pos: L2)
-        "fmt_write": 17 + 8 + csv_per_site,            # the same + the records written
+        "fmt_len": 17 + 8 + 16,                        # code + confs, line offset, header pair read
+        "fmt_write": 17 + 8 + 16 + csv_per_site,       # the same + the records written
     }[stage]
 
 

@@ -325,7 +325,8 @@ extern "C" int sid_synth_text_device(sid_ctx* c, uint64_t seed, double mean_dept
     sid_synth_gen_ws ws;
     const hipStream_t st = (hipStream_t)stream;
     uint64_t res[2] = {0, 0};
-    hipError_t e = sid_launch_synth_text(seed, c->d_cdf, c->cdf_k, first_site, n, sites_per_chrom, &ws, out, cap, st);
+    hipError_t e = sid_launch_synth_text(seed, c->d_cdf, c->cdf_k, first_site, n, sites_per_chrom, &ws, out, cap, st,
+                                         mean_depth);
     if (e == hipSuccess) e = hipMemcpyAsync(res, ws.res, sizeof res, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     sid_synth_gen_release(&ws);

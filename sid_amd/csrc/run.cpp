@@ -812,7 +812,7 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
         } else if (e->src == SRC_SYNTH_DEVICE) {
             sid_synth_gen_ws& G = e->gen_ws[d.index];
             x = sid_launch_synth_text(e->synth_seed, e->d_cdf_dev[d.index], (uint32_t)e->synth_cdf.size(), r.site0,
-                                      r.nsites, e->synth_spc, &G, dst, dcap - PAD, d.s_up);
+                                      r.nsites, e->synth_spc, &G, dst, dcap - PAD, d.s_up, e->synth_depth);
             if (x == hipSuccess) x = hipMemcpyAsync(d.h_small + 6, G.res, 16, hipMemcpyDeviceToHost, d.s_up);
             if (x == hipSuccess) x = hipStreamSynchronize(d.s_up);
             if (x == hipSuccess) {

@@ -97,7 +97,7 @@ struct sid_chunk_ws {
     uint64_t site_cap = 0, tile_cap = 0;
     uint64_t* starts = nullptr;   // line start offsets (relative to the chunk's base)
     uint64_t* counts = nullptr;   // profile_t per site
-    uint64_t* hdr = nullptr;      // chrom / position per site for the formatter
+    uint64_t* hdr = nullptr;      // per site for the formatter: (chrom / position word, chrom's first 8 bytes)
     uint32_t* fb = nullptr;       // lines for the general parse routine (count in state[6])
     uint8_t* code = nullptr;
     double* hom = nullptr;
@@ -131,7 +131,7 @@ struct sid_synth_gen_ws {
 };
 hipError_t sid_launch_synth_text(uint64_t seed, const uint64_t* d_cdf, uint32_t kmax, uint64_t first, uint64_t n,
                                  uint64_t sites_per_chrom, sid_synth_gen_ws* ws, char* out, uint64_t cap,
-                                 hipStream_t st);
+                                 hipStream_t st, double mean_depth);
 void sid_synth_gen_release(sid_synth_gen_ws* ws);
 // textpath.hip: exclusive u32 -> u64 scan (three kernels) from *base
 size_t sid_scan_ws_bytes(uint64_t m);

@@ -32,6 +32,8 @@ extern "C" hipError_t sid_launch_synth(uint64_t seed, uint64_t first, size_t n,
 // lane per site: a length pass (only the read marks are drawn), a scan, and a
 // write pass.  Used to stream the C4/C5 configs (3G / 500M sites) through the
 // engine without ever storing them.
+#include <algorithm>
+
 #include "sid_internal.h"
 
 namespace {
@@ -95,17 +97,13 @@ __global__ __launch_bounds__(256) void sid_synth_len_kernel(uint64_t seed, uint6
     len[i] = l;
 }
 
-__global__ __launch_bounds__(256) void sid_synth_write_kernel(uint64_t seed, uint64_t first, uint64_t n,
-                                                              uint64_t spc, const uint64_t* __restrict__ cdf,
-                                                              uint32_t kmax, const uint64_t* __restrict__ off,
-                                                              const uint32_t* __restrict__ len, uint64_t cap,
-                                                              char* __restrict__ out)
+// The line of site i (l bytes) into o (any address space): one walk over the
+// reads writes each base with its marks and its quality character (the
+// qualities are the depth bytes before the final '\n').
+__device__ __forceinline__ void synth_write_line(const SynthLine& L, uint32_t l, char* o)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n || off[i] + len[i] > cap) return;   // overflow: reported by res[1], nothing past cap
     const char UP[4] = {'A', 'C', 'G', 'T'}, LO[4] = {'a', 'c', 'g', 't'};
-    const SynthLine L = synth_line(seed, first + i, spc, cdf, kmax);
-    char* o = out + off[i];
+    char* const o0 = o;
     *o++ = 'c';
     *o++ = 'h';
     *o++ = 'r';
@@ -121,30 +119,57 @@ __global__ __launch_bounds__(256) void sid_synth_write_kernel(uint64_t seed, uin
         *o++ = '*';
         *o++ = '\t';
         *o++ = '*';
-        *o++ = '\n';
+        *o = '\n';
         return;
     }
+    char* q = o0 + l - 1 - L.s.depth;
     for (uint32_t r = 0; r < L.s.depth; ++r) {
         uint32_t strand;
         const uint32_t b = sid_synth_read_base(&L.s, r, &strand);
         int st, en;
-        uint32_t q;
-        sid_synth_read_marks(&L.s, r, &st, &en, &q);
+        uint32_t ql;
+        sid_synth_read_marks(&L.s, r, &st, &en, &ql);
         if (st) {
             *o++ = '^';
             *o++ = ']';
         }
         *o++ = b == L.s.ref ? (strand ? '.' : ',') : (strand ? UP[b] : LO[b]);
         if (en) *o++ = '$';
+        *q++ = (char)('!' + ql);
     }
-    *o++ = '\t';
-    for (uint32_t r = 0; r < L.s.depth; ++r) {
-        int st, en;
-        uint32_t q;
-        sid_synth_read_marks(&L.s, r, &st, &en, &q);
-        *o++ = (char)('!' + q);
+    *o = '\t';
+    *q = '\n';
+}
+
+__global__ void sid_synth_write_kernel(uint64_t seed, uint64_t first, uint64_t n, uint64_t spc,
+                                       const uint64_t* __restrict__ cdf, uint32_t kmax,
+                                       const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+                                       uint64_t cap, char* __restrict__ out, uint32_t lds_cap)
+{
+    extern __shared__ __attribute__((aligned(16))) char buf[];
+    const uint32_t B = blockDim.x;
+    const uint64_t i0 = (uint64_t)blockIdx.x * B, i = i0 + threadIdx.x;
+    const uint64_t i1 = i0 + B < n ? i0 + B : n;
+    const uint64_t b0 = off[i0], b1 = off[i1 - 1] + len[i1 - 1];   // the block's bytes [b0, b1)
+    const bool staged = b1 <= cap && b1 - b0 + 16 <= lds_cap;
+    const uint32_t phase = (uint32_t)((uintptr_t)(out + b0) & 15u);
+    if (i < n && off[i] + len[i] <= cap) {
+        const SynthLine L = synth_line(seed, first + i, spc, cdf, kmax);
+        char* o = staged ? buf + phase + (off[i] - b0) : out + off[i];
+        synth_write_line(L, len[i], o);
     }
-    *o = '\n';
+    if (!staged) return;
+    __syncthreads();
+    char* dst = out + b0 - phase;   // 16-B aligned
+    const uint32_t span = phase + (uint32_t)(b1 - b0);
+    for (uint32_t k = threadIdx.x * 16; k < span; k += B * 16) {
+        if (k >= phase && k + 16 <= span) {
+            *(uint4*)(dst + k) = *(const uint4*)(buf + k);
+        } else {
+            for (uint32_t j = k; j < k + 16 && j < span; ++j)
+                if (j >= phase) dst[j] = buf[j];
+        }
+    }
 }
 
 __global__ void sid_synth_check_kernel(uint64_t* res, uint64_t cap)
@@ -162,7 +187,8 @@ void sid_synth_gen_release(sid_synth_gen_ws* ws)
 }
 
 hipError_t sid_launch_synth_text(uint64_t seed, const uint64_t* d_cdf, uint32_t kmax, uint64_t first, uint64_t n,
-                                 uint64_t spc, sid_synth_gen_ws* ws, char* out, uint64_t cap, hipStream_t st)
+                                 uint64_t spc, sid_synth_gen_ws* ws, char* out, uint64_t cap, hipStream_t st,
+                                 double mean_depth)
 {
     hipError_t e = hipSuccess;
     if (!ws->res && (e = hipMalloc(&ws->res, 2 * sizeof(uint64_t))) != hipSuccess) return e;
@@ -185,6 +211,12 @@ hipError_t sid_launch_synth_text(uint64_t seed, const uint64_t* d_cdf, uint32_t 
     sid_synth_check_kernel<<<1, 1, 0, st>>>(ws->res, cap);
     // no host sync between the passes: a line is written only when it ends
     // within cap, and res[1] tells the caller the text is incomplete
-    sid_synth_write_kernel<<<g, 256, 0, st>>>(seed, first, n, spc, d_cdf, kmax, ws->off, ws->len, cap, out);
+    // lines assembled in LDS, stored 16 B at a time: 256 sites a block up to a
+    // mean depth of ~60 (about 20 KiB), 64 beyond (a 200x block is ~27 KiB);
+    // a block whose lines do not fit stores them byte by byte
+    const uint32_t B = mean_depth > 60.0 ? 64u : 256u;
+    const uint32_t lds = std::min<uint32_t>(64u << 10, (uint32_t)(B * (40.0 + 4.2 * mean_depth)) + 64u);
+    const unsigned gw = (unsigned)((n + B - 1) / B);
+    sid_synth_write_kernel<<<gw, B, lds, st>>>(seed, first, n, spc, d_cdf, kmax, ws->off, ws->len, cap, out, lds);
     return hipGetLastError();
 }

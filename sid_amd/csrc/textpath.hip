@@ -641,7 +641,14 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
         pos = in ? pos * 10u + d : pos;
     }
     // chrom (offset, length) and position for the formatter (bit 63: valid)
-    *hdr = pos_ok ? (1ull << 63) | ((uint64_t)t0 << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
+    hdr[0] = pos_ok ? (1ull << 63) | ((uint64_t)t0 << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
+    // the chrom's first 8 bytes: the formatter then never reads the text for
+    // names up to 8 bytes (reading them back fetched every line's cache lines)
+    uint64_t c8 = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        c8 |= k < l0 ? (uint64_t)(uint8_t)stage[sh + t0 + k] << (8 * k) : 0ull;
+    hdr[1] = c8;
     const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
     const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
     const uint32_t kd = cls[up], kc = cls[lw];
@@ -721,10 +728,10 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
     for (; i < hi; i += stride) {
         const uint64_t s0 = s_next;
         if (i + stride < hi) s_next = starts[i + stride];   // the next line's offset in flight
-        uint64_t c = 0, h = 0;
-        if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, &h)) {
+        uint64_t c = 0, h[2] = {0, 0};
+        if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
             counts[i] = c;
-            hdr[i] = h;
+            *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h[0], h[1]);
         } else {
             fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
         }
@@ -750,7 +757,7 @@ __global__ __launch_bounds__(TB) void sid_parse_serial_kernel(const char* __rest
         uint64_t c = 0;
         parse_line_serial(text, len, starts[i], cls, &c, err, qmode);
         counts[i] = c;
-        hdr[i] = 0;   // the formatter tokenises these lines itself
+        hdr[2 * i] = 0;   // the formatter tokenises these lines itself
     }
 }
 
@@ -786,15 +793,20 @@ struct Head {
     uint64_t cb;
     uint32_t clen;
     int32_t pos;
+    uint64_t c8;   // the chrom's bytes when clen <= 8 and the header word is valid (else 0)
 };
 
-__device__ __forceinline__ Head site_head(Reader& R, uint64_t start, uint64_t hdr)
+// hdr: the parse's (header word, chrom's first 8 bytes) of the site, or null
+__device__ __forceinline__ Head site_head(Reader& R, uint64_t start, const uint64_t* hdr)
 {
     Head h;
-    if (hdr >> 63) {
-        h.cb = start + ((hdr >> 44) & 0x7FFFFull);
-        h.clen = (uint32_t)(hdr >> 32) & 0xFFFu;
-        h.pos = (int32_t)(uint32_t)hdr;
+    h.c8 = 0;
+    const ulonglong2 hw = hdr ? *(const ulonglong2*)hdr : make_ulonglong2(0, 0);
+    if (hw.x >> 63) {
+        h.cb = start + ((hw.x >> 44) & 0x7FFFFull);
+        h.clen = (uint32_t)(hw.x >> 32) & 0xFFFu;
+        h.pos = (int32_t)(uint32_t)hw.x;
+        h.c8 = h.clen <= 8 ? hw.y : 0;
         return h;
     }
     uint64_t q = start;
@@ -825,7 +837,13 @@ __device__ __forceinline__ int record_len(const Head& h, uint8_t c, const sid_g6
 __device__ __forceinline__ void record_put(Reader& R, const Head& h, uint8_t c, const sid_g6& gh, const sid_g6& gt,
                                            const CType& ct, char* out)
 {
-    for (uint32_t k = 0; k < h.clen; ++k) out[k] = (char)R.at(h.cb + k);
+    if (h.c8 || h.clen == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (k < (int)h.clen) out[k] = (char)(h.c8 >> (8 * k));
+    } else {
+        for (uint32_t k = 0; k < h.clen; ++k) out[k] = (char)R.at(h.cb + k);
+    }
     int n = (int)h.clen;
     out[n++] = ',';
     n += sid_fmt_i32(h.pos, out + n);
@@ -872,7 +890,7 @@ __global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict_
         const uint8_t c = code[i];
         if (!(c & 0x40)) {
             Reader R{text, len};
-            const Head h = site_head(R, starts[i], hdr ? hdr[i] : 0);
+            const Head h = site_head(R, starts[i], hdr ? hdr + 2 * i : nullptr);
             l = record_len(h, c, sid_g6_prep(hom[i], p10), sid_g6_prep(het[i], p10), ct.len);
             if (l < 0) {
                 atomicExch(bad, 1);
@@ -903,12 +921,12 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
     Reader R{text, len};
     int l = 0;
     uint8_t c = 0x40;
-    Head h{0, 0, 0};
+    Head h{0, 0, 0, 0};
     sid_g6 gh{}, gt{};
     if (i < s1) {
         c = code[i];
         if (!(c & 0x40)) {
-            h = site_head(R, starts[i], hdr ? hdr[i] : 0);
+            h = site_head(R, starts[i], hdr ? hdr + 2 * i : nullptr);
             gh = sid_g6_prep(hom[i], p10);
             gt = sid_g6_prep(het[i], p10);
             l = record_len(h, c, gh, gt, ct.len);
@@ -1236,7 +1254,7 @@ static int dtext_index_parse(sid_dtext* T, hipStream_t st, uint64_t* err_offset)
     T->nsites = total;
     const size_t m = std::max<uint64_t>(total, 1);
     if ((e = hipMalloc(&T->d_starts, m * 8)) != hipSuccess || (e = hipMalloc(&T->d_counts, m * 8)) != hipSuccess ||
-        (e = hipMalloc(&T->d_hdr, m * 8)) != hipSuccess || (e = hipMalloc(&T->d_fb, m * 4)) != hipSuccess)
+        (e = hipMalloc(&T->d_hdr, m * 16)) != hipSuccess || (e = hipMalloc(&T->d_fb, m * 4)) != hipSuccess)
         return sid_set_hip_error(e);
     sid_lines_emit_kernel<<<(unsigned)tiles, TB, 0, st>>>(T->d_text, 0, 0, len, T->d_toff, T->d_starts);
     launch_parse(T->d_text, len, T->d_starts, T->d_state + 1, total, T->d_counts, T->d_hdr, T->d_fb,
@@ -1680,7 +1698,7 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         const uint64_t nb = (m + TB - 1) / TB + 1;
         WCHECK(hipMalloc(&W->starts, m * 8));
         WCHECK(hipMalloc(&W->counts, m * 8));
-        WCHECK(hipMalloc(&W->hdr, m * 8));
+        WCHECK(hipMalloc(&W->hdr, m * 16));
         WCHECK(hipMalloc(&W->fb, m * 4));
         WCHECK(hipMalloc(&W->code, m));
         WCHECK(hipMalloc(&W->hom, m * 8));

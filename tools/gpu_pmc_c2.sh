@@ -14,4 +14,5 @@ run() {   # group counters...
 run insts SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES || exit $?
 run fetch FETCH_SIZE || exit $?
 run write WRITE_SIZE || exit $?
+timeout -k 10 200 python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-extras > $O/pmc_bench.json 2>/dev/null || exit $?
 python3 $GRAFT_REPO_ROOT/tools/pmc_summary.py $O

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Per-stage HBM traffic of the engine from the rocprofv3 --pmc passes of
+tools/gpu_pmc_c2.sh, written as profiles/pmc_<stage>_<tag>.json for bench.py's
+roofline.traffic (bytes per site x the sites of a launch).
+
+Bytes per launch of a kernel: FETCH_SIZE x 1024 x 2 (gfx950 reports half the
+bytes of a wide coalesced read, MI355X_MICROARCH.md §HBM) + WRITE_SIZE x 1024;
+a stage's bytes = the sum over its kernels (bench.py STAGE_KERNELS).
+
+usage: tools/pmc_stages.py <gpurun_out dir> <bench json of the same run> <tag>
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STAGES = {
+    "index": ["sid_index_count_kernel", "sid_scan_reduce_kernel", "sid_scan_top_kernel", "sid_scan_down_kernel"],
+    "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_serial_kernel"],
+    "call": ["sid_local_table_p2", "sid_local_table_x1", "sid_local_fixup"],
+    "fmt_len": ["sid_fmt_len_kernel"],
+    "fmt_write": ["sid_fmt_write_kernel"],
+}
+
+
+def main():
+    src, bench, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    tmp = os.path.join(src, "pmc_summary.json")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), src, "--json", tmp],
+                   check=True, stdout=subprocess.DEVNULL)
+    pm = json.load(open(tmp))
+    b = json.load(open(bench))
+    sites = b["roofline"]["sites_per_launch"]
+    # the scans run twice per chunk (index and fmt_len): their bytes are shared
+    for stage, ks in STAGES.items():
+        tot, parts = 0.0, {}
+        for k in ks:
+            r = pm.get(k)
+            if not r or "hbm_bytes" not in r:
+                continue
+            share = 0.5 if k.startswith("sid_scan_") else 1.0
+            parts[k] = r["hbm_bytes"] * share
+            tot += parts[k]
+        if not parts:
+            continue
+        out = {"stage": stage, "hbm_bytes_per_launch": tot, "sites_per_launch": sites,
+               "hbm_bytes_per_site": tot / sites, "kernels": parts,
+               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/gpu_pmc_c2.sh); "
+                         "FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 per launch, averaged over launches",
+               "bench": os.path.basename(bench)}
+        with open(os.path.join(ROOT, "profiles", f"pmc_{stage}_{tag}.json"), "w") as f:
+            json.dump(out, f, indent=1)
+        print(stage, round(tot / sites, 2), "B/site")
+
+
+if __name__ == "__main__":
+    main()
