@@ -181,6 +181,8 @@ struct ChunkRec {
     uint64_t held_cap = 0, held_len = 0;
     char* kept = nullptr;            // text kept for pass 2 (device)
     uint64_t kept_cap = 0, kept_len = 0;
+    char* pre = nullptr;             // Lynch paths: the pass-1 parse (line offsets, counts, formatter
+    uint64_t pre_cap = 0;            // header pairs: n x 32 B) kept for pass 2, which skips index + parse
     uint64_t err = ~0ull;            // min(offset * 8 + kind) of the chunk's malformed lines
 };
 
@@ -515,7 +517,8 @@ static void drop_source(sid_engine* e)
         Dev& d = *e->devs[r.dev];
         if (r.held) d.pool.put(r.held, r.held_cap, nullptr);
         if (r.kept) d.pool.put(r.kept, r.kept_cap, nullptr);
-        r.held = r.kept = nullptr;
+        if (r.pre) d.pool.put(r.pre, r.pre_cap, nullptr);
+        r.held = r.kept = r.pre = nullptr;
     }
     e->recs.clear();
     e->src = SRC_NONE;
@@ -895,26 +898,68 @@ void compute(sid_engine* e, Dev& d, int pass)
         if (P) d.prof_chunks++;
         const uint64_t tbytes = L.c1 - (L.c0 & ~(uint64_t)15);
         if (x == hipSuccess) rc = sid_chunk_reserve(&W, tbytes, 0);
-        hipEvent_t pe = d.prof_begin(P);
-        if (rc == SID_OK && x == hipSuccess) rc = sid_chunk_index(&W, L.base, L.c0, L.c1, d.s_comp);
-        d.prof_end(0, pe);
-        if (rc == SID_OK && x == hipSuccess) x = hipMemcpyAsync(hs, W.state, 8, hipMemcpyDeviceToHost, d.s_comp);
-        if (rc == SID_OK && x == hipSuccess) x = sync();
-        if (x != hipSuccess) return (void)hipfail(e, x);
-        if (rc != SID_OK) return (void)fail(e, rc);
-        const uint64_t n = hs[0];
-        rc = sid_chunk_reserve(&W, 0, n);
-        if (rc != SID_OK) return (void)fail(e, rc);
-        r.parsed = n;
-        pe = d.prof_begin(P);
-        if (rc == SID_OK) rc = sid_chunk_parse(&W, L.base, L.c0, L.c1, n, qmode, d.s_comp);
-        d.prof_end(1, pe);
-        if (rc != SID_OK) return (void)fail(e, rc);
+        // pass 2 of a Lynch path: the parse kept since pass 1 stands in for the
+        // workspace's line offsets, counts and header pairs (restored below)
+        struct View {
+            sid_chunk_ws& W;
+            uint64_t *starts, *counts, *hdr;
+            bool on = false;
+            ~View()
+            {
+                if (on) W.starts = starts, W.counts = counts, W.hdr = hdr;
+            }
+        } view{W, W.starts, W.counts, W.hdr};
+        hipEvent_t pe = nullptr;
+        uint64_t n = 0;
+        if (pass == 2 && r.pre) {
+            n = r.parsed;
+            rc = sid_chunk_reserve(&W, 0, n);
+            if (rc != SID_OK) return (void)fail(e, rc);
+            view.starts = W.starts, view.counts = W.counts, view.hdr = W.hdr, view.on = true;
+            W.starts = (uint64_t*)r.pre;
+            W.counts = W.starts + n;
+            W.hdr = W.counts + n;
+            if (x == hipSuccess) x = hipMemsetAsync(W.state + 4, 0xFF, sizeof(uint64_t), d.s_comp);   // no parse error
+            if (x != hipSuccess) return (void)hipfail(e, x);
+        } else {
+            pe = d.prof_begin(P);
+            if (rc == SID_OK && x == hipSuccess) rc = sid_chunk_index(&W, L.base, L.c0, L.c1, d.s_comp);
+            d.prof_end(0, pe);
+            if (rc == SID_OK && x == hipSuccess) x = hipMemcpyAsync(hs, W.state, 8, hipMemcpyDeviceToHost, d.s_comp);
+            if (rc == SID_OK && x == hipSuccess) x = sync();
+            if (x != hipSuccess) return (void)hipfail(e, x);
+            if (rc != SID_OK) return (void)fail(e, rc);
+            n = hs[0];
+            rc = sid_chunk_reserve(&W, 0, n);
+            if (rc != SID_OK) return (void)fail(e, rc);
+            r.parsed = n;
+            pe = d.prof_begin(P);
+            if (rc == SID_OK) rc = sid_chunk_parse(&W, L.base, L.c0, L.c1, n, qmode, d.s_comp);
+            d.prof_end(1, pe);
+            if (rc != SID_OK) return (void)fail(e, rc);
+        }
         const bool lynch_hist = pass == 1 && e->lynch;
         const bool format = pass == 2 || (needs_format_pass1(e) && !d.hold_full.load());
         if (lynch_hist) {
             x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
             if (x != hipSuccess) return (void)hipfail(e, x);
+            // keep the parse for pass 2 while the retain budget allows (32 B a
+            // site: cheaper than indexing and parsing the text again)
+            if (n && !qmode && d.retain_used.load() + 32 * n <= d.retain_budget) {
+                uint64_t pc = 0;
+                char* pre = d.pool.get(32 * n, &pc, d.s_comp);
+                if (pre) {
+                    x = hipMemcpyAsync(pre, W.starts, 8 * n, hipMemcpyDeviceToDevice, d.s_comp);
+                    if (x == hipSuccess)
+                        x = hipMemcpyAsync(pre + 8 * n, W.counts, 8 * n, hipMemcpyDeviceToDevice, d.s_comp);
+                    if (x == hipSuccess)
+                        x = hipMemcpyAsync(pre + 16 * n, W.hdr, 16 * n, hipMemcpyDeviceToDevice, d.s_comp);
+                    if (x != hipSuccess) return (void)hipfail(e, x);
+                    r.pre = pre;
+                    r.pre_cap = pc;
+                    d.retain_used += pc;
+                }
+            }
             pe = d.prof_begin(P);
             rc = sid_profile_accumulate(d.ctx, (const uint16_t*)W.counts, n, d.s_comp);   // synchronises
             d.prof_end(3, pe);
@@ -969,6 +1014,10 @@ void compute(sid_engine* e, Dev& d, int pass)
         if (pass == 2 && r.kept) {   // kept text done with: back to the pool after this stream's work
             d.pool.put(r.kept, r.kept_cap, d.s_comp);
             r.kept = nullptr;
+        }
+        if (pass == 2 && r.pre) {
+            d.pool.put(r.pre, r.pre_cap, d.s_comp);
+            r.pre = nullptr;
         }
         if (pass == 1) {
             r.held = out;
@@ -1058,7 +1107,8 @@ static void reset_run(sid_engine* e)
         Dev& d = *e->devs[r.dev];
         if (r.held) d.pool.put(r.held, r.held_cap, nullptr);
         if (r.kept) d.pool.put(r.kept, r.kept_cap, nullptr);
-        r.held = r.kept = nullptr;
+        if (r.pre) d.pool.put(r.pre, r.pre_cap, nullptr);
+        r.held = r.kept = r.pre = nullptr;
         r.held_len = r.kept_len = 0;
         r.err = ~0ull;
         r.parsed = 0;
@@ -1323,7 +1373,8 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
         Dev& d = *e->devs[r.dev];
         if (r.held) d.pool.put(r.held, r.held_cap, nullptr);
         if (r.kept) d.pool.put(r.kept, r.kept_cap, nullptr);
-        r.held = r.kept = nullptr;
+        if (r.pre) d.pool.put(r.pre, r.pre_cap, nullptr);
+        r.held = r.kept = r.pre = nullptr;
     }
     e->ingested = false;
     return e->rc.load();
