@@ -311,6 +311,7 @@ int main(int argc, char** argv)
         cfg.verbose = 1;
         sid_engine* eng = nullptr;
         CHECK(sid_engine_create(&opt.o, &cfg, &eng), "engine");
+        const double tc = now();
         if (in.fd >= 0 && !in.data) CHECK(sid_engine_source_file(eng, in.fd, 0, in.len), "input");
         else CHECK(sid_engine_source_text(eng, in.data, in.len), "input");
         sid_run_stats st;
@@ -340,11 +341,11 @@ int main(int argc, char** argv)
         if (opt.stats)
             std::fprintf(stderr,
                          "{\"sites\": %llu, \"devices\": %d, \"threads\": %d, \"path\": \"stream\", "
-                         "\"parse_s\": %.6f, \"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, "
+                         "\"create_s\": %.6f, \"parse_s\": %.6f, \"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, "
                          "\"sites_per_s\": %.1f, \"chunks\": %llu, \"chunks_held\": %llu, "
                          "\"chunks_retained\": %llu, \"chunks_reloaded\": %llu, \"bytes_in\": %llu, "
                          "\"bytes_out\": %llu}\n",
-                         (unsigned long long)st.sites, D, T, t1 - t0, t2 - t1, t3 - t2, t3 - t0,
+                         (unsigned long long)st.sites, D, T, tc - t0, t1 - t0, t2 - t1, t3 - t2, t3 - t0,
                          st.sites / std::max(1e-9, t3 - t0), (unsigned long long)st.chunks,
                          (unsigned long long)st.chunks_held, (unsigned long long)st.chunks_retained,
                          (unsigned long long)st.chunks_reloaded, (unsigned long long)st.bytes_in,

@@ -311,6 +311,9 @@ struct sid_engine {
     std::atomic<uint64_t> first_err{UINT64_MAX};
     std::atomic<uint64_t> reloaded{0};
     std::atomic<uint64_t> sink_bytes{0};   // device sink: CSV bytes formatted and dropped
+    // SID_ENGINE_TIMING: host time (ns) spent in compute-stream syncs and in
+    // the writer's waits for D2H pieces, printed per phase
+    std::atomic<uint64_t> t_comp_sync{0}, t_write_wait{0};
     // host-generated input: pinned buffers
     std::vector<char*> gen_buf;
     std::vector<uint64_t> gen_cap;
@@ -866,7 +869,12 @@ void compute(sid_engine* e, Dev& d, int pass)
     sid_chunk_ws& W = d.ws;
     uint64_t* hs = d.h_small;
     const int qmode = e->quality ? 1 : 0;
-    auto sync = [&]() { return hipStreamSynchronize(d.s_comp); };
+    auto sync = [&]() {
+        const double a = wall();
+        const hipError_t r = hipStreamSynchronize(d.s_comp);
+        e->t_comp_sync += (uint64_t)((wall() - a) * 1e9);
+        return r;
+    };
     Loaded L;
     while (d.loaded.pop(L)) {
         if (e->rc.load() != SID_OK) break;
@@ -1095,6 +1103,16 @@ void drain(sid_engine* e, Dev& d)
 }  // namespace
 
 // ------------------------------------------------------------------ phases --
+static void timing_report(sid_engine* e, const char* phase, double s)
+{
+    static const bool on = std::getenv("SID_ENGINE_TIMING") != nullptr;
+    if (on)
+        std::fprintf(stderr,
+                     "{\"engine_phase\": \"%s\", \"s\": %.6f, \"compute_sync_s\": %.6f, \"writer_wait_s\": %.6f}\n",
+                     phase, s, e->t_comp_sync.load() * 1e-9, e->t_write_wait.load() * 1e-9);
+    e->t_comp_sync = e->t_write_wait = 0;
+}
+
 static void reset_run(sid_engine* e)
 {
     e->rc = SID_OK;
@@ -1213,6 +1231,7 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         st->err_offset = 0;
         st->ingest_s = wall() - t0;
     }
+    timing_report(e, "ingest", wall() - t0);
     const uint64_t fe = e->first_err.load();
     if (fe != UINT64_MAX) {
         const ChunkRec& r = e->recs[fe];
@@ -1302,6 +1321,7 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
     start_queues(e);
     const int D = (int)e->devs.size();
     // pinned ring per device: 4 x 16 MiB (pinned once, reused by every run)
+    // (8 x 16, 4 x 64 and 16 x 8 MiB measured slower: the pinning costs more)
     const uint64_t PC = 16ull << 20;
     const int NP = 4;
     if (sink != 1)
@@ -1338,7 +1358,10 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
             bool got_last = false;
             while (d.out_q.pop(p)) {
                 if (p.ps >= 0) {
-                    if (hipEventSynchronize(d.pinned_ev[p.ps]) != hipSuccess) {
+                    const double w0 = wall();
+                    const hipError_t ws = hipEventSynchronize(d.pinned_ev[p.ps]);
+                    e->t_write_wait += (uint64_t)((wall() - w0) * 1e9);
+                    if (ws != hipSuccess) {
                         fail(e, SID_EHIP);
                         break;
                     }
@@ -1368,6 +1391,7 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
         st->bytes_out = sink == 1 ? e->sink_bytes.load() : out_bytes.load();
         st->emit_s = wall() - t0;
     }
+    timing_report(e, "emit", wall() - t0);
     // every held / kept buffer went back to the pools
     for (auto& r : e->recs) {
         Dev& d = *e->devs[r.dev];
