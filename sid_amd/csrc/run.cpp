@@ -919,14 +919,20 @@ void compute(sid_engine* e, Dev& d, int pass)
         } view{W, W.starts, W.counts, W.hdr};
         hipEvent_t pe = nullptr;
         uint64_t n = 0;
+        // the kept parse's layout: starts, counts, header pairs, each at a
+        // 16-B aligned offset (the lookup reads counts as 16-B site pairs)
+        auto use_pre = [&](char* pre, uint64_t m) {
+            view.starts = W.starts, view.counts = W.counts, view.hdr = W.hdr, view.on = true;
+            const uint64_t m2 = (m + 1) & ~(uint64_t)1;
+            W.starts = (uint64_t*)pre;
+            W.counts = W.starts + m2;
+            W.hdr = W.counts + m2;
+        };
         if (pass == 2 && r.pre) {
             n = r.parsed;
             rc = sid_chunk_reserve(&W, 0, n);
             if (rc != SID_OK) return (void)fail(e, rc);
-            view.starts = W.starts, view.counts = W.counts, view.hdr = W.hdr, view.on = true;
-            W.starts = (uint64_t*)r.pre;
-            W.counts = W.starts + n;
-            W.hdr = W.counts + n;
+            use_pre(r.pre, n);
             if (x == hipSuccess) x = hipMemsetAsync(W.state + 4, 0xFF, sizeof(uint64_t), d.s_comp);   // no parse error
             if (x != hipSuccess) return (void)hipfail(e, x);
         } else {
@@ -941,6 +947,21 @@ void compute(sid_engine* e, Dev& d, int pass)
             rc = sid_chunk_reserve(&W, 0, n);
             if (rc != SID_OK) return (void)fail(e, rc);
             r.parsed = n;
+            // Lynch paths: the parse goes straight into a buffer kept for
+            // pass 2 (which then skips index and parse) while the retain
+            // budget allows: 32 B a site, cheaper than indexing and parsing
+            // the text again
+            const uint64_t pre_bytes = 32 * ((n + 1) & ~(uint64_t)1);
+            if (pass == 1 && e->lynch && n && !qmode && d.retain_used.load() + pre_bytes <= d.retain_budget) {
+                uint64_t pc = 0;
+                char* pre = d.pool.get(pre_bytes, &pc, d.s_comp);
+                if (pre) {
+                    r.pre = pre;
+                    r.pre_cap = pc;
+                    d.retain_used += pc;
+                    use_pre(pre, n);
+                }
+            }
             pe = d.prof_begin(P);
             if (rc == SID_OK) rc = sid_chunk_parse(&W, L.base, L.c0, L.c1, n, qmode, d.s_comp);
             d.prof_end(1, pe);
@@ -951,23 +972,6 @@ void compute(sid_engine* e, Dev& d, int pass)
         if (lynch_hist) {
             x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
             if (x != hipSuccess) return (void)hipfail(e, x);
-            // keep the parse for pass 2 while the retain budget allows (32 B a
-            // site: cheaper than indexing and parsing the text again)
-            if (n && !qmode && d.retain_used.load() + 32 * n <= d.retain_budget) {
-                uint64_t pc = 0;
-                char* pre = d.pool.get(32 * n, &pc, d.s_comp);
-                if (pre) {
-                    x = hipMemcpyAsync(pre, W.starts, 8 * n, hipMemcpyDeviceToDevice, d.s_comp);
-                    if (x == hipSuccess)
-                        x = hipMemcpyAsync(pre + 8 * n, W.counts, 8 * n, hipMemcpyDeviceToDevice, d.s_comp);
-                    if (x == hipSuccess)
-                        x = hipMemcpyAsync(pre + 16 * n, W.hdr, 16 * n, hipMemcpyDeviceToDevice, d.s_comp);
-                    if (x != hipSuccess) return (void)hipfail(e, x);
-                    r.pre = pre;
-                    r.pre_cap = pc;
-                    d.retain_used += pc;
-                }
-            }
             pe = d.prof_begin(P);
             rc = sid_profile_accumulate(d.ctx, (const uint16_t*)W.counts, n, d.s_comp);   // synchronises
             d.prof_end(3, pe);
