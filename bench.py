@@ -101,8 +101,9 @@ def stage_bytes(stage, text_per_site, csv_per_site):
         "parse": text_per_site + text_per_site / 8 + 8 + 8 + 16,
         "call": LOCAL_BYTES_PER_SITE,                  # counts in, code + confs out
         "hist": 8,                                     # counts read
-        "fmt_len": 17 + 8 + 16,                        # code + confs, line offset, header pair read
-        "fmt_write": 17 + 8 + 16 + csv_per_site,       # the same + the records written
+        # one-pass formatter: code + confs and the header pair read (the line
+        # offset only for chrom names over 8 bytes), the records written
+        "fmt_write": 17 + 16 + csv_per_site,
     }[stage]
 
 
@@ -192,7 +193,7 @@ def main():
     prof = eng.profile_read()
     eng.profile(False)
     sites_rank = st.sites
-    stages = {k[:-3]: v / a.steps for k, v in prof.items() if k.endswith("_ms")}
+    stages = {k[:-3]: v / a.steps for k, v in prof.items() if k.endswith("_ms") and k != "fmt_len_ms"}
     if dist:
         vec = torch.tensor([elapsed] + [stages[k] for k in sorted(stages)], dtype=torch.float64, device=dev)
         dist.all_reduce(vec, op=dist.ReduceOp.MAX)
@@ -270,8 +271,7 @@ STAGE_KERNELS = {
     "parse": ["sid_lines_emit_kernel", "sid_parse_kernel"],
     "call": ["sid_local_table_p2", "sid_local_fixup"],
     "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
-    "fmt_len": ["sid_fmt_len_kernel", "sid_scan_*"],
-    "fmt_write": ["sid_fmt_write_kernel"],
+    "fmt_write": ["sid_fmt_fused_kernel"],
 }
 
 

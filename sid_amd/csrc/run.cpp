@@ -130,7 +130,7 @@ public:
     // its stream has run
     void put(char* p, uint64_t cap, hipStream_t after)
     {
-        if (!p) return;
+        if (!p || !cap) return;   // cap 0: not a pooled buffer (the hold arena)
         std::lock_guard<std::mutex> l(m_);
         Entry en{p, nullptr};
         if (after) {
@@ -236,8 +236,33 @@ struct Dev {
     std::vector<hipEvent_t> pinned_ev;
     uint64_t pinned_cap = 0;
     sid_chunk_ws ws;
-    uint64_t* h_small = nullptr;   // pinned: state[0..5] read back
+    uint64_t* h_small = nullptr;   // pinned, 16 words: [0] sites [4] error key [6..7] generator [8..11] formatter
     DevPool pool;
+    // hold arena: the records formatted in pass 1, packed one after another
+    // in segments of HBM kept across runs; a chunk reserves its upper bound
+    // and commits its exact bytes
+    std::vector<std::pair<char*, uint64_t>> arena;
+    size_t arena_seg = 0;
+    uint64_t arena_off = 0;
+    char* arena_reserve(uint64_t need)
+    {
+        while (arena_seg < arena.size() && arena_off + need > arena[arena_seg].second) ++arena_seg, arena_off = 0;
+        if (arena_seg == arena.size()) {
+            const uint64_t c = std::max<uint64_t>(need, 4ull << 30);
+            char* p = nullptr;
+            if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+            arena.push_back({p, c});
+            arena_off = 0;
+        }
+        return arena[arena_seg].first + arena_off;
+    }
+    void arena_commit(uint64_t bytes) { arena_off += (bytes + 255) & ~(uint64_t)255; }
+    uint64_t arena_bytes() const
+    {
+        uint64_t b = 0;
+        for (auto& a : arena) b += a.second;
+        return b;
+    }
     uint64_t hold_budget = 0, retain_budget = 0;
     std::atomic<uint64_t> hold_used{0}, retain_used{0};
     std::atomic<bool> hold_full{false};
@@ -494,7 +519,7 @@ extern "C" int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg
             x = hipStreamCreateWithFlags(&d->s_up, hipStreamNonBlocking);
             if (x == hipSuccess) x = hipStreamCreateWithFlags(&d->s_comp, hipStreamNonBlocking);
             if (x == hipSuccess) x = hipStreamCreateWithFlags(&d->s_d2h, hipStreamNonBlocking);
-            if (x == hipSuccess) x = hipHostMalloc((void**)&d->h_small, 64, hipHostMallocDefault);
+            if (x == hipSuccess) x = hipHostMalloc((void**)&d->h_small, 128, hipHostMallocDefault);
             d->slots.resize(R);
             for (auto& s : d->slots) {
                 if (x == hipSuccess) x = hipEventCreateWithFlags(&s.ev_up, hipEventDisableTiming);
@@ -552,6 +577,7 @@ extern "C" int sid_engine_destroy(sid_engine* e)
         for (hipStream_t s : {d->s_up, d->s_comp, d->s_d2h})
             if (s) (void)hipStreamDestroy(s);
         d->pool.release();
+        for (auto& a : d->arena) (void)hipFree(a.first);
         sid_destroy(d->ctx);
     }
     for (size_t i = 0; i < e->d_cdf_dev.size(); ++i)
@@ -978,21 +1004,43 @@ void compute(sid_engine* e, Dev& d, int pass)
             if (rc == SID_OK && n == 0) x = sync();
             if (rc != SID_OK) return (void)fail(e, rc);
             if (x != hipSuccess) return (void)hipfail(e, x);
-        } else if (format) {
+        }
+        // -m local / quality (and pass 2 of the Lynch paths): call, then the
+        // one-pass formatter into a buffer of the records' upper bound -- the
+        // device's hold arena in pass 1 (committed to the exact bytes after),
+        // else a pooled scratch buffer
+        char* out = nullptr;
+        uint64_t cap = 0;   // 0: arena memory (never returned to the pool)
+        if (format && !lynch_hist) {
             pe = d.prof_begin(P);
             rc = call_sites(e, d, L, n);
             d.prof_end(2, pe);
-            pe = d.prof_begin(P);
-            if (rc == SID_OK) rc = sid_chunk_fmt_len(&W, L.base, L.c1, n, e->conf_type, d.s_comp);
-            d.prof_end(4, pe);
             if (rc != SID_OK) return (void)fail(e, rc);
-            x = hipMemcpyAsync(hs + 3, W.state + 3, 24, hipMemcpyDeviceToHost, d.s_comp);
-            if (x == hipSuccess) x = sync();
-            if (x != hipSuccess) return (void)hipfail(e, x);
-        } else {
+            const uint64_t bound = sid_chunk_fmt_bound(n, L.c1 - L.c0);
+            if (n == 0) {
+            } else if (pass == 1 && d.hold_used.load() + bound > d.hold_budget) {
+                d.hold_full = true;   // this chunk and the rest: formatted in pass 2
+            } else if (pass == 1) {
+                if (!(out = d.arena_reserve(bound))) return (void)fail(e, SID_ENOMEM);
+            } else {
+                if (!(out = d.pool.get(bound, &cap, d.s_comp))) return (void)fail(e, SID_ENOMEM);
+            }
+            if (out) {
+                pe = d.prof_begin(P);
+                rc = sid_chunk_fmt(&W, L.base, L.c1, n, e->conf_type, out, d.s_comp);
+                d.prof_end(5, pe);
+                if (rc != SID_OK) return (void)fail(e, rc);
+                x = hipMemcpyAsync(hs + 8, W.lb + 1, 32, hipMemcpyDeviceToHost, d.s_comp);   // bytes, flags, error
+                if (x == hipSuccess) x = sync();
+                if (x != hipSuccess) return (void)hipfail(e, x);
+                hs[4] = hs[11];
+            }
+        }
+        if (!lynch_hist && !out) {
             x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
             if (x == hipSuccess) x = sync();
             if (x != hipSuccess) return (void)hipfail(e, x);
+            hs[8] = 0;
         }
         const uint64_t err = hs[4];
         if (err != ~0ull) {   // a malformed line: the rest of the input is moot
@@ -1004,24 +1052,13 @@ void compute(sid_engine* e, Dev& d, int pass)
             if (pass == 2) return (void)fail(e, SID_EMALFORMED);   // cannot happen: pass 1 validated
             continue;
         }
-        if (!format || lynch_hist) {
+        if (!format || lynch_hist || (pass == 1 && !out)) {
             release_slot();
             continue;
         }
-        if (hs[5]) return (void)fail(e, SID_ERANGE);
-        const uint64_t bytes = hs[3];
-        if (pass == 1 && d.hold_used.load() + bytes > d.hold_budget) {
-            d.hold_full = true;   // this chunk and the rest: formatted in pass 2
-            release_slot();
-            continue;
-        }
-        uint64_t cap = 0;
-        char* out = d.pool.get(bytes + 16, &cap, d.s_comp);
-        if (!out) return (void)fail(e, SID_ENOMEM);
-        pe = d.prof_begin(P);
-        rc = sid_chunk_fmt_write(&W, L.base, L.c1, n, e->conf_type, out, d.s_comp);
-        d.prof_end(5, pe);
-        if (rc != SID_OK) return (void)fail(e, rc);
+        if (out && hs[9]) return (void)fail(e, SID_ERANGE);
+        if (out && hs[10]) return (void)fail(e, SID_EHIP);   // a formatter look-back timed out
+        const uint64_t bytes = hs[8];
         release_slot();
         if (pass == 2 && r.kept) {   // kept text done with: back to the pool after this stream's work
             d.pool.put(r.kept, r.kept_cap, d.s_comp);
@@ -1032,10 +1069,11 @@ void compute(sid_engine* e, Dev& d, int pass)
             r.pre = nullptr;
         }
         if (pass == 1) {
+            d.arena_commit(bytes);
             r.held = out;
-            r.held_cap = cap;
+            r.held_cap = 0;
             r.held_len = bytes;
-            d.hold_used += cap;
+            d.hold_used += (bytes + 255) & ~(uint64_t)255;
             continue;
         }
         if (e->cfg.device_sink == 1) {
@@ -1140,6 +1178,8 @@ static void reset_run(sid_engine* e)
         d.hold_used = 0;
         d.retain_used = 0;
         d.hold_full = false;
+        d.arena_seg = 0;
+        d.arena_off = 0;
     }
 }
 
@@ -1163,7 +1203,7 @@ static int setup_budgets(sid_engine* e)
         if (hipSetDevice(d.device) != hipSuccess) return SID_EHIP;
         size_t fr = 0, tot = 0;
         if (hipMemGetInfo(&fr, &tot) != hipSuccess) return SID_EHIP;
-        const uint64_t avail = fr + d.pool.bytes();   // pooled buffers are reusable
+        const uint64_t avail = fr + d.pool.bytes() + d.arena_bytes();   // pooled buffers and the arena are reusable
         d.hold_budget = e->cfg.hold_bytes ? e->cfg.hold_bytes : (uint64_t)(avail * 0.40);
         d.retain_budget = e->cfg.retain_bytes ? e->cfg.retain_bytes : (uint64_t)(avail * 0.40);
     }

@@ -107,6 +107,7 @@ struct sid_chunk_ws {
     uint32_t* bsum = nullptr;     // per 256-site block record bytes (+ scan workspace)
     uint64_t* boff = nullptr;
     uint16_t* masks = nullptr;    // line-start masks of the index, a u16 per lane per 4 KiB tile
+    unsigned long long* lb = nullptr;   // one-pass formatter: ticket + per-block look-back status words
     uint64_t* state = nullptr;    // [0] sites [1..2] parse range [3] CSV bytes [4] first error key [5] range flag
                                   // [6] fallback lines
 };
@@ -115,10 +116,12 @@ void sid_chunk_release(sid_chunk_ws* W);
 int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, hipStream_t st);
 int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint64_t n, int qmode,
                     hipStream_t st);
-int sid_chunk_fmt_len(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type,
-                      hipStream_t st);
-int sid_chunk_fmt_write(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
-                        hipStream_t st);
+// the one-pass formatter: records of the n sites into out, which must hold
+// sid_chunk_fmt_bound(n, text bytes); afterwards lb[1..4] = {bytes, range
+// flag, look-back timeout, the chunk's parse error key (state[4])}
+uint64_t sid_chunk_fmt_bound(uint64_t n, uint64_t text_bytes);
+int sid_chunk_fmt(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
+                  hipStream_t st);
 int sid_chunk_quality(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st);
 // synth.hip: the synthetic text of sites [first, first + n) (the bytes of
 // sid_synth_text) generated on the device into out (cap bytes): res[0] =

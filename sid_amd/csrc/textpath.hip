@@ -52,9 +52,10 @@ constexpr int SCAN_TB = 1024;
 // ------------------------------------------------------------ block scan --
 // exclusive scan of one u32 per thread over a 256-thread block; returns the
 // prefix, *total = block sum
+template <int NT = TB>
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* total)
 {
-    __shared__ uint32_t wsum[TB / 64];
+    __shared__ uint32_t wsum[NT / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t x = v;
     for (int off = 1; off < 64; off <<= 1) {
@@ -64,7 +65,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* total)
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
     uint32_t base = 0, tot = 0;
-    for (int w = 0; w < TB / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
         if (w < wid) base += wsum[w];
         tot += wsum[w];
     }
@@ -796,20 +797,22 @@ struct Head {
     uint64_t c8;   // the chrom's bytes when clen <= 8 and the header word is valid (else 0)
 };
 
-// hdr: the parse's (header word, chrom's first 8 bytes) of the site, or null
-__device__ __forceinline__ Head site_head(Reader& R, uint64_t start, const uint64_t* hdr)
+// hdr: the parse's (header word, chrom's first 8 bytes) of the site, or null;
+// the line's offset (*startp) is read only when the text is (a chrom longer
+// than 8 bytes, or no valid header word)
+__device__ __forceinline__ Head site_head(Reader& R, const uint64_t* startp, const uint64_t* hdr)
 {
     Head h;
     h.c8 = 0;
     const ulonglong2 hw = hdr ? *(const ulonglong2*)hdr : make_ulonglong2(0, 0);
     if (hw.x >> 63) {
-        h.cb = start + ((hw.x >> 44) & 0x7FFFFull);
         h.clen = (uint32_t)(hw.x >> 32) & 0xFFFu;
         h.pos = (int32_t)(uint32_t)hw.x;
         h.c8 = h.clen <= 8 ? hw.y : 0;
+        h.cb = (h.c8 || h.clen == 0) ? 0 : *startp + ((hw.x >> 44) & 0x7FFFFull);
         return h;
     }
-    uint64_t q = start;
+    uint64_t q = *startp;
     while (is_sep(R.at(q))) ++q;
     h.cb = q;
     for (uint32_t ch = R.at(q); !is_sep(ch) && ch != '\n' && ch != 0; ch = R.at(++q)) {
@@ -870,7 +873,7 @@ __device__ __forceinline__ void record_put(Reader& R, const Head& h, uint8_t c, 
 // global load per confidence otherwise); synchronises the block
 __device__ __forceinline__ void load_p10(double* p10)
 {
-    for (int k = threadIdx.x; k < SID_P10_N; k += TB) p10[k] = sid_p10_d[k];
+    for (int k = threadIdx.x; k < SID_P10_N; k += blockDim.x) p10[k] = sid_p10_d[k];
     __syncthreads();
 }
 
@@ -890,7 +893,7 @@ __global__ __launch_bounds__(TB) void sid_fmt_len_kernel(const char* __restrict_
         const uint8_t c = code[i];
         if (!(c & 0x40)) {
             Reader R{text, len};
-            const Head h = site_head(R, starts[i], hdr ? hdr + 2 * i : nullptr);
+            const Head h = site_head(R, starts + i, hdr ? hdr + 2 * i : nullptr);
             l = record_len(h, c, sid_g6_prep(hom[i], p10), sid_g6_prep(het[i], p10), ct.len);
             if (l < 0) {
                 atomicExch(bad, 1);
@@ -926,7 +929,7 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
     if (i < s1) {
         c = code[i];
         if (!(c & 0x40)) {
-            h = site_head(R, starts[i], hdr ? hdr + 2 * i : nullptr);
+            h = site_head(R, starts + i, hdr ? hdr + 2 * i : nullptr);
             gh = sid_g6_prep(hom[i], p10);
             gt = sid_g6_prep(het[i], p10);
             l = record_len(h, c, gh, gt, ct.len);
@@ -952,6 +955,156 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
         } else {
             for (uint32_t j = k; j < k + 16 && j < span; ++j)
                 if (j >= phase) dst[j] = buf[j];
+        }
+    }
+}
+
+// The engine's formatter in one pass (record lengths, their offsets and the
+// records) with a decoupled look-back across blocks instead of a length
+// kernel, a scan and a write kernel that reads every input again.
+//
+// Blocks are dispatched in index order (per XCD), so a block only ever waits
+// on blocks already running or done (a ticket taken with an atomic -- one
+// address hit by every block -- cost 300 us per 49k blocks).  Each block
+// publishes one 8-byte status word --
+// bits 63-62 flag (1: the block's own byte count, 2: the bytes up to and
+// including it), bits 61-0 the count -- with relaxed agent-scope atomics: the
+// value is the flag's own payload, so no fence orders anything (the per-XCD
+// L2s are not coherent; these words go through to memory, MI355X_MICROARCH.md
+// "visibility", form R2).  One wave looks back 64 blocks per step.  A bounded
+// spin: a block that waits too long sets *timeout and goes on (the host then
+// fails the run), so every wave of the grid finishes.
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = LB_AGG - 1;
+constexpr uint32_t LB_SPIN_MAX = 1u << 22;
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// wave 0: bytes before virtual block b (b > 0)
+__device__ __forceinline__ uint64_t lookback(unsigned long long* st, uint32_t b, unsigned long long* timeout)
+{
+    const int lane = threadIdx.x & 63;
+    uint64_t excl = 0;
+    int64_t j = (int64_t)b - 1;   // window: blocks j, j-1, ..., j-63
+    uint32_t spins = 0;
+    while (true) {
+        const int64_t k = j - lane;
+        const uint64_t w = k >= 0 ? __hip_atomic_load(st + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : LB_INC;
+        const uint64_t flag = w & ~LB_VAL;
+        const uint64_t inc = __ballot(flag == LB_INC);
+        const int first = inc ? __ffsll((long long)inc) - 1 : 64;   // nearest block with an inclusive count
+        const uint64_t none = __ballot(flag == 0);
+        if (none & (first == 64 ? ~0ull : ((2ull << first) - 1))) {   // a block before it has not published
+            if (++spins > LB_SPIN_MAX) {
+                if (lane == 0) atomicExch(timeout, 1ull);
+                return excl;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += wave_sum64(lane <= first ? (w & LB_VAL) : 0);
+        if (inc) return excl;
+        j -= 64;
+    }
+}
+
+// lb (zeroed before the launch): [0] unused, [1] the records' bytes and [4]
+// a copy of state[4] (the chunk's parse error key), written by the last block,
+// [2] != 0: a confidence outside the formatter's range, [3] != 0: a look-back
+// timed out, [5 ..] the status words
+constexpr int FTB = 512;                  // threads (= sites) per block of the one-pass formatter (256: 451 us, 1024: 531 us per 12.5M sites)
+constexpr int FMT_LDS2 = 32 * 1024;       // its record buffer: 4 blocks (32 waves) per CU
+
+__global__ __launch_bounds__(FTB) void sid_fmt_fused_kernel(const char* __restrict__ text, uint64_t len,
+                                                           const uint64_t* __restrict__ starts,
+                                                           const uint64_t* __restrict__ hdr, uint64_t n,
+                                                           const uint8_t* __restrict__ code,
+                                                           const double* __restrict__ hom,
+                                                           const double* __restrict__ het, CType ct,
+                                                           unsigned long long* lb, const uint64_t* state,
+                                                           char* __restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) char buf[FMT_LDS2 + 32];
+    __shared__ double p10[SID_P10_N];
+    __shared__ uint64_t s_excl;
+    load_p10(p10);
+    const uint32_t b = blockIdx.x;
+    const uint64_t i = (uint64_t)b * FTB + threadIdx.x;
+    Reader R{text, len};
+    int l = 0;
+    uint8_t c = 0x40;
+    Head h{0, 0, 0, 0};
+    sid_g6 gh{}, gt{};
+    if (i < n) {
+        c = code[i];
+        if (!(c & 0x40)) {
+            h = site_head(R, starts + i, hdr + 2 * i);
+            gh = sid_g6_prep(hom[i], p10);
+            gt = sid_g6_prep(het[i], p10);
+            l = record_len(h, c, gh, gt, ct.len);
+            if (l < 0) {
+                atomicExch(lb + 2, 1ull);
+                l = 0;
+            }
+        }
+    }
+    uint32_t tot;
+    const uint32_t my = block_exscan<FTB>((uint32_t)l, &tot);
+    unsigned long long* st = lb + 5;
+    // publish this block's byte count first, assemble its records in LDS
+    // (at phase 0), and only then look back: by then the blocks before it
+    // have mostly published too, so one poll usually finds an inclusive count
+    if (threadIdx.x == 0)
+        __hip_atomic_store(st + b, (b == 0 ? LB_INC : LB_AGG) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool staged = tot <= FMT_LDS2;
+    if (staged && l) record_put(R, h, c, gh, gt, ct, buf + my);
+    if (threadIdx.x < 64) {
+        const uint64_t excl = b == 0 ? 0 : lookback(st, b, lb + 3);
+        if (threadIdx.x == 0) {
+            if (b != 0) __hip_atomic_store(st + b, LB_INC | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_excl = excl;
+            if ((uint64_t)(b + 1) * FTB >= n) {   // the last block
+                lb[1] = excl + tot;
+                lb[4] = state[4];
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t base = s_excl;
+    if (!staged) {   // long records (long chromosome names): straight to global
+        if (l) record_put(R, h, c, gh, gt, ct, out + base + my);
+        return;
+    }
+    // 16-B aligned stores: destination window k covers out[g0 + 16k, +16),
+    // i.e. buf[16k - phase, +16); the inner windows read two aligned LDS
+    // quads and shift them by the block-uniform (-phase) & 15 bytes
+    const uint32_t phase = (uint32_t)((uintptr_t)(out + base) & 15u);
+    char* dst = out + base - phase;   // 16-B aligned
+    const uint32_t span = phase + tot;
+    const uint32_t sh = (16u - phase) & 15u, q = sh >> 2, r = sh & 3u;
+    const uint4* B = (const uint4*)buf;
+    for (uint32_t k = threadIdx.x * 16; k < span; k += FTB * 16) {
+        if (k >= phase && k + 16 <= span) {
+            const uint32_t a16 = (k - phase) >> 4;   // quad holding byte k - phase
+            const uint4 lo = B[a16], hi = B[a16 + 1];
+            const uint32_t x0 = q == 0 ? lo.x : q == 1 ? lo.y : q == 2 ? lo.z : lo.w;
+            const uint32_t x1 = q == 0 ? lo.y : q == 1 ? lo.z : q == 2 ? lo.w : hi.x;
+            const uint32_t x2 = q == 0 ? lo.z : q == 1 ? lo.w : q == 2 ? hi.x : hi.y;
+            const uint32_t x3 = q == 0 ? lo.w : q == 1 ? hi.x : q == 2 ? hi.y : hi.z;
+            const uint32_t x4 = q == 0 ? hi.x : q == 1 ? hi.y : q == 2 ? hi.z : hi.w;
+            uint4 v;
+            v.x = __builtin_amdgcn_alignbyte(x1, x0, r);
+            v.y = __builtin_amdgcn_alignbyte(x2, x1, r);
+            v.z = __builtin_amdgcn_alignbyte(x3, x2, r);
+            v.w = __builtin_amdgcn_alignbyte(x4, x3, r);
+            *(uint4*)(dst + k) = v;
+        } else {
+            for (uint32_t j = k; j < k + 16 && j < span; ++j)
+                if (j >= phase) dst[j] = buf[j - phase];
         }
     }
 }
@@ -1686,8 +1839,9 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
     if (sites > W->site_cap) {
         const uint64_t m = std::max<uint64_t>(sites, W->site_cap + W->site_cap / 2);
         for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
-                        (void*)W->bsum, (void*)W->boff, (void*)W->hdr, (void*)W->fb})
+                        (void*)W->bsum, (void*)W->boff, (void*)W->hdr, (void*)W->fb, (void*)W->lb})
             if (p) (void)hipFree(p);
+        W->lb = nullptr;
         W->starts = W->counts = W->hdr = nullptr;
         W->fb = nullptr;
         W->code = nullptr;
@@ -1705,6 +1859,7 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         WCHECK(hipMalloc(&W->het, m * 8));
         WCHECK(hipMalloc(&W->bsum, ((nb * 4 + 7) & ~(size_t)7) + scan_ws_bytes(nb)));
         WCHECK(hipMalloc(&W->boff, (nb + 1) * 8));
+        WCHECK(hipMalloc(&W->lb, (nb + 5) * 8));
         W->site_cap = m;
     }
     return SID_OK;
@@ -1714,7 +1869,7 @@ void sid_chunk_release(sid_chunk_ws* W)
 {
     for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
                     (void*)W->bsum, (void*)W->boff, (void*)W->tcnt, (void*)W->toff, (void*)W->state,
-                    (void*)W->hdr, (void*)W->fb, (void*)W->masks})
+                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb})
         if (p) (void)hipFree(p);
     *W = sid_chunk_ws{};
 }
@@ -1763,36 +1918,24 @@ static int chunk_ctype(const char* conf_type, CType* ct)
     return SID_OK;
 }
 
-// record lengths of the n sites (code/hom/het in the workspace) and their
-// block offsets; state[3] = CSV bytes of the chunk, state[5] != 0: a
-// confidence outside the formatter's range
-int sid_chunk_fmt_len(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type,
-                      hipStream_t st)
-{
-    CType ct;
-    if (chunk_ctype(conf_type, &ct)) return SID_EINVAL;
-    WCHECK(hipMemsetAsync(W->state + 3, 0, sizeof(uint64_t), st));   // ([4] holds the error key)
-    WCHECK(hipMemsetAsync(W->state + 5, 0, sizeof(uint64_t), st));
-    if (n == 0) return SID_OK;
-    const uint64_t nb = (n + TB - 1) / TB;
-    sid_fmt_len_kernel<<<(unsigned)nb, TB, 0, st>>>(base, c1, W->starts, W->hdr, 0, n, W->code, W->hom, W->het, ct, W->bsum,
-                                                    (int*)(W->state + 5));
-    launch_scan(W->bsum, nb, W->boff, W->state + 3, nullptr,
-                (uint64_t*)((char*)W->bsum + ((nb * 4 + 7) & ~(size_t)7)), st);
-    WCHECK(hipGetLastError());
-    return SID_OK;
-}
+// a record is its chrom plus at most 64 bytes (call.hpp:29-38: an int
+// position of <= 11 characters, two %g fields of <= 13, a conf_type of <= 15,
+// six separators and "hom"/"het" + two bases), and the chroms are bytes of
+// their lines
+uint64_t sid_chunk_fmt_bound(uint64_t n, uint64_t text_bytes) { return 64 * n + text_bytes + 64; }
 
-// the chunk's records into out (state[3] bytes, 16-B aligned buffer)
-int sid_chunk_fmt_write(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
-                        hipStream_t st)
+int sid_chunk_fmt(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
+                  hipStream_t st)
 {
     CType ct;
     if (chunk_ctype(conf_type, &ct)) return SID_EINVAL;
-    if (n == 0) return SID_OK;
-    const uint64_t nb = (n + TB - 1) / TB;
-    sid_fmt_write_kernel<<<(unsigned)nb, TB, 0, st>>>(base, c1, W->starts, W->hdr, 0, n, W->code, W->hom, W->het, ct, W->boff,
-                                                      0, out);
+    if (n > W->site_cap) return SID_EINVAL;
+    const uint64_t nb = (n + FTB - 1) / FTB;
+    WCHECK(hipMemsetAsync(W->lb, 0, (nb + 5) * 8, st));
+    if (n == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
+                           ? SID_OK : SID_EHIP;
+    sid_fmt_fused_kernel<<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->code, W->hom, W->het, ct,
+                                                      W->lb, W->state, out);
     WCHECK(hipGetLastError());
     return SID_OK;
 }
