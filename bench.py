@@ -267,8 +267,8 @@ def main():
 
 
 STAGE_KERNELS = {
-    "index": ["sid_lines_count_kernel", "sid_scan_*"],
-    "parse": ["sid_lines_emit_kernel", "sid_parse_kernel"],
+    "index": ["sid_index_count_kernel", "sid_scan_*"],
+    "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_serial_kernel"],
     "call": ["sid_local_table_p2", "sid_local_fixup"],
     "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
     "fmt_write": ["sid_fmt_fused_kernel"],
