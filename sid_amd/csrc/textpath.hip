@@ -279,9 +279,10 @@ __global__ __launch_bounds__(TB) void sid_lines_emit_kernel(const char* __restri
 }
 
 // Line index of a chunk (the engine's path), two passes over 16 KiB tiles:
-//   sid_index_count_kernel  4 lane-contiguous 4 KiB sub-tiles per block, one
+//   sid_index_count_kernel  4 lane-contiguous 4 KiB sub-tiles per tile, one
 //                           16-B load per lane each (4 loads in flight per
-//                           lane; 8 measured slower): line-start masks (u16
+//                           lane, the next tile's 4 issued before this one is
+//                           counted; 8 measured slower): line-start masks (u16
 //                           per lane and sub-tile, 1/8 of the text) and the
 //                           tile's count
 //   (scan of the tile counts -> tile offsets, state[0] = sites)
@@ -291,28 +292,86 @@ __global__ __launch_bounds__(TB) void sid_lines_emit_kernel(const char* __restri
 constexpr int IX_SUB = 4;
 constexpr uint64_t IX_TILE = (uint64_t)TILE * IX_SUB;   // 16 KiB
 
+// the 16 bytes of a lane's window and, for a wave's first lane, the byte
+// before it (1 when there is none: the window starts the range)
+struct IxWin {
+    uint4 v;
+    uint32_t prev;
+};
+__device__ __forceinline__ IxWin ix_load(const char* __restrict__ text, uint64_t at, uint64_t c0, uint64_t c1)
+{
+    IxWin w{make_uint4(0, 0, 0, 0), 1u};
+    if (at < c1 && at + 16 > c0) w.v = *(const uint4*)(text + at);
+    if ((threadIdx.x & 63) == 0 && at > c0 && at - 1 < c1) w.prev = text[at - 1] == '\n';
+    return w;
+}
+// line_start_mask's arithmetic on a loaded window
+__device__ __forceinline__ uint32_t ix_mask(const IxWin& w, uint64_t at, uint64_t c0, uint64_t c1)
+{
+    const uint4 v = w.v;
+    uint32_t nl = compress4(eq_bytes(v.x, 0x0A0A0A0Au)) | (compress4(eq_bytes(v.y, 0x0A0A0A0Au)) << 4) |
+                  (compress4(eq_bytes(v.z, 0x0A0A0A0Au)) << 8) | (compress4(eq_bytes(v.w, 0x0A0A0A0Au)) << 12);
+    uint32_t prev = (uint32_t)__shfl_up((int)(nl >> 15), 1, 64);
+    if ((threadIdx.x & 63) == 0) prev = w.prev;
+    uint32_t m = ((nl << 1) | prev) & ~nl & 0xFFFFu;
+    if (at + 16 > c0 && at <= c0) {
+        const uint32_t j = (uint32_t)(c0 - at);
+        m = (m | ((1u << j) & ~nl)) & ~((1u << j) - 1u);
+    }
+    if (at + 16 > c1) m &= c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
+    if (at + 16 <= c0) m = 0;
+    return m;
+}
+
+// Blocks stride over the tiles (a fixed grid of a few per CU), the next
+// tile's four windows per lane in flight while this one is counted; the tile
+// count is a block reduction (two LDS slots alternate: one barrier a tile).
 __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restrict__ text, uint64_t tile_base,
-                                                             uint64_t c0, uint64_t c1, uint16_t* __restrict__ masks,
+                                                             uint64_t c0, uint64_t c1, uint64_t ntiles,
+                                                             uint16_t* __restrict__ masks,
                                                              uint32_t* __restrict__ cnt, uint64_t* __restrict__ state)
 {
-    const uint64_t t0 = tile_base + (uint64_t)blockIdx.x * IX_TILE;
-    uint32_t m[IX_SUB];
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < IX_SUB; ++k) {
-        m[k] = line_start_mask(text, t0 + (uint64_t)k * TILE, c0, c1);
-        c += __popc(m[k]);
+    __shared__ uint32_t red[2][TB / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // the scan's running base, and no parse error yet
+        state[0] = 0;
+        state[4] = ~0ull;
     }
-    uint16_t* mo = masks + (uint64_t)blockIdx.x * (IX_SUB * TB) + threadIdx.x;
+    uint64_t t = blockIdx.x;
+    IxWin w[IX_SUB];
+    if (t < ntiles) {
 #pragma unroll
-    for (int k = 0; k < IX_SUB; ++k) mo[k * TB] = (uint16_t)m[k];
-    uint32_t tot;
-    block_exscan(c, &tot);
-    if (threadIdx.x == 0) {
-        cnt[blockIdx.x] = tot;
-        if (blockIdx.x == 0) {   // the scan's running base, and no parse error yet
-            state[0] = 0;
-            state[4] = ~0ull;
+        for (int k = 0; k < IX_SUB; ++k)
+            w[k] = ix_load(text, tile_base + t * IX_TILE + (uint64_t)k * TILE + threadIdx.x * 16, c0, c1);
+    }
+    for (int par = 0; t < ntiles; t += gridDim.x, par ^= 1) {
+        const uint64_t t0 = tile_base + t * IX_TILE;
+        IxWin cur[IX_SUB];
+#pragma unroll
+        for (int k = 0; k < IX_SUB; ++k) cur[k] = w[k];
+        const uint64_t tn = t + gridDim.x;
+        if (tn < ntiles) {
+#pragma unroll
+            for (int k = 0; k < IX_SUB; ++k)
+                w[k] = ix_load(text, tile_base + tn * IX_TILE + (uint64_t)k * TILE + threadIdx.x * 16, c0, c1);
+        }
+        uint32_t c = 0;
+        uint16_t* mo = masks + t * (IX_SUB * TB) + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < IX_SUB; ++k) {
+            const uint32_t m = ix_mask(cur[k], t0 + (uint64_t)k * TILE + threadIdx.x * 16, c0, c1);
+            c += __popc(m);
+            mo[k * TB] = (uint16_t)m;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+        if (lane == 0) red[par][wid] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+#pragma unroll
+            for (int k = 0; k < TB / 64; ++k) tot += red[par][k];
+            cnt[t] = tot;
         }
     }
 }
@@ -1886,7 +1945,9 @@ int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
         WCHECK(hipMemsetAsync(W->state + 4, 0xFF, sizeof(uint64_t), st));
         return SID_OK;
     }
-    sid_index_count_kernel<<<(unsigned)ntiles, TB, 0, st>>>(base, t0, c0, c1, W->masks, W->tcnt, W->state);
+    static const unsigned IX_GRID = std::getenv("SID_IX_GRID") ? (unsigned)std::atoi(std::getenv("SID_IX_GRID")) : 4096;   // 512: 1.89, 1024: 1.25, 2048: 0.99, 4096: 0.97 ms per 50M sites
+    const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, std::max(1u, IX_GRID));
+    sid_index_count_kernel<<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state);
     launch_scan(W->tcnt, ntiles, W->toff, W->state, W->state + 1,
                 (uint64_t*)((char*)W->tcnt + ((ntiles * 4 + 7) & ~(size_t)7)), st);
     WCHECK(hipGetLastError());
