@@ -19,8 +19,7 @@ STAGES = {
     "index": ["sid_index_count_kernel", "sid_scan_reduce_kernel", "sid_scan_top_kernel", "sid_scan_down_kernel"],
     "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_serial_kernel"],
     "call": ["sid_local_table_p2", "sid_local_table_x1", "sid_local_fixup"],
-    "fmt_len": ["sid_fmt_len_kernel"],
-    "fmt_write": ["sid_fmt_write_kernel"],
+    "fmt_write": ["sid_fmt_fused_kernel"],
 }
 
 
@@ -32,15 +31,13 @@ def main():
     pm = json.load(open(tmp))
     b = json.load(open(bench))
     sites = b["roofline"]["sites_per_launch"]
-    # the scans run twice per chunk (index and fmt_len): their bytes are shared
     for stage, ks in STAGES.items():
         tot, parts = 0.0, {}
         for k in ks:
             r = pm.get(k)
             if not r or "hbm_bytes" not in r:
                 continue
-            share = 0.5 if k.startswith("sid_scan_") else 1.0
-            parts[k] = r["hbm_bytes"] * share
+            parts[k] = r["hbm_bytes"]
             tot += parts[k]
         if not parts:
             continue
