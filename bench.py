@@ -81,6 +81,7 @@ def parse_args():
                    help="alias: local = C2, likelihood_ratio = C3")
     p.add_argument("--sites", type=int, default=None, help="override: sites per GPU (C2/C3) or in total (C4/C5)")
     p.add_argument("--chunk-mib", type=int, default=0, help="engine chunk size (0 = 128 MiB)")
+    p.add_argument("--lanes", type=int, default=2, help="engine pipelines per GPU (concurrent streams)")
     p.add_argument("--no-extras", action="store_true", help="skip kernel_local, e2e and cpu_baseline")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--allow-shared-gpu", action="store_true",
@@ -154,13 +155,18 @@ def main():
         text[ln:ln + 512].zero_()
         torch.cuda.synchronize(dev)
         ctx.close()
+    lynch = cfg["method"] != "local" or cfg["R"]
+    # two pipelines per GPU for -m local (C2 5.51 -> 5.37 ms/step); one for the
+    # Lynch paths (their per-chunk histogram syncs and the lanes' table merge
+    # cost more: C3 6.95 -> 8.51 ms), where the multi-rank exchange also reads
+    # one context
+    lanes = 1 if lynch else max(1, a.lanes)
     eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=gpu,
-                         chunk_bytes=a.chunk_mib << 20, device_sink=1)
+                         chunk_bytes=a.chunk_mib << 20, device_sink=1, lanes=lanes)
     if cfg["resident"]:
         eng.source_device_text(text.data_ptr(), ln, keep=text)
     else:
         eng.source_synth(cfg["seed"], n, cfg["depth"], first=first, sites_per_chrom=cfg["spc"], on_device=True)
-    lynch = cfg["method"] != "local" or cfg["R"]
     est_box = {}
 
     def step():
@@ -239,7 +245,7 @@ def main():
                        "text_bytes_rank0": text_bytes, "csv_bytes_rank0": st2.bytes_out,
                        "parallelism": f"site-range shards x{world}" + (" + RCCL histogram all-gather"
                                                                        if lynch and world > 1 else ""),
-                       "ranks": world, "oversubscribed": oversub},
+                       "ranks": world, "oversubscribed": oversub, "engine_lanes_per_gpu": lanes},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"engine stage '{dom}'", "stage_kernels": STAGE_KERNELS[dom],

@@ -265,7 +265,8 @@ int sid_format_g6_device(sid_ctx* ctx, const double* values, size_t n, char* out
  *   [second pass over the chunks not formatted yet: parse, call / lookup,
  *    format] --D2H (pinned ring)--> write() in file order
  *
- * Chunk j runs on device j % devices; every device formats and copies back
+ * Chunk j runs on pipeline j % (devices x lanes) (pipeline i on GPU i / lanes);
+ * every pipeline formats and copies back
  * concurrently and one writer keeps file order.  As in the reference, no
  * record is written before the whole input has parsed: the first malformed
  * line in file order is reported (its input byte offset in err_offset) and
@@ -297,6 +298,10 @@ typedef struct {
                                nothing is copied back (measurement); 2: records
                                copied back to pinned host memory and dropped
                                (measurement of the PCIe path, no write)          */
+    int lanes;              /* pipelines per GPU (0 = 1): each its own streams,
+                               context and workspace, chunks dealt over all of
+                               them, so one chunk's kernels run while another
+                               waits on its host sync                            */
 } sid_engine_cfg;
 typedef struct {
     uint64_t sites;              /* non-empty lines parsed                           */

@@ -60,7 +60,7 @@ class EngineCfg(C.Structure):
     """sid_engine_cfg (include/sid.h, streaming engine)."""
     _fields_ = [("devices", C.c_int), ("first_device", C.c_int), ("chunk_bytes", C.c_uint64),
                 ("slots", C.c_int), ("hold_bytes", C.c_uint64), ("retain_bytes", C.c_uint64),
-                ("host_threads", C.c_int), ("verbose", C.c_int), ("device_sink", C.c_int)]
+                ("host_threads", C.c_int), ("verbose", C.c_int), ("device_sink", C.c_int), ("lanes", C.c_int)]
 
 
 class RunStats(C.Structure):
@@ -438,13 +438,13 @@ class Engine:
     line-aligned chunks over one or more devices."""
 
     def __init__(self, method="local", devices=1, first_device=0, chunk_bytes=0, slots=0, hold_bytes=0,
-                 retain_bytes=0, host_threads=0, verbose=False, device_sink=False, **opts):
+                 retain_bytes=0, host_threads=0, verbose=False, device_sink=False, lanes=0, **opts):
         self.opts = make_opts(method=method, **opts)
         cfg = EngineCfg()
         lib().sid_engine_cfg_default(C.byref(cfg))
         cfg.devices, cfg.first_device, cfg.chunk_bytes, cfg.slots = devices, first_device, chunk_bytes, slots
         cfg.hold_bytes, cfg.retain_bytes, cfg.host_threads = hold_bytes, retain_bytes, host_threads
-        cfg.verbose, cfg.device_sink = int(bool(verbose)), int(device_sink)
+        cfg.verbose, cfg.device_sink, cfg.lanes = int(bool(verbose)), int(device_sink), lanes
         self.cfg = cfg
         h = C.c_void_p()
         check(lib().sid_engine_create(C.byref(self.opts), C.byref(cfg), C.byref(h)), "sid_engine_create")

@@ -506,12 +506,14 @@ extern "C" int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg
     sid_engine* e = new sid_engine();
     if (opts) e->opts = *opts; else sid_opts_default(&e->opts);
     if (cfg) e->cfg = *cfg; else sid_engine_cfg_default(&e->cfg);
-    const int D = e->cfg.devices > 0 ? e->cfg.devices : nvis;
+    const int G = e->cfg.devices > 0 ? e->cfg.devices : nvis;
+    const int lanes = std::max(1, e->cfg.lanes);
+    const int D = G * lanes;   // pipelines
     const int R = e->cfg.slots > 0 ? e->cfg.slots : 3;
     for (int i = 0; i < D; ++i) {
         auto d = std::make_unique<Dev>();
         d->index = i;
-        d->device = (e->cfg.first_device + i) % nvis;
+        d->device = (e->cfg.first_device + i / lanes) % nvis;
         d->pool.device = d->device;
         int rc = sid_create(d->device, &e->opts, &d->ctx);
         hipError_t x = hipSuccess;
@@ -679,7 +681,9 @@ extern "C" int sid_engine_source_device_text(sid_engine* e, const char* d_text, 
         e->recs.push_back(r);
         at = c;
     }
-    for (auto& r : e->recs) r.dev = 0;   // the text lives on the first device
+    // the text lives on the first GPU: its pipelines take the chunks in turn
+    const int lanes = std::max(1, e->cfg.lanes);
+    for (size_t j = 0; j < e->recs.size(); ++j) e->recs[j].dev = (int)(j % std::min<size_t>(lanes, e->devs.size()));
     return SID_OK;
 }
 
@@ -1204,8 +1208,10 @@ static int setup_budgets(sid_engine* e)
         size_t fr = 0, tot = 0;
         if (hipMemGetInfo(&fr, &tot) != hipSuccess) return SID_EHIP;
         const uint64_t avail = fr + d.pool.bytes() + d.arena_bytes();   // pooled buffers and the arena are reusable
-        d.hold_budget = e->cfg.hold_bytes ? e->cfg.hold_bytes : (uint64_t)(avail * 0.40);
-        d.retain_budget = e->cfg.retain_bytes ? e->cfg.retain_bytes : (uint64_t)(avail * 0.40);
+        // the GPU's pipelines share its memory (avail: what this one sees free)
+        const double share = 0.40 / std::max(1, e->cfg.lanes);
+        d.hold_budget = e->cfg.hold_bytes ? e->cfg.hold_bytes : (uint64_t)(avail * share);
+        d.retain_budget = e->cfg.retain_bytes ? e->cfg.retain_bytes : (uint64_t)(avail * share);
     }
     return SID_OK;
 }
