@@ -225,3 +225,22 @@ def test_c4_layout_slice_across_devices(sid, oracle, tmp_path):
     a = run(sid.CLI_PATH, ["--devices", "8", "--chunk-bytes", str(4 << 20), str(p)])
     assert a.returncode == 0, a.stderr
     assert a.stdout == ref.stdout
+
+
+@pytest.mark.parametrize("lanes,source", [(2, "text"), (3, "device"), (2, "synth_device")])
+@pytest.mark.parametrize("method", ["local", "likelihood_ratio"])
+def test_engine_lanes_agree_with_oracle(sid, oracle, tmp_path, lanes, source, method):
+    """Several pipelines per GPU (own streams, contexts, workspaces; chunks
+    dealt over all of them; the Lynch histograms of the lanes merged) write the
+    oracle's CSV, in file order."""
+    n, seed, depth, spc = 50_000, 21, 30.0, 20_000
+    text = sid.synth_text(seed, n, depth, first=3, sites_per_chrom=spc)
+    p = tmp_path / "l.plp"
+    p.write_bytes(text)
+    flags = [] if method == "local" else ["-R", "-m", method]
+    ref = oracle.run_cli(flags + [str(p)])
+    assert ref.returncode == 0
+    out, st = engine_csv(sid, method, source, text, n=n, seed=seed, depth=depth, first=3, spc=spc,
+                         chunk_bytes=256 << 10, estimate_prior=method != "local", lanes=lanes)
+    assert st.sites == n and st.chunks >= 2 * lanes
+    assert out == ref.stdout
