@@ -81,7 +81,9 @@ def parse_args():
                    help="alias: local = C2, likelihood_ratio = C3")
     p.add_argument("--sites", type=int, default=None, help="override: sites per GPU (C2/C3) or in total (C4/C5)")
     p.add_argument("--chunk-mib", type=int, default=0, help="engine chunk size (0 = 128 MiB)")
-    p.add_argument("--lanes", type=int, default=2, help="engine pipelines per GPU (concurrent streams)")
+    p.add_argument("--lanes", type=int, default=1,
+                   help="engine pipelines per GPU (concurrent streams; their kernels overlap, so the per-stage "
+                        "event times of the roofline are only clean at 1)")
     p.add_argument("--no-extras", action="store_true", help="skip kernel_local, e2e and cpu_baseline")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--allow-shared-gpu", action="store_true",
@@ -156,10 +158,10 @@ def main():
         torch.cuda.synchronize(dev)
         ctx.close()
     lynch = cfg["method"] != "local" or cfg["R"]
-    # two pipelines per GPU for -m local (C2 5.51 -> 5.37 ms/step); one for the
-    # Lynch paths (their per-chunk histogram syncs and the lanes' table merge
-    # cost more: C3 6.95 -> 8.51 ms), where the multi-rank exchange also reads
-    # one context
+    # one pipeline per GPU: with 2 GiB chunks a second one measured no gain
+    # for -m local (5.50-5.54 vs 5.51-5.59 ms/step) and a loss for the Lynch
+    # paths (per-chunk histogram syncs, the lanes' table merge: C3 6.95 ->
+    # 8.51 ms), whose multi-rank exchange also reads one context
     lanes = 1 if lynch else max(1, a.lanes)
     eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=gpu,
                          chunk_bytes=a.chunk_mib << 20, device_sink=1, lanes=lanes)
