@@ -7,7 +7,10 @@ export TMPDIR=/tmp
 run() {  # name, timeout, args...
   local n=$1 t=$2; shift 2
   timeout -k 10 $t "$@" > $O/$n.json 2> $O/$n.err || { echo "$n failed rc=$?"; tail -8 $O/$n.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/$n.json')); print('$n', 'value=%.4g' % d['value'], 'ms=%.2f' % d['ms_per_step'], d.get('n_gpus'), {k: round(v, 2) for k, v in d['stages_ms'].items()})"
+  python3 -c "
+import json
+d = json.loads([l for l in open('$O/$n.json') if l.startswith('{')][-1])
+print('$n', 'value=%.4g' % d['value'], 'ms=%.2f' % d['ms_per_step'], d.get('n_gpus'), {k: round(v, 2) for k, v in d['stages_ms'].items()})"
 }
 run bench_c3 300 python3 -u bench.py --config C3 --steps 10 --no-cpu
 run bench_c4 400 python3 -u bench.py --config C4 --steps 2 --warmup 1
