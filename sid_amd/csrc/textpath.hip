@@ -283,13 +283,15 @@ __global__ __launch_bounds__(TB) void sid_lines_emit_kernel(const char* __restri
 //                           16-B load per lane each (4 loads in flight per
 //                           lane, the next tile's 4 issued before this one is
 //                           counted; 8 measured slower): line-start masks (u16
-//                           per lane and sub-tile, 1/8 of the text) and the
+//                           per lane and sub-tile, a lane's four in one 8-B
+//                           word; 1/8 of the text) and the
 //                           tile's count
 //   (scan of the tile counts -> tile offsets, state[0] = sites)
 //   sid_index_emit_kernel   the offsets of every line start, from the masks
 // (A single pass with a decoupled look-back was measured 25x slower: the
 // prefix chain crosses XCDs, whose L2s only meet in memory, ~0.4 us a link.)
-constexpr int IX_SUB = 4;
+constexpr int IX_SUB = 4;   // (a lane's IX_SUB 16-bit masks share one 8-B word)
+static_assert(IX_SUB == 4, "masks are packed four to a u64");
 constexpr uint64_t IX_TILE = (uint64_t)TILE * IX_SUB;   // 16 KiB
 
 // the 16 bytes of a lane's window and, for a wave's first lane, the byte
@@ -356,13 +358,14 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
                 w[k] = ix_load(text, tile_base + tn * IX_TILE + (uint64_t)k * TILE + threadIdx.x * 16, c0, c1);
         }
         uint32_t c = 0;
-        uint16_t* mo = masks + t * (IX_SUB * TB) + threadIdx.x;
+        uint64_t mw = 0;   // the lane's four sub-tile masks in one 8-B word
 #pragma unroll
         for (int k = 0; k < IX_SUB; ++k) {
             const uint32_t m = ix_mask(cur[k], t0 + (uint64_t)k * TILE + threadIdx.x * 16, c0, c1);
             c += __popc(m);
-            mo[k * TB] = (uint16_t)m;
+            mw |= (uint64_t)m << (16 * k);
         }
+        ((uint64_t*)masks)[t * TB + threadIdx.x] = mw;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
         if (lane == 0) red[par][wid] = c;
@@ -377,27 +380,33 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
 }
 
 __global__ __launch_bounds__(TB) void sid_index_emit_kernel(const uint16_t* __restrict__ masks, uint64_t tile_base,
-                                                            const uint64_t* __restrict__ toff,
+                                                            uint64_t ntiles, const uint64_t* __restrict__ toff,
                                                             uint64_t* __restrict__ starts)
 {
-    const uint16_t* mi = masks + (uint64_t)blockIdx.x * (IX_SUB * TB) + threadIdx.x;
-    uint32_t m[IX_SUB];
+    // blocks stride over the tiles as in the count kernel, the next tile's
+    // masks loaded ahead (measured the same as a block per tile: 137 vs 140 us
+    // per 2 GiB chunk; the scattered 8-B offset stores set its pace)
+    uint64_t t = blockIdx.x;
+    uint64_t mw_next = t < ntiles ? ((const uint64_t*)masks)[t * TB + threadIdx.x] : 0;
+    for (; t < ntiles; t += gridDim.x) {
+        const uint64_t mw = mw_next;
+        const uint64_t tn = t + gridDim.x;
+        if (tn < ntiles) mw_next = ((const uint64_t*)masks)[tn * TB + threadIdx.x];
+        uint32_t m[IX_SUB];
 #pragma unroll
-    for (int k = 0; k < IX_SUB; ++k) m[k] = mi[k * TB];
-    uint64_t o = toff[blockIdx.x];
-    const uint64_t t0 = tile_base + (uint64_t)blockIdx.x * IX_TILE;
-#pragma unroll
-    for (int g = 0; g < IX_SUB; g += 4) {   // four sub-tiles per block scan: 16-bit fields stay < 2^16
+        for (int k = 0; k < IX_SUB; ++k) m[k] = (uint32_t)(mw >> (16 * k)) & 0xFFFFu;
+        uint64_t o = toff[t];
+        const uint64_t t0 = tile_base + t * IX_TILE;
         uint64_t packed = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) packed |= (uint64_t)__popc(m[g + k]) << (16 * k);
+        for (int k = 0; k < IX_SUB; ++k) packed |= (uint64_t)__popc(m[k]) << (16 * k);
         uint64_t tot;
-        const uint64_t pre = block_exscan64(packed, &tot);
+        const uint64_t pre = block_exscan64(packed, &tot);   // four sub-tiles: 16-bit fields stay < 2^16
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < IX_SUB; ++k) {
             uint64_t q = o + ((pre >> (16 * k)) & 0xFFFF);
-            const uint64_t at = t0 + (uint64_t)(g + k) * TILE + (uint64_t)threadIdx.x * 16;
-            uint32_t mk = m[g + k];
+            const uint64_t at = t0 + (uint64_t)k * TILE + (uint64_t)threadIdx.x * 16;
+            uint32_t mk = m[k];
             while (mk) {
                 const int j = __ffs(mk) - 1;
                 starts[q++] = at + j;
@@ -1933,6 +1942,15 @@ void sid_chunk_release(sid_chunk_ws* W)
     *W = sid_chunk_ws{};
 }
 
+// blocks of the strided index kernels (SID_IX_GRID; count kernel, index stage
+// per 50M sites: 512 blocks 1.89, 1024 1.25, 2048 0.99, 4096 0.97 ms)
+static unsigned ix_grid()
+{
+    static const unsigned g = std::getenv("SID_IX_GRID") ? (unsigned)std::max(1, std::atoi(std::getenv("SID_IX_GRID")))
+                                                         : 4096u;
+    return g;
+}
+
 // line starts of [c0, c1): masks and per-tile counts, scan; state[0] = sites
 // (the caller reads it back), state[1..2] = [0, sites), state[4] = no error yet
 int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, hipStream_t st)
@@ -1945,8 +1963,7 @@ int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
         WCHECK(hipMemsetAsync(W->state + 4, 0xFF, sizeof(uint64_t), st));
         return SID_OK;
     }
-    static const unsigned IX_GRID = std::getenv("SID_IX_GRID") ? (unsigned)std::atoi(std::getenv("SID_IX_GRID")) : 4096;   // 512: 1.89, 1024: 1.25, 2048: 0.99, 4096: 0.97 ms per 50M sites
-    const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, std::max(1u, IX_GRID));
+    const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, ix_grid());
     sid_index_count_kernel<<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state);
     launch_scan(W->tcnt, ntiles, W->toff, W->state, W->state + 1,
                 (uint64_t*)((char*)W->tcnt + ((ntiles * 4 + 7) & ~(size_t)7)), st);
@@ -1963,7 +1980,8 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     if (n == 0) return SID_OK;
     const uint64_t t0 = c0 & ~(uint64_t)15;
     const uint64_t ntiles = (c1 - t0 + IX_TILE - 1) / IX_TILE;
-    sid_index_emit_kernel<<<(unsigned)ntiles, TB, 0, st>>>(W->masks, t0, W->toff, W->starts);
+    sid_index_emit_kernel<<<(unsigned)std::min<uint64_t>(ntiles, ix_grid()), TB, 0, st>>>(W->masks, t0, ntiles,
+                                                                                          W->toff, W->starts);
     launch_parse(base, c1, W->starts, W->state + 1, n, W->counts, W->hdr, W->fb,
                  (unsigned long long*)(W->state + 6), (unsigned long long*)(W->state + 4), qmode, st);
     WCHECK(hipGetLastError());
