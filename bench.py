@@ -252,7 +252,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"engine stage '{dom}'", "stage_kernels": STAGE_KERNELS[dom],
                          "launch_ms": launch_ms, "sites_per_launch": per_launch_sites,
-                         "bytes_per_site": bps},
+                         "bytes_per_site": bps, "valu": valu_issue(dom, per_launch_sites, launch_ms)},
             "stages_ms": stages,
             "path": {"bytes_per_site": tps + cps, "text_per_site": tps, "csv_per_site": cps,
                      "GBps": step_bytes / (elapsed / a.steps) / 1e9 if text_bytes else None,
@@ -281,6 +281,32 @@ STAGE_KERNELS = {
     "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
     "fmt_write": ["sid_fmt_fused_kernel"],
 }
+
+
+VALU_ISSUE_PER_S = 256 * 4 / 2 * 2.4e9   # wave64 VALU instructions/s: 1024 SIMDs, one per 2 cycles, 2.4 GHz
+
+
+def valu_issue(stage, sites, launch_ms):
+    """The stage's VALU work against the chip's VALU issue rate: SQ_INSTS_VALU
+    per site of its kernels (profiles/pmc_c2_r02_summary.json, the committed
+    PMC pass of tools/gpu_pmc_c2.sh) x the sites of a launch, at one wave64
+    instruction per SIMD per 2 cycles (MI355X_MICROARCH.md); None when absent."""
+    try:
+        pm = json.load(open(os.path.join(ROOT, "profiles", "pmc_c2_r02_summary.json")))
+        sites_pmc = json.load(open(os.path.join(ROOT, "profiles", f"pmc_{stage}_r02.json")))["sites_per_launch"]
+    except Exception:
+        return None
+    insts = 0.0
+    for k in STAGE_KERNELS[stage]:
+        for name, r in pm.items():
+            if name.startswith(k.rstrip("*")) and "SQ_INSTS_VALU" in r:
+                insts += r["SQ_INSTS_VALU"] / sites_pmc
+    if not insts:
+        return None
+    per_launch = insts * sites
+    issue_ms = per_launch / VALU_ISSUE_PER_S * 1e3
+    return {"insts_per_launch": per_launch, "issue_bound_ms": issue_ms, "frac": issue_ms / launch_ms,
+            "note": "VALU instructions of the stage's kernels (PMC) at the chip's issue rate vs the measured launch"}
 
 
 def pmc_traffic(stage, sites):
