@@ -734,16 +734,17 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
         const uint4 v = vn;
         vn = *(const uint4*)(text + a + 16);   // the next window in flight while this one is processed
         const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-        const uint64_t room = len > a ? len - a : 0;   // bytes of this window inside the text
+        // bytes of this window inside [q, len) as 16 bits, once per window
+        const uint32_t room = len > a ? (uint32_t)min(len - a, (uint64_t)16) : 0u;
+        const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t x = ws[k];
             const int b0 = 4 * k;
-            // bytes of this word inside [q, len) and not after the token's end
-            const int lo_b = (int)lead - b0;                                    // first byte from the lead
-            const int hi_b = room >= (uint64_t)(b0 + 4) ? 4 : (int)room - b0;   // bytes before the end
-            uint32_t vm = lo_b <= 0 ? 0x80808080u : (lo_b >= 4 ? 0u : (0x80808080u << (8 * lo_b)));
-            vm &= hi_b >= 4 ? 0xFFFFFFFFu : (hi_b <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - hi_b))));
+            // the word's 4 valid bits as bit 7 of its bytes (24-bit multiply;
+            // the partial products are disjoint: no carries)
+            uint32_t vm = ((((valid >> b0) & 15u) * 0x00204081u) & 0x01010101u) << 7;
+            const int hi_b = (int)room - b0;   // bytes of this word before the end of the text (< 4: the last)
             vm = done ? 0u : vm;
             const uint32_t lo = low_bytes(x) & vm;
             const uint32_t first = lo & (0u - lo);                  // the token's end, if in this word
