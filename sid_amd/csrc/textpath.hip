@@ -671,18 +671,26 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     *(uint4*)(stage + 16) = v1;
     *(uint4*)(stage + 32) = v2;
     const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
-    uint64_t S = 0, L = 0;
+    // S: separator bytes as a 48-bit mask; fbad: window offset of the first
+    // control byte ('\n', NUL, < 0x20 but '\t') at or after the line's start
+    // (per word, no second compressed mask)
+    uint64_t S = 0;
+    uint32_t fbad = 64;
+    const uint32_t from = (0xFFFFu << sh) & 0xFFFFu;   // the line's bytes among the first 16
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
-        S |= (uint64_t)compress4(eq_bytes(w[k], 0x20202020u) | eq_bytes(w[k], 0x09090909u)) << (4 * k);
-        L |= (uint64_t)compress4(low_bytes(w[k])) << (4 * k);
+        const uint32_t sp = eq_bytes(w[k], 0x20202020u) | eq_bytes(w[k], 0x09090909u);
+        S |= (uint64_t)compress4(sp) << (4 * k);
+        uint32_t bl = low_bytes(w[k]) & ~sp;
+        if (k < 4) bl &= (__umul24((from >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) << 7;
+        const uint32_t f = (uint32_t)__ffs(bl);
+        fbad = min(fbad, f ? 4u * k + ((f - 1u) >> 3) : 64u);
     }
     // bit j = byte s0 + j, for the bytes inside the text and the 48 staged
     const uint64_t avail = len > s0 ? len - s0 : 0;
     const uint32_t nb = (uint32_t)min((uint64_t)(HDR_BYTES - sh), avail);
     const uint64_t valid = nb >= 64 ? ~0ull : ((1ull << nb) - 1);
     S = (S >> sh) & valid;
-    L = (L >> sh) & valid;
     const uint64_t N = ~S & valid;
     uint64_t T = N & ~(N << 1);   // token starts
     const int t0 = ctz64(T);
@@ -694,7 +702,7 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     T &= T - 1;
     const int t4 = ctz64(T);
     bool ok = t4 < (int)nb;                                          // token 4 starts inside the staged bytes
-    ok = ok && ((L & ~S) & ((1ull << (t4 & 63)) - 1)) == 0;          // no '\n', NUL, control byte before it
+    ok = ok && fbad - sh >= (uint32_t)t4;                            // no '\n', NUL, control byte before it
     ok = ok && ((S >> ((t2 + 1) & 63)) & 1);                         // token 2 is one byte
     if (!ok) return false;
     const int l0 = ctz64(S >> t0);
@@ -743,7 +751,7 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
             const int b0 = 4 * k;
             // the word's 4 valid bits as bit 7 of its bytes (24-bit multiply;
             // the partial products are disjoint: no carries)
-            uint32_t vm = ((((valid >> b0) & 15u) * 0x00204081u) & 0x01010101u) << 7;
+            uint32_t vm = (__umul24((valid >> b0) & 15u, 0x00204081u) & 0x01010101u) << 7;
             const int hi_b = (int)room - b0;   // bytes of this word before the end of the text (< 4: the last)
             vm = done ? 0u : vm;
             const uint32_t lo = low_bytes(x) & vm;
