@@ -643,6 +643,23 @@ __device__ __forceinline__ int ctz64(uint64_t x) { return x ? __builtin_ctzll(x)
 
 constexpr int HDR_BYTES = 48;   // bytes staged per lane for the header (3 aligned windows)
 
+// 8 bytes from a lane's staged header at any offset < HDR_BYTES + 16: two
+// aligned 8-B LDS reads and a funnel shift (past the lane's 48 bytes: the next
+// lane's, or the block's padding -- garbage, masked by the caller)
+__device__ __forceinline__ uint64_t stage_u64(const char* stage, uint32_t off)
+{
+    const uint32_t a = off & ~7u, r = off & 7u;
+    const uint64_t lo = *(const uint64_t*)(stage + a), hi = *(const uint64_t*)(stage + a + 8);
+    return r ? (lo >> (8 * r)) | (hi << (64 - 8 * r)) : lo;
+}
+// bit 7 of each byte of x that is not an ASCII digit
+__device__ __forceinline__ uint32_t not_digit(uint32_t x)
+{
+    const uint32_t lt30 = ~(((x & 0x7F7F7F7Fu) + 0x50505050u) | x) & 0x80808080u;   // b < '0'
+    const uint32_t lt3a = ~(((x & 0x7F7F7F7Fu) + 0x46464646u) | x) & 0x80808080u;   // b < ':'
+    return lt30 | (~lt3a & 0x80808080u);
+}
+
 // The fast path of one line (pileup.cpp:13-46 + :70-153 for the lines that
 // need none of the general routine's cases), branch-free over SWAR byte masks:
 //   header   the 48 bytes from the line's 16-B window: separator (' ', '\t')
@@ -708,23 +725,32 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     const int l0 = ctz64(S >> t0);
     const int lp = ctz64(S >> t1);
     const uint32_t ref = (uint8_t)stage[sh + t2];
-    uint32_t pos = 0;
-    bool pos_ok = lp <= 9;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const uint32_t d = (uint32_t)(uint8_t)stage[sh + t1 + k] - '0';
-        const bool in = k < lp;
-        pos_ok = pos_ok && (!in || d < 10u);
-        pos = in ? pos * 10u + d : pos;
-    }
+    // the position: its first 8 bytes by two aligned 8-B LDS reads and a
+    // funnel shift, digit-checked in SWAR, left-padded with zero digits and
+    // summed by v_dot4 pairs (10, 1) and two 24-bit multiply-adds; a 9th digit
+    // on top (at most 9: < 2^31, as the per-digit loop this replaces)
+    const uint32_t L8 = min((uint32_t)lp, 8u);
+    const uint64_t p8 = stage_u64(stage, sh + t1);
+    const uint32_t plo = (uint32_t)p8, phi = (uint32_t)(p8 >> 32);
+    const uint64_t nd = (uint64_t)not_digit(plo) | ((uint64_t)not_digit(phi) << 32);
+    const uint64_t inl = L8 >= 8 ? ~0ull : ((1ull << (8 * L8)) - 1);
+    const uint32_t d9 = (uint32_t)(uint8_t)stage[sh + t1 + 8] - '0';
+    const bool pos_ok = lp >= 1 && lp <= 9 && (nd & inl) == 0 && (lp < 9 || d9 < 10u);
+    // digit values (garbage above the digits only borrows upward, then shifts out)
+    const uint64_t dv = ((uint64_t)(phi - 0x30303030u) << 32) | (plo - 0x30303030u);
+    const uint64_t dz = L8 == 0 ? 0 : dv << ((8 * (8 - L8)) & 63);
+    const uint32_t q0 = (uint32_t)dz, q1 = (uint32_t)(dz >> 32);
+    const uint32_t h4 = __umul24(__builtin_amdgcn_udot4(q0, 0x0000010Au, 0u, false), 100u) +
+                        __builtin_amdgcn_udot4(q0, 0x010A0000u, 0u, false);
+    const uint32_t l4 = __umul24(__builtin_amdgcn_udot4(q1, 0x0000010Au, 0u, false), 100u) +
+                        __builtin_amdgcn_udot4(q1, 0x010A0000u, 0u, false);
+    uint32_t pos = __umul24(h4, 10000u) + l4;
+    if (lp == 9) pos = pos * 10u + d9;
     // chrom (offset, length) and position for the formatter (bit 63: valid)
     hdr[0] = pos_ok ? (1ull << 63) | ((uint64_t)t0 << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
     // the chrom's first 8 bytes: the formatter then never reads the text for
     // names up to 8 bytes (reading them back fetched every line's cache lines)
-    uint64_t c8 = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        c8 |= k < l0 ? (uint64_t)(uint8_t)stage[sh + t0 + k] << (8 * k) : 0ull;
+    const uint64_t c8 = stage_u64(stage, sh + t0) & (l0 >= 8 ? ~0ull : ((1ull << (8 * l0)) - 1));
     hdr[1] = c8;
     const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
     const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
