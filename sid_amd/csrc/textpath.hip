@@ -217,13 +217,14 @@ __device__ __forceinline__ uint32_t low_bytes(uint32_t w)
     return ~(((w & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | w) & 0x80808080u;
 }
 
-// bit 7 of each byte of m -> 4 bits
-__device__ __forceinline__ uint32_t compress4(uint32_t m)
+// bit 7 of each byte of a and b -> 8 bits (a's in bits 0-3): the two words'
+// flags interleaved by nibble, then one shift-or ladder for both
+__device__ __forceinline__ uint32_t compress8(uint32_t a, uint32_t b)
 {
-    uint32_t t = m >> 7;
-    t |= t >> 7;
-    t |= t >> 14;
-    return t & 0xFu;
+    uint32_t x = (a >> 7) | (b >> 3);   // a: bits 0, 8, 16, 24; b: 4, 12, 20, 28
+    x |= x >> 7;                        // bits 1, 5 <- 8, 12
+    x |= x >> 14;                       // bits 2, 3, 6, 7 <- 16, 17, 20, 21
+    return x & 0xFFu;
 }
 // ------------------------------------------------------------ line index --
 // 16 bytes per lane; bit j of the result = byte j starts a non-empty line.
@@ -236,8 +237,8 @@ __device__ __forceinline__ uint32_t line_start_mask(const char* __restrict__ tex
     const uint64_t at = tile0 + (uint64_t)threadIdx.x * 16;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (at < c1 && at + 16 > c0) v = *(const uint4*)(text + at);
-    uint32_t nl = compress4(eq_bytes(v.x, 0x0A0A0A0Au)) | (compress4(eq_bytes(v.y, 0x0A0A0A0Au)) << 4) |
-                  (compress4(eq_bytes(v.z, 0x0A0A0A0Au)) << 8) | (compress4(eq_bytes(v.w, 0x0A0A0A0Au)) << 12);
+    uint32_t nl = compress8(eq_bytes(v.x, 0x0A0A0A0Au), eq_bytes(v.y, 0x0A0A0A0Au)) |
+                  (compress8(eq_bytes(v.z, 0x0A0A0A0Au), eq_bytes(v.w, 0x0A0A0A0Au)) << 8);
     // is the byte before `at` a '\n': the neighbour lane's bit 15, or a load at a wave start
     uint32_t prev = (uint32_t)__shfl_up((int)(nl >> 15), 1, 64);
     if ((threadIdx.x & 63) == 0) prev = (at > c0 && at - 1 < c1) ? (text[at - 1] == '\n') : 1u;
@@ -311,8 +312,8 @@ __device__ __forceinline__ IxWin ix_load(const char* __restrict__ text, uint64_t
 __device__ __forceinline__ uint32_t ix_mask(const IxWin& w, uint64_t at, uint64_t c0, uint64_t c1)
 {
     const uint4 v = w.v;
-    uint32_t nl = compress4(eq_bytes(v.x, 0x0A0A0A0Au)) | (compress4(eq_bytes(v.y, 0x0A0A0A0Au)) << 4) |
-                  (compress4(eq_bytes(v.z, 0x0A0A0A0Au)) << 8) | (compress4(eq_bytes(v.w, 0x0A0A0A0Au)) << 12);
+    uint32_t nl = compress8(eq_bytes(v.x, 0x0A0A0A0Au), eq_bytes(v.y, 0x0A0A0A0Au)) |
+                  (compress8(eq_bytes(v.z, 0x0A0A0A0Au), eq_bytes(v.w, 0x0A0A0A0Au)) << 8);
     uint32_t prev = (uint32_t)__shfl_up((int)(nl >> 15), 1, 64);
     if ((threadIdx.x & 63) == 0) prev = w.prev;
     uint32_t m = ((nl << 1) | prev) & ~nl & 0xFFFFu;
@@ -691,18 +692,21 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     // S: separator bytes as a 48-bit mask; fbad: window offset of the first
     // control byte ('\n', NUL, < 0x20 but '\t') at or after the line's start
     // (per word, no second compressed mask)
-    uint64_t S = 0;
     uint32_t fbad = 64;
     const uint32_t from = (0xFFFFu << sh) & 0xFFFFu;   // the line's bytes among the first 16
+    uint32_t sp[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
-        const uint32_t sp = eq_bytes(w[k], 0x20202020u) | eq_bytes(w[k], 0x09090909u);
-        S |= (uint64_t)compress4(sp) << (4 * k);
-        uint32_t bl = low_bytes(w[k]) & ~sp;
+        sp[k] = eq_bytes(w[k], 0x20202020u) | eq_bytes(w[k], 0x09090909u);
+        uint32_t bl = low_bytes(w[k]) & ~sp[k];
         if (k < 4) bl &= (__umul24((from >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) << 7;
         const uint32_t f = (uint32_t)__ffs(bl);
         fbad = min(fbad, f ? 4u * k + ((f - 1u) >> 3) : 64u);
     }
+    const uint32_t s_lo = compress8(sp[0], sp[1]) | (compress8(sp[2], sp[3]) << 8) |
+                          (compress8(sp[4], sp[5]) << 16) | (compress8(sp[6], sp[7]) << 24);
+    const uint32_t s_hi = compress8(sp[8], sp[9]) | (compress8(sp[10], sp[11]) << 8);
+    uint64_t S = ((uint64_t)s_hi << 32) | s_lo;
     // bit j = byte s0 + j, for the bytes inside the text and the 48 staged
     const uint64_t avail = len > s0 ? len - s0 : 0;
     const uint32_t nb = (uint32_t)min((uint64_t)(HDR_BYTES - sh), avail);
