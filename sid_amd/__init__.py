@@ -19,7 +19,8 @@ from dataclasses import dataclass
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(ROOT, "build", "libsid.so")
+# SID_LIB_PATH: another build of the same sources (A/B measurements only)
+LIB_PATH = os.environ.get("SID_LIB_PATH") or os.path.join(ROOT, "build", "libsid.so")
 CLI_PATH = os.path.join(ROOT, "build", "sid")
 
 METHOD_LOCAL, METHOD_LIKELIHOOD_RATIO, METHOD_BAYES, METHOD_QUALITY = 0, 1, 2, 3
