@@ -874,7 +874,9 @@ static void launch_parse(const char* text, uint64_t len, const uint64_t* starts,
                          uint64_t* counts, uint64_t* hdr, uint32_t* fb, unsigned long long* fbn,
                          unsigned long long* err, int qmode, hipStream_t st)
 {
-    const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + TB - 1) / TB, 1), 16384);
+    static const uint64_t PG = std::getenv("SID_PARSE_GRID") ? (uint64_t)std::max(1, std::atoi(std::getenv("SID_PARSE_GRID")))
+                                                             : 16384;   // blocks of the grid-stride parse
+    const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + TB - 1) / TB, 1), PG);
     if (qmode) {
         sid_parse_serial_kernel<<<pg, TB, 0, st>>>(text, len, starts, range, counts, hdr, nullptr, nullptr, err, 1);
         return;
