@@ -1,10 +1,10 @@
 #!/bin/bash
-# A/B of two builds in one box: build/ (A) and build_b/ (B), C2 bench (no
-# extras) interleaved, REPS rounds; the kernel of interest from a trace of each
+# A/B of builds on one box: BUILDS (default "build build_b"), C2 bench (no
+# extras) interleaved, REPS rounds
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out; mkdir -p $O
 for r in $(seq ${REPS:-3}); do
-  for v in build build_b; do
+  for v in ${BUILDS:-build build_b}; do
     SID_LIB_PATH=$PWD/$v/libsid.so timeout -k 10 200 python3 -u bench.py --no-extras "$@" > $O/ab.json 2> $O/ab.err || { echo "$v failed"; tail -5 $O/ab.err; exit 1; }
     python3 -c "
 import json; d=json.load(open('$O/ab.json'))
