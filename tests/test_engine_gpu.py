@@ -244,3 +244,32 @@ def test_engine_lanes_agree_with_oracle(sid, oracle, tmp_path, lanes, source, me
                          chunk_bytes=256 << 10, estimate_prior=method != "local", lanes=lanes)
     assert st.sites == n and st.chunks >= 2 * lanes
     assert out == ref.stdout
+
+
+@pytest.mark.parametrize("namelen", [12, 40, 70])
+def test_engine_long_chrom_names(sid, oracle, tmp_path, namelen):
+    """Chrom names past the parse's 8 kept bytes (the formatter reads them from
+    the text), records past a formatter tile's 32 KiB LDS buffer (512 sites of
+    >64 B: stored straight to global memory), and headers past the parse's 48
+    staged bytes (70: the general routine) -- byte for byte against the oracle."""
+    n = 30_000
+    text = sid.synth_text(31, n, 30.0, sites_per_chrom=7_000)
+    lines = text.split(b"\n")
+    out = []
+    for ln in lines:
+        if not ln:
+            out.append(ln)
+            continue
+        chrom, rest = ln.split(b"\t", 1)
+        name = (b"scaffold_" + chrom + b"_" + b"x" * namelen)[:namelen]
+        out.append(name + b"\t" + rest)
+    text = b"\n".join(out)
+    p = tmp_path / "long.plp"
+    p.write_bytes(text)
+    for flags in ([], ["-R", "-m", "likelihood_ratio"]):
+        ref = oracle.run_cli(flags + [str(p)])
+        assert ref.returncode == 0
+        got, st = engine_csv(sid, "local" if not flags else "likelihood_ratio", "text", text,
+                             chunk_bytes=1 << 20, estimate_prior=bool(flags))
+        assert st.sites == n
+        assert got == ref.stdout
