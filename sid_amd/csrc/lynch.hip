@@ -244,6 +244,9 @@ __device__ __forceinline__ void sid_fallback_append(bool fb, uint64_t key, unsig
     if (off < cap) list[off] = key;
 }
 
+#ifndef SID_HIST_PAIRS
+#define SID_HIST_PAIRS 4
+#endif
 template <bool PAIRS>
 __global__ __launch_bounds__(1024) void sid_hist_dense_kernel(const uint64_t* __restrict__ counts, size_t n,
                                                               uint32_t* __restrict__ part,
@@ -258,23 +261,29 @@ __global__ __launch_bounds__(1024) void sid_hist_dense_kernel(const uint64_t* __
     if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
     if (PAIRS) {
+        // SID_HIST_PAIRS site pairs per lane in flight (16 B each): one block of
+        // 16 waves per CU (the 64 KiB table) is too few waves to cover the
+        // HBM latency with two
         const ulonglong2* pairs = (const ulonglong2*)counts;
         const size_t npairs = n / 2;
         const size_t stride = (size_t)gridDim.x * blockDim.x;
-        for (size_t base = (size_t)blockIdx.x * blockDim.x; base < npairs; base += 2 * stride) {
-            const size_t p0 = base + threadIdx.x, p1 = p0 + stride;
-            ulonglong2 c0 = {0, 0}, c1 = {0, 0};
-            const bool v0 = p0 < npairs, v1 = p1 < npairs;
-            if (v0) c0 = pairs[p0];
-            if (v1) c1 = pairs[p1];
-            const uint64_t w[4] = {c0.x, c0.y, c1.x, c1.y};
-            const bool v[4] = {v0, v0, v1, v1};
+        for (size_t base = (size_t)blockIdx.x * blockDim.x; base < npairs; base += SID_HIST_PAIRS * stride) {
+            ulonglong2 c[SID_HIST_PAIRS];
+            bool v[SID_HIST_PAIRS];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t d = sid_dense_code(w[k]);
-                const bool fb = v[k] && d == SID_DENSE_NONE;
-                if (v[k] && !fb) atomicAdd(&H[sid_dense_slot(d)], 1u);
-                sid_fallback_append(fb, sid_profile_key(w[k]), llist, &lcnt, list, cap, ctr);
+            for (int u = 0; u < SID_HIST_PAIRS; ++u) {
+                const size_t p = base + threadIdx.x + u * stride;
+                v[u] = p < npairs;
+                c[u] = v[u] ? pairs[p] : make_ulonglong2(0, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < 2 * SID_HIST_PAIRS; ++k) {
+                const uint64_t w = (k & 1) ? c[k >> 1].y : c[k >> 1].x;
+                const bool vk = v[k >> 1];
+                const uint32_t d = sid_dense_code(w);
+                const bool fb = vk && d == SID_DENSE_NONE;
+                if (vk && !fb) atomicAdd(&H[sid_dense_slot(d)], 1u);
+                sid_fallback_append(fb, sid_profile_key(w), llist, &lcnt, list, cap, ctr);
             }
         }
         // odd last site
