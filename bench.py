@@ -89,6 +89,9 @@ def parse_args():
     p.add_argument("--allow-shared-gpu", action="store_true",
                    help="rehearsal: more ranks than GPUs share them round-robin")
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
+    p.add_argument("--resident", action="store_true",
+                   help="C4/C5: generate the rank's shard into HBM before the timed region (when it fits) "
+                        "instead of on the device inside the step")
     a = p.parse_args()
     if a.config is None:
         a.config = "C3" if a.method == "likelihood_ratio" else "C2"
@@ -112,7 +115,9 @@ def stage_bytes(stage, text_per_site, csv_per_site):
 
 def main():
     a = parse_args()
-    cfg = CONFIGS[a.config]
+    cfg = dict(CONFIGS[a.config])
+    gen_resident = a.resident and not cfg["resident"]   # C4/C5 shard text generated into HBM up front
+
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
@@ -148,7 +153,13 @@ def main():
         first, hi = total * rank // world, total * (rank + 1) // world
         n = hi - first
     text = None
-    if cfg["resident"]:
+    if gen_resident:
+        text, ln = generate_resident(torch, sid_amd, dev, gpu, cfg, first, n)
+        if not a.chunk_mib:   # 2 GiB chunks' record bounds and hold arena overran the HBM the text leaves (C4, 1 GPU)
+            a.chunk_mib = 1024
+        cfg["resident"] = True
+        cfg["desc"] += "; the shard's text generated into HBM before the timed region"
+    elif cfg["resident"]:
         ctx = sid_amd.Context(gpu)
         cap = int(n * (24 + 2.9 * cfg["depth"])) + (64 << 20)
         text = torch.empty(cap + 512, dtype=torch.uint8, device=dev)
@@ -233,11 +244,14 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak" if cfg["resident"] else "strong",
+            "scaling": "strong" if cfg["total"] else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic (counter-based pileup generator, BASELINE.md): pileup text "
-                     + ("resident in HBM before the timed region" if cfg["resident"] else
+                     + ("resident in HBM before the timed region" + (" (the rank's shard of the fixed total, "
+                                                                      "generated in 50M-site pieces)"
+                                                                      if gen_resident else "")
+                        if cfg["resident"] else
                         "generated on the device chunk by chunk inside the step (never stored)")
                      + "; CSV records formatted into HBM"),
             "config": {"workload": f"{a.config}: {cfg['desc']}", "method": cfg["method"],
@@ -262,7 +276,7 @@ def main():
             e = est_box["est"]
             out["estimate"] = {"pi": e.heterozygosity, "eps": e.error_rate, "iterations": e.iterations,
                                "n_unique": e.n_unique}
-        if world == 1 and cfg["resident"] and not a.no_extras:
+        if world == 1 and cfg["resident"] and not gen_resident and not a.no_extras:
             out["kernel_local"] = bench_kernel_local(torch, dev, cfg, n)
             out["e2e"] = bench_e2e(torch, sid_amd, cfg, text, ln, n, a)
             if not a.no_cpu:
@@ -319,6 +333,33 @@ def pmc_traffic(stage, sites):
         return pm["hbm_bytes_per_site"] * sites
     except Exception:
         return None
+
+
+def generate_resident(torch, sid_amd, dev, gpu, cfg, first, n):
+    """The rank's shard of C4/C5 as text in HBM: one buffer sized to the
+    text (the rest, at least a 24 GiB reserve, stays free for the engine's
+    chunk workspace, pooled record buffers and hold arena), filled by the device generator in 50M-site pieces
+    laid end to end (every line stands alone, so the pieces concatenate to the
+    shard's text); refuses a shard that does not fit."""
+    free, _ = torch.cuda.mem_get_info(dev)
+    reserve = 24 << 30
+    cap = free - reserve
+    need = int(n * (2.72 * cfg["depth"] + 2))   # ~81 B/site at 30x, ~564 at 200x (measured)
+    if cap < need:
+        raise SystemExit(f"bench.py --resident: the shard's ~{need / 1e9:.0f} GB of text does not fit "
+                         f"({free / 1e9:.0f} GB free, {reserve >> 30} GiB kept for the engine)")
+    cap = min(cap, int(need * 1.03) + (1 << 30))   # the rest stays free for the engine
+    text = torch.empty(cap, dtype=torch.uint8, device=dev)
+    ctx = sid_amd.Context(gpu)
+    ln, piece = 0, 50_000_000
+    for lo in range(0, n, piece):
+        m = min(piece, n - lo)
+        ln += ctx.synth_text_device(cfg["seed"], cfg["depth"], first + lo, m, text.data_ptr() + ln,
+                                    cap - 512 - ln, sites_per_chrom=cfg["spc"])
+    text[ln:ln + 512].zero_()
+    torch.cuda.synchronize(dev)
+    ctx.close()
+    return text, ln
 
 
 def exchange_histogram(torch, dist, eng, dev, rank):
