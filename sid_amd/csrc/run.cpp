@@ -77,6 +77,15 @@ public:
         q_.pop_front();
         return true;
     }
+    // without waiting: false when nothing is queued right now
+    bool try_pop(T& v)
+    {
+        std::lock_guard<std::mutex> l(m_);
+        if (q_.empty()) return false;
+        v = std::move(q_.front());
+        q_.pop_front();
+        return true;
+    }
     void close()
     {
         std::lock_guard<std::mutex> l(m_);
@@ -905,8 +914,23 @@ void compute(sid_engine* e, Dev& d, int pass)
         e->t_comp_sync += (uint64_t)((wall() - a) * 1e9);
         return r;
     };
+    // the next chunk, taken early so that its line index runs behind this
+    // chunk's formatter (the GPU then does not idle over the host round trip
+    // that reads the formatter's byte count); indexed: its site count is in hs[0]
+    Loaded nextL;
+    bool have_next = false, next_indexed = false;
+    auto take = [&](Loaded& out) {
+        if (have_next) {
+            out = nextL;
+            have_next = false;
+            return true;
+        }
+        return d.loaded.pop(out);
+    };
     Loaded L;
-    while (d.loaded.pop(L)) {
+    while (take(L)) {
+        const bool pre_indexed = next_indexed;
+        next_indexed = false;
         if (e->rc.load() != SID_OK) break;
         ChunkRec& r = e->recs[L.j];
         auto release_slot = [&]() {
@@ -931,11 +955,11 @@ void compute(sid_engine* e, Dev& d, int pass)
         }
         int rc = SID_OK;
         hipError_t x = hipSuccess;
-        if (L.ev) x = hipStreamWaitEvent(d.s_comp, L.ev, 0);
+        if (L.ev && !pre_indexed) x = hipStreamWaitEvent(d.s_comp, L.ev, 0);
         const bool P = e->prof;
         if (P) d.prof_chunks++;
         const uint64_t tbytes = L.c1 - (L.c0 & ~(uint64_t)15);
-        if (x == hipSuccess) rc = sid_chunk_reserve(&W, tbytes, 0);
+        if (x == hipSuccess && !pre_indexed) rc = sid_chunk_reserve(&W, tbytes, 0);
         // pass 2 of a Lynch path: the parse kept since pass 1 stands in for the
         // workspace's line offsets, counts and header pairs (restored below)
         struct View {
@@ -966,11 +990,13 @@ void compute(sid_engine* e, Dev& d, int pass)
             if (x == hipSuccess) x = hipMemsetAsync(W.state + 4, 0xFF, sizeof(uint64_t), d.s_comp);   // no parse error
             if (x != hipSuccess) return (void)hipfail(e, x);
         } else {
-            pe = d.prof_begin(P);
-            if (rc == SID_OK && x == hipSuccess) rc = sid_chunk_index(&W, L.base, L.c0, L.c1, d.s_comp);
-            d.prof_end(0, pe);
-            if (rc == SID_OK && x == hipSuccess) x = hipMemcpyAsync(hs, W.state, 8, hipMemcpyDeviceToHost, d.s_comp);
-            if (rc == SID_OK && x == hipSuccess) x = sync();
+            if (!pre_indexed) {
+                pe = d.prof_begin(P);
+                if (rc == SID_OK && x == hipSuccess) rc = sid_chunk_index(&W, L.base, L.c0, L.c1, d.s_comp);
+                d.prof_end(0, pe);
+                if (rc == SID_OK && x == hipSuccess) x = hipMemcpyAsync(hs, W.state, 8, hipMemcpyDeviceToHost, d.s_comp);
+                if (rc == SID_OK && x == hipSuccess) x = sync();
+            }
             if (x != hipSuccess) return (void)hipfail(e, x);
             if (rc != SID_OK) return (void)fail(e, rc);
             n = hs[0];
@@ -1035,6 +1061,26 @@ void compute(sid_engine* e, Dev& d, int pass)
                 d.prof_end(5, pe);
                 if (rc != SID_OK) return (void)fail(e, rc);
                 x = hipMemcpyAsync(hs + 8, W.lb + 1, 32, hipMemcpyDeviceToHost, d.s_comp);   // bytes, flags, error
+                // the next chunk's line index behind the formatter (stream
+                // order: it rewrites W.state only after the formatter has read it)
+                if (x == hipSuccess && d.loaded.try_pop(nextL)) {
+                    have_next = true;
+                    const ChunkRec& r2 = e->recs[nextL.j];
+                    if (nextL.kind == 0 && !(pass == 2 && r2.pre) && !(pass == 1 && nextL.j > e->first_err.load())) {
+                        if (nextL.ev) x = hipStreamWaitEvent(d.s_comp, nextL.ev, 0);
+                        int rc2 = SID_OK;
+                        // growth frees buffers: hipFree waits for the queued work first
+                        if (x == hipSuccess) rc2 = sid_chunk_reserve(&W, nextL.c1 - (nextL.c0 & ~(uint64_t)15), 0);
+                        hipEvent_t pe2 = d.prof_begin(P);
+                        if (rc2 == SID_OK && x == hipSuccess)
+                            rc2 = sid_chunk_index(&W, nextL.base, nextL.c0, nextL.c1, d.s_comp);
+                        d.prof_end(0, pe2);
+                        if (rc2 == SID_OK && x == hipSuccess)
+                            x = hipMemcpyAsync(hs, W.state, 8, hipMemcpyDeviceToHost, d.s_comp);
+                        if (rc2 != SID_OK) return (void)fail(e, rc2);
+                        next_indexed = x == hipSuccess;
+                    }
+                }
                 if (x == hipSuccess) x = sync();
                 if (x != hipSuccess) return (void)hipfail(e, x);
                 hs[4] = hs[11];
