@@ -869,6 +869,27 @@ __global__ __launch_bounds__(TB) void sid_parse_serial_kernel(const char* __rest
     }
 }
 
+// Grid of a kernel in which every lane walks its own line: the lines a CU
+// has in flight are its cache working set.  At 30x (~81 B a line) a full CU
+// fits; at 200x (~430 B) 32 waves of lines thrash L1/L2 and the text is
+// fetched again.  Blocks per CU ~ 1000 B / bytes per line, at most 8 (the
+// full grid, `cap`).  Parse on a C5 shard (200x): 8 blocks a CU 14.1 ms, 4:
+// 10.9, 2: 10.5, 1: 13.8; C2 best at the full grid.
+static unsigned line_walk_grid(uint64_t n, uint64_t len, unsigned cap)
+{
+    if (!n) return cap;
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const long bpc = std::lround(1000.0 * (double)n / (double)std::max<uint64_t>(len, 1));
+    if (bpc >= 8) return cap;
+    return (unsigned)std::min<uint64_t>(cap, (uint64_t)std::max(1L, bpc) * (uint64_t)ncu);
+}
+
 // the two passes over sites [range[0], range[1]) (the range lives on the device)
 static void launch_parse(const char* text, uint64_t len, const uint64_t* starts, const uint64_t* range, uint64_t n,
                          uint64_t* counts, uint64_t* hdr, uint32_t* fb, unsigned long long* fbn,
@@ -877,27 +898,11 @@ static void launch_parse(const char* text, uint64_t len, const uint64_t* starts,
     static const char* env = std::getenv("SID_PARSE_GRID");
     static const uint64_t PG = env ? (uint64_t)std::max(1, std::atoi(env)) : 16384;   // blocks of the grid-stride parse
     const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + TB - 1) / TB, 1), PG);
-    if (qmode) {
+    if (qmode) {   // (the byte-wise walks of -m quality measured slower on the smaller grid: 925 vs 626 us at 200x)
         sid_parse_serial_kernel<<<pg, TB, 0, st>>>(text, len, starts, range, counts, hdr, nullptr, nullptr, err, 1);
         return;
     }
-    // Every lane walks its own line, so a CU's lines in flight are its cache
-    // working set: at 30x (~81 B a line) a full CU (8 blocks, 32 waves) fits,
-    // at 200x (~430 B) it thrashes L1/L2 and the lines are fetched again.
-    // Blocks per CU ~ 1000 B / bytes per line (C5 shard, 200x: 8 blocks a
-    // CU 14.1 ms, 4: 10.9, 2: 10.5, 1: 13.8; C2 best at the full grid)
-    unsigned pgf = pg;
-    if (!env && n) {
-        static int ncu = 0;
-        if (!ncu) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-                ncu = 256;
-        }
-        const long bpc = std::lround(1000.0 * (double)n / (double)std::max<uint64_t>(len, 1));
-        if (bpc < 8) pgf = (unsigned)std::min<uint64_t>(pg, (uint64_t)std::max(1L, bpc) * (uint64_t)ncu);
-    }
+    const unsigned pgf = env ? pg : line_walk_grid(n, len, pg);
     (void)hipMemsetAsync(fbn, 0, sizeof *fbn, st);
     sid_parse_kernel<<<pgf, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn);
     sid_parse_serial_kernel<<<256, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, err, 0);
