@@ -2,17 +2,28 @@
 """bench.py — genome sites/s of sid's pileup -> CSV path on MI355X.
 
 Headline (BASELINE.json metric, configs[1] = "C2"): 50,000,000 synthetic 30x
-diploid sites per GPU, `-m local`.  A step is one whole sid run over the rank's
-pileup text, already resident in HBM when the timed region starts:
+diploid sites per GPU, `-m local`.  A step is one whole sid run over the
+rank's pileup text, in host memory when the timed region starts, with the CSV
+in host memory when it ends -- the reference's file-in / stdout-out path
+(sid.cpp:84-105) without the file system:
 
-    line index -> parse (counts) -> per-site call -> CSV records formatted
+    pinned host text -H2D-> line index -> parse (counts) -> per-site call
+      -> CSV records formatted -D2H-> the engine's pinned host arena
 
 i.e. readFile + callSiteMLError + the output loop (call.cpp:11-20, :213-289,
 sid.cpp:102-105) through the streaming engine (include/sid.h sid_engine_*,
-device-text source, 128 MiB chunks); the CSV records are left in HBM.  The
-PCIe-inclusive rate (text in host memory -> CSV copied back to host memory) is
-reported beside it as `e2e`, and the CLI (build/sid, file -> /dev/null) as
-`e2e.cli`; they are never `value`.
+host-text source, 128 MiB chunks, host_hold_bytes: each chunk's records are
+copied back while later chunks upload, so PCIe runs both ways at once).
+Beside it, in the same line:
+
+  device_path   the same run over the text already resident in HBM with the
+                records left in HBM (device_sink 1): the kernels alone, per
+                stage, with the roofline of the dominant stage
+  kernel_local  sid_call_local alone over resident counts (25 B/site)
+  cli           build/sid on the same text as a file, CSV to /dev/null (wall)
+  cpu_baseline  the oracle CLI (the reference's path restated in C) on the
+                same 50M-site text, 16 line-aligned shard processes, plus a
+                1-core figure on a 4M-site sample (rank 0, N=1 only)
 
 Configs (--config):
   C2  -m local, seed 2, 50M sites per GPU (weak scaling)           [default]
@@ -21,28 +32,18 @@ Configs (--config):
       backend "nccl"), rank 0 runs the one Nelder-Mead estimate and broadcasts
       (pi, eps) over RCCL; then every rank formats its records
   C4  -m local, seed 4, 3G sites in total = 24 chromosomes x 125M (strong
-      scaling: rank r takes sites [r*3G/N, (r+1)*3G/N)); the text is generated
-      on the device chunk by chunk inside the step (never stored: 244 GB)
-  C5  -m local, seed 5, 200x, 500M sites in total (strong), generated as C4
+      scaling: rank r takes sites [r*3G/N, (r+1)*3G/N)); device path: the
+      shard's text generated into HBM before the timed region when it fits
+      (--stream: generated chunk by chunk inside the step, never stored)
+  C5  -m local, seed 5, 200x, 500M sites in total (strong), as C4
 
-Multi-GPU: one rank per GPU (torchrun).  -m local has no data-path exchange;
-the Lynch path exchanges only the O(U) profile histogram.  Ranks beyond the
-visible GPUs are refused unless --allow-shared-gpu (a rehearsal: n_gpus then
-counts distinct devices and "oversubscribed" is set).
-
-The JSON line also carries
-  roofline      the dominant kernel stage of the step (device time from HIP
-                events on the engine's compute stream over the timed region),
-                its algorithmic bytes per launch / average launch duration vs
-                8 TB/s, and the PMC-measured HBM bytes per launch
-                (profiles/pmc_<stage>_r02.json) when present
-  stages_ms     device time per stage per step
-  kernel_local  sid_call_local alone over resident counts (25 B/site)
-  e2e           host-memory text -> CSV in host memory (PCIe both ways),
-                engine clock; and the CLI on a 50M-site file
-  cpu_baseline  the oracle CLI (the reference's path restated in C) on the
-                same 50M-site text, 16 line-aligned shard processes, plus a
-                1-core figure on a 4M-site sample (rank 0, N=1 only)
+Multi-GPU: one rank per GPU.  Under torchrun (WORLD_SIZE set) each process is
+a rank; without it, `--gpus N` (N > 1) starts N rank processes itself (before
+anything touches a GPU) and relays rank 0's line.  -m local has no data-path
+exchange; the Lynch path exchanges only the O(U) profile histogram.  Ranks
+beyond the visible GPUs are refused unless --allow-shared-gpu (a rehearsal:
+n_gpus then counts distinct devices and "oversubscribed" is set).  Each rank
+pins its host buffers on its GPU's NUMA node (the PCI device's local CPUs).
 """
 import argparse
 import json
@@ -58,20 +59,21 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 LOCAL_BYTES_PER_SITE = 25    # sid_call_local: 8 B counts in, 1 B code + 2 x 8 B confs out
+METRIC = "genome sites/sec (whole node) on 30x synthetic pileup; 1/2/4/8 GPU scaling"
 
 CONFIGS = {
     "C2": dict(method="local", R=False, seed=2, depth=30.0, per_gpu=50_000_000, total=None, spc=0,
-               resident=True, desc="-m local, 50M-site 30x synthetic pileup per GPU"),
+               desc="-m local, 50M-site 30x synthetic pileup per GPU"),
     "C3": dict(method="likelihood_ratio", R=True, seed=3, depth=30.0, per_gpu=50_000_000, total=None, spc=0,
-               resident=True, desc="-R -m likelihood_ratio, 50M-site 30x synthetic pileup per GPU"),
+               desc="-R -m likelihood_ratio, 50M-site 30x synthetic pileup per GPU"),
     "C4": dict(method="local", R=False, seed=4, depth=30.0, per_gpu=None, total=3_000_000_000, spc=125_000_000,
-               resident=False, desc="-m local, 3G-site whole-genome 30x pileup (24 x 125M), site-range shards"),
+               desc="-m local, 3G-site whole-genome 30x pileup (24 x 125M), site-range shards"),
     "C5": dict(method="local", R=False, seed=5, depth=200.0, per_gpu=None, total=500_000_000, spc=125_000_000,
-               resident=False, desc="-m local, 500M-site 200x pileup, site-range shards"),
+               desc="-m local, 500M-site 200x pileup, site-range shards"),
 }
 
 
-def parse_args():
+def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -80,24 +82,86 @@ def parse_args():
     p.add_argument("--method", default=None, choices=["local", "likelihood_ratio"],
                    help="alias: local = C2, likelihood_ratio = C3")
     p.add_argument("--sites", type=int, default=None, help="override: sites per GPU (C2/C3) or in total (C4/C5)")
-    p.add_argument("--chunk-mib", type=int, default=0, help="engine chunk size (0 = 128 MiB)")
-    p.add_argument("--lanes", type=int, default=1,
-                   help="engine pipelines per GPU (concurrent streams; their kernels overlap, so the per-stage "
-                        "event times of the roofline are only clean at 1)")
-    p.add_argument("--no-extras", action="store_true", help="skip kernel_local, e2e and cpu_baseline")
+    p.add_argument("--chunk-mib", type=int, default=0, help="engine chunk size (0 = the engine's default)")
+    p.add_argument("--device-steps", type=int, default=0, help="device_path steps (0 = max(steps, 10))")
+    p.add_argument("--no-extras", action="store_true", help="skip kernel_local, cli and cpu_baseline")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--allow-shared-gpu", action="store_true",
                    help="rehearsal: more ranks than GPUs share them round-robin")
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
-    p.add_argument("--resident", action="store_true",
-                   help="C4/C5: generate the rank's shard into HBM before the timed region (when it fits) "
-                        "instead of on the device inside the step")
-    a = p.parse_args()
+    p.add_argument("--stream", action="store_true",
+                   help="C4/C5: generate the text on the device chunk by chunk inside the step, even when the "
+                        "rank's shard would fit in HBM")
+    a = p.parse_args(argv)
     if a.config is None:
         a.config = "C3" if a.method == "likelihood_ratio" else "C2"
     return a
 
 
+# ------------------------------------------------------------- launcher ----
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a):
+    """`--gpus N` without torchrun: N rank processes of this script, started
+    before this process touches any GPU (device_count() does not initialise
+    one on this image); rank 0's line goes to stdout.  Returns the exit code."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    if a.gpus > ndev and not a.allow_shared_gpu:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but {ndev} GPU(s) visible; pass --allow-shared-gpu "
+                         "for a rehearsal with ranks sharing GPUs")
+    env = dict(os.environ, WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = []
+    for r in range(a.gpus):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:   # a failed rank leaves the others at a barrier: stop them
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def numa_bind(torch, gpu):
+    """Run this rank on its GPU's NUMA node (the PCI device's local CPUs, within
+    the CPUs this process may use), so pinned host buffers are allocated there
+    and the DMA does not cross sockets.  Returns the CPU list used, or None."""
+    try:
+        pr = torch.cuda.get_device_properties(gpu)
+        bdf = "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id)
+        txt = open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read().strip()
+        cpus = set()
+        for part in txt.split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        mine = cpus & os.sched_getaffinity(0)
+        if not mine or mine == os.sched_getaffinity(0):
+            return None
+        os.sched_setaffinity(0, mine)
+        return {"pci": bdf, "cpus": len(mine)}
+    except Exception:
+        return None
+
+
+# ----------------------------------------------------------------- ranks ----
 def stage_bytes(stage, text_per_site, csv_per_site):
     """Algorithmic HBM bytes per site of each engine stage."""
     return {
@@ -107,185 +171,10 @@ def stage_bytes(stage, text_per_site, csv_per_site):
         "parse": text_per_site + text_per_site / 8 + 8 + 8 + 16,
         "call": LOCAL_BYTES_PER_SITE,                  # counts in, code + confs out
         "hist": 8,                                     # counts read
-        # one-pass formatter: code + confs and the header pair read (the line
-        # offset only for chrom names over 8 bytes), the records written
+        # formatter: code + confs and the header pair read (the line offset
+        # only for chrom names over 8 bytes), the records written
         "fmt_write": 17 + 16 + csv_per_site,
     }[stage]
-
-
-def main():
-    a = parse_args()
-    cfg = dict(CONFIGS[a.config])
-    gen_resident = a.resident and not cfg["resident"]   # C4/C5 shard text generated into HBM up front
-
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local_rank = int(os.environ.get("LOCAL_RANK", 0))
-    import torch  # plumbing: device memory, events, process group
-    ndev = torch.cuda.device_count()
-    if ndev == 0:
-        raise SystemExit("bench.py: no HIP device visible")
-    if local_rank >= ndev and not a.allow_shared_gpu:
-        raise SystemExit(f"bench.py: rank {rank} (local {local_rank}) has no GPU of its own ({ndev} visible); "
-                         "pass --allow-shared-gpu for a rehearsal")
-    gpu = local_rank % ndev
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    dist = None
-    n_gpus, oversub = 1, False
-    if world > 1:
-        import torch.distributed as dist
-        backend = a.backend or "nccl"
-        dist.init_process_group(backend, rank=rank, world_size=world, device_id=dev if backend == "nccl" else None)
-        ids = [None] * world
-        dist.all_gather_object(ids, (socket.gethostname(), gpu))
-        n_gpus = len(set(ids))
-        oversub = n_gpus < world
-    import sid_amd
-
-    # ---------------------------------------------------------------- input --
-    if cfg["resident"]:
-        n = a.sites or cfg["per_gpu"]
-        first = rank * n
-        total = n * world
-    else:
-        total = a.sites or cfg["total"]
-        first, hi = total * rank // world, total * (rank + 1) // world
-        n = hi - first
-    text = None
-    if gen_resident:
-        text, ln = generate_resident(torch, sid_amd, dev, gpu, cfg, first, n)
-        if not a.chunk_mib:   # 2 GiB chunks' record bounds and hold arena overran the HBM the text leaves (C4, 1 GPU)
-            a.chunk_mib = 1024
-        cfg["resident"] = True
-        cfg["desc"] += "; the shard's text generated into HBM before the timed region"
-    elif cfg["resident"]:
-        ctx = sid_amd.Context(gpu)
-        cap = int(n * (24 + 2.9 * cfg["depth"])) + (64 << 20)
-        text = torch.empty(cap + 512, dtype=torch.uint8, device=dev)
-        ln = ctx.synth_text_device(cfg["seed"], cfg["depth"], first, n, text.data_ptr(), cap,
-                                   sites_per_chrom=cfg["spc"])
-        text[ln:ln + 512].zero_()
-        torch.cuda.synchronize(dev)
-        ctx.close()
-    lynch = cfg["method"] != "local" or cfg["R"]
-    # one pipeline per GPU: with 2 GiB chunks a second one measured no gain
-    # for -m local (5.50-5.54 vs 5.51-5.59 ms/step) and a loss for the Lynch
-    # paths (per-chunk histogram syncs, the lanes' table merge: C3 6.95 ->
-    # 8.51 ms), whose multi-rank exchange also reads one context
-    lanes = 1 if lynch else max(1, a.lanes)
-    eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=gpu,
-                         chunk_bytes=a.chunk_mib << 20, device_sink=1, lanes=lanes)
-    if cfg["resident"]:
-        eng.source_device_text(text.data_ptr(), ln, keep=text)
-    else:
-        eng.source_synth(cfg["seed"], n, cfg["depth"], first=first, sites_per_chrom=cfg["spc"], on_device=True)
-    est_box = {}
-
-    def step():
-        st = eng.ingest()
-        if lynch and dist is not None:
-            exchange_histogram(torch, dist, eng, dev, rank)
-        if lynch and dist is not None and world > 1:
-            est = broadcast_estimate(torch, dist, eng, dev, rank)
-        else:
-            est = eng.estimate()
-        _, st2 = eng.emit()
-        est_box["est"] = est
-        return st, st2
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    eng.profile(True)   # HIP event pairs around every stage on the compute stream
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        st, st2 = step()
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if dist:
-        dist.barrier()
-    elapsed = t1 - t0
-    prof = eng.profile_read()
-    eng.profile(False)
-    sites_rank = st.sites
-    stages = {k[:-3]: v / a.steps for k, v in prof.items() if k.endswith("_ms") and k != "fmt_len_ms"}
-    if dist:
-        vec = torch.tensor([elapsed] + [stages[k] for k in sorted(stages)], dtype=torch.float64, device=dev)
-        dist.all_reduce(vec, op=dist.ReduceOp.MAX)
-        elapsed = float(vec[0])
-        stages = {k: float(v) for k, v in zip(sorted(stages), vec[1:].tolist())}
-        tot = torch.tensor([float(sites_rank)], dtype=torch.float64, device=dev)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        sites_all = int(tot.item())
-    else:
-        sites_all = sites_rank
-
-    if rank == 0:
-        text_bytes = st.bytes_in if cfg["resident"] else None
-        tps = (text_bytes / sites_rank) if text_bytes else (24 + 2.7 * cfg["depth"])
-        cps = st2.bytes_out / sites_rank if sites_rank else 0.0
-        dom = max(stages, key=lambda k: stages[k])
-        bps = stage_bytes(dom, tps, cps)
-        per_launch_sites = sites_rank / max(1, prof["chunks"] / a.steps)
-        launch_ms = stages[dom] / max(1, prof["chunks"] / a.steps)
-        achieved = bps * per_launch_sites / (launch_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(dom, per_launch_sites)
-        step_bytes = (text_bytes or 0) + st2.bytes_out
-        out = {
-            "metric": "genome sites/sec (whole node) on 30x synthetic pileup; 1/2/4/8 GPU scaling",
-            "value": sites_all * a.steps / elapsed,
-            "unit": "sites/s",
-            "n_gpus": n_gpus,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "strong" if cfg["total"] else "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": ("synthetic (counter-based pileup generator, BASELINE.md): pileup text "
-                     + ("resident in HBM before the timed region" + (" (the rank's shard of the fixed total, "
-                                                                      "generated in 50M-site pieces)"
-                                                                      if gen_resident else "")
-                        if cfg["resident"] else
-                        "generated on the device chunk by chunk inside the step (never stored)")
-                     + "; CSV records formatted into HBM"),
-            "config": {"workload": f"{a.config}: {cfg['desc']}", "method": cfg["method"],
-                       "estimate_prior": cfg["R"], "seed": cfg["seed"], "depth": cfg["depth"],
-                       "sites_per_gpu": n, "sites_total": sites_all,
-                       "sites_per_chrom": cfg["spc"] or None, "chunks_per_step_rank0": prof["chunks"] / a.steps,
-                       "text_bytes_rank0": text_bytes, "csv_bytes_rank0": st2.bytes_out,
-                       "parallelism": f"site-range shards x{world}" + (" + RCCL histogram all-gather"
-                                                                       if lynch and world > 1 else ""),
-                       "ranks": world, "oversubscribed": oversub, "engine_lanes_per_gpu": lanes},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"engine stage '{dom}'", "stage_kernels": STAGE_KERNELS[dom],
-                         "launch_ms": launch_ms, "sites_per_launch": per_launch_sites,
-                         "bytes_per_site": bps, "valu": valu_issue(dom, per_launch_sites, launch_ms)},
-            "stages_ms": stages,
-            "path": {"bytes_per_site": tps + cps, "text_per_site": tps, "csv_per_site": cps,
-                     "GBps": step_bytes / (elapsed / a.steps) / 1e9 if text_bytes else None,
-                     "note": "text in + CSV out per step (the path's minimum HBM traffic) / ms_per_step"},
-        }
-        if lynch:
-            e = est_box["est"]
-            out["estimate"] = {"pi": e.heterozygosity, "eps": e.error_rate, "iterations": e.iterations,
-                               "n_unique": e.n_unique}
-        if world == 1 and cfg["resident"] and not gen_resident and not a.no_extras:
-            out["kernel_local"] = bench_kernel_local(torch, dev, cfg, n)
-            out["e2e"] = bench_e2e(torch, sid_amd, cfg, text, ln, n, a)
-            if not a.no_cpu:
-                out["cpu_baseline"] = bench_cpu(cfg, text, ln, n)
-        print(json.dumps(out), flush=True)
-    eng.close()
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 STAGE_KERNELS = {
@@ -297,17 +186,379 @@ STAGE_KERNELS = {
 }
 
 
+class Rank:
+    def __init__(self, a):
+        self.a = a
+        self.rank = int(os.environ.get("RANK", 0))
+        self.world = int(os.environ.get("WORLD_SIZE", 1))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", 0))
+        import torch  # plumbing: device memory, events, process group
+        self.torch = torch
+        ndev = torch.cuda.device_count()
+        if ndev == 0:
+            raise SystemExit("bench.py: no HIP device visible")
+        if self.local_rank >= ndev and not a.allow_shared_gpu:
+            raise SystemExit(f"bench.py: rank {self.rank} (local {self.local_rank}) has no GPU of its own "
+                             f"({ndev} visible); pass --allow-shared-gpu for a rehearsal")
+        if self.world > 1 and a.gpus not in (1, self.world):
+            raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {self.world}")
+        self.gpu = self.local_rank % ndev
+        torch.cuda.set_device(self.gpu)
+        self.dev = torch.device("cuda", self.gpu)
+        self.numa = numa_bind(torch, self.gpu)
+        self.dist = None
+        self.backend = None
+        self.n_gpus, self.oversub = 1, False
+        if self.world > 1:
+            import torch.distributed as dist
+            # RCCL takes one rank per GPU: a rehearsal with ranks sharing GPUs runs over gloo
+            backend = a.backend or ("nccl" if self.world <= ndev else "gloo")
+            dist.init_process_group(backend, rank=self.rank, world_size=self.world,
+                                    device_id=self.dev if backend == "nccl" else None)
+            ids = [None] * self.world
+            dist.all_gather_object(ids, (socket.gethostname(), self.gpu))
+            self.n_gpus = len(set(ids))
+            self.oversub = self.n_gpus < self.world
+            self.dist = dist
+            self.backend = backend
+
+    # -- timing harness: warmup, barrier + sync, K steps, barrier + sync, max over ranks
+    def timed(self, step, steps, warmup):
+        torch, dist = self.torch, self.dist
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(self.dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = step()
+        torch.cuda.synchronize(self.dev)
+        t1 = time.perf_counter()
+        if dist:
+            dist.barrier()
+        return t1 - t0, res
+
+    def max_over_ranks(self, vals):
+        if not self.dist:
+            return vals
+        v = self.torch.tensor(vals, dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(v, op=self.dist.ReduceOp.MAX)
+        return v.tolist()
+
+    def sum_over_ranks(self, x):
+        if not self.dist:
+            return x
+        v = self.torch.tensor([float(x)], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(v, op=self.dist.ReduceOp.SUM)
+        return int(v.item())
+
+    def lynch_step_exchange(self, eng):
+        """The one exchange of the Lynch path at N > 1: every rank's unique-
+        profile table (O(U) x 16 B) all-gathered as device tensors over RCCL,
+        loaded; rank 0 runs the one Nelder-Mead estimate, (pi, eps) broadcast
+        over RCCL, the others classify with it."""
+        import sid_amd
+        from sid_amd import dist as sdist
+        keys, cnts = eng.profile_table()
+        keys, cnts = sdist.allgather_profile_table(keys, cnts, device=self.dev)
+        eng.profile_load(keys, cnts)
+        torch = self.torch
+        if self.rank == 0:
+            est = eng.estimate()
+            vec = torch.tensor([est.heterozygosity, est.error_rate, float(est.iterations)], dtype=torch.float64,
+                               device=self.dev)
+        else:
+            vec = torch.zeros(3, dtype=torch.float64, device=self.dev)
+        self.dist.broadcast(vec, 0)
+        if self.rank != 0:
+            g = sid_amd.Estimate()
+            g.heterozygosity, g.error_rate, g.iterations = float(vec[0]), float(vec[1]), int(vec[2])
+            est = eng.estimate(given=g)
+        return est
+
+    def run_step(self, eng, lynch):
+        st = eng.ingest()
+        if lynch and self.dist is not None:
+            est = self.lynch_step_exchange(eng)
+        else:
+            est = eng.estimate()
+        _, st2 = eng.emit()
+        return st, st2, est
+
+
+def main():
+    a = parse_args()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    R = Rank(a)
+    cfg = dict(CONFIGS[a.config])
+    if cfg["total"]:
+        out, eng_keep = bench_strong(R, a, cfg)
+    else:
+        out, eng_keep = bench_weak(R, a, cfg)
+    if R.rank == 0:
+        print(json.dumps(out), flush=True)
+    for e in eng_keep:
+        e.close()
+    if R.dist:
+        R.dist.barrier()
+        R.dist.destroy_process_group()
+
+
+def bench_weak(R, a, cfg):
+    """C2 / C3: 50M sites per GPU; value = the PCIe-inclusive run."""
+    import sid_amd
+    from sid_amd import gpu as G
+    torch = R.torch
+    n = a.sites or cfg["per_gpu"]
+    first = R.rank * n
+    lynch = cfg["method"] != "local" or cfg["R"]
+    text, ln = G.synth_text_hbm(cfg["seed"], cfg["depth"], first, n, device=R.gpu)
+    host = text[:ln].cpu().pin_memory()     # the rank's input, in host memory (its GPU's NUMA node)
+    # the CSV is ~0.53 of the text at 30x: the arena never runs out
+    hh = int(ln * 0.6) + (64 << 20)
+    eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=R.gpu,
+                         chunk_bytes=a.chunk_mib << 20, device_sink=2, host_hold_bytes=hh)
+    eng.source_host_ptr(host.data_ptr(), ln, keep=host)
+    elapsed, (st, st2, est) = R.timed(lambda: R.run_step(eng, lynch), a.steps, a.warmup)
+    elapsed = R.max_over_ranks([elapsed])[0]
+    sites_all = R.sum_over_ranks(st.sites)
+    # the same records in host memory as the CLI writes (spot check)
+    if st2.bytes_out == 0 and st.sites:
+        raise SystemExit("bench.py: no records came back")
+    pcie = {"text_bytes": ln, "csv_bytes": st2.bytes_out,
+            "GBps_h2d": ln / (elapsed / a.steps) / 1e9, "GBps_d2h": st2.bytes_out / (elapsed / a.steps) / 1e9,
+            "chunks": st.chunks, "chunks_held_in_host_arena": st.chunks_held, "ingest_s": st.ingest_s,
+            "emit_s": st2.emit_s}
+    eng.close()
+    del host
+
+    dp = device_path(R, a, cfg, text, ln, lynch)
+    out = {
+        "metric": METRIC,
+        "value": sites_all * a.steps / elapsed,
+        "unit": "sites/s",
+        "n_gpus": R.n_gpus,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": ("synthetic (counter-based pileup generator, BASELINE.md): each rank's pileup text in pinned host "
+                 "memory when the timed region starts, the CSV records in pinned host memory when it ends "
+                 "(H2D, index, parse, call, format, D2H inside every step)"),
+        "config": {"workload": f"{a.config}: {cfg['desc']}", "method": cfg["method"],
+                   "estimate_prior": cfg["R"], "seed": cfg["seed"], "depth": cfg["depth"],
+                   "sites_per_gpu": n, "sites_total": sites_all, "text_bytes_rank0": ln,
+                   "csv_bytes_rank0": st2.bytes_out,
+                   "parallelism": f"site-range shards x{R.world}" + (" + RCCL histogram all-gather"
+                                                                     if lynch and R.world > 1 else ""),
+                   "ranks": R.world, "oversubscribed": R.oversub,
+                   "rccl_world": R.world if R.dist is not None and R.backend == "nccl" else None,
+                   "numa": R.numa},
+        "pcie": pcie,
+        "roofline": dp.pop("roofline"),
+        "device_path": dp,
+    }
+    if lynch:
+        out["estimate"] = {"pi": est.heterozygosity, "eps": est.error_rate, "iterations": est.iterations,
+                           "n_unique": est.n_unique}
+    if R.world == 1 and not a.no_extras:
+        out["kernel_local"] = bench_kernel_local(torch, R.dev, cfg, n)
+        out["cli"] = bench_cli(cfg, text, ln, n)
+        if not a.no_cpu:
+            out["cpu_baseline"] = bench_cpu(cfg, text, ln, n)
+    return out, []
+
+
+def device_path(R, a, cfg, text, ln, lynch, gen=None):
+    """The same sid run over text resident in HBM, records left in HBM, with
+    HIP event pairs around every engine stage on the compute stream: the
+    kernels' own rate and the roofline of the dominant stage."""
+    import sid_amd
+    steps = a.device_steps or max(a.steps, 10)
+    eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=R.gpu,
+                         chunk_bytes=a.chunk_mib << 20, device_sink=1)
+    if gen is None:
+        eng.source_device_text(text.data_ptr(), ln, keep=text)
+    else:
+        eng.source_synth(cfg["seed"], gen[1], cfg["depth"], first=gen[0], sites_per_chrom=cfg["spc"],
+                         on_device=True)
+    eng.profile(False)
+
+    def step():
+        eng.profile(True)
+        return R.run_step(eng, lynch)
+    for _ in range(2):
+        R.run_step(eng, lynch)
+    eng.profile_read()
+    elapsed, (st, st2, _) = R.timed(step, steps, 0)
+    prof = eng.profile_read()
+    eng.profile(False)
+    eng.close()
+    stages = {k[:-3]: v / steps for k, v in prof.items() if k.endswith("_ms") and k != "fmt_len_ms"}
+    vals = R.max_over_ranks([elapsed] + [stages[k] for k in sorted(stages)])
+    elapsed = vals[0]
+    stages = dict(zip(sorted(stages), vals[1:]))
+    sites_rank = st.sites
+    sites_all = R.sum_over_ranks(sites_rank)
+    text_bytes = ln if gen is None else None
+    tps = (text_bytes / sites_rank) if text_bytes else (24 + 2.7 * cfg["depth"])
+    cps = st2.bytes_out / sites_rank if sites_rank else 0.0
+    chunks = prof["chunks"] / steps
+    per_launch_sites = sites_rank / max(1.0, chunks)
+    roofs = {}
+    for k, ms in stages.items():
+        if not ms:
+            continue
+        launch_ms = ms / max(1.0, chunks)
+        bps = stage_bytes(k, tps, cps)
+        ach = bps * per_launch_sites / (launch_ms * 1e-3) / 1e9
+        roofs[k] = {"ms_per_step": ms, "launch_ms": launch_ms, "bytes_per_site": bps, "GBps": ach,
+                    "frac": ach / HBM_PEAK_GBS}
+    dom = max(roofs, key=lambda k: roofs[k]["ms_per_step"])
+    d = roofs[dom]
+    roofline = {"bound": "hbm", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": d["frac"], "traffic": pmc_traffic(dom, per_launch_sites),
+                "kernel": f"engine stage '{dom}'", "stage_kernels": STAGE_KERNELS[dom],
+                "launch_ms": d["launch_ms"], "sites_per_launch": per_launch_sites, "bytes_per_site": d["bytes_per_site"],
+                "valu": valu_issue(dom, per_launch_sites, d["launch_ms"]),
+                "source": "device_path: HIP event pairs around each engine stage on the compute stream"}
+    return {"sites_per_s": sites_all * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
+            "stages_ms": stages, "stage_roofline": roofs, "roofline": roofline,
+            "chunks_per_step": chunks,
+            "path": {"bytes_per_site": tps + cps, "text_per_site": tps, "csv_per_site": cps,
+                     "GBps": (text_bytes + st2.bytes_out) / (elapsed / steps) / 1e9 if text_bytes else None,
+                     "note": "text in + CSV out per step (the path's minimum HBM traffic) / ms_per_step"},
+            "note": "text resident in HBM before the timed region, records formatted into HBM (device_sink 1)"}
+
+
+def bench_strong(R, a, cfg):
+    """C4 / C5: a fixed total split by site range; the device path (text in
+    HBM, or generated inside the step with --stream / when it does not fit).
+    The generator's time is reported apart from sid's stages."""
+    import sid_amd
+    torch = R.torch
+    total = a.sites or cfg["total"]
+    first, hi = total * R.rank // R.world, total * (R.rank + 1) // R.world
+    n = hi - first
+    need = int(n * (2.72 * cfg["depth"] + 2))
+    free, _ = torch.cuda.mem_get_info(R.dev)
+    resident = not a.stream and need + (24 << 30) < free
+    gen_ms = None
+    text, ln = None, None
+    if resident:
+        t0 = time.perf_counter()
+        text, ln = generate_resident(torch, sid_amd, R.dev, R.gpu, cfg, first, n)
+        gen_ms = (time.perf_counter() - t0) * 1e3
+        if not a.chunk_mib:   # 2 GiB chunks' record bounds and hold arena overran the HBM the text leaves (C4, 1 GPU)
+            a.chunk_mib = 1024
+        dp = device_path(R, a, cfg, text, ln, False)
+    else:
+        dp = device_path(R, a, cfg, None, None, False, gen=(first, n))
+        gen_ms = generator_probe(R, cfg, first, n)
+    out = {
+        "metric": METRIC,
+        "value": dp["sites_per_s"],
+        "unit": "sites/s",
+        "n_gpus": R.n_gpus,
+        "steps": dp["steps"],
+        "warmup": 2,
+        "ms_per_step": dp["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": ("synthetic (counter-based pileup generator, BASELINE.md): "
+                 + ("the rank's shard of text generated into HBM before the timed region"
+                    if resident else "text generated on the device chunk by chunk inside the step (never stored)")
+                 + "; CSV records formatted into HBM (device path; C2 is the PCIe-inclusive headline)"),
+        "config": {"workload": f"{a.config}: {cfg['desc']}", "method": cfg["method"], "seed": cfg["seed"],
+                   "depth": cfg["depth"], "sites_total": total, "sites_rank0": n, "sites_per_chrom": cfg["spc"],
+                   "resident": resident, "parallelism": f"site-range shards x{R.world}", "ranks": R.world,
+                   "oversubscribed": R.oversub, "numa": R.numa},
+        "roofline": dp.pop("roofline"),
+        "device_path": dp,
+        "generator": {"ms": gen_ms, "inside_step": not resident,
+                      "note": ("generating the shard's text into HBM, before the timed region" if resident else
+                               "the device generator alone over the rank's sites (no sid stage), measured apart; "
+                               "inside the step it runs on the upload stream beside sid's kernels")},
+    }
+    return out, []
+
+
+def generator_probe(R, cfg, first, n):
+    """Device time of the generator alone over the rank's sites, in 50M-site
+    pieces into one reusable buffer (the inside-the-step generator's work)."""
+    import sid_amd
+    torch = R.torch
+    piece = min(n, 20_000_000)
+    cap = int(piece * (24 + 2.9 * cfg["depth"])) + (64 << 20)
+    buf = torch.empty(cap + 512, dtype=torch.uint8, device=R.dev)
+    ctx = sid_amd.Context(R.gpu)
+    torch.cuda.synchronize(R.dev)
+    t0 = time.perf_counter()
+    for lo in range(0, n, piece):
+        ctx.synth_text_device(cfg["seed"], cfg["depth"], first + lo, min(piece, n - lo), buf.data_ptr(), cap,
+                              sites_per_chrom=cfg["spc"])
+    torch.cuda.synchronize(R.dev)
+    ms = (time.perf_counter() - t0) * 1e3
+    ctx.close()
+    return ms
+
+
+def generate_resident(torch, sid_amd, dev, gpu, cfg, first, n):
+    """The rank's shard of C4/C5 as text in HBM: one buffer sized to the
+    text (the rest, at least a 24 GiB reserve, stays free for the engine's
+    chunk workspace, pooled record buffers and hold arena), filled by the device generator in 50M-site pieces
+    laid end to end (every line stands alone, so the pieces concatenate to the
+    shard's text)."""
+    free, _ = torch.cuda.mem_get_info(dev)
+    need = int(n * (2.72 * cfg["depth"] + 2))   # ~81 B/site at 30x, ~564 at 200x (measured)
+    cap = min(free - (24 << 30), int(need * 1.03) + (1 << 30))
+    text = torch.empty(cap, dtype=torch.uint8, device=dev)
+    ctx = sid_amd.Context(gpu)
+    ln, piece = 0, 50_000_000
+    for lo in range(0, n, piece):
+        m = min(piece, n - lo)
+        ln += ctx.synth_text_device(cfg["seed"], cfg["depth"], first + lo, m, text.data_ptr() + ln,
+                                    cap - 512 - ln, sites_per_chrom=cfg["spc"])
+    text[ln:ln + 512].zero_()
+    torch.cuda.synchronize(dev)
+    ctx.close()
+    return text, ln
+
+
 VALU_ISSUE_PER_S = 256 * 4 / 2 * 2.4e9   # wave64 VALU instructions/s: 1024 SIMDs, one per 2 cycles, 2.4 GHz
+PMC_ROUND = os.environ.get("SID_PMC_ROUND", "r03")
+
+
+def pmc_file(stage):
+    for r in (PMC_ROUND, "r02"):
+        p = os.path.join(ROOT, "profiles", f"pmc_{stage}_{r}.json")
+        if os.path.exists(p):
+            return p
+    return None
 
 
 def valu_issue(stage, sites, launch_ms):
     """The stage's VALU work against the chip's VALU issue rate: SQ_INSTS_VALU
-    per site of its kernels (profiles/pmc_c2_r02_summary.json, the committed
-    PMC pass of tools/gpu_pmc_c2.sh) x the sites of a launch, at one wave64
-    instruction per SIMD per 2 cycles (MI355X_MICROARCH.md); None when absent."""
+    per site of its kernels (the committed PMC pass, tools/gpu_pmc_c2.sh) x
+    the sites of a launch, at one wave64 instruction per SIMD per 2 cycles
+    (MI355X_MICROARCH.md); None when absent."""
     try:
-        pm = json.load(open(os.path.join(ROOT, "profiles", "pmc_c2_r02_summary.json")))
-        sites_pmc = json.load(open(os.path.join(ROOT, "profiles", f"pmc_{stage}_r02.json")))["sites_per_launch"]
+        summ = None
+        for r in (PMC_ROUND, "r02"):
+            p = os.path.join(ROOT, "profiles", f"pmc_c2_{r}_summary.json")
+            if os.path.exists(p):
+                summ = p
+                break
+        pm = json.load(open(summ))
+        sites_pmc = json.load(open(pmc_file(stage)))["sites_per_launch"]
     except Exception:
         return None
     insts = 0.0
@@ -327,72 +578,11 @@ def pmc_traffic(stage, sites):
     """HBM bytes per launch of the stage from the committed PMC summary
     (tools/pmc_traffic.py over separate FETCH_SIZE / WRITE_SIZE passes), scaled
     to this launch's sites; None when absent."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{stage}_r02.json")
+    p = pmc_file(stage)
     try:
-        pm = json.load(open(p))
-        return pm["hbm_bytes_per_site"] * sites
+        return json.load(open(p))["hbm_bytes_per_site"] * sites
     except Exception:
         return None
-
-
-def generate_resident(torch, sid_amd, dev, gpu, cfg, first, n):
-    """The rank's shard of C4/C5 as text in HBM: one buffer sized to the
-    text (the rest, at least a 24 GiB reserve, stays free for the engine's
-    chunk workspace, pooled record buffers and hold arena), filled by the device generator in 50M-site pieces
-    laid end to end (every line stands alone, so the pieces concatenate to the
-    shard's text); refuses a shard that does not fit."""
-    free, _ = torch.cuda.mem_get_info(dev)
-    reserve = 24 << 30
-    cap = free - reserve
-    need = int(n * (2.72 * cfg["depth"] + 2))   # ~81 B/site at 30x, ~564 at 200x (measured)
-    if cap < need:
-        raise SystemExit(f"bench.py --resident: the shard's ~{need / 1e9:.0f} GB of text does not fit "
-                         f"({free / 1e9:.0f} GB free, {reserve >> 30} GiB kept for the engine)")
-    cap = min(cap, int(need * 1.03) + (1 << 30))   # the rest stays free for the engine
-    text = torch.empty(cap, dtype=torch.uint8, device=dev)
-    ctx = sid_amd.Context(gpu)
-    ln, piece = 0, 50_000_000
-    for lo in range(0, n, piece):
-        m = min(piece, n - lo)
-        ln += ctx.synth_text_device(cfg["seed"], cfg["depth"], first + lo, m, text.data_ptr() + ln,
-                                    cap - 512 - ln, sites_per_chrom=cfg["spc"])
-    text[ln:ln + 512].zero_()
-    torch.cuda.synchronize(dev)
-    ctx.close()
-    return text, ln
-
-
-def exchange_histogram(torch, dist, eng, dev, rank):
-    """The one exchange of the Lynch path: every rank's unique-profile table
-    (O(U) x 16 B) all-gathered as device tensors over RCCL, merged, loaded."""
-    from sid_amd import dist as sdist
-    ctx = sid_amd_ctx(eng)
-    keys, cnts = ctx.profile_table()
-    keys, cnts = sdist.allgather_profile_table(keys, cnts, device=dev)
-    ctx.profile_load(keys, cnts)
-
-
-def broadcast_estimate(torch, dist, eng, dev, rank):
-    """Rank 0 runs the one Nelder-Mead estimate on the merged table; (pi, eps)
-    go to the other ranks over RCCL, which classify with them."""
-    import sid_amd
-    if rank == 0:
-        est = eng.estimate()
-        vec = torch.tensor([est.heterozygosity, est.error_rate, float(est.iterations)], dtype=torch.float64,
-                           device=dev)
-    else:
-        vec = torch.zeros(3, dtype=torch.float64, device=dev)
-    dist.broadcast(vec, 0)
-    if rank != 0:
-        g = sid_amd.Estimate()
-        g.heterozygosity, g.error_rate, g.iterations = float(vec[0]), float(vec[1]), int(vec[2])
-        est = eng.estimate(given=g)
-    return est
-
-
-def sid_amd_ctx(eng):
-    import sid_amd
-    return sid_amd.Context.wrap(eng.context(0))
 
 
 def bench_kernel_local(torch, dev, cfg, n):
@@ -436,32 +626,13 @@ def bench_kernel_local(torch, dev, cfg, n):
             "traffic": pm, "note": "counts resident in HBM -> code + confs (the round-1 headline kernel)"}
 
 
-def bench_e2e(torch, sid_amd, cfg, text, ln, n, a):
-    """PCIe-inclusive: (1) the engine over the text in pinned host memory, CSV
-    copied back into pinned host memory (engine clock); (2) the CLI on the same
-    text as a file in the page cache, CSV to /dev/null (wall clock and the
-    CLI's own clock)."""
-    res = {"sites": n, "text_bytes": ln}
-    host = text[:ln].cpu().pin_memory()
-    eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], device_sink=2,
-                         chunk_bytes=a.chunk_mib << 20)
-    eng.source_host_ptr(host.data_ptr(), ln, keep=host)
-    runs = []
-    for r in range(3):
-        t0 = time.perf_counter()
-        st = eng.ingest()
-        eng.estimate()
-        _, st2 = eng.emit()
-        runs.append(time.perf_counter() - t0)
-    eng.close()
-    dt = min(runs[1:])
-    res["host_memory"] = {"sites_per_s": n / dt, "s": dt, "runs_s": runs, "csv_bytes": st2.bytes_out,
-                          "note": "pinned host text -> H2D -> index/parse/call/format -> D2H into pinned host "
-                                  "memory (records dropped there), one GPU, engine clock"}
-    del host
+def bench_cli(cfg, text, ln, n):
+    """build/sid on the same text as a file in the page cache, CSV to
+    /dev/null: wall clock (process start, HIP init, mapping, both PCIe legs,
+    write) and the CLI's own clock."""
     cli = os.path.join(ROOT, "build", "sid")
     if not os.path.exists(cli):
-        return res
+        return None
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "c.plp")
         write_text_file(text, ln, path)
@@ -473,19 +644,17 @@ def bench_e2e(torch, sid_amd, cfg, text, ln, n, a):
                 r = subprocess.run([cli, "--stats"] + flags + [path], stdout=dn, stderr=subprocess.PIPE)
                 dt = time.perf_counter() - t0
             if r.returncode != 0:
-                res["cli"] = {"error": r.returncode, "stderr": r.stderr.decode()[-400:]}
-                return res
+                return {"error": r.returncode, "stderr": r.stderr.decode()[-400:]}
             try:
                 stt = json.loads(r.stderr.decode().strip().splitlines()[-1])
             except Exception:
                 stt = {}
             cli_runs.append((dt, stt))
         dt, stt = min(cli_runs[1:], key=lambda x: x[0])
-        res["cli"] = {"wall_s": dt, "sites_per_s_wall": n / dt, "sites_per_s_cli_clock": stt.get("sites_per_s"),
-                      "wall_s_runs": [x[0] for x in cli_runs], "cli_stats": stt,
-                      "note": "build/sid FILE > /dev/null, one GPU: wall = process start + HIP init + mmap + "
-                              "H2D + parse/call/format + D2H + write; cli_clock = input mapping to last write"}
-    return res
+        return {"wall_s": dt, "sites_per_s_wall": n / dt, "sites_per_s_cli_clock": stt.get("sites_per_s"),
+                "wall_s_runs": [x[0] for x in cli_runs], "cli_stats": stt,
+                "note": "build/sid FILE > /dev/null, one GPU: wall = process start + HIP init + mmap + "
+                        "H2D + parse/call/format + D2H + write; cli_clock = input mapping to last write"}
 
 
 def write_text_file(text, ln, path):

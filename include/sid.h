@@ -296,12 +296,22 @@ typedef struct {
     int verbose;            /* the reference's "# ..." lines on stderr             */
     int device_sink;        /* 0: write() in file order; 1: records stay in HBM,
                                nothing is copied back (measurement); 2: records
-                               copied back to pinned host memory and dropped
-                               (measurement of the PCIe path, no write)          */
+                               copied back to pinned host memory, no write
+                               (measurement of the PCIe path; with
+                               host_hold_bytes they stay there for
+                               sid_engine_records)                               */
     int lanes;              /* pipelines per GPU (0 = 1): each its own streams,
                                context and workspace, chunks dealt over all of
                                them, so one chunk's kernels run while another
                                waits on its host sync                            */
+    uint64_t host_hold_bytes; /* per pipeline, pinned host memory (made once,
+                               reused by every run) for the records: -m local /
+                               quality copy each chunk's records into it during
+                               the ingest, while later chunks upload (PCIe both
+                               ways at once), and the emit only write()s them;
+                               the second pass copies into it instead of the
+                               pinned ring.  Chunks beyond it take the HBM hold.
+                               0 = off.  Ignored with device_sink 1             */
 } sid_engine_cfg;
 typedef struct {
     uint64_t sites;              /* non-empty lines parsed                           */
@@ -343,6 +353,17 @@ int sid_engine_ingest(sid_engine* e, sid_run_stats* stats);
 int sid_engine_estimate(sid_engine* e, const sid_estimate* given, sid_estimate* out);
 int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn write, void* user, sid_run_stats* stats);
 int sid_engine_run(sid_engine* e, const char* header, sid_write_fn write, void* user, sid_run_stats* stats);
+/* Multi-rank Lynch runs: after ingest, the merged unique-
+ * profile table of all the engine's pipelines (sid_profile_table layout;
+ * keys == NULL: only *u), and the load of a table merged across ranks into
+ * every pipeline (it is not merged again by sid_engine_estimate). */
+int sid_engine_profile_table(sid_engine* e, uint64_t* keys, uint64_t* counts64, size_t cap, size_t* u);
+int sid_engine_profile_load(sid_engine* e, const uint64_t* keys, const uint64_t* counts64, size_t u);
+/* With host_hold_bytes: the CSV records of chunk `chunk` (0 .. stats.chunks-1,
+ * file order) in the host arena, after the emit (device_sink 2: the records
+ * are not written anywhere else), valid until the next ingest or source;
+ * SID_ESTATE when that chunk's records did not go through the host arena. */
+int sid_engine_records(sid_engine* e, uint64_t chunk, const char** bytes, uint64_t* len);
 /* Measurement: with profiling on, every stage of every chunk is bracketed by
  * a pair of HIP events on its device's compute stream; _read sums the stages'
  * device time over the chunks and devices since the last read (synchronises). */

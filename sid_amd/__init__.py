@@ -61,7 +61,8 @@ class EngineCfg(C.Structure):
     """sid_engine_cfg (include/sid.h, streaming engine)."""
     _fields_ = [("devices", C.c_int), ("first_device", C.c_int), ("chunk_bytes", C.c_uint64),
                 ("slots", C.c_int), ("hold_bytes", C.c_uint64), ("retain_bytes", C.c_uint64),
-                ("host_threads", C.c_int), ("verbose", C.c_int), ("device_sink", C.c_int), ("lanes", C.c_int)]
+                ("host_threads", C.c_int), ("verbose", C.c_int), ("device_sink", C.c_int), ("lanes", C.c_int),
+                ("host_hold_bytes", C.c_uint64)]
 
 
 class RunStats(C.Structure):
@@ -139,6 +140,9 @@ SIGNATURES = [
     ("sid_engine_estimate", _I, [_P, C.POINTER(Estimate), C.POINTER(Estimate)]),
     ("sid_engine_emit", _I, [_P, C.c_char_p, WRITE_FN, _P, C.POINTER(RunStats)]),
     ("sid_engine_run", _I, [_P, C.c_char_p, WRITE_FN, _P, C.POINTER(RunStats)]),
+    ("sid_engine_profile_table", _I, [_P, _P, _P, _SZ, C.POINTER(C.c_size_t)]),
+    ("sid_engine_profile_load", _I, [_P, _P, _P, _SZ]),
+    ("sid_engine_records", _I, [_P, _U64, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("sid_engine_profile", _I, [_P, _I]),
     ("sid_engine_profile_read", _I, [_P, C.POINTER(EngineProf)]),
 ]
@@ -439,13 +443,15 @@ class Engine:
     line-aligned chunks over one or more devices."""
 
     def __init__(self, method="local", devices=1, first_device=0, chunk_bytes=0, slots=0, hold_bytes=0,
-                 retain_bytes=0, host_threads=0, verbose=False, device_sink=False, lanes=0, **opts):
+                 retain_bytes=0, host_threads=0, verbose=False, device_sink=False, lanes=0, host_hold_bytes=0,
+                 **opts):
         self.opts = make_opts(method=method, **opts)
         cfg = EngineCfg()
         lib().sid_engine_cfg_default(C.byref(cfg))
         cfg.devices, cfg.first_device, cfg.chunk_bytes, cfg.slots = devices, first_device, chunk_bytes, slots
         cfg.hold_bytes, cfg.retain_bytes, cfg.host_threads = hold_bytes, retain_bytes, host_threads
         cfg.verbose, cfg.device_sink, cfg.lanes = int(bool(verbose)), int(device_sink), lanes
+        cfg.host_hold_bytes = host_hold_bytes
         self.cfg = cfg
         h = C.c_void_p()
         check(lib().sid_engine_create(C.byref(self.opts), C.byref(cfg), C.byref(h)), "sid_engine_create")
@@ -510,15 +516,50 @@ class Engine:
         parts = []
 
         def w(_user, data, n):
-            if isinstance(sink, int):
-                os.write(sink, C.string_at(data, n))
-            else:
-                parts.append(C.string_at(data, n))
-            return 0
+            try:
+                if isinstance(sink, int):   # every byte, across partial writes
+                    mv = memoryview(C.string_at(data, n))
+                    while len(mv):
+                        mv = mv[os.write(sink, mv):]
+                else:
+                    parts.append(C.string_at(data, n))
+                return 0
+            except Exception:   # the engine reports SID_EIO
+                return -1
         cb = WRITE_FN(w)
         st = stats if stats is not None else RunStats()
         check(lib().sid_engine_emit(self.h, header, cb, None, C.byref(st)), "sid_engine_emit")
         return b"".join(parts), st
+
+    def profile_table(self):
+        """The merged unique-profile table of all pipelines (after ingest)."""
+        u = C.c_size_t(0)
+        check(lib().sid_engine_profile_table(self.h, None, None, 0, C.byref(u)), "sid_engine_profile_table")
+        keys = np.zeros(u.value, np.uint64)
+        cnts = np.zeros(u.value, np.uint64)
+        if u.value:
+            check(lib().sid_engine_profile_table(self.h, _ptr(keys), _ptr(cnts), u.value, C.byref(u)),
+                  "sid_engine_profile_table")
+        return keys, cnts
+
+    def profile_load(self, keys: np.ndarray, cnts: np.ndarray):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        cnts = np.ascontiguousarray(cnts, np.uint64)
+        check(lib().sid_engine_profile_load(self.h, _ptr(keys), _ptr(cnts), len(keys)), "sid_engine_profile_load")
+
+    def records(self, chunk: int):
+        """(address, length) of a chunk's records in the host arena."""
+        p, n = C.c_void_p(), C.c_uint64(0)
+        check(lib().sid_engine_records(self.h, chunk, C.byref(p), C.byref(n)), "sid_engine_records")
+        return p.value or 0, n.value
+
+    def records_bytes(self, nchunks: int) -> bytes:
+        """Every chunk's records from the host arena, in file order."""
+        out = []
+        for j in range(nchunks):
+            p, n = self.records(j)
+            out.append(C.string_at(p, n) if n else b"")
+        return b"".join(out)
 
     def profile(self, enable=True):
         check(lib().sid_engine_profile(self.h, int(bool(enable))), "sid_engine_profile")

@@ -10,7 +10,7 @@
 //
 // Extra long options (no short letter, so they cannot collide with the
 // reference's flags): --devices N, --threads N, --stats, --host-parse,
-// --chunk-bytes N, --hold-bytes N, --retain-bytes N.
+// --chunk-bytes N, --hold-bytes N, --retain-bytes N, --host-hold N.
 //
 // --host-parse keeps the round-1 path instead: the whole input parsed on the
 // host (sid_parse_text), counts to the devices, records formatted on the host
@@ -51,6 +51,7 @@ struct Options {
     bool host_parse = false;   // parse and format on the host (sid_parse_text / sid_format_csv)
     uint64_t chunk_bytes = 0;  // engine knobs (0 = defaults)
     uint64_t hold_bytes = 0;
+    uint64_t host_hold = 0;   // --host-hold: sid_engine_cfg.host_hold_bytes
     uint64_t retain_bytes = 0;
 };
 
@@ -185,6 +186,7 @@ int main(int argc, char** argv)
                                          {"chunk-bytes", required_argument, nullptr, 5},
                                          {"hold-bytes", required_argument, nullptr, 6},
                                          {"retain-bytes", required_argument, nullptr, 7},
+                                         {"host-hold", required_argument, nullptr, 8},
                                          {nullptr, 0, nullptr, 0}};
     int flag;
     while ((flag = getopt_long(argc, argv, "E:Rhm:p:r:", LONG, nullptr)) != -1) {
@@ -209,6 +211,7 @@ int main(int argc, char** argv)
         case 5: opt.chunk_bytes = std::strtoull(optarg, nullptr, 10); break;
         case 6: opt.hold_bytes = std::strtoull(optarg, nullptr, 10); break;
         case 7: opt.retain_bytes = std::strtoull(optarg, nullptr, 10); break;
+        case 8: opt.host_hold = std::strtoull(optarg, nullptr, 10); break;
         default: std::exit(EXIT_FAILURE);
         }
     }
@@ -307,6 +310,7 @@ int main(int argc, char** argv)
         cfg.chunk_bytes = opt.chunk_bytes;
         cfg.hold_bytes = opt.hold_bytes;
         cfg.retain_bytes = opt.retain_bytes;
+        cfg.host_hold_bytes = opt.host_hold;
         cfg.host_threads = T;
         cfg.verbose = 1;
         sid_engine* eng = nullptr;

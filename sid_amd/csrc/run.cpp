@@ -27,6 +27,7 @@
 
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -193,6 +194,9 @@ struct ChunkRec {
     char* pre = nullptr;             // Lynch paths: the pass-1 parse (line offsets, counts, formatter
     uint64_t pre_cap = 0;            // header pairs: n x 32 B) kept for pass 2, which skips index + parse
     uint64_t err = ~0ull;            // min(offset * 8 + kind) of the chunk's malformed lines
+    const char* host = nullptr;      // its records in the host arena (host_hold_bytes), or null
+    uint64_t host_len = 0;
+    bool host1 = false;              // copied there during pass 1 (the emit only writes them)
 };
 
 enum SrcKind { SRC_NONE, SRC_HOST, SRC_FILE, SRC_DEVICE, SRC_SYNTH_HOST, SRC_SYNTH_DEVICE };
@@ -221,6 +225,8 @@ struct Piece {
     bool last = false;
     char* buf = nullptr;      // the chunk's device CSV buffer, returned after the last piece
     uint64_t cap = 0;
+    const char* host = nullptr;  // the whole chunk copied into the host arena instead (ps = -1)
+    hipEvent_t hev = nullptr;    // that copy done
 };
 
 struct Slot {
@@ -253,11 +259,15 @@ struct Dev {
     std::vector<std::pair<char*, uint64_t>> arena;
     size_t arena_seg = 0;
     uint64_t arena_off = 0;
-    char* arena_reserve(uint64_t need)
+    // `left`: what the hold budget still allows (a new segment is not made
+    // larger than that, nor than 4 GiB, nor smaller than `need`); null when
+    // the HBM is not there (the caller formats the chunk in pass 2 instead)
+    char* arena_reserve(uint64_t need, uint64_t left)
     {
         while (arena_seg < arena.size() && arena_off + need > arena[arena_seg].second) ++arena_seg, arena_off = 0;
         if (arena_seg == arena.size()) {
-            const uint64_t c = std::max<uint64_t>(need, 4ull << 30);
+            const uint64_t want = std::min<uint64_t>(4ull << 30, std::max(need, left));
+            const uint64_t c = (std::max(need, want) + (2u << 20) - 1) & ~(uint64_t)((2u << 20) - 1);
             char* p = nullptr;
             if (hipMalloc(&p, c) != hipSuccess) return nullptr;
             arena.push_back({p, c});
@@ -271,6 +281,20 @@ struct Dev {
         uint64_t b = 0;
         for (auto& a : arena) b += a.second;
         return b;
+    }
+    // host arena (sid_engine_cfg.host_hold_bytes): pinned host memory, made
+    // once and reused by every run, that receives the records D2H -- in pass
+    // 1 while later chunks upload (full duplex), in pass 2 instead of the
+    // pinned ring; bump-allocated, reset by every ingest
+    char* hh = nullptr;
+    uint64_t hh_cap = 0, hh_off = 0;
+    bool hh_full = false;
+    char* hh_take(uint64_t bytes)
+    {
+        if (!hh || hh_off + bytes > hh_cap) return nullptr;
+        char* p = hh + hh_off;
+        hh_off += (bytes + 255) & ~(uint64_t)255;
+        return p;
     }
     uint64_t hold_budget = 0, retain_budget = 0;
     std::atomic<uint64_t> hold_used{0}, retain_used{0};
@@ -340,6 +364,7 @@ struct sid_engine {
     std::vector<ChunkRec> recs;
     // run state
     bool lynch = false, quality = false, ingested = false, estimated = false;
+    bool hist_merged = false;        // the pipelines' Lynch histograms hold the merged table
     const char* conf_type = "p_value";
     std::atomic<int> rc{SID_OK};
     std::atomic<uint64_t> first_err{UINT64_MAX};
@@ -579,6 +604,7 @@ extern "C" int sid_engine_destroy(sid_engine* e)
             if (s.ev_free) (void)hipEventDestroy(s.ev_free);
         }
         for (char* p : d->pinned) (void)hipHostFree(p);
+        if (d->hh) (void)hipHostFree(d->hh);
         for (hipEvent_t ev : d->pinned_ev) (void)hipEventDestroy(ev);
         for (hipEvent_t ev : d->ev_cache) (void)hipEventDestroy(ev);
         for (auto& pr : d->prof_pending) (void)hipEventDestroy(pr.second.first), (void)hipEventDestroy(pr.second.second);
@@ -633,6 +659,11 @@ extern "C" int sid_engine_source_text(sid_engine* e, const char* text, uint64_t 
 extern "C" int sid_engine_source_file(sid_engine* e, int fd, uint64_t offset, uint64_t len)
 {
     if (!e || fd < 0) return SID_EINVAL;
+    struct stat sb;
+    // a range past the end of the file would fault (SIGBUS) on the first read
+    if (fstat(fd, &sb) != 0) return SID_EIO;
+    if (S_ISREG(sb.st_mode) && (offset > (uint64_t)sb.st_size || len > (uint64_t)sb.st_size - offset))
+        return SID_EINVAL;
     drop_source(e);
     if (len == 0) {
         e->src = SRC_HOST;
@@ -754,6 +785,7 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
         ChunkRec& r = e->recs[j];
         Loaded L;
         L.j = j;
+        if (pass == 2 && r.host1) continue;   // already in host memory: the writer takes it from there
         if (pass == 2 && r.held) {
             L.kind = 1;
             if (!d.loaded.push(L)) break;
@@ -778,17 +810,18 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
         uint64_t need = e->src == SRC_SYNTH_HOST || e->src == SRC_SYNTH_DEVICE ? e->per_chunk_cap : r.len;
         // keep it for pass 2?  Lynch always needs a second pass; local and
         // quality only once the hold budget ran out
-        const bool want_keep = pass == 1 && (e->lynch || d.hold_full.load()) &&
-                               d.retain_used.load() + need + PAD <= d.retain_budget;
+        bool want_keep = pass == 1 && (e->lynch || d.hold_full.load()) &&
+                         d.retain_used.load() + need + PAD <= d.retain_budget;
         char* dst = nullptr;
         uint64_t dcap = 0;
         int slot = -1;
         hipError_t x = hipSuccess;
         if (want_keep) {
             dst = d.pool.get(need + PAD, &dcap, d.s_up);
-            if (!dst) return (void)fail(e, SID_ENOMEM);
-            d.retain_used += dcap;
-        } else {
+            if (dst) d.retain_used += dcap;
+            else want_keep = false;   // no HBM for it: a ring slot, read again in pass 2
+        }
+        if (!want_keep) {
             if (!d.free_slots.pop(slot)) break;
             Slot& s = d.slots[slot];
             if (s.cap < need) {   // grow: wait for the slot's last reader first
@@ -1041,17 +1074,24 @@ void compute(sid_engine* e, Dev& d, int pass)
         // else a pooled scratch buffer
         char* out = nullptr;
         uint64_t cap = 0;   // 0: arena memory (never returned to the pool)
+        bool via_host = false;   // pass 1: records go on to the host arena (a pooled device buffer meanwhile)
         if (format && !lynch_hist) {
             pe = d.prof_begin(P);
             rc = call_sites(e, d, L, n);
             d.prof_end(2, pe);
             if (rc != SID_OK) return (void)fail(e, rc);
             const uint64_t bound = sid_chunk_fmt_bound(n, L.c1 - L.c0);
-            if (n == 0) {
+            if (n && pass == 1 && d.hh && !d.hh_full) {
+                out = d.pool.get(bound, &cap, d.s_comp);
+                via_host = out != nullptr;
+                if (!out) cap = 0;
+            }
+            if (n == 0 || via_host) {
             } else if (pass == 1 && d.hold_used.load() + bound > d.hold_budget) {
                 d.hold_full = true;   // this chunk and the rest: formatted in pass 2
             } else if (pass == 1) {
-                if (!(out = d.arena_reserve(bound))) return (void)fail(e, SID_ENOMEM);
+                // no HBM for the arena: formatted in pass 2 instead
+                if (!(out = d.arena_reserve(bound, d.hold_budget - d.hold_used.load()))) d.hold_full = true;
             } else {
                 if (!(out = d.pool.get(bound, &cap, d.s_comp))) return (void)fail(e, SID_ENOMEM);
             }
@@ -1095,6 +1135,7 @@ void compute(sid_engine* e, Dev& d, int pass)
         const uint64_t err = hs[4];
         if (err != ~0ull) {   // a malformed line: the rest of the input is moot
             r.err = err - 8 * L.c0;
+            if (out && cap) d.pool.put(out, cap, d.s_comp);
             uint64_t cur = e->first_err.load();
             while (L.j < cur && !e->first_err.compare_exchange_weak(cur, L.j)) {
             }
@@ -1117,6 +1158,36 @@ void compute(sid_engine* e, Dev& d, int pass)
         if (pass == 2 && r.pre) {
             d.pool.put(r.pre, r.pre_cap, d.s_comp);
             r.pre = nullptr;
+        }
+        if (pass == 1 && via_host) {
+            char* hp = d.hh_take(bytes);
+            if (hp) {   // D2H behind this chunk's formatter, while the next chunks upload
+                hipEvent_t ev = d.take_event();
+                if (!ev) return (void)fail(e, SID_EHIP);
+                x = hipEventRecord(ev, d.s_comp);
+                if (x == hipSuccess) x = hipStreamWaitEvent(d.s_d2h, ev, 0);
+                d.give_event(ev);
+                if (x == hipSuccess && bytes) x = hipMemcpyAsync(hp, out, bytes, hipMemcpyDeviceToHost, d.s_d2h);
+                if (x != hipSuccess) return (void)hipfail(e, x);
+                d.pool.put(out, cap, d.s_d2h);   // reusable once the copy is done
+                r.host = hp;
+                r.host_len = bytes;
+                r.host1 = true;
+                continue;
+            }
+            // the host arena is full: keep the records on the device while
+            // the hold budget allows, else format the chunk again in pass 2
+            d.hh_full = true;
+            if (d.hold_used.load() + cap <= d.hold_budget) {
+                r.held = out;
+                r.held_cap = cap;
+                r.held_len = bytes;
+                d.hold_used += cap;
+            } else {
+                d.hold_full = true;
+                d.pool.put(out, cap, d.s_comp);
+            }
+            continue;
         }
         if (pass == 1) {
             d.arena_commit(bytes);
@@ -1161,12 +1232,32 @@ void drain(sid_engine* e, Dev& d)
         }
         if (x != hipSuccess) return (void)hipfail(e, x);
         if (it.len == 0) {
+            if (d.hh) e->recs[it.j].host = d.hh, e->recs[it.j].host_len = 0;
             Piece p;
             p.j = it.j;
             p.last = true;
             p.buf = it.buf;
             p.cap = it.cap;
             if (!d.out_q.push(p)) break;
+            continue;
+        }
+        if (char* hp = d.hh_take(it.len)) {   // the whole chunk into the host arena, one copy
+            hipEvent_t ev = d.take_event();
+            if (!ev) return (void)fail(e, SID_EHIP);
+            x = hipMemcpyAsync(hp, it.buf, it.len, hipMemcpyDeviceToHost, d.s_d2h);
+            if (x == hipSuccess) x = hipEventRecord(ev, d.s_d2h);
+            if (x != hipSuccess) return (void)hipfail(e, x);
+            e->recs[it.j].host = hp;
+            e->recs[it.j].host_len = it.len;
+            Piece p;
+            p.j = it.j;
+            p.len = it.len;
+            p.last = true;
+            p.buf = it.buf;
+            p.cap = it.cap;
+            p.host = hp;
+            p.hev = ev;
+            if (!d.out_q.push(p)) return;
             continue;
         }
         for (uint64_t o = 0; o < it.len;) {
@@ -1220,6 +1311,9 @@ static void reset_run(sid_engine* e)
         if (r.pre) d.pool.put(r.pre, r.pre_cap, nullptr);
         r.held = r.kept = r.pre = nullptr;
         r.held_len = r.kept_len = 0;
+        r.host = nullptr;
+        r.host_len = 0;
+        r.host1 = false;
         r.err = ~0ull;
         r.parsed = 0;
     }
@@ -1230,7 +1324,10 @@ static void reset_run(sid_engine* e)
         d.hold_full = false;
         d.arena_seg = 0;
         d.arena_off = 0;
+        d.hh_off = 0;
+        d.hh_full = false;
     }
+    e->hist_merged = false;
 }
 
 static void start_queues(sid_engine* e)
@@ -1258,6 +1355,15 @@ static int setup_budgets(sid_engine* e)
         const double share = 0.40 / std::max(1, e->cfg.lanes);
         d.hold_budget = e->cfg.hold_bytes ? e->cfg.hold_bytes : (uint64_t)(avail * share);
         d.retain_budget = e->cfg.retain_bytes ? e->cfg.retain_bytes : (uint64_t)(avail * share);
+        // the host arena: pinned (and so populated) once, reused by every run
+        const uint64_t hb = e->cfg.device_sink == 1 ? 0 : e->cfg.host_hold_bytes;
+        if (hb && d.hh_cap < hb) {
+            if (d.hh) (void)hipHostFree(d.hh);
+            d.hh = nullptr;
+            d.hh_cap = 0;
+            if (hipHostMalloc((void**)&d.hh, hb, hipHostMallocDefault) != hipSuccess) return SID_ENOMEM;
+            d.hh_cap = hb;
+        }
     }
     return SID_OK;
 }
@@ -1306,14 +1412,15 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
     }
     for (auto& dp : e->devs) {
         (void)hipSetDevice(dp->device);
-        if (hipStreamSynchronize(dp->s_comp) != hipSuccess || hipStreamSynchronize(dp->s_up) != hipSuccess)
+        if (hipStreamSynchronize(dp->s_comp) != hipSuccess || hipStreamSynchronize(dp->s_up) != hipSuccess ||
+            hipStreamSynchronize(dp->s_d2h) != hipSuccess)
             return SID_EHIP;
     }
     uint64_t sites = 0, bytes = 0, held = 0, kept = 0;
     for (auto& r : e->recs) {
         sites += r.parsed;
         bytes += r.len;
-        held += r.held != nullptr;
+        held += r.held != nullptr || r.host1;
         kept += r.kept != nullptr;
     }
     if (st) {
@@ -1345,6 +1452,76 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
     return SID_OK;
 }
 
+// the pipelines' Lynch histograms merged (KB-sized tables) and loaded into
+// every context, once per ingest (a second estimate, or a table loaded with
+// sid_engine_profile_load, must not be merged again)
+static int merge_histograms(sid_engine* e)
+{
+    const int D = (int)e->devs.size();
+    if (D == 1 || e->hist_merged) {
+        e->hist_merged = true;
+        return SID_OK;
+    }
+    std::vector<std::vector<uint64_t>> k(D), v(D);
+    std::vector<int> rcs(D, SID_OK);
+    std::vector<std::thread> th;
+    for (int i = 0; i < D; ++i)
+        th.emplace_back([&, i] {
+            size_t u = 0;
+            sid_ctx* c = e->devs[i]->ctx;
+            rcs[i] = sid_profile_table(c, nullptr, nullptr, 0, &u);
+            if (rcs[i]) return;
+            k[i].resize(u);
+            v[i].resize(u);
+            rcs[i] = sid_profile_table(c, k[i].data(), v[i].data(), u, &u);
+        });
+    for (auto& t : th) t.join();
+    for (int r : rcs)
+        if (r) return r;
+    std::vector<uint64_t> K, V;
+    for (int i = 0; i < D; ++i) {
+        K.insert(K.end(), k[i].begin(), k[i].end());
+        V.insert(V.end(), v[i].begin(), v[i].end());
+    }
+    for (int i = 0; i < D; ++i) {
+        const int rc = sid_profile_load(e->devs[i]->ctx, K.data(), V.data(), K.size());
+        if (rc != SID_OK) return rc;
+    }
+    e->hist_merged = true;
+    return SID_OK;
+}
+
+extern "C" int sid_engine_profile_table(sid_engine* e, uint64_t* keys, uint64_t* counts64, size_t cap, size_t* u)
+{
+    if (!e || !u) return SID_EINVAL;
+    if (!e->ingested || !e->lynch) return SID_ESTATE;
+    const int rc = merge_histograms(e);
+    if (rc != SID_OK) return rc;
+    return sid_profile_table(e->devs[0]->ctx, keys, counts64, cap, u);
+}
+
+extern "C" int sid_engine_profile_load(sid_engine* e, const uint64_t* keys, const uint64_t* counts64, size_t u)
+{
+    if (!e || (!keys && u) || (!counts64 && u)) return SID_EINVAL;
+    if (!e->ingested || !e->lynch) return SID_ESTATE;
+    for (auto& dp : e->devs) {
+        const int rc = sid_profile_load(dp->ctx, keys, counts64, u);
+        if (rc != SID_OK) return rc;
+    }
+    e->hist_merged = true;
+    return SID_OK;
+}
+
+extern "C" int sid_engine_records(sid_engine* e, uint64_t chunk, const char** bytes, uint64_t* len)
+{
+    if (!e || !bytes || !len || chunk >= e->recs.size()) return SID_EINVAL;
+    const ChunkRec& r = e->recs[chunk];
+    if (!r.host) return SID_ESTATE;
+    *bytes = r.host;
+    *len = r.host_len;
+    return SID_OK;
+}
+
 extern "C" int sid_engine_estimate(sid_engine* e, const sid_estimate* given, sid_estimate* out)
 {
     if (!e || !e->ingested) return SID_ESTATE;
@@ -1354,32 +1531,8 @@ extern "C" int sid_engine_estimate(sid_engine* e, const sid_estimate* given, sid
     }
     const int D = (int)e->devs.size();
     const int verbose = e->cfg.verbose;
-    int rc = SID_OK;
-    if (D > 1) {   // merge the device histograms (KB-sized tables)
-        std::vector<std::vector<uint64_t>> k(D), v(D);
-        std::vector<int> rcs(D, SID_OK);
-        std::vector<std::thread> th;
-        for (int i = 0; i < D; ++i)
-            th.emplace_back([&, i] {
-                size_t u = 0;
-                sid_ctx* c = e->devs[i]->ctx;
-                rcs[i] = sid_profile_table(c, nullptr, nullptr, 0, &u);
-                if (rcs[i]) return;
-                k[i].resize(u);
-                v[i].resize(u);
-                rcs[i] = sid_profile_table(c, k[i].data(), v[i].data(), u, &u);
-            });
-        for (auto& t : th) t.join();
-        for (int r : rcs)
-            if (r) return r;
-        std::vector<uint64_t> K, V;
-        for (int i = 0; i < D; ++i) {
-            K.insert(K.end(), k[i].begin(), k[i].end());
-            V.insert(V.end(), v[i].begin(), v[i].end());
-        }
-        for (int i = 0; i < D; ++i)
-            if ((rc = sid_profile_load(e->devs[i]->ctx, K.data(), V.data(), K.size())) != SID_OK) return rc;
-    }
+    int rc = merge_histograms(e);
+    if (rc != SID_OK) return rc;
     // one estimate (device 0, prints the reference's lines), the others
     // classify with its (pi, eps)
     sid_estimate est{};
@@ -1450,10 +1603,28 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
         if (sink == 0 && header && write(user, header, std::strlen(header)) != 0) ok = false;
         for (uint64_t j = 0; j < e->recs.size() && e->rc.load() == SID_OK; ++j) {
             Dev& d = *e->devs[e->recs[j].dev];
+            const ChunkRec& rj = e->recs[j];
+            if (rj.host1) {   // copied back during the ingest (which waited for the copies)
+                if (ok && sink == 0 && rj.host_len && write(user, rj.host, rj.host_len) != 0) ok = false;
+                out_bytes += rj.host_len;
+                if (!ok) break;
+                continue;
+            }
             Piece p;
             bool got_last = false;
             while (d.out_q.pop(p)) {
-                if (p.ps >= 0) {
+                if (p.host) {
+                    const double w0 = wall();
+                    const hipError_t ws = hipEventSynchronize(p.hev);
+                    e->t_write_wait += (uint64_t)((wall() - w0) * 1e9);
+                    d.give_event(p.hev);
+                    if (ws != hipSuccess) {
+                        fail(e, SID_EHIP);
+                        break;
+                    }
+                    if (ok && sink == 0 && write(user, p.host, p.len) != 0) ok = false;
+                    out_bytes += p.len;
+                } else if (p.ps >= 0) {
                     const double w0 = wall();
                     const hipError_t ws = hipEventSynchronize(d.pinned_ev[p.ps]);
                     e->t_write_wait += (uint64_t)((wall() - w0) * 1e9);

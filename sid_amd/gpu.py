@@ -94,3 +94,19 @@ def run_method(counts_np: np.ndarray, method: str = "local", device: int = 0, ve
     torch.cuda.synchronize(device)
     ctx.close()
     return code[:n].cpu().numpy(), hom[:n].cpu().numpy(), het[:n].cpu().numpy(), est
+
+
+def synth_text_hbm(seed: int, depth: float, first: int, n: int, sites_per_chrom: int = 0, device: int = 0):
+    """The generator's pileup text of sites [first, first + n) written into a
+    device buffer by the device generator (sid_synth_text_device), followed by
+    512 zero bytes: (tensor, text length).  bench.py's C2/C3 input."""
+    torch = _torch()
+    dev = torch.device("cuda", device)
+    ctx = Context(device)
+    cap = int(n * (24 + 2.9 * depth)) + (64 << 20)
+    text = torch.empty(cap + 512, dtype=torch.uint8, device=dev)
+    ln = ctx.synth_text_device(seed, depth, first, n, text.data_ptr(), cap, sites_per_chrom=sites_per_chrom)
+    text[ln:ln + 512].zero_()
+    torch.cuda.synchronize(dev)
+    ctx.close()
+    return text, ln

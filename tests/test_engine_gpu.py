@@ -273,3 +273,106 @@ def test_engine_long_chrom_names(sid, oracle, tmp_path, namelen):
                              chunk_bytes=1 << 20, estimate_prior=bool(flags))
         assert st.sites == n
         assert got == ref.stdout
+
+
+@pytest.mark.parametrize("hh", ["67108864", "150000", "1"], ids=["fits", "fills-midway", "too-small"])
+@pytest.mark.parametrize("flags", [[], ["-R", "-m", "likelihood_ratio"], ["-m", "quality"], ["-m", "bayes"]],
+                         ids=lambda f: " ".join(f) or "default")
+def test_host_hold_cli_matches_oracle(sid, oracle, inputs, flags, hh):
+    """--host-hold (sid_engine_cfg.host_hold_bytes): -m local / quality copy
+    every chunk's records into pinned host memory during the ingest (the
+    Lynch paths in the emit, instead of the pinned ring); chunks beyond the
+    arena fall back to the HBM hold.  Byte for byte the oracle's output."""
+    name = "quality" if "quality" in flags else "c1"
+    for extra in (["--chunk-bytes", "32768"], ["--chunk-bytes", "50000", "--devices", "3"],
+                  ["--chunk-bytes", "40000", "--hold-bytes", "1"]):
+        a = run(sid.CLI_PATH, ["--stats", "--host-hold", hh] + extra + flags + [inputs[name]])
+        b = oracle.run_cli(flags + [inputs[name]])
+        assert a.returncode == b.returncode == 0, a.stderr
+        assert a.stdout == b.stdout, (extra, hh)
+        lines = a.stderr.splitlines(keepends=True)
+        assert b"".join(lines[:-1]) == b.stderr
+        st = json.loads(lines[-1])
+        local = not ("-R" in flags or "likelihood_ratio" in flags or "bayes" in flags)
+        if local and hh != "1":
+            assert st["chunks_held"] > 0
+
+
+def test_host_hold_first_error(sid, oracle, tmp_path):
+    good = b"".join(b"chr1\t%d\tA\t3\t.,.\tIII\n" % i for i in range(1, 3000))
+    p = tmp_path / "bad.plp"
+    p.write_bytes(good * 3 + b"chr1\t1\tAC\t3\t...\tIII\n" + good)
+    b = oracle.run_cli([str(p)])
+    for extra in (["--chunk-bytes", "4096"], ["--chunk-bytes", "10000", "--devices", "2"]):
+        a = run(sid.CLI_PATH, ["--host-hold", str(1 << 24)] + extra + [str(p)])
+        assert (a.returncode, a.stdout, a.stderr) == (b.returncode, b.stdout, b.stderr)
+
+
+@pytest.mark.parametrize("method", ["local", "likelihood_ratio"])
+def test_engine_host_arena_records(sid, oracle, tmp_path, method):
+    """device_sink 2 + host_hold_bytes (bench.py's PCIe-inclusive step): the
+    records land in the engine's pinned host arena, in file order, equal to
+    the oracle's CSV; an engine run twice reuses the arena."""
+    import torch
+    n, seed, spc = 80_000, 17, 30_000
+    text = sid.synth_text(seed, n, 30.0, sites_per_chrom=spc)
+    p = tmp_path / "h.plp"
+    p.write_bytes(text)
+    flags = [] if method == "local" else ["-R", "-m", method]
+    ref = oracle.run_cli(flags + [str(p)])
+    assert ref.returncode == 0
+    host = torch.frombuffer(bytearray(text), dtype=torch.uint8).pin_memory()
+    eng = sid.Engine(method=method, estimate_prior=method != "local", device_sink=2, chunk_bytes=1 << 20,
+                     host_hold_bytes=len(text))
+    eng.source_host_ptr(host.data_ptr(), len(text), keep=host)
+    for _ in range(2):
+        st = eng.ingest()
+        eng.estimate()
+        _, st2 = eng.emit()
+        assert st.sites == n and st.chunks >= 4
+        got = eng.records_bytes(st.chunks)
+        assert st2.bytes_out == len(got)
+        assert sid.HEADER + got == ref.stdout
+    eng.close()
+
+
+def test_engine_profile_exchange_api(sid, oracle, tmp_path):
+    """sid_engine_profile_table / _load: the multi-rank Lynch exchange with
+    several pipelines per rank -- two engines over the two halves of a text,
+    each exporting its merged table, each loading the sum; the estimate is
+    not merged again (a second estimate() gives the same answer)."""
+    n = 60_000
+    text = sid.synth_text(23, n, 30.0)
+    cut = text.index(b"\n", len(text) // 2) + 1
+    p = tmp_path / "x.plp"
+    p.write_bytes(text)
+    ref = oracle.run_cli(["-R", "-m", "likelihood_ratio", str(p)])
+    engs = []
+    for part in (text[:cut], text[cut:]):
+        e = sid.Engine(method="likelihood_ratio", estimate_prior=True, devices=2, chunk_bytes=1 << 18)
+        e.source_text(part)
+        e.ingest()
+        engs.append(e)
+    tabs = [e.profile_table() for e in engs]
+    keys = np.concatenate([t[0] for t in tabs])
+    cnts = np.concatenate([t[1] for t in tabs])
+    outs = []
+    for e in engs:
+        e.profile_load(keys, cnts)
+        est = e.estimate()
+        est2 = e.estimate()
+        assert (est.heterozygosity, est.error_rate, est.n_unique) == \
+            (est2.heterozygosity, est2.error_rate, est2.n_unique)
+        outs.append(e.emit(header=None)[0])
+        e.close()
+    assert sid.HEADER + b"".join(outs) == ref.stdout
+
+
+def test_source_file_range_past_eof(sid, tmp_path):
+    p = tmp_path / "short.plp"
+    p.write_bytes(b"chr1\t1\tA\t1\t.\tI\n")
+    eng = sid.Engine()
+    with open(p, "rb") as f:
+        with pytest.raises(sid.SidError):
+            eng.source_file(f.fileno(), 0, 1 << 20)
+    eng.close()
