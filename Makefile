@@ -2,12 +2,14 @@
 # test-only oracle (oracle/_build, oracle/_ref).  `make -j8`.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-BUILD := build
+BUILD ?= build
 SRC := sid_amd/csrc
 # -ffp-contract=off: device doubles round like the reference's x86-64 SSE2 build (no
 # FMA contraction), and the double-double error-free transforms stay exact
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -Wall -Wno-unused-function -Iinclude
 HOSTFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Iinclude
+# EXTRA: A/B variants of the same sources (make BUILD=build_b EXTRA=-DNAME=VALUE)
+HIPFLAGS += $(EXTRA)
 
 KERNELS := local synth lynch textpath
 HOSTSRC := capi lynch_host parse emit run

@@ -86,6 +86,8 @@ def parse_args(argv=None):
     p.add_argument("--device-steps", type=int, default=0, help="device_path steps (0 = max(steps, 10))")
     p.add_argument("--no-extras", action="store_true", help="skip kernel_local, cli and cpu_baseline")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--device-only", action="store_true",
+                   help="profiling: only the device_path leg (its line's value is then the device path's)")
     p.add_argument("--allow-shared-gpu", action="store_true",
                    help="rehearsal: more ranks than GPUs share them round-robin")
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
@@ -123,7 +125,20 @@ def launch_ranks(a):
     procs = []
     for r in range(a.gpus):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
+        # stdout: only rank 0's JSON line (collective libraries print to stdout too)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    import threading
+
+    def relay(f):
+        for line in iter(f.readline, b""):
+            if line.startswith(b'{"metric"'):
+                sys.stdout.buffer.write(line)
+                sys.stdout.flush()
+            else:
+                sys.stderr.buffer.write(line)
+    th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    th.start()
     rc = 0
     live = list(procs)
     while live:
@@ -137,6 +152,7 @@ def launch_ranks(a):
                 for q in live:   # a failed rank leaves the others at a barrier: stop them
                     q.terminate()
         time.sleep(0.05)
+    th.join(timeout=10)
     return rc
 
 
@@ -162,28 +178,37 @@ def numa_bind(torch, gpu):
 
 
 # ----------------------------------------------------------------- ranks ----
-def stage_bytes(stage, text_per_site, csv_per_site):
-    """Algorithmic HBM bytes per site of each engine stage."""
+def stage_bytes(stage, text_per_site, csv_per_site, fused):
+    """Algorithmic HBM bytes per site of each engine stage.
+    fused: -m local, the call fused into the formatter (it reads the 8 B
+    counts instead of the call kernel's 17 B code + confs)."""
+    site_in = 8 if fused else 17
     return {
         "index": text_per_site + text_per_site / 8,    # text read once, line-start masks written
         # text read; line-start masks (1/8 of the text) and offsets read back;
         # counts (8) and the formatter's header pair (16) written
         "parse": text_per_site + text_per_site / 8 + 8 + 8 + 16,
-        "call": LOCAL_BYTES_PER_SITE,                  # counts in, code + confs out
+        "call": 8 + 17,                                # counts in, code + confs out (Lynch lookup, quality)
         "hist": 8,                                     # counts read
-        # formatter: code + confs and the header pair read (the line offset
-        # only for chrom names over 8 bytes), the records written
-        "fmt_write": 17 + 16 + csv_per_site,
+        # formatter: the site's counts (or code + confs) and header pair read
+        # (the line offset only for chrom names over 8 bytes); record bytes per
+        # 512-site block written (0.01 B/site); then the same reads again and
+        # the records written
+        "fmt_len": site_in + 16,
+        "fmt_write": site_in + 16 + csv_per_site,
     }[stage]
 
 
-STAGE_KERNELS = {
-    "index": ["sid_index_count_kernel", "sid_scan_*"],
-    "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_serial_kernel"],
-    "call": ["sid_local_table_p2", "sid_local_fixup"],
-    "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
-    "fmt_write": ["sid_fmt_fused_kernel"],
-}
+def stage_kernels(stage, fused):
+    return {
+        "index": ["sid_index_count_kernel", "sid_scan_*"],
+        "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_serial_kernel"],
+        "call": ["sid_lookup_rec_kernel"],
+        "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
+        "fmt_len": (["sid_local_len_kernel", "sid_local_fixlen_kernel"] if fused else ["sid_fmt_blen_kernel"])
+                   + ["sid_scan_*"],
+        "fmt_write": ["sid_local_put_kernel"] if fused else ["sid_fmt_put_kernel"],
+    }[stage]
 
 
 class Rank:
@@ -316,6 +341,11 @@ def bench_weak(R, a, cfg):
     first = R.rank * n
     lynch = cfg["method"] != "local" or cfg["R"]
     text, ln = G.synth_text_hbm(cfg["seed"], cfg["depth"], first, n, device=R.gpu)
+    if a.device_only:
+        dp = device_path(R, a, cfg, text, ln, lynch)
+        return {"metric": METRIC, "value": dp["sites_per_s"], "unit": "sites/s", "n_gpus": R.n_gpus,
+                "steps": dp["steps"], "ms_per_step": dp["ms_per_step"], "roofline": dp.pop("roofline"),
+                "device_path": dp, "note": "--device-only (profiling): value is the device path's"}, []
     host = text[:ln].cpu().pin_memory()     # the rank's input, in host memory (its GPU's NUMA node)
     # the CSV is ~0.53 of the text at 30x: the arena never runs out
     hh = int(ln * 0.6) + (64 << 20)
@@ -400,7 +430,8 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
     prof = eng.profile_read()
     eng.profile(False)
     eng.close()
-    stages = {k[:-3]: v / steps for k, v in prof.items() if k.endswith("_ms") and k != "fmt_len_ms"}
+    stages = {k[:-3]: v / steps for k, v in prof.items() if k.endswith("_ms")}
+    fused = cfg["method"] == "local"   # the call fused into the formatter (-R: in pass 2)
     vals = R.max_over_ranks([elapsed] + [stages[k] for k in sorted(stages)])
     elapsed = vals[0]
     stages = dict(zip(sorted(stages), vals[1:]))
@@ -416,7 +447,7 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
         if not ms:
             continue
         launch_ms = ms / max(1.0, chunks)
-        bps = stage_bytes(k, tps, cps)
+        bps = stage_bytes(k, tps, cps, fused)
         ach = bps * per_launch_sites / (launch_ms * 1e-3) / 1e9
         roofs[k] = {"ms_per_step": ms, "launch_ms": launch_ms, "bytes_per_site": bps, "GBps": ach,
                     "frac": ach / HBM_PEAK_GBS}
@@ -424,9 +455,9 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
     d = roofs[dom]
     roofline = {"bound": "hbm", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": d["frac"], "traffic": pmc_traffic(dom, per_launch_sites),
-                "kernel": f"engine stage '{dom}'", "stage_kernels": STAGE_KERNELS[dom],
+                "kernel": f"engine stage '{dom}'", "stage_kernels": stage_kernels(dom, fused),
                 "launch_ms": d["launch_ms"], "sites_per_launch": per_launch_sites, "bytes_per_site": d["bytes_per_site"],
-                "valu": valu_issue(dom, per_launch_sites, d["launch_ms"]),
+                "valu": valu_issue(dom, per_launch_sites, d["launch_ms"], stage_kernels(dom, fused)),
                 "source": "device_path: HIP event pairs around each engine stage on the compute stream"}
     return {"sites_per_s": sites_all * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
             "stages_ms": stages, "stage_roofline": roofs, "roofline": roofline,
@@ -545,7 +576,7 @@ def pmc_file(stage):
     return None
 
 
-def valu_issue(stage, sites, launch_ms):
+def valu_issue(stage, sites, launch_ms, kernels):
     """The stage's VALU work against the chip's VALU issue rate: SQ_INSTS_VALU
     per site of its kernels (the committed PMC pass, tools/gpu_pmc_c2.sh) x
     the sites of a launch, at one wave64 instruction per SIMD per 2 cycles
@@ -562,7 +593,7 @@ def valu_issue(stage, sites, launch_ms):
     except Exception:
         return None
     insts = 0.0
-    for k in STAGE_KERNELS[stage]:
+    for k in kernels:
         for name, r in pm.items():
             if name.startswith(k.rstrip("*")) and "SQ_INSTS_VALU" in r:
                 insts += r["SQ_INSTS_VALU"] / sites_pmc

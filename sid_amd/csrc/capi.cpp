@@ -115,6 +115,7 @@ static hipError_t sid_build_table(sid_ctx* c)
 {
     if (c->K.general) return hipSuccess;
     hipError_t e = sid_launch_local_table_build(&c->K, c->d_lnt, c->ws.table, c->ws.table2, nullptr);
+    if (e == hipSuccess) e = sid_launch_local_str_build(&c->K, c->ws.table, c->ws.table2, &c->ws, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     return e;
 }
@@ -147,6 +148,10 @@ extern "C" int sid_create(int device, const sid_opts* opts, sid_ctx** out)
     if (e == hipSuccess) e = hipMemcpy(c->d_lnt, lnt.data(), SID_LUTN * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&c->ws.table, tab * sizeof(double));
     if (e == hipSuccess) e = hipMalloc(&c->ws.table2, SID_TAB2_N * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&c->ws.str1, tab * SID_STR_BYTES);
+    if (e == hipSuccess) e = hipMalloc(&c->ws.len1, tab);
+    if (e == hipSuccess) e = hipMalloc(&c->ws.str2, (size_t)SID_TAB2_N * SID_STR_BYTES);
+    if (e == hipSuccess) e = hipMalloc(&c->ws.len2, SID_TAB2_N);
     if (e == hipSuccess) e = hipMalloc(&c->ws.miss, (size_t)c->ws.cap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&c->ws.ctr, 2 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c->ws.ctr, 0, 2 * sizeof(uint32_t));
@@ -168,6 +173,8 @@ extern "C" int sid_destroy(sid_ctx* c)
     if (c->d_cdf) (void)hipFree(c->d_cdf);
     if (c->ws.table) (void)hipFree(c->ws.table);
     if (c->ws.table2) (void)hipFree(c->ws.table2);
+    for (void* p : {(void*)c->ws.str1, (void*)c->ws.len1, (void*)c->ws.str2, (void*)c->ws.len2})
+        if (p) (void)hipFree(p);
     if (c->ws.miss) (void)hipFree(c->ws.miss);
     if (c->ws.ctr) (void)hipFree(c->ws.ctr);
     if (c->lynch) sid_lynch_dev_destroy(c->lynch);

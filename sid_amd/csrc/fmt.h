@@ -117,7 +117,7 @@ __host__ __device__ inline bool sid_dec6_exact(double v, uint32_t& D, int& X);
 // the exact path out of line (its limb array lives in scratch), its results
 // returned by value -- (ok << 63) | (X + 1024) << 32 | D -- so that the
 // caller's locals never have their address taken (they would live in scratch)
-__host__ __device__ __noinline__ uint64_t sid_dec6_exact_packed(double v)
+static __host__ __device__ __noinline__ uint64_t sid_dec6_exact_packed(double v)
 {
     uint32_t D = 0;
     int X = 0;

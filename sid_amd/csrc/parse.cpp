@@ -249,6 +249,7 @@ extern "C" int sid_parse_text(const char* text, size_t len, int nthreads, sid_si
     std::vector<std::thread> cp;
     for (int t = 0; t < T; ++t)
         cp.emplace_back([&, t] {
+            if (parts[t].pos.empty()) return;   // (memcpy from a null pointer is undefined, even of 0 bytes)
             std::memcpy(S->counts.data() + 4 * off[t], parts[t].counts.data(), parts[t].counts.size() * 2);
             std::memcpy(S->pos.data() + off[t], parts[t].pos.data(), parts[t].pos.size() * 4);
         });

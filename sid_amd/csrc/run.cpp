@@ -1075,11 +1075,15 @@ void compute(sid_engine* e, Dev& d, int pass)
         char* out = nullptr;
         uint64_t cap = 0;   // 0: arena memory (never returned to the pool)
         bool via_host = false;   // pass 1: records go on to the host arena (a pooled device buffer meanwhile)
+        // -m local: the call fused into the formatter (sid_chunk_local_*)
+        const bool fused = e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx);
         if (format && !lynch_hist) {
-            pe = d.prof_begin(P);
-            rc = call_sites(e, d, L, n);
-            d.prof_end(2, pe);
-            if (rc != SID_OK) return (void)fail(e, rc);
+            if (!fused) {
+                pe = d.prof_begin(P);
+                rc = call_sites(e, d, L, n);
+                d.prof_end(2, pe);
+                if (rc != SID_OK) return (void)fail(e, rc);
+            }
             const uint64_t bound = sid_chunk_fmt_bound(n, L.c1 - L.c0);
             if (n && pass == 1 && d.hh && !d.hh_full) {
                 out = d.pool.get(bound, &cap, d.s_comp);
@@ -1097,7 +1101,13 @@ void compute(sid_engine* e, Dev& d, int pass)
             }
             if (out) {
                 pe = d.prof_begin(P);
-                rc = sid_chunk_fmt(&W, L.base, L.c1, n, e->conf_type, out, d.s_comp);
+                rc = fused ? sid_chunk_local_len(d.ctx, &W, L.base, L.c1, n, e->conf_type, d.s_comp)
+                           : sid_chunk_fmt_len(&W, L.base, L.c1, n, e->conf_type, d.s_comp);
+                d.prof_end(4, pe);
+                if (rc != SID_OK) return (void)fail(e, rc);
+                pe = d.prof_begin(P);
+                rc = fused ? sid_chunk_local_put(d.ctx, &W, L.base, L.c1, n, e->conf_type, out, d.s_comp)
+                           : sid_chunk_fmt_put(&W, L.base, L.c1, n, e->conf_type, out, d.s_comp);
                 d.prof_end(5, pe);
                 if (rc != SID_OK) return (void)fail(e, rc);
                 x = hipMemcpyAsync(hs + 8, W.lb + 1, 32, hipMemcpyDeviceToHost, d.s_comp);   // bytes, flags, error
@@ -1148,7 +1158,6 @@ void compute(sid_engine* e, Dev& d, int pass)
             continue;
         }
         if (out && hs[9]) return (void)fail(e, SID_ERANGE);
-        if (out && hs[10]) return (void)fail(e, SID_EHIP);   // a formatter look-back timed out
         const uint64_t bytes = hs[8];
         release_slot();
         if (pass == 2 && r.kept) {   // kept text done with: back to the pool after this stream's work

@@ -32,7 +32,15 @@ struct sid_local_ws {
     int chunk = 0;               // SID_TABLE_CHUNK=1: one contiguous tile range per block
     int tail = 1;                // SID_TABLE_TAIL=0: no inline second-level lookup, every miss to the fix-up (A/B)
     hipEvent_t ev_mid = nullptr; // set only while timing: recorded between main and fix-up
+    // the record tails per class entry (the engine's -m local formatter):
+    // SID_STR_BYTES per entry of table / table2 (local.hip), and their lengths
+    char* str1 = nullptr;
+    uint8_t* len1 = nullptr;
+    char* str2 = nullptr;
+    uint8_t* len2 = nullptr;
 };
+#define SID_STR_BYTES 48   // entry: [0] tail length, [1] het, [8..48) the tail, zero-padded
+#define SID_STR_TEXT 8
 
 struct sid_timing_ev {
     hipEvent_t start, mid, end;
@@ -45,6 +53,8 @@ extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t
                                        hipStream_t stream);
 extern "C" hipError_t sid_launch_local_table_build(const sid_local_k* K, const double* d_lnt,
                                                    double* d_table, double* d_table2, hipStream_t stream);
+extern "C" hipError_t sid_launch_local_str_build(const sid_local_k* K, const double* d_table, const double* d_table2,
+                                                 const sid_local_ws* ws, hipStream_t stream);
 extern "C" hipError_t sid_launch_synth(uint64_t seed, uint64_t first, size_t n,
                                        const uint64_t* d_cdf, uint32_t kmax, uint16_t* counts,
                                        hipStream_t stream);
@@ -107,7 +117,7 @@ struct sid_chunk_ws {
     uint32_t* bsum = nullptr;     // per 256-site block record bytes (+ scan workspace)
     uint64_t* boff = nullptr;
     uint16_t* masks = nullptr;    // line-start masks of the index, a u16 per lane per 4 KiB tile
-    unsigned long long* lb = nullptr;   // one-pass formatter: ticket + per-block look-back status words
+    unsigned long long* lb = nullptr;   // formatter flags and totals (sid_chunk_fmt_len)
     uint64_t* state = nullptr;    // [0] sites [1..2] parse range [3] CSV bytes [4] first error key [5] range flag
                                   // [6] fallback lines
 };
@@ -116,12 +126,23 @@ void sid_chunk_release(sid_chunk_ws* W);
 int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, hipStream_t st);
 int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint64_t n, int qmode,
                     hipStream_t st);
-// the one-pass formatter: records of the n sites into out, which must hold
-// sid_chunk_fmt_bound(n, text bytes); afterwards lb[1..4] = {bytes, range
-// flag, look-back timeout, the chunk's parse error key (state[4])}
+// the formatter: records of the n sites into out, which must hold
+// sid_chunk_fmt_bound(n, text bytes).  _len: record bytes per 512-site block
+// and their offsets; _put: the records.  Afterwards lb[1], lb[2], lb[4] =
+// {bytes, range flag, the chunk's parse error key (state[4])}.  The fmt_
+// pair formats code / hom / het (any method's call kernel); the local_ pair
+// is -m local fused with the call (counts in; sid_chunk_local_ok: options
+// the class tables cover)
 uint64_t sid_chunk_fmt_bound(uint64_t n, uint64_t text_bytes);
-int sid_chunk_fmt(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
-                  hipStream_t st);
+int sid_chunk_fmt_len(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type,
+                      hipStream_t st);
+int sid_chunk_fmt_put(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
+                      hipStream_t st);
+bool sid_chunk_local_ok(const sid_ctx* ctx);
+int sid_chunk_local_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n,
+                        const char* conf_type, hipStream_t st);
+int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n,
+                        const char* conf_type, char* out, hipStream_t st);
 int sid_chunk_quality(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st);
 // synth.hip: the synthetic text of sites [first, first + n) (the bytes of
 // sid_synth_text) generated on the device into out (cap bytes): res[0] =

@@ -41,7 +41,7 @@
 
 #include "../../include/sid.h"
 #include "fmt.h"
-#include "sid_internal.h"
+#include "local_site.h"
 
 namespace {
 
@@ -1090,131 +1090,49 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
     }
 }
 
-// The engine's formatter in one pass (record lengths, their offsets and the
-// records) with a decoupled look-back across blocks instead of a length
-// kernel, a scan and a write kernel that reads every input again.
+// The engine's formatter: the records of a chunk's sites, in file order,
+// with no block ever waiting on another (a decoupled look-back across blocks
+// stalls when another process's kernels share the GPU and its waves are
+// swapped out): (1) every FTB-site block's record bytes, (2) a scan of the
+// block sums into block offsets, (3) every block assembles its records in LDS
+// and stores them at its offset with 16-B stores.
 //
-// Blocks are dispatched in index order (per XCD), so a block only ever waits
-// on blocks already running or done (a ticket taken with an atomic -- one
-// address hit by every block -- cost 300 us per 49k blocks).  Each block
-// publishes one 8-byte status word --
-// bits 63-62 flag (1: the block's own byte count, 2: the bytes up to and
-// including it), bits 61-0 the count -- with relaxed agent-scope atomics: the
-// value is the flag's own payload, so no fence orders anything (the per-XCD
-// L2s are not coherent; these words go through to memory, MI355X_MICROARCH.md
-// "visibility", form R2).  One wave looks back 64 blocks per step.  A bounded
-// spin: a block that waits too long sets *timeout and goes on (the host then
-// fails the run), so every wave of the grid finishes.
-constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = LB_AGG - 1;
-constexpr uint32_t LB_SPIN_MAX = 1u << 22;
+// lb (zeroed before (1)): [1] the records' bytes (the scan's running total),
+// [2] != 0: a confidence outside the formatter's range, [4] a copy of
+// state[4] (the chunk's parse error key), written by (3)
+constexpr int FTB = 512;                  // threads (= sites) per formatter block
+constexpr int FMT_LDS2 = 32 * 1024;       // its record buffer: 4 blocks (32 waves) per CU
+constexpr int LPB = 8;                    // formatter blocks per workgroup of the -m local length kernel
+#ifndef SID_PUT_BYTES
+#define SID_PUT_BYTES 0                   // the -m local writer: 1 branch-free byte stores, 0 OR-ed 8-B pieces
+#endif
+#ifndef SID_PUT_WAVES
+#define SID_PUT_WAVES 8                   // the -m local writer's waves per SIMD (its LDS allows 8)
+#endif
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
+// sum of one u32 per thread over an NT-thread block (every thread gets it)
+template <int NT>
+__device__ __forceinline__ uint32_t block_sum(uint32_t v)
 {
+    __shared__ uint32_t wsum[NT / 64];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-// wave 0: bytes before virtual block b (b > 0)
-__device__ __forceinline__ uint64_t lookback(unsigned long long* st, uint32_t b, unsigned long long* timeout)
-{
-    const int lane = threadIdx.x & 63;
-    uint64_t excl = 0;
-    int64_t j = (int64_t)b - 1;   // window: blocks j, j-1, ..., j-63
-    uint32_t spins = 0;
-    while (true) {
-        const int64_t k = j - lane;
-        const uint64_t w = k >= 0 ? __hip_atomic_load(st + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : LB_INC;
-        const uint64_t flag = w & ~LB_VAL;
-        const uint64_t inc = __ballot(flag == LB_INC);
-        const int first = inc ? __ffsll((long long)inc) - 1 : 64;   // nearest block with an inclusive count
-        const uint64_t none = __ballot(flag == 0);
-        if (none & (first == 64 ? ~0ull : ((2ull << first) - 1))) {   // a block before it has not published
-            if (++spins > LB_SPIN_MAX) {
-                if (lane == 0) atomicExch(timeout, 1ull);
-                return excl;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        excl += wave_sum64(lane <= first ? (w & LB_VAL) : 0);
-        if (inc) return excl;
-        j -= 64;
-    }
-}
-
-// lb (zeroed before the launch): [0] unused, [1] the records' bytes and [4]
-// a copy of state[4] (the chunk's parse error key), written by the last block,
-// [2] != 0: a confidence outside the formatter's range, [3] != 0: a look-back
-// timed out, [5 ..] the status words
-constexpr int FTB = 512;                  // threads (= sites) per block of the one-pass formatter (256: 451 us, 1024: 531 us per 12.5M sites)
-constexpr int FMT_LDS2 = 32 * 1024;       // its record buffer: 4 blocks (32 waves) per CU
-
-__global__ __launch_bounds__(FTB) void sid_fmt_fused_kernel(const char* __restrict__ text, uint64_t len,
-                                                           const uint64_t* __restrict__ starts,
-                                                           const uint64_t* __restrict__ hdr, uint64_t n,
-                                                           const uint8_t* __restrict__ code,
-                                                           const double* __restrict__ hom,
-                                                           const double* __restrict__ het, CType ct,
-                                                           unsigned long long* lb, const uint64_t* state,
-                                                           char* __restrict__ out)
-{
-    __shared__ __attribute__((aligned(16))) char buf[FMT_LDS2 + 32];
-    __shared__ double p10[SID_P10_N];
-    __shared__ uint64_t s_excl;
-    load_p10(p10);
-    const uint32_t b = blockIdx.x;
-    const uint64_t i = (uint64_t)b * FTB + threadIdx.x;
-    Reader R{text, len};
-    int l = 0;
-    uint8_t c = 0x40;
-    Head h{0, 0, 0, 0};
-    sid_g6 gh{}, gt{};
-    if (i < n) {
-        c = code[i];
-        if (!(c & 0x40)) {
-            h = site_head(R, starts + i, hdr + 2 * i);
-            gh = sid_g6_prep(hom[i], p10);
-            gt = sid_g6_prep(het[i], p10);
-            l = record_len(h, c, gh, gt, ct.len);
-            if (l < 0) {
-                atomicExch(lb + 2, 1ull);
-                l = 0;
-            }
-        }
-    }
-    uint32_t tot;
-    const uint32_t my = block_exscan<FTB>((uint32_t)l, &tot);
-    unsigned long long* st = lb + 5;
-    // publish this block's byte count first, assemble its records in LDS
-    // (at phase 0), and only then look back: by then the blocks before it
-    // have mostly published too, so one poll usually finds an inclusive count
-    if (threadIdx.x == 0)
-        __hip_atomic_store(st + b, (b == 0 ? LB_INC : LB_AGG) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool staged = tot <= FMT_LDS2;
-    if (staged && l) record_put(R, h, c, gh, gt, ct, buf + my);
-    if (threadIdx.x < 64) {
-        const uint64_t excl = b == 0 ? 0 : lookback(st, b, lb + 3);
-        if (threadIdx.x == 0) {
-            if (b != 0) __hip_atomic_store(st + b, LB_INC | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_excl = excl;
-            if ((uint64_t)(b + 1) * FTB >= n) {   // the last block
-                lb[1] = excl + tot;
-                lb[4] = state[4];
-            }
-        }
-    }
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
     __syncthreads();
-    const uint64_t base = s_excl;
-    if (!staged) {   // long records (long chromosome names): straight to global
-        if (l) record_put(R, h, c, gh, gt, ct, out + base + my);
-        return;
-    }
-    // 16-B aligned stores: destination window k covers out[g0 + 16k, +16),
-    // i.e. buf[16k - phase, +16); the inner windows read two aligned LDS
-    // quads and shift them by the block-uniform (-phase) & 15 bytes
-    const uint32_t phase = (uint32_t)((uintptr_t)(out + base) & 15u);
-    char* dst = out + base - phase;   // 16-B aligned
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) t += wsum[w];
+    __syncthreads();   // wsum reused by the next call
+    return t;
+}
+
+// the block's records, assembled at buf[0, tot), to dst (any alignment):
+// destination window k covers dst - phase + 16k; the inner windows read two
+// aligned LDS quads and shift them by the block-uniform (-phase) & 15 bytes
+__device__ __forceinline__ void block_store(const char* buf, uint32_t tot, char* __restrict__ dst0)
+{
+    const uint32_t phase = (uint32_t)((uintptr_t)dst0 & 15u);
+    char* dst = dst0 - phase;   // 16-B aligned
     const uint32_t span = phase + tot;
     const uint32_t sh = (16u - phase) & 15u, q = sh >> 2, r = sh & 3u;
     const uint4* B = (const uint4*)buf;
@@ -1238,6 +1156,449 @@ __global__ __launch_bounds__(FTB) void sid_fmt_fused_kernel(const char* __restri
                 if (j >= phase) dst[j] = buf[j - phase];
         }
     }
+}
+
+// ---- any method: code / hom_conf / het_conf per site (call kernels) ----
+__global__ __launch_bounds__(FTB) void sid_fmt_blen_kernel(const char* __restrict__ text, uint64_t len,
+                                                          const uint64_t* __restrict__ starts,
+                                                          const uint64_t* __restrict__ hdr, uint64_t n,
+                                                          const uint8_t* __restrict__ code,
+                                                          const double* __restrict__ hom,
+                                                          const double* __restrict__ het, CType ct,
+                                                          uint32_t* __restrict__ bsum, unsigned long long* lb)
+{
+    __shared__ double p10[SID_P10_N];
+    load_p10(p10);
+    const uint64_t i = (uint64_t)blockIdx.x * FTB + threadIdx.x;
+    int l = 0;
+    if (i < n) {
+        const uint8_t c = code[i];
+        if (!(c & 0x40)) {
+            Reader R{text, len};
+            const Head h = site_head(R, starts + i, hdr + 2 * i);
+            l = record_len(h, c, sid_g6_prep(hom[i], p10), sid_g6_prep(het[i], p10), ct.len);
+            if (l < 0) {
+                atomicExch(lb + 2, 1ull);
+                l = 0;
+            }
+        }
+    }
+    const uint32_t tot = block_sum<FTB>((uint32_t)l);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(FTB) void sid_fmt_put_kernel(const char* __restrict__ text, uint64_t len,
+                                                         const uint64_t* __restrict__ starts,
+                                                         const uint64_t* __restrict__ hdr, uint64_t n,
+                                                         const uint8_t* __restrict__ code,
+                                                         const double* __restrict__ hom,
+                                                         const double* __restrict__ het, CType ct,
+                                                         const uint64_t* __restrict__ boff, const uint64_t* state,
+                                                         unsigned long long* lb, char* __restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) char buf[FMT_LDS2 + 32];
+    __shared__ double p10[SID_P10_N];
+    load_p10(p10);
+    const uint64_t i = (uint64_t)blockIdx.x * FTB + threadIdx.x;
+    Reader R{text, len};
+    int l = 0;
+    uint8_t c = 0x40;
+    Head h{0, 0, 0, 0};
+    sid_g6 gh{}, gt{};
+    if (i < n) {
+        c = code[i];
+        if (!(c & 0x40)) {
+            h = site_head(R, starts + i, hdr + 2 * i);
+            gh = sid_g6_prep(hom[i], p10);
+            gt = sid_g6_prep(het[i], p10);
+            l = record_len(h, c, gh, gt, ct.len);
+            if (l < 0) l = 0;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) lb[4] = state[4];
+    uint32_t tot;
+    const uint32_t my = block_exscan<FTB>((uint32_t)l, &tot);
+    char* const dst = out + boff[blockIdx.x];
+    if (tot > FMT_LDS2) {   // long records (long chromosome names): straight to global
+        if (l) record_put(R, h, c, gh, gt, ct, dst + my);
+        return;
+    }
+    if (l) record_put(R, h, c, gh, gt, ct, buf + my);
+    __syncthreads();
+    block_store(buf, tot, dst);
+}
+
+// ---- -m local, fused with the call: the class of a site (local_site.h)
+// gives its code and the text of its two confidences (the class tables'
+// string tables, built with them per option set), so the call kernel's
+// code / hom_conf / het_conf never round-trip HBM and no %g is computed
+// per site.  Sites neither class table covers go through the fix-up (the
+// fast / emulated evaluation of call.cpp:238-273), which adds their record
+// bytes to the block sums and leaves code / confs for the writer.
+
+// the class-table entry of a profile: 0 .. SID_TAB_N-1 (LDS table), then
+// SID_TAB_N + the second-level index, or UINT32_MAX (neither)
+__device__ __forceinline__ uint32_t local_entry(uint32_t nf, uint32_t ns, uint32_t r2)
+{
+    if (nf < SID_TAB_NF && ns < SID_TAB_NS && r2 < SID_TAB_NR) return sid_tab_slot(nf, ns, r2);
+    if (nf < SID_TAB2_NF && ns < SID_TAB2_NS && r2 < SID_TAB2_NR)
+        return SID_TAB_N + (nf * SID_TAB2_NS + ns) * SID_TAB2_NR + r2;
+    return UINT32_MAX;
+}
+
+// chrom , pos , "hom,XY," / "het,XY," then the class's tail (the entry's
+// "hom_conf,het_conf,p_value\n")
+__device__ __forceinline__ int local_rec_len(const Head& h, uint32_t tail)
+{
+    return (int)h.clen + 1 + sid_i32_len(h.pos) + 1 + 7 + (int)tail;
+}
+
+__global__ __launch_bounds__(FTB) void sid_local_len_kernel(const char* __restrict__ text, uint64_t len,
+                                                           const uint64_t* __restrict__ starts,
+                                                           const uint64_t* __restrict__ hdr, uint64_t n,
+                                                           const uint64_t* __restrict__ counts,
+                                                           const uint8_t* __restrict__ len1,
+                                                           const uint8_t* __restrict__ len2,
+                                                           uint32_t* __restrict__ bsum, uint32_t* __restrict__ miss,
+                                                           unsigned long long* nmiss)
+{
+    static_assert(SID_TAB_N == FTB * 16, "one 16-B load per thread fills the LDS length table");
+    __shared__ __attribute__((aligned(16))) uint8_t L1[SID_TAB_N];
+    ((uint4*)L1)[threadIdx.x] = ((const uint4*)len1)[threadIdx.x];
+    __syncthreads();
+    const uint64_t nb = (n + FTB - 1) / FTB;
+    for (int it = 0; it < LPB; ++it) {
+        const uint64_t b = (uint64_t)blockIdx.x * LPB + it;
+        if (b >= nb) break;
+        const uint64_t i = b * FTB + threadIdx.x;
+        int l = 0;
+        if (i < n) {
+            uint32_t f, s, nf, ns, cov;
+            sid_major(counts[i], f, s, nf, ns, cov);
+            const uint32_t k = local_entry(nf, ns, cov - nf - ns);
+            const uint32_t L = k < SID_TAB_N ? L1[k] : k != UINT32_MAX ? len2[k - SID_TAB_N] : 0xFFu;
+            if (L == 0xFFu) {
+                miss[atomicAdd(nmiss, 1ull)] = (uint32_t)i;   // its bytes: the fix-up's
+            } else {
+                Reader R{text, len};
+                l = local_rec_len(site_head(R, starts + i, hdr + 2 * i), L);
+            }
+        }
+        const uint32_t tot = block_sum<FTB>((uint32_t)l);
+        if (threadIdx.x == 0) bsum[b] = tot;
+    }
+}
+
+__global__ __launch_bounds__(TB) void sid_local_fixlen_kernel(const char* __restrict__ text, uint64_t len,
+                                                             const uint64_t* __restrict__ starts,
+                                                             const uint64_t* __restrict__ hdr,
+                                                             const uint64_t* __restrict__ counts,
+                                                             const uint32_t* __restrict__ miss,
+                                                             const unsigned long long* nmiss, sid_local_k K,
+                                                             const double* __restrict__ lnt, CType ct,
+                                                             uint8_t* __restrict__ code, double* __restrict__ hom,
+                                                             double* __restrict__ het, uint32_t* bsum,
+                                                             unsigned long long* lb)
+{
+    const uint64_t m = *nmiss;
+    for (uint64_t j = (uint64_t)blockIdx.x * TB + threadIdx.x; j < m; j += (uint64_t)gridDim.x * TB) {
+        const uint32_t i = miss[j];
+        double h, t;
+        const uint32_t c = fixup_site(counts[i], nullptr, K, lnt, h, t);
+        code[i] = (uint8_t)c;
+        hom[i] = h;
+        het[i] = t;
+        Reader R{text, len};
+        int l = record_len(site_head(R, starts + i, hdr + 2 * i), (uint8_t)c, sid_g6_prep(h), sid_g6_prep(t),
+                           ct.len);
+        if (l < 0) {
+            atomicExch(lb + 2, 1ull);
+            l = 0;
+        }
+        atomicAdd(bsum + i / FTB, (uint32_t)l);
+    }
+}
+
+// The -m local writer assembles its records in a zeroed LDS buffer by OR-ing
+// 8-byte pieces that are zero beyond their fields: a record's neighbours are
+// untouched whatever the alignment, and no lane branches per byte (through
+// predicated byte stores the writer was branch- and SALU-bound).
+// v[0..CNT) = the bytes from buffer offset q on: CNT + 1 ds_or_b64
+template <int CNT>
+__device__ __forceinline__ void lds_or_run(unsigned long long* B, uint32_t q, const uint64_t (&v)[CNT])
+{
+    const uint32_t w = q >> 3, sh = (q & 7u) * 8u;
+    uint64_t prev = 0;
+#pragma unroll
+    for (int m = 0; m <= CNT; ++m) {
+        const uint64_t cur = m < CNT ? v[m] : 0ull;
+        const uint64_t x = (cur << sh) | (sh ? prev >> (64u - sh) : 0ull);
+        atomicOr(B + w + m, x);
+        prev = cur;
+    }
+}
+
+__device__ __forceinline__ void lds_or_byte(unsigned long long* B, uint32_t q, uint32_t ch)
+{
+    atomicOr((unsigned*)B + (q >> 2), (ch & 0xFFu) << (8u * (q & 3u)));
+}
+
+// "," + the decimal of 0 <= v < 10^10 + ",", left-aligned in 16 bytes (lo,
+// hi), zero after; nd = its digits
+__device__ __forceinline__ void comma_num_comma(uint32_t v, int nd, uint64_t& lo, uint64_t& hi)
+{
+    // right-aligned first: byte 15 ',', byte 14 - j digit j (units first),
+    // byte 14 - nd the leading ','
+    uint64_t L = 0, H = (uint64_t)',' << 56;
+#pragma unroll
+    for (int j = 0; j <= 10; ++j) {
+        const uint32_t d = v % 10u;
+        v /= 10u;
+        const uint64_t byte = j < nd ? (uint64_t)('0' + d) : (j == nd ? (uint64_t)',' : 0ull);
+        const int p = 14 - j;
+        if (p >= 8) H |= byte << (8 * (p - 8));
+        else L |= byte << (8 * p);
+    }
+    const uint32_t sh = 8u * (uint32_t)(14 - nd);   // 32 .. 104 bits
+    if (sh >= 64) {
+        lo = H >> (sh - 64);
+        hi = 0;
+    } else {
+        lo = (L >> sh) | (H << (64 - sh));
+        hi = H >> sh;
+    }
+}
+
+// any record (the fix-up's sites, chroms the parse did not keep, positions
+// from the text) byte by byte into the OR buffer
+__device__ __noinline__ void record_or(Reader& R, const Head& h, uint8_t c, const sid_g6& gh, const sid_g6& gt, const CType& ct,
+                          unsigned long long* B, uint32_t q)
+{
+    uint32_t n = 0;
+    if (h.c8 || h.clen == 0) {
+        for (uint32_t k = 0; k < h.clen; ++k) lds_or_byte(B, q + n++, (uint32_t)(h.c8 >> (8 * k)));
+    } else {
+        for (uint32_t k = 0; k < h.clen; ++k) lds_or_byte(B, q + n++, R.at(h.cb + k));
+    }
+    lds_or_byte(B, q + n++, ',');
+    const int pl = sid_i32_len(h.pos);
+    uint32_t u = h.pos < 0 ? 0u - (uint32_t)h.pos : (uint32_t)h.pos;
+    if (h.pos < 0) lds_or_byte(B, q + n, '-');
+    for (int k = pl - 1; k >= (h.pos < 0 ? 1 : 0); --k) {
+        lds_or_byte(B, q + n + k, '0' + u % 10u);
+        u /= 10u;
+    }
+    n += pl;
+    lds_or_byte(B, q + n++, ',');
+    const bool het = c & 0x80;
+    lds_or_byte(B, q + n++, 'h');
+    lds_or_byte(B, q + n++, het ? 'e' : 'o');
+    lds_or_byte(B, q + n++, het ? 't' : 'm');
+    lds_or_byte(B, q + n++, ',');
+    lds_or_byte(B, q + n++, "ACGT"[c & 3]);
+    lds_or_byte(B, q + n++, "ACGT"[(c >> 2) & 3]);
+    lds_or_byte(B, q + n++, ',');
+    char tmp[SID_FMT_MAX];
+    int k = sid_g6_put(gh, tmp);
+    for (int j = 0; j < k; ++j) lds_or_byte(B, q + n++, (uint8_t)tmp[j]);
+    lds_or_byte(B, q + n++, ',');
+    k = sid_g6_put(gt, tmp);
+    for (int j = 0; j < k; ++j) lds_or_byte(B, q + n++, (uint8_t)tmp[j]);
+    lds_or_byte(B, q + n++, ',');
+    for (int j = 0; j < ct.len; ++j) lds_or_byte(B, q + n++, (uint8_t)ct.s[j]);
+    lds_or_byte(B, q + n, '\n');
+}
+
+// a tabulated site's record byte by byte through put(k, byte): chrom, pos,
+// label, gt, then the entry's tail (rare: chroms the parse did not keep,
+// positions from the text, blocks of records past the LDS buffer)
+template <class Put>
+__device__ void record_tail_bytes(Reader& R, const Head& h, uint8_t c, uint4 ea, uint4 eb, uint4 ec, Put put)
+{
+    uint32_t n = 0;
+    if (h.c8 || h.clen == 0) {
+        for (uint32_t k = 0; k < h.clen; ++k) put(n++, (uint32_t)(h.c8 >> (8 * k)) & 0xFFu);
+    } else {
+        for (uint32_t k = 0; k < h.clen; ++k) put(n++, R.at(h.cb + k));
+    }
+    put(n++, ',');
+    const int pl = sid_i32_len(h.pos);
+    uint32_t u = h.pos < 0 ? 0u - (uint32_t)h.pos : (uint32_t)h.pos;
+    if (h.pos < 0) put(n, '-');
+    for (int k = pl - 1; k >= (h.pos < 0 ? 1 : 0); --k) {
+        put(n + k, '0' + u % 10u);
+        u /= 10u;
+    }
+    n += pl;
+    put(n++, ',');
+    const bool het = c & 0x80;
+    put(n++, 'h');
+    put(n++, het ? 'e' : 'o');
+    put(n++, het ? 't' : 'm');
+    put(n++, ',');
+    put(n++, "ACGT"[c & 3]);
+    put(n++, "ACGT"[(c >> 2) & 3]);
+    put(n++, ',');
+    const uint32_t L = ea.x & 0xFFu;
+    const uint32_t w[10] = {ea.z, ea.w, eb.x, eb.y, eb.z, eb.w, ec.x, ec.y, ec.z, ec.w};
+#pragma unroll
+    for (int j = 0; j < 40; ++j)
+        if ((uint32_t)j < L) put(n + j, (w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+}
+
+__device__ __noinline__ void record_put_tail(Reader& R, const Head& h, uint8_t c, uint4 ea, uint4 eb, uint4 ec,
+                                                char* out)
+{
+    record_tail_bytes(R, h, c, ea, eb, ec, [&](uint32_t k, uint32_t ch) { out[k] = (char)ch; });
+}
+
+__device__ __noinline__ void record_or_tail(Reader& R, const Head& h, uint8_t c, uint4 ea, uint4 eb, uint4 ec,
+                                               unsigned long long* B, uint32_t q)
+{
+    record_tail_bytes(R, h, c, ea, eb, ec, [&](uint32_t k, uint32_t ch) { lds_or_byte(B, q + k, ch); });
+}
+
+// the fix-up's sites (rare), out of line so that their %g code does not set
+// the writer's register count: the record length, and the record
+__device__ __noinline__ int miss_len(const Head& h, uint8_t c, double hm, double ht, const CType& ct)
+{
+    const int l = record_len(h, c, sid_g6_prep(hm), sid_g6_prep(ht), ct.len);
+    return l < 0 ? 0 : l;
+}
+
+__device__ __noinline__ void miss_or(Reader& R, const Head& h, uint8_t c, double hm, double ht, const CType& ct,
+                                     unsigned long long* B, uint32_t q)
+{
+    record_or(R, h, c, sid_g6_prep(hm), sid_g6_prep(ht), ct, B, q);
+}
+
+__device__ __noinline__ void miss_put(Reader& R, const Head& h, uint8_t c, double hm, double ht, const CType& ct,
+                                      char* out)
+{
+    record_put(R, h, c, sid_g6_prep(hm), sid_g6_prep(ht), ct, out);
+}
+
+__global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const char* __restrict__ text, uint64_t len,
+                                                           const uint64_t* __restrict__ starts,
+                                                           const uint64_t* __restrict__ hdr, uint64_t n,
+                                                           const uint64_t* __restrict__ counts,
+                                                           const char* __restrict__ str1,
+                                                           const char* __restrict__ str2,
+                                                           const uint8_t* __restrict__ code,
+                                                           const double* __restrict__ hom,
+                                                           const double* __restrict__ het, CType ct,
+                                                           const uint64_t* __restrict__ boff, const uint64_t* state,
+                                                           unsigned long long* lb, char* __restrict__ out)
+{
+    constexpr int NQ = (FMT_LDS2 + 64 + (SID_PUT_BYTES ? 4 * FTB : 0)) / 16;   // records, slack, spare dwords
+    __shared__ uint4 buf4[NQ];
+    for (int k = threadIdx.x; k < NQ; k += FTB) buf4[k] = make_uint4(0, 0, 0, 0);
+    unsigned long long* const B = (unsigned long long*)buf4;
+    const uint64_t i = (uint64_t)blockIdx.x * FTB + threadIdx.x;
+    Reader R{text, len};
+    int l = 0;
+    Head h{0, 0, 0, 0};
+    uint32_t f = 0, s = 0;
+    uint4 ea = make_uint4(0, 0, 0, 0), eb = ea, ec = ea;
+    bool tab = false;
+    uint8_t c = 0;
+    if (i < n) {
+        uint32_t nf, ns, cov;
+        sid_major(counts[i], f, s, nf, ns, cov);
+        const uint32_t k = local_entry(nf, ns, cov - nf - ns);
+        h = site_head(R, starts + i, hdr + 2 * i);
+        if (k != UINT32_MAX) {
+            const uint4* e = (const uint4*)(k < SID_TAB_N ? str1 + (size_t)k * SID_STR_BYTES
+                                                          : str2 + (size_t)(k - SID_TAB_N) * SID_STR_BYTES);
+            ea = e[0];
+            eb = e[1];
+            ec = e[2];
+            tab = (ea.x & 0xFFu) != 0xFFu;
+        }
+        if (tab) {
+            const bool het_l = (ea.x >> 8) & 1u;
+            c = (uint8_t)(f | ((het_l ? s : f) << 2) | (het_l ? 0x80u : 0u));
+            l = local_rec_len(h, ea.x & 0xFFu);
+        } else {   // the fix-up's site
+            c = code[i];
+            l = miss_len(h, c, hom[i], het[i], ct);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) lb[4] = state[4];
+    uint32_t tot;
+    const uint32_t my = block_exscan<FTB>((uint32_t)l, &tot);   // (its barriers also order the zeroing)
+    char* const dst = out + boff[blockIdx.x];
+    if (tot > FMT_LDS2) {   // long records (long chromosome names): straight to global, byte by byte
+        if (l && tab) record_put_tail(R, h, c, ea, eb, ec, dst + my);
+        else if (l) miss_put(R, h, c, hom[i], het[i], ct, dst + my);
+        return;
+    }
+#if SID_PUT_BYTES
+    if (l && tab && (h.c8 || h.clen == 0) && h.pos >= 0) {
+        // byte stores, branch-free: a byte past its field goes to this lane's
+        // own spare byte past the records instead
+        char* const o = (char*)buf4 + my;
+        char* const spare = (char*)buf4 + FMT_LDS2 + 64 + 4 * threadIdx.x;   // a dword (bank) per lane
+#pragma unroll
+        for (int k = 0; k < 8; ++k) *((uint32_t)k < h.clen ? o + k : spare) = (char)(h.c8 >> (8 * k));
+        uint32_t q = h.clen;
+        const int pl = sid_i32_len(h.pos);
+        o[q] = ',';
+        uint32_t u = (uint32_t)h.pos;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            *(k < pl ? o + q + pl - k : spare) = (char)('0' + u % 10u);
+            u /= 10u;
+        }
+        q += pl + 1;
+        const bool het_l = c & 0x80u;
+        o[q] = ',';
+        o[q + 1] = 'h';
+        o[q + 2] = het_l ? 'e' : 'o';
+        o[q + 3] = het_l ? 't' : 'm';
+        o[q + 4] = ',';
+        o[q + 5] = "ACGT"[c & 3u];
+        o[q + 6] = "ACGT"[(c >> 2) & 3u];
+        o[q + 7] = ',';
+        q += 8;
+        const uint32_t L = ea.x & 0xFFu;
+        const uint32_t w[10] = {ea.z, ea.w, eb.x, eb.y, eb.z, eb.w, ec.x, ec.y, ec.z, ec.w};
+#pragma unroll
+        for (int k = 0; k < 40; ++k) *((uint32_t)k < L ? o + q + k : spare) = (char)(w[k >> 2] >> (8 * (k & 3)));
+    } else if (l && tab) {
+        record_or_tail(R, h, c, ea, eb, ec, B, my);
+    } else if (l) {
+        miss_or(R, h, c, hom[i], het[i], ct, B, my);
+    }
+#else
+    if (l && tab && (h.c8 || h.clen == 0) && h.pos >= 0) {
+        const uint64_t c8[1] = {h.c8};
+        lds_or_run<1>(B, my, c8);
+        const int pl = sid_i32_len(h.pos);
+        uint64_t pv[2];
+        comma_num_comma((uint32_t)h.pos, pl, pv[0], pv[1]);
+        const uint32_t q1 = my + h.clen;
+        lds_or_run<2>(B, q1, pv);
+        const uint64_t ACGT = 0x54474341ull;
+        const bool het_l = c & 0x80u;
+        const uint64_t lab[1] = {(uint64_t)'h' | ((uint64_t)(het_l ? 'e' : 'o') << 8) |
+                                 ((uint64_t)(het_l ? 't' : 'm') << 16) | ((uint64_t)',' << 24) |
+                                 (((ACGT >> (8 * (c & 3u))) & 0xFF) << 32) |
+                                 (((ACGT >> (8 * ((c >> 2) & 3u))) & 0xFF) << 40) | ((uint64_t)',' << 48)};
+        const uint32_t q2 = q1 + (uint32_t)pl + 2;
+        lds_or_run<1>(B, q2, lab);
+        const uint64_t tv[5] = {((uint64_t)ea.w << 32) | ea.z, ((uint64_t)eb.y << 32) | eb.x,
+                                ((uint64_t)eb.w << 32) | eb.z, ((uint64_t)ec.y << 32) | ec.x,
+                                ((uint64_t)ec.w << 32) | ec.z};
+        lds_or_run<5>(B, q2 + 7, tv);
+    } else if (l && tab) {
+        record_or_tail(R, h, c, ea, eb, ec, B, my);
+    } else if (l) {
+        miss_or(R, h, c, hom[i], het[i], ct, B, my);
+    }
+#endif
+    __syncthreads();
+    block_store((const char*)buf4, tot, dst);
 }
 
 // ------------------------------------------------------------ -m quality --
@@ -1990,7 +2351,7 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         WCHECK(hipMalloc(&W->het, m * 8));
         WCHECK(hipMalloc(&W->bsum, ((nb * 4 + 7) & ~(size_t)7) + scan_ws_bytes(nb)));
         WCHECK(hipMalloc(&W->boff, (nb + 1) * 8));
-        WCHECK(hipMalloc(&W->lb, (nb + 5) * 8));
+        WCHECK(hipMalloc(&W->lb, std::max<uint64_t>(nb + 5, 8) * 8));
         W->site_cap = m;
     }
     return SID_OK;
@@ -2066,18 +2427,87 @@ static int chunk_ctype(const char* conf_type, CType* ct)
 // their lines
 uint64_t sid_chunk_fmt_bound(uint64_t n, uint64_t text_bytes) { return 64 * n + text_bytes + 64; }
 
-int sid_chunk_fmt(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
-                  hipStream_t st)
+// the formatter's steps 1-2 (record bytes per block, their offsets); lb[1]
+// = the chunk's bytes afterwards
+static int fmt_scan(sid_chunk_ws* W, uint64_t nb, hipStream_t st)
+{
+    launch_scan(W->bsum, nb, W->boff, (uint64_t*)(W->lb + 1), nullptr,
+                (uint64_t*)((char*)W->bsum + ((nb * 4 + 7) & ~(size_t)7)), st);
+    WCHECK(hipGetLastError());
+    return SID_OK;
+}
+
+int sid_chunk_fmt_len(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type,
+                      hipStream_t st)
 {
     CType ct;
     if (chunk_ctype(conf_type, &ct)) return SID_EINVAL;
     if (n > W->site_cap) return SID_EINVAL;
+    WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));
     const uint64_t nb = (n + FTB - 1) / FTB;
-    WCHECK(hipMemsetAsync(W->lb, 0, (nb + 5) * 8, st));
-    if (n == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
-                           ? SID_OK : SID_EHIP;
-    sid_fmt_fused_kernel<<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->code, W->hom, W->het, ct,
-                                                      W->lb, W->state, out);
+    if (nb) sid_fmt_blen_kernel<<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->code, W->hom,
+                                                              W->het, ct, W->bsum, W->lb);
+    WCHECK(hipGetLastError());
+    return fmt_scan(W, nb, st);
+}
+
+int sid_chunk_fmt_put(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, const char* conf_type, char* out,
+                      hipStream_t st)
+{
+    CType ct;
+    if (chunk_ctype(conf_type, &ct)) return SID_EINVAL;
+    const uint64_t nb = (n + FTB - 1) / FTB;
+    if (nb == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
+                            ? SID_OK : SID_EHIP;
+    sid_fmt_put_kernel<<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->code, W->hom, W->het, ct,
+                                                    W->boff, W->state, W->lb, out);
+    WCHECK(hipGetLastError());
+    return SID_OK;
+}
+
+bool sid_chunk_local_ok(const sid_ctx* ctx)
+{
+    return ctx->opts.method == SID_METHOD_LOCAL && !ctx->K.general && !ctx->ws.direct && ctx->ws.str1;
+}
+
+// the string tables hold -m local's record tails, conf_type "p_value" included
+static int local_ctype(const sid_ctx* ctx, const char* conf_type, CType* ct)
+{
+    if (chunk_ctype(conf_type, ct) || !sid_chunk_local_ok(ctx) || std::strcmp(conf_type, "p_value") != 0)
+        return SID_EINVAL;
+    return SID_OK;
+}
+
+int sid_chunk_local_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n,
+                        const char* conf_type, hipStream_t st)
+{
+    CType ct;
+    if (local_ctype(ctx, conf_type, &ct)) return SID_EINVAL;
+    if (n > W->site_cap || n >= (1ull << 32)) return SID_EINVAL;
+    WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));   // [0] the miss count, [1] bytes, [2] range flag
+    const uint64_t nb = (n + FTB - 1) / FTB;
+    if (nb) {
+        const unsigned grid = (unsigned)((nb + LPB - 1) / LPB);
+        sid_local_len_kernel<<<grid, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, ctx->ws.len1,
+                                                   ctx->ws.len2, W->bsum, W->fb, W->lb);
+        sid_local_fixlen_kernel<<<64, TB, 0, st>>>(base, c1, W->starts, W->hdr, W->counts, W->fb, W->lb, ctx->K,
+                                                   ctx->d_lnt, ct, W->code, W->hom, W->het, W->bsum, W->lb);
+    }
+    WCHECK(hipGetLastError());
+    return fmt_scan(W, nb, st);
+}
+
+int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n,
+                        const char* conf_type, char* out, hipStream_t st)
+{
+    CType ct;
+    if (local_ctype(ctx, conf_type, &ct)) return SID_EINVAL;
+    const uint64_t nb = (n + FTB - 1) / FTB;
+    if (nb == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
+                            ? SID_OK : SID_EHIP;
+    sid_local_put_kernel<<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, ctx->ws.str1,
+                                                      ctx->ws.str2, W->code, W->hom, W->het, ct, W->boff, W->state,
+                                                      W->lb, out);
     WCHECK(hipGetLastError());
     return SID_OK;
 }
