@@ -259,6 +259,7 @@ __global__ __launch_bounds__(256) void sid_local_str_build(const double* __restr
     if (i >= N) return;
     const double v = table[i];
     char* e = str + (size_t)i * SID_STR_BYTES;
+    char buf[2 * SID_FMT_MAX + 16];   // the text, then copied when it fits
     for (int k = 0; k < SID_STR_BYTES; ++k) e[k] = 0;
     if (isinf(v)) {
         len[i] = 0xFF;
@@ -267,12 +268,19 @@ __global__ __launch_bounds__(256) void sid_local_str_build(const double* __restr
     }
     double p1, p2;
     const uint32_t c = table_decode(v, 0, 0, sig, p1, p2);
-    char* t = e + SID_STR_TEXT;
+    char* t = buf;
     int n = sid_g6_put(sid_g6_prep(p1), t);
     t[n++] = ',';
     n += sid_g6_put(sid_g6_prep(p2), t + n);
+    if (n + 9 > SID_STR_BYTES - SID_STR_TEXT) {   // (one of p1, p2 is 1 or both are 0: at most 12 + 1 + 1)
+        for (int k = 0; k < SID_STR_BYTES; ++k) e[k] = 0;
+        len[i] = 0xFF;
+        e[0] = (char)0xFF;
+        return;
+    }
     const char tail[] = ",p_value\n";
     for (int k = 0; k < 9; ++k) t[n++] = tail[k];
+    for (int k = 0; k < n; ++k) e[SID_STR_TEXT + k] = buf[k];
     e[0] = (char)n;
     e[1] = (char)((c & 0x80u) ? 1 : 0);
     len[i] = (uint8_t)n;

@@ -39,7 +39,7 @@ struct sid_local_ws {
     char* str2 = nullptr;
     uint8_t* len2 = nullptr;
 };
-#define SID_STR_BYTES 48   // entry: [0] tail length, [1] het, [8..48) the tail, zero-padded
+#define SID_STR_BYTES 32   // entry: [0] tail length, [1] het, [8..32) the tail, zero-padded
 #define SID_STR_TEXT 8
 
 struct sid_timing_ev {

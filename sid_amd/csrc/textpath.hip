@@ -1104,10 +1104,10 @@ constexpr int FTB = 512;                  // threads (= sites) per formatter blo
 constexpr int FMT_LDS2 = 32 * 1024;       // its record buffer: 4 blocks (32 waves) per CU
 constexpr int LPB = 8;                    // formatter blocks per workgroup of the -m local length kernel
 #ifndef SID_PUT_BYTES
-#define SID_PUT_BYTES 0                   // the -m local writer: 1 branch-free byte stores, 0 OR-ed 8-B pieces
+#define SID_PUT_BYTES 0                   // the -m local writer: 0 OR-ed 8-B pieces, 1 branch-free LDS byte stores, 2 flat byte stores
 #endif
 #ifndef SID_PUT_WAVES
-#define SID_PUT_WAVES 8                   // the -m local writer's waves per SIMD (its LDS allows 8)
+#define SID_PUT_WAVES 8                   // the -m local writer's min waves per SIMD (its LDS allows 8)
 #endif
 
 // sum of one u32 per thread over an NT-thread block (every thread gets it)
@@ -1413,7 +1413,7 @@ __device__ __noinline__ void record_or(Reader& R, const Head& h, uint8_t c, cons
 // label, gt, then the entry's tail (rare: chroms the parse did not keep,
 // positions from the text, blocks of records past the LDS buffer)
 template <class Put>
-__device__ void record_tail_bytes(Reader& R, const Head& h, uint8_t c, uint4 ea, uint4 eb, uint4 ec, Put put)
+__device__ void record_tail_bytes(Reader& R, const Head& h, uint8_t c, uint4 ea, uint4 eb, Put put)
 {
     uint32_t n = 0;
     if (h.c8 || h.clen == 0) {
@@ -1440,22 +1440,24 @@ __device__ void record_tail_bytes(Reader& R, const Head& h, uint8_t c, uint4 ea,
     put(n++, "ACGT"[(c >> 2) & 3]);
     put(n++, ',');
     const uint32_t L = ea.x & 0xFFu;
-    const uint32_t w[10] = {ea.z, ea.w, eb.x, eb.y, eb.z, eb.w, ec.x, ec.y, ec.z, ec.w};
+    const uint32_t w[6] = {ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
 #pragma unroll
-    for (int j = 0; j < 40; ++j)
+    for (int j = 0; j < 24; ++j)
         if ((uint32_t)j < L) put(n + j, (w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
 }
 
-__device__ __noinline__ void record_put_tail(Reader& R, const Head& h, uint8_t c, uint4 ea, uint4 eb, uint4 ec,
-                                                char* out)
+__device__ __noinline__ void record_put_tail(const char* text, uint64_t len, const Head& h, uint8_t c, uint4 ea,
+                                             uint4 eb, char* out)
 {
-    record_tail_bytes(R, h, c, ea, eb, ec, [&](uint32_t k, uint32_t ch) { out[k] = (char)ch; });
+    Reader R{text, len};
+    record_tail_bytes(R, h, c, ea, eb, [&](uint32_t k, uint32_t ch) { out[k] = (char)ch; });
 }
 
-__device__ __noinline__ void record_or_tail(Reader& R, const Head& h, uint8_t c, uint4 ea, uint4 eb, uint4 ec,
-                                               unsigned long long* B, uint32_t q)
+__device__ __noinline__ void record_or_tail(const char* text, uint64_t len, const Head& h, uint8_t c, uint4 ea,
+                                            uint4 eb, unsigned long long* B, uint32_t q)
 {
-    record_tail_bytes(R, h, c, ea, eb, ec, [&](uint32_t k, uint32_t ch) { lds_or_byte(B, q + k, ch); });
+    Reader R{text, len};
+    record_tail_bytes(R, h, c, ea, eb, [&](uint32_t k, uint32_t ch) { lds_or_byte(B, q + k, ch); });
 }
 
 // the fix-up's sites (rare), out of line so that their %g code does not set
@@ -1466,15 +1468,17 @@ __device__ __noinline__ int miss_len(const Head& h, uint8_t c, double hm, double
     return l < 0 ? 0 : l;
 }
 
-__device__ __noinline__ void miss_or(Reader& R, const Head& h, uint8_t c, double hm, double ht, const CType& ct,
-                                     unsigned long long* B, uint32_t q)
+__device__ __noinline__ void miss_or(const char* text, uint64_t len, const Head& h, uint8_t c, double hm, double ht,
+                                     const CType& ct, unsigned long long* B, uint32_t q)
 {
+    Reader R{text, len};
     record_or(R, h, c, sid_g6_prep(hm), sid_g6_prep(ht), ct, B, q);
 }
 
-__device__ __noinline__ void miss_put(Reader& R, const Head& h, uint8_t c, double hm, double ht, const CType& ct,
-                                      char* out)
+__device__ __noinline__ void miss_put(const char* text, uint64_t len, const Head& h, uint8_t c, double hm, double ht,
+                                      const CType& ct, char* out)
 {
+    Reader R{text, len};
     record_put(R, h, c, sid_g6_prep(hm), sid_g6_prep(ht), ct, out);
 }
 
@@ -1490,29 +1494,30 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
                                                            const uint64_t* __restrict__ boff, const uint64_t* state,
                                                            unsigned long long* lb, char* __restrict__ out)
 {
-    constexpr int NQ = (FMT_LDS2 + 64 + (SID_PUT_BYTES ? 4 * FTB : 0)) / 16;   // records, slack, spare dwords
+    constexpr int NQ = (FMT_LDS2 + 64 + (SID_PUT_BYTES == 1 ? 4 * FTB : 0)) / 16;   // records, slack, spare dwords
     __shared__ uint4 buf4[NQ];
     for (int k = threadIdx.x; k < NQ; k += FTB) buf4[k] = make_uint4(0, 0, 0, 0);
     unsigned long long* const B = (unsigned long long*)buf4;
     const uint64_t i = (uint64_t)blockIdx.x * FTB + threadIdx.x;
-    Reader R{text, len};
     int l = 0;
     Head h{0, 0, 0, 0};
     uint32_t f = 0, s = 0;
-    uint4 ea = make_uint4(0, 0, 0, 0), eb = ea, ec = ea;
+    uint4 ea = make_uint4(0, 0, 0, 0), eb = ea;
     bool tab = false;
     uint8_t c = 0;
     if (i < n) {
         uint32_t nf, ns, cov;
         sid_major(counts[i], f, s, nf, ns, cov);
         const uint32_t k = local_entry(nf, ns, cov - nf - ns);
-        h = site_head(R, starts + i, hdr + 2 * i);
+        {
+            Reader R{text, len};
+            h = site_head(R, starts + i, hdr + 2 * i);
+        }
         if (k != UINT32_MAX) {
             const uint4* e = (const uint4*)(k < SID_TAB_N ? str1 + (size_t)k * SID_STR_BYTES
                                                           : str2 + (size_t)(k - SID_TAB_N) * SID_STR_BYTES);
             ea = e[0];
             eb = e[1];
-            ec = e[2];
             tab = (ea.x & 0xFFu) != 0xFFu;
         }
         if (tab) {
@@ -1529,11 +1534,43 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     const uint32_t my = block_exscan<FTB>((uint32_t)l, &tot);   // (its barriers also order the zeroing)
     char* const dst = out + boff[blockIdx.x];
     if (tot > FMT_LDS2) {   // long records (long chromosome names): straight to global, byte by byte
-        if (l && tab) record_put_tail(R, h, c, ea, eb, ec, dst + my);
-        else if (l) miss_put(R, h, c, hom[i], het[i], ct, dst + my);
+        if (l && tab) record_put_tail(text, len, h, c, ea, eb, dst + my);
+        else if (l) miss_put(text, len, h, c, hom[i], het[i], ct, dst + my);
         return;
     }
-#if SID_PUT_BYTES
+#if SID_PUT_BYTES == 2
+    if (l && tab && (h.c8 || h.clen == 0) && h.pos >= 0) {
+        // predicated byte stores through a pointer the compiler cannot place
+        // (flat stores that land in LDS)
+        char* o = (char*)buf4 + my;
+        asm volatile("" : "+v"(o));
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if ((uint32_t)k < h.clen) o[k] = (char)(h.c8 >> (8 * k));
+        uint32_t q = h.clen;
+        o[q++] = ',';
+        q += sid_fmt_i32(h.pos, o + q);
+        const bool het_l = c & 0x80u;
+        o[q] = ',';
+        o[q + 1] = 'h';
+        o[q + 2] = het_l ? 'e' : 'o';
+        o[q + 3] = het_l ? 't' : 'm';
+        o[q + 4] = ',';
+        o[q + 5] = "ACGT"[c & 3u];
+        o[q + 6] = "ACGT"[(c >> 2) & 3u];
+        o[q + 7] = ',';
+        q += 8;
+        const uint32_t L = ea.x & 0xFFu;
+        const uint32_t w[6] = {ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
+#pragma unroll
+        for (int k = 0; k < 24; ++k)
+            if ((uint32_t)k < L) o[q + k] = (char)(w[k >> 2] >> (8 * (k & 3)));
+    } else if (l && tab) {
+        record_or_tail(text, len, h, c, ea, eb, B, my);
+    } else if (l) {
+        miss_or(text, len, h, c, hom[i], het[i], ct, B, my);
+    }
+#elif SID_PUT_BYTES == 1
     if (l && tab && (h.c8 || h.clen == 0) && h.pos >= 0) {
         // byte stores, branch-free: a byte past its field goes to this lane's
         // own spare byte past the records instead
@@ -1562,13 +1599,13 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         o[q + 7] = ',';
         q += 8;
         const uint32_t L = ea.x & 0xFFu;
-        const uint32_t w[10] = {ea.z, ea.w, eb.x, eb.y, eb.z, eb.w, ec.x, ec.y, ec.z, ec.w};
+        const uint32_t w[6] = {ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
 #pragma unroll
-        for (int k = 0; k < 40; ++k) *((uint32_t)k < L ? o + q + k : spare) = (char)(w[k >> 2] >> (8 * (k & 3)));
+        for (int k = 0; k < 24; ++k) *((uint32_t)k < L ? o + q + k : spare) = (char)(w[k >> 2] >> (8 * (k & 3)));
     } else if (l && tab) {
-        record_or_tail(R, h, c, ea, eb, ec, B, my);
+        record_or_tail(text, len, h, c, ea, eb, B, my);
     } else if (l) {
-        miss_or(R, h, c, hom[i], het[i], ct, B, my);
+        miss_or(text, len, h, c, hom[i], het[i], ct, B, my);
     }
 #else
     if (l && tab && (h.c8 || h.clen == 0) && h.pos >= 0) {
@@ -1587,14 +1624,13 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
                                  (((ACGT >> (8 * ((c >> 2) & 3u))) & 0xFF) << 40) | ((uint64_t)',' << 48)};
         const uint32_t q2 = q1 + (uint32_t)pl + 2;
         lds_or_run<1>(B, q2, lab);
-        const uint64_t tv[5] = {((uint64_t)ea.w << 32) | ea.z, ((uint64_t)eb.y << 32) | eb.x,
-                                ((uint64_t)eb.w << 32) | eb.z, ((uint64_t)ec.y << 32) | ec.x,
-                                ((uint64_t)ec.w << 32) | ec.z};
-        lds_or_run<5>(B, q2 + 7, tv);
+        const uint64_t tv[3] = {((uint64_t)ea.w << 32) | ea.z, ((uint64_t)eb.y << 32) | eb.x,
+                                ((uint64_t)eb.w << 32) | eb.z};
+        lds_or_run<3>(B, q2 + 7, tv);
     } else if (l && tab) {
-        record_or_tail(R, h, c, ea, eb, ec, B, my);
+        record_or_tail(text, len, h, c, ea, eb, B, my);
     } else if (l) {
-        miss_or(R, h, c, hom[i], het[i], ct, B, my);
+        miss_or(text, len, h, c, hom[i], het[i], ct, B, my);
     }
 #endif
     __syncthreads();
