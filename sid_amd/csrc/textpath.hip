@@ -1103,9 +1103,6 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
 constexpr int FTB = 512;                  // threads (= sites) per formatter block
 constexpr int FMT_LDS2 = 32 * 1024;       // its record buffer: 4 blocks (32 waves) per CU
 constexpr int LPB = 8;                    // formatter blocks per workgroup of the -m local length kernel
-#ifndef SID_PUT_BYTES
-#define SID_PUT_BYTES 0                   // the -m local writer: 0 OR-ed 8-B pieces, 1 branch-free LDS byte stores, 2 flat byte stores
-#endif
 #ifndef SID_PUT_WAVES
 #define SID_PUT_WAVES 8                   // the -m local writer's min waves per SIMD (its LDS allows 8)
 #endif
@@ -1129,8 +1126,11 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v)
 // the block's records, assembled at buf[0, tot), to dst (any alignment):
 // destination window k covers dst - phase + 16k; the inner windows read two
 // aligned LDS quads and shift them by the block-uniform (-phase) & 15 bytes
+template <bool SWZ = false>
 __device__ __forceinline__ void block_store(const char* buf, uint32_t tot, char* __restrict__ dst0)
 {
+    // SWZ: buf's quads are swizzled as swz_quad (the -m local writer's buffer)
+    auto quad = [](uint32_t Q) { return SWZ ? (Q ^ ((Q >> 3) & 7u)) : Q; };
     const uint32_t phase = (uint32_t)((uintptr_t)dst0 & 15u);
     char* dst = dst0 - phase;   // 16-B aligned
     const uint32_t span = phase + tot;
@@ -1139,7 +1139,7 @@ __device__ __forceinline__ void block_store(const char* buf, uint32_t tot, char*
     for (uint32_t k = threadIdx.x * 16; k < span; k += FTB * 16) {
         if (k >= phase && k + 16 <= span) {
             const uint32_t a16 = (k - phase) >> 4;   // quad holding byte k - phase
-            const uint4 lo = B[a16], hi = B[a16 + 1];
+            const uint4 lo = B[quad(a16)], hi = B[quad(a16 + 1)];
             const uint32_t x0 = q == 0 ? lo.x : q == 1 ? lo.y : q == 2 ? lo.z : lo.w;
             const uint32_t x1 = q == 0 ? lo.y : q == 1 ? lo.z : q == 2 ? lo.w : hi.x;
             const uint32_t x2 = q == 0 ? lo.z : q == 1 ? lo.w : q == 2 ? hi.x : hi.y;
@@ -1153,7 +1153,7 @@ __device__ __forceinline__ void block_store(const char* buf, uint32_t tot, char*
             *(uint4*)(dst + k) = v;
         } else {
             for (uint32_t j = k; j < k + 16 && j < span; ++j)
-                if (j >= phase) dst[j] = buf[j - phase];
+                if (j >= phase) dst[j] = buf[quad((j - phase) >> 4) * 16 + ((j - phase) & 15u)];
         }
     }
 }
@@ -1324,6 +1324,13 @@ __global__ __launch_bounds__(TB) void sid_local_fixlen_kernel(const char* __rest
 // untouched whatever the alignment, and no lane branches per byte (through
 // predicated byte stores the writer was branch- and SALU-bound).
 // v[0..CNT) = the bytes from buffer offset q on: CNT + 1 ds_or_b64
+// The buffer's 16-B quads are swizzled within each 128-B row (quad Q at
+// Q ^ (row & 7)): records ~43 B apart put lanes three apart on the same LDS
+// bank (3 x 43 = 129), 10-way conflicts on every piece, and the XOR spreads
+// them (quads stay whole, so the 16-B copy-out reads are unchanged).
+__device__ __forceinline__ uint32_t swz_quad(uint32_t Q) { return Q ^ ((Q >> 3) & 7u); }
+__device__ __forceinline__ uint32_t swz_qword(uint32_t w) { return (swz_quad(w >> 1) << 1) | (w & 1u); }
+
 template <int CNT>
 __device__ __forceinline__ void lds_or_run(unsigned long long* B, uint32_t q, const uint64_t (&v)[CNT])
 {
@@ -1333,14 +1340,14 @@ __device__ __forceinline__ void lds_or_run(unsigned long long* B, uint32_t q, co
     for (int m = 0; m <= CNT; ++m) {
         const uint64_t cur = m < CNT ? v[m] : 0ull;
         const uint64_t x = (cur << sh) | (sh ? prev >> (64u - sh) : 0ull);
-        atomicOr(B + w + m, x);
+        atomicOr(B + swz_qword(w + m), x);
         prev = cur;
     }
 }
 
 __device__ __forceinline__ void lds_or_byte(unsigned long long* B, uint32_t q, uint32_t ch)
 {
-    atomicOr((unsigned*)B + (q >> 2), (ch & 0xFFu) << (8u * (q & 3u)));
+    atomicOr((unsigned*)B + ((swz_qword(q >> 3) << 1) | ((q >> 2) & 1u)), (ch & 0xFFu) << (8u * (q & 3u)));
 }
 
 // "," + the decimal of 0 <= v < 10^10 + ",", left-aligned in 16 bytes (lo,
@@ -1494,7 +1501,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
                                                            const uint64_t* __restrict__ boff, const uint64_t* state,
                                                            unsigned long long* lb, char* __restrict__ out)
 {
-    constexpr int NQ = (FMT_LDS2 + 64 + (SID_PUT_BYTES == 1 ? 4 * FTB : 0)) / 16;   // records, slack, spare dwords
+    constexpr int NQ = (FMT_LDS2 + 64) / 16;   // records, slack
     __shared__ uint4 buf4[NQ];
     for (int k = threadIdx.x; k < NQ; k += FTB) buf4[k] = make_uint4(0, 0, 0, 0);
     unsigned long long* const B = (unsigned long long*)buf4;
@@ -1538,76 +1545,6 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         else if (l) miss_put(text, len, h, c, hom[i], het[i], ct, dst + my);
         return;
     }
-#if SID_PUT_BYTES == 2
-    if (l && tab && (h.c8 || h.clen == 0) && h.pos >= 0) {
-        // predicated byte stores through a pointer the compiler cannot place
-        // (flat stores that land in LDS)
-        char* o = (char*)buf4 + my;
-        asm volatile("" : "+v"(o));
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if ((uint32_t)k < h.clen) o[k] = (char)(h.c8 >> (8 * k));
-        uint32_t q = h.clen;
-        o[q++] = ',';
-        q += sid_fmt_i32(h.pos, o + q);
-        const bool het_l = c & 0x80u;
-        o[q] = ',';
-        o[q + 1] = 'h';
-        o[q + 2] = het_l ? 'e' : 'o';
-        o[q + 3] = het_l ? 't' : 'm';
-        o[q + 4] = ',';
-        o[q + 5] = "ACGT"[c & 3u];
-        o[q + 6] = "ACGT"[(c >> 2) & 3u];
-        o[q + 7] = ',';
-        q += 8;
-        const uint32_t L = ea.x & 0xFFu;
-        const uint32_t w[6] = {ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
-#pragma unroll
-        for (int k = 0; k < 24; ++k)
-            if ((uint32_t)k < L) o[q + k] = (char)(w[k >> 2] >> (8 * (k & 3)));
-    } else if (l && tab) {
-        record_or_tail(text, len, h, c, ea, eb, B, my);
-    } else if (l) {
-        miss_or(text, len, h, c, hom[i], het[i], ct, B, my);
-    }
-#elif SID_PUT_BYTES == 1
-    if (l && tab && (h.c8 || h.clen == 0) && h.pos >= 0) {
-        // byte stores, branch-free: a byte past its field goes to this lane's
-        // own spare byte past the records instead
-        char* const o = (char*)buf4 + my;
-        char* const spare = (char*)buf4 + FMT_LDS2 + 64 + 4 * threadIdx.x;   // a dword (bank) per lane
-#pragma unroll
-        for (int k = 0; k < 8; ++k) *((uint32_t)k < h.clen ? o + k : spare) = (char)(h.c8 >> (8 * k));
-        uint32_t q = h.clen;
-        const int pl = sid_i32_len(h.pos);
-        o[q] = ',';
-        uint32_t u = (uint32_t)h.pos;
-#pragma unroll
-        for (int k = 0; k < 10; ++k) {
-            *(k < pl ? o + q + pl - k : spare) = (char)('0' + u % 10u);
-            u /= 10u;
-        }
-        q += pl + 1;
-        const bool het_l = c & 0x80u;
-        o[q] = ',';
-        o[q + 1] = 'h';
-        o[q + 2] = het_l ? 'e' : 'o';
-        o[q + 3] = het_l ? 't' : 'm';
-        o[q + 4] = ',';
-        o[q + 5] = "ACGT"[c & 3u];
-        o[q + 6] = "ACGT"[(c >> 2) & 3u];
-        o[q + 7] = ',';
-        q += 8;
-        const uint32_t L = ea.x & 0xFFu;
-        const uint32_t w[6] = {ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
-#pragma unroll
-        for (int k = 0; k < 24; ++k) *((uint32_t)k < L ? o + q + k : spare) = (char)(w[k >> 2] >> (8 * (k & 3)));
-    } else if (l && tab) {
-        record_or_tail(text, len, h, c, ea, eb, B, my);
-    } else if (l) {
-        miss_or(text, len, h, c, hom[i], het[i], ct, B, my);
-    }
-#else
     if (l && tab && (h.c8 || h.clen == 0) && h.pos >= 0) {
         const uint64_t c8[1] = {h.c8};
         lds_or_run<1>(B, my, c8);
@@ -1632,9 +1569,8 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     } else if (l) {
         miss_or(text, len, h, c, hom[i], het[i], ct, B, my);
     }
-#endif
     __syncthreads();
-    block_store((const char*)buf4, tot, dst);
+    block_store<true>((const char*)buf4, tot, dst);
 }
 
 // ------------------------------------------------------------ -m quality --
