@@ -1378,8 +1378,8 @@ __device__ __forceinline__ void comma_num_comma(uint32_t v, int nd, uint64_t& lo
 
 // any record (the fix-up's sites, chroms the parse did not keep, positions
 // from the text) byte by byte into the OR buffer
-__device__ __noinline__ void record_or(Reader& R, const Head& h, uint8_t c, const sid_g6& gh, const sid_g6& gt, const CType& ct,
-                          unsigned long long* B, uint32_t q)
+__device__ __forceinline__ void record_or(Reader& R, const Head& h, uint8_t c, const sid_g6& gh, const sid_g6& gt,
+                                          const CType& ct, unsigned long long* B, uint32_t q)
 {
     uint32_t n = 0;
     if (h.c8 || h.clen == 0) {
@@ -1453,15 +1453,15 @@ __device__ void record_tail_bytes(Reader& R, const Head& h, uint8_t c, uint4 ea,
         if ((uint32_t)j < L) put(n + j, (w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
 }
 
-__device__ __noinline__ void record_put_tail(const char* text, uint64_t len, const Head& h, uint8_t c, uint4 ea,
-                                             uint4 eb, char* out)
+__device__ __noinline__ void record_put_tail(const char* text, uint64_t len, Head h, uint8_t c, uint4 ea, uint4 eb,
+                                             char* out)
 {
     Reader R{text, len};
     record_tail_bytes(R, h, c, ea, eb, [&](uint32_t k, uint32_t ch) { out[k] = (char)ch; });
 }
 
-__device__ __noinline__ void record_or_tail(const char* text, uint64_t len, const Head& h, uint8_t c, uint4 ea,
-                                            uint4 eb, unsigned long long* B, uint32_t q)
+__device__ __noinline__ void record_or_tail(const char* text, uint64_t len, Head h, uint8_t c, uint4 ea, uint4 eb,
+                                            unsigned long long* B, uint32_t q)
 {
     Reader R{text, len};
     record_tail_bytes(R, h, c, ea, eb, [&](uint32_t k, uint32_t ch) { lds_or_byte(B, q + k, ch); });
@@ -1469,21 +1469,21 @@ __device__ __noinline__ void record_or_tail(const char* text, uint64_t len, cons
 
 // the fix-up's sites (rare), out of line so that their %g code does not set
 // the writer's register count: the record length, and the record
-__device__ __noinline__ int miss_len(const Head& h, uint8_t c, double hm, double ht, const CType& ct)
+__device__ __noinline__ int miss_len(Head h, uint8_t c, double hm, double ht, CType ct)
 {
     const int l = record_len(h, c, sid_g6_prep(hm), sid_g6_prep(ht), ct.len);
     return l < 0 ? 0 : l;
 }
 
-__device__ __noinline__ void miss_or(const char* text, uint64_t len, const Head& h, uint8_t c, double hm, double ht,
-                                     const CType& ct, unsigned long long* B, uint32_t q)
+__device__ __noinline__ void miss_or(const char* text, uint64_t len, Head h, uint8_t c, double hm, double ht,
+                                     CType ct, unsigned long long* B, uint32_t q)
 {
     Reader R{text, len};
     record_or(R, h, c, sid_g6_prep(hm), sid_g6_prep(ht), ct, B, q);
 }
 
-__device__ __noinline__ void miss_put(const char* text, uint64_t len, const Head& h, uint8_t c, double hm, double ht,
-                                      const CType& ct, char* out)
+__device__ __noinline__ void miss_put(const char* text, uint64_t len, Head h, uint8_t c, double hm, double ht,
+                                      CType ct, char* out)
 {
     Reader R{text, len};
     record_put(R, h, c, sid_g6_prep(hm), sid_g6_prep(ht), ct, out);
