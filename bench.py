@@ -56,6 +56,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# the copy engines (SDMA) for every host<->device copy, set before the HIP
+# runtime starts: with the runtime's default, device->host copies ran at 30
+# GB/s; with SDMA both directions reach ~57 GB/s at the same time
+# (tools/debug/pcie_probe.cpp, profiles/pcie_probe_r03.txt)
+os.environ.setdefault("HSA_ENABLE_SDMA", "1")
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 LOCAL_BYTES_PER_SITE = 25    # sid_call_local: 8 B counts in, 1 B code + 2 x 8 B confs out
@@ -84,6 +89,8 @@ def parse_args(argv=None):
     p.add_argument("--sites", type=int, default=None, help="override: sites per GPU (C2/C3) or in total (C4/C5)")
     p.add_argument("--chunk-mib", type=int, default=0, help="engine chunk size (0 = the engine's default)")
     p.add_argument("--device-steps", type=int, default=0, help="device_path steps (0 = max(steps, 10))")
+    p.add_argument("--slots", type=int, default=0, help="PCIe path: device text buffers per GPU (0 = the engine's 3)")
+    p.add_argument("--pcie-chunk-mib", type=int, default=0, help="PCIe path chunk size (0 = the engine's 128 MiB)")
     p.add_argument("--no-extras", action="store_true", help="skip kernel_local, cli and cpu_baseline")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--device-only", action="store_true",
@@ -350,7 +357,7 @@ def bench_weak(R, a, cfg):
     # the CSV is ~0.53 of the text at 30x: the arena never runs out
     hh = int(ln * 0.6) + (64 << 20)
     eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=R.gpu,
-                         chunk_bytes=a.chunk_mib << 20, device_sink=2, host_hold_bytes=hh)
+                         chunk_bytes=a.pcie_chunk_mib << 20, slots=a.slots, device_sink=2, host_hold_bytes=hh)
     eng.source_host_ptr(host.data_ptr(), ln, keep=host)
     elapsed, (st, st2, est) = R.timed(lambda: R.run_step(eng, lynch), a.steps, a.warmup)
     elapsed = R.max_over_ranks([elapsed])[0]

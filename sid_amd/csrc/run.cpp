@@ -443,7 +443,11 @@ void split_host_text(sid_engine* e, const char* t, uint64_t len)
     e->recs.clear();
     uint64_t at = 0;
     while (at < len) {
-        uint64_t end = next_line_start(t, len, std::max(at + 1, std::min(len, at + C)));
+        // the last chunk's work (compute, then its records' copy back) runs
+        // after the last upload: the tail is cut in halves down to 16 MiB
+        const uint64_t rem = len - at;
+        const uint64_t want = (rem <= C && rem > (32ull << 20)) ? rem / 2 : C;
+        uint64_t end = next_line_start(t, len, std::max(at + 1, std::min(len, at + want)));
         if (end <= at) end = len;
         ChunkRec r;
         r.off = at;
@@ -898,7 +902,12 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
                 len = d.h_small[6];
             }
         }
-        if (x == hipSuccess) x = hipMemsetAsync(dst + len, 0, PAD, d.s_up);
+        // the bytes past the chunk only need to be readable (every kernel
+        // bounds its reads by the chunk's end), which the buffers' PAD
+        // guarantees; zeroing them per chunk put a fill kernel between every
+        // two copies of the upload stream (copy engine -> shader -> copy
+        // engine), so it is done only where a kernel already wrote the text
+        if (x == hipSuccess && e->src == SRC_SYNTH_DEVICE) x = hipMemsetAsync(dst + len, 0, PAD, d.s_up);
         hipEvent_t ev = nullptr;
         if (slot >= 0) {
             ev = d.slots[slot].ev_up;
