@@ -838,7 +838,10 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
                 if (x == hipSuccess) s.cap = c;
                 s.used = false;
             } else if (s.used) {
-                x = hipStreamWaitEvent(d.s_up, s.ev_free, 0);
+                // the slot's last reader (compute stream) is long done by now:
+                // waited for here, not by the copy engine's queue (a cross-
+                // queue wait in front of every copy)
+                x = hipEventSynchronize(s.ev_free);
             }
             if (x != hipSuccess) return (void)hipfail(e, x);
             dst = s.text;
@@ -1585,6 +1588,26 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
     e->rc = SID_OK;
     e->reloaded = 0;
     e->sink_bytes = 0;
+    // every chunk's records already in the host arena (-m local / quality
+    // with host_hold_bytes): nothing left for the devices, only the writes
+    bool all_host = sink != 1;
+    for (const auto& r : e->recs) all_host = all_host && r.host1;
+    if (all_host) {
+        uint64_t out = 0;
+        bool ok = !(sink == 0 && header && write(user, header, std::strlen(header)) != 0);
+        for (const auto& r : e->recs) {
+            if (ok && sink == 0 && r.host_len && write(user, r.host, r.host_len) != 0) ok = false;
+            out += r.host_len;
+        }
+        if (st) {
+            st->chunks_reloaded = 0;
+            st->bytes_out = out;
+            st->emit_s = wall() - t0;
+        }
+        timing_report(e, "emit", wall() - t0);
+        e->ingested = false;
+        return ok ? SID_OK : SID_EIO;
+    }
     start_queues(e);
     const int D = (int)e->devs.size();
     // pinned ring per device: 4 x 16 MiB (pinned once, reused by every run)
