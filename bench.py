@@ -185,10 +185,20 @@ def numa_bind(torch, gpu):
 
 
 # ----------------------------------------------------------------- ranks ----
+def fmt_kind(cfg):
+    """The formatter the engine runs: "local" (-m local, the call fused into
+    it), "lynch" (likelihood_ratio / bayes pass 2, the class lookup fused into
+    it; SID_LYNCH_FUSED=0 turns that off) or None (the generic one, after the
+    call / lookup kernel)."""
+    if cfg["method"] == "local":
+        return "local"
+    return None if os.environ.get("SID_LYNCH_FUSED", "1") == "0" else "lynch"
+
+
 def stage_bytes(stage, text_per_site, csv_per_site, fused):
     """Algorithmic HBM bytes per site of each engine stage.
-    fused: -m local, the call fused into the formatter (it reads the 8 B
-    counts instead of the call kernel's 17 B code + confs)."""
+    fused: a fmt_kind, the call / lookup fused into the formatter (it reads
+    the 8 B counts instead of the call kernel's 17 B code + confs)."""
     site_in = 8 if fused else 17
     return {
         "index": text_per_site + text_per_site / 8,    # text read once, line-start masks written
@@ -212,9 +222,10 @@ def stage_kernels(stage, fused):
         "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_serial_kernel"],
         "call": ["sid_lookup_rec_kernel"],
         "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
-        "fmt_len": (["sid_local_len_kernel", "sid_local_fixlen_kernel"] if fused else ["sid_fmt_blen_kernel"])
-                   + ["sid_scan_*"],
-        "fmt_write": ["sid_local_put_kernel"] if fused else ["sid_fmt_put_kernel"],
+        "fmt_len": {"local": ["sid_local_len_kernel", "sid_local_fixlen_kernel"],
+                    "lynch": ["sid_lynch_len_kernel"]}.get(fused, ["sid_fmt_blen_kernel"]) + ["sid_scan_*"],
+        "fmt_write": {"local": ["sid_local_put_kernel"], "lynch": ["sid_lynch_put_kernel"]}.get(
+            fused, ["sid_fmt_put_kernel"]),
     }[stage]
 
 
@@ -438,7 +449,7 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
     eng.profile(False)
     eng.close()
     stages = {k[:-3]: v / steps for k, v in prof.items() if k.endswith("_ms")}
-    fused = cfg["method"] == "local"   # the call fused into the formatter (-R: in pass 2)
+    fused = fmt_kind(cfg)
     vals = R.max_over_ranks([elapsed] + [stages[k] for k in sorted(stages)])
     elapsed = vals[0]
     stages = dict(zip(sorted(stages), vals[1:]))

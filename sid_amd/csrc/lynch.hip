@@ -25,25 +25,7 @@
 #include "sid_math.h"
 #include "sid_nm.h"
 
-#define SID_EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
 #define SID_LN_LDBL_TRUE_MIN (-SID_LDBL_DENORM_SHIFT)
-
-__device__ __forceinline__ uint64_t sid_hash64(uint64_t k)
-{
-    k ^= k >> 33;
-    k *= 0xFF51AFD7ED558CCDull;
-    k ^= k >> 33;
-    k *= 0xC4CEB9FE1A85EC53ull;
-    k ^= k >> 33;
-    return k;
-}
-
-// profile_t (A,C,G,T little-endian u16) -> key with lexicographic numeric order
-__device__ __forceinline__ uint64_t sid_profile_key(uint64_t w)
-{
-    return ((w & 0xffffull) << 48) | (((w >> 16) & 0xffffull) << 32) | (((w >> 32) & 0xffffull) << 16) |
-           (w >> 48);
-}
 
 __device__ __forceinline__ void sid_global_insert(unsigned long long* gkeys, unsigned long long* gcnt,
                                                   uint64_t gmask, unsigned long long* distinct,

@@ -174,6 +174,12 @@ struct sid_lynch_dev {
     int* d_odd = nullptr;                  // BH saw NaN / -0 p-values: host BH instead
     uint64_t cmask = 0;
     uint32_t special_idx = 0xFFFFFFFFu;
+    // record tails per class for the engine's fused formatter (sid_lynch_fmt)
+    char* d_lstr = nullptr;                // [cap_s][SID_LSTR_BYTES]
+    uint8_t* d_dlen = nullptr;             // SID_DENSE_N
+    uint32_t* d_strbad = nullptr;          // a confidence the %g cannot print (never a p-value)
+    size_t cap_s = 0;
+    bool have_str = false;
 };
 
 sid_lynch_dev* sid_lynch_dev_create(int* err)
@@ -182,7 +188,11 @@ sid_lynch_dev* sid_lynch_dev_create(int* err)
     return new sid_lynch_dev();
 }
 
-static void free_class(sid_lynch_dev* L) { L->prepared = false; }
+static void free_class(sid_lynch_dev* L)
+{
+    L->prepared = false;
+    L->have_str = false;
+}
 
 static void free_setup(sid_lynch_dev* L)
 {
@@ -212,6 +222,10 @@ static void release_buffers(sid_lynch_dev* L)
     dfree(L->d_rcode);
     dfree(L->d_bhws);
     dfree(L->d_odd);
+    dfree(L->d_lstr);
+    dfree(L->d_dlen);
+    dfree(L->d_strbad);
+    L->cap_s = 0;
     L->bhws_bytes = 0;
     dfree(L->d_exp);
     dfree(L->d_sexp);
@@ -1103,7 +1117,22 @@ extern "C" int sid_lynch_prepare_given(sid_ctx* c, int verbose, const sid_estima
         HIPCHECK(hipMalloc(&L->d_rcode, SID_REC_N + SID_DENSE_N));
     }
     HIPCHECK(sid_launch_rec_build(L->d_dense_cidx, L->d_pcode, L->d_cc, L->d_rec, L->d_rcode, 0));
+    // the classes' record tails for the engine's fused formatter
+    if (U > L->cap_s) {
+        dfree(L->d_lstr);
+        L->cap_s = 0;
+        HIPCHECK(hipMalloc(&L->d_lstr, U * SID_LSTR_BYTES));
+        L->cap_s = U;
+    }
+    if (!L->d_dlen) HIPCHECK(hipMalloc(&L->d_dlen, SID_DENSE_N));
+    if (!L->d_strbad) HIPCHECK(hipMalloc(&L->d_strbad, 4));
+    HIPCHECK(hipMemsetAsync(L->d_strbad, 0, 4, 0));
+    HIPCHECK(sid_launch_lynch_str_build(L->d_pcode, L->d_cc, (uint32_t)U, mode == 1 ? "probability" : "p_value",
+                                        L->d_dense_cidx, L->d_lstr, L->d_dlen, L->d_strbad, 0));
+    uint32_t strbad = 0;
+    HIPCHECK(hipMemcpyAsync(&strbad, L->d_strbad, 4, hipMemcpyDeviceToHost, 0));
     HIPCHECK(hipStreamSynchronize(0));
+    L->have_str = strbad == 0;
     L->prepared = true;
     if (timing)
         std::fprintf(stderr,
@@ -1113,6 +1142,24 @@ extern "C" int sid_lynch_prepare_given(sid_ctx* c, int verbose, const sid_estima
                      ms(t0, t1), ms(t1, t2), (unsigned long long)est.evaluations, (unsigned long long)L->launches,
                      (int)L->nm_device, (unsigned long long)L->nm_rounds, (unsigned long long)L->nm_points,
                      ms(t2, t3), ms(t3, now()));
+    return SID_OK;
+}
+
+int sid_lynch_fmt_view(const sid_ctx* c, sid_lynch_fmt* v)
+{
+    const sid_lynch_dev* L = c ? c->lynch : nullptr;
+    if (!L || !L->prepared || !v) return SID_ESTATE;
+    const int m = c->opts.method;
+    if (m != SID_METHOD_LIKELIHOOD_RATIO && m != SID_METHOD_BAYES) return SID_ESTATE;
+    if (!L->empty_classes && !L->have_str) return SID_ESTATE;
+    v->dense_cidx = L->d_dense_cidx;
+    v->ckeys = L->d_ckeys;
+    v->cidx = L->d_cidx;
+    v->cmask = L->cmask;
+    v->special_idx = L->special_idx;
+    v->lstr = L->d_lstr;
+    v->dlen = L->d_dlen;
+    v->empty = L->empty_classes ? 1 : 0;
     return SID_OK;
 }
 

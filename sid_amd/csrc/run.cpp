@@ -1089,8 +1089,17 @@ void compute(sid_engine* e, Dev& d, int pass)
         bool via_host = false;   // pass 1: records go on to the host arena (a pooled device buffer meanwhile)
         // -m local: the call fused into the formatter (sid_chunk_local_*)
         const bool fused = e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx);
+        // likelihood_ratio / bayes pass 2: the class lookup fused into the
+        // formatter (sid_chunk_lynch_*; the records' tails prebuilt per class)
+        // (SID_LYNCH_FUSED=0: lookup, then the generic formatter; A/B)
+        static const bool lynch_fused = [] {
+            const char* v = std::getenv("SID_LYNCH_FUSED");
+            return !v || std::atoi(v) != 0;
+        }();
+        sid_lynch_fmt lv;
+        const bool lfused = lynch_fused && pass == 2 && !fused && sid_lynch_fmt_view(d.ctx, &lv) == SID_OK;
         if (format && !lynch_hist) {
-            if (!fused) {
+            if (!fused && !lfused) {
                 pe = d.prof_begin(P);
                 rc = call_sites(e, d, L, n);
                 d.prof_end(2, pe);
@@ -1113,13 +1122,15 @@ void compute(sid_engine* e, Dev& d, int pass)
             }
             if (out) {
                 pe = d.prof_begin(P);
-                rc = fused ? sid_chunk_local_len(d.ctx, &W, L.base, L.c1, n, e->conf_type, d.s_comp)
-                           : sid_chunk_fmt_len(&W, L.base, L.c1, n, e->conf_type, d.s_comp);
+                rc = fused    ? sid_chunk_local_len(d.ctx, &W, L.base, L.c1, n, e->conf_type, d.s_comp)
+                     : lfused ? sid_chunk_lynch_len(d.ctx, &W, L.base, L.c1, n, d.s_comp)
+                              : sid_chunk_fmt_len(&W, L.base, L.c1, n, e->conf_type, d.s_comp);
                 d.prof_end(4, pe);
                 if (rc != SID_OK) return (void)fail(e, rc);
                 pe = d.prof_begin(P);
-                rc = fused ? sid_chunk_local_put(d.ctx, &W, L.base, L.c1, n, e->conf_type, out, d.s_comp)
-                           : sid_chunk_fmt_put(&W, L.base, L.c1, n, e->conf_type, out, d.s_comp);
+                rc = fused    ? sid_chunk_local_put(d.ctx, &W, L.base, L.c1, n, e->conf_type, out, d.s_comp)
+                     : lfused ? sid_chunk_lynch_put(d.ctx, &W, L.base, L.c1, n, out, d.s_comp)
+                              : sid_chunk_fmt_put(&W, L.base, L.c1, n, e->conf_type, out, d.s_comp);
                 d.prof_end(5, pe);
                 if (rc != SID_OK) return (void)fail(e, rc);
                 x = hipMemcpyAsync(hs + 8, W.lb + 1, 32, hipMemcpyDeviceToHost, d.s_comp);   // bytes, flags, error

@@ -64,6 +64,30 @@ struct sid_lynch_dev;
 sid_lynch_dev* sid_lynch_dev_create(int* err);
 void sid_lynch_dev_destroy(sid_lynch_dev* L);
 
+// The Lynch classes as the engine's fused formatter reads them (after
+// sid_lynch_prepare for likelihood_ratio / bayes): a site's class is
+// dense_cidx[dense code] or, for the other profiles, the class hash
+// (ckeys / cidx / cmask / special_idx); none = the profile was filtered (no
+// record).  Per class SID_LSTR_BYTES of record tail: [0] its length, from
+// [8] "label,gt,conf1,conf2,conf_type\n"; dlen[d] = the tail length of
+// dense code d's class (0: none).
+#define SID_LSTR_BYTES 64
+struct sid_lynch_fmt {
+    const uint32_t* dense_cidx;
+    const unsigned long long* ckeys;
+    const uint32_t* cidx;
+    uint64_t cmask;
+    uint32_t special_idx;
+    const char* lstr;
+    const uint8_t* dlen;
+    int empty;   // no class at all: every site dropped
+};
+int sid_lynch_fmt_view(const sid_ctx* c, sid_lynch_fmt* v);
+// textpath.hip: the tails of the U classes and the dense codes' lengths
+hipError_t sid_launch_lynch_str_build(const uint8_t* pcode, const double* cc, uint32_t U, const char* conf_type,
+                                      const uint32_t* dense_cidx, char* lstr, uint8_t* dlen, uint32_t* bad,
+                                      hipStream_t st);
+
 #define SID_STAGE_N 8                   // reader threads / pinned input buffers
 #define SID_STAGE_BYTES (16u << 20)     // bytes per input buffer
 
@@ -143,6 +167,10 @@ int sid_chunk_local_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
                         const char* conf_type, hipStream_t st);
 int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n,
                         const char* conf_type, char* out, hipStream_t st);
+// likelihood_ratio / bayes fused with the class lookup (sid_lynch_fmt_view)
+int sid_chunk_lynch_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st);
+int sid_chunk_lynch_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, char* out,
+                        hipStream_t st);
 int sid_chunk_quality(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st);
 // synth.hip: the synthetic text of sites [first, first + n) (the bytes of
 // sid_synth_text) generated on the device into out (cap bytes): res[0] =

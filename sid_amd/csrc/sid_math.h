@@ -281,6 +281,25 @@ __host__ __device__ __forceinline__ void sid_major(uint64_t w, uint32_t& f, uint
 // in index order.  Typical iff m < 64 and every o <= 3: at 30x that is every
 // homozygous site with at most 3 reads of each other base (~99.9% of sites).
 // code = f<<12 | m<<6 | o0<<4 | o1<<2 | o2; decode() inverts it exactly.
+// profile hash keys (the Lynch histogram and class hash)
+#define SID_EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
+__device__ __forceinline__ uint64_t sid_hash64(uint64_t k)
+{
+    k ^= k >> 33;
+    k *= 0xFF51AFD7ED558CCDull;
+    k ^= k >> 33;
+    k *= 0xC4CEB9FE1A85EC53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+// profile_t (A,C,G,T little-endian u16) -> key with lexicographic numeric order
+__device__ __forceinline__ uint64_t sid_profile_key(uint64_t w)
+{
+    return ((w & 0xffffull) << 48) | (((w >> 16) & 0xffffull) << 32) | (((w >> 32) & 0xffffull) << 16) |
+           (w >> 48);
+}
+
 #define SID_DENSE_N 16384u
 #define SID_DENSE_NONE 0xFFFFFFFFu
 #define SID_DENSE_ROWS 16   // u64 rows the per-block dense counters are folded into

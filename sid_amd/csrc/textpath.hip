@@ -1573,6 +1573,219 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     block_store<true>((const char*)buf4, tot, dst);
 }
 
+// ---- likelihood_ratio / bayes, fused with the class lookup: a site's
+// class (the Lynch classes of the merged histogram, sid_lynch_fmt) gives its
+// whole record tail "label,gt,conf1,conf2,conf_type\n" (built once per class
+// by sid_lynch_str_build), so the lookup kernel's code / confs never
+// round-trip HBM and no %g is computed per site; a filtered profile
+// (coverage < 4, call.cpp:131-140) has no record.
+__device__ __forceinline__ uint32_t lynch_class(uint64_t w, const sid_lynch_fmt& V)
+{
+    const uint32_t d = sid_dense_code(w);
+    if (d != SID_DENSE_NONE) return V.dense_cidx[d];   // SID_DENSE_NONE: filtered
+    const uint64_t key = sid_profile_key(w);
+    if (key == SID_EMPTY_KEY) return V.special_idx;
+    uint64_t h = sid_hash64(key) & V.cmask;
+    for (uint64_t probe = 0; probe <= V.cmask; ++probe) {
+        const unsigned long long k = V.ckeys[h];
+        if (k == key) return V.cidx[h];
+        if (k == SID_EMPTY_KEY) break;
+        h = (h + 1) & V.cmask;
+    }
+    return 0xFFFFFFFFu;
+}
+
+// chrom , pos , then the class's tail
+__device__ __forceinline__ int lynch_rec_len(const Head& h, uint32_t tail)
+{
+    return (int)h.clen + 1 + sid_i32_len(h.pos) + 1 + (int)tail;
+}
+
+__global__ __launch_bounds__(FTB) void sid_lynch_len_kernel(const char* __restrict__ text, uint64_t len,
+                                                           const uint64_t* __restrict__ starts,
+                                                           const uint64_t* __restrict__ hdr, uint64_t n,
+                                                           const uint64_t* __restrict__ counts, sid_lynch_fmt V,
+                                                           uint32_t* __restrict__ bsum)
+{
+    static_assert(SID_DENSE_N == FTB * 32, "two 16-B loads per thread fill the LDS length table");
+    __shared__ __attribute__((aligned(16))) uint8_t DL[SID_DENSE_N];
+    ((uint4*)DL)[2 * threadIdx.x] = ((const uint4*)V.dlen)[2 * threadIdx.x];
+    ((uint4*)DL)[2 * threadIdx.x + 1] = ((const uint4*)V.dlen)[2 * threadIdx.x + 1];
+    __syncthreads();
+    const uint64_t nb = (n + FTB - 1) / FTB;
+    for (int it = 0; it < LPB; ++it) {
+        const uint64_t b = (uint64_t)blockIdx.x * LPB + it;
+        if (b >= nb) break;
+        const uint64_t i = b * FTB + threadIdx.x;
+        int l = 0;
+        if (i < n && !V.empty) {
+            const uint64_t w = counts[i];
+            const uint32_t d = sid_dense_code(w);
+            uint32_t L = 0;
+            if (d != SID_DENSE_NONE) {
+                L = DL[d];
+            } else {
+                const uint32_t idx = lynch_class(w, V);
+                L = idx == 0xFFFFFFFFu ? 0u : (uint8_t)V.lstr[(size_t)idx * SID_LSTR_BYTES];
+            }
+            if (L) {
+                Reader R{text, len};
+                l = lynch_rec_len(site_head(R, starts + i, hdr + 2 * i), L);
+            }
+        }
+        const uint32_t tot = block_sum<FTB>((uint32_t)l);
+        if (threadIdx.x == 0) bsum[b] = tot;
+    }
+}
+
+// a record byte by byte through put(k, byte): chrom, pos, the tail (rare:
+// chroms the parse did not keep, positions from the text, blocks past the
+// LDS buffer)
+template <class Put>
+__device__ void lynch_record_bytes(Reader& R, const Head& h, const uint4 (&e)[4], Put put)
+{
+    uint32_t n = 0;
+    if (h.c8 || h.clen == 0) {
+        for (uint32_t k = 0; k < h.clen; ++k) put(n++, (uint32_t)(h.c8 >> (8 * k)) & 0xFFu);
+    } else {
+        for (uint32_t k = 0; k < h.clen; ++k) put(n++, R.at(h.cb + k));
+    }
+    put(n++, ',');
+    const int pl = sid_i32_len(h.pos);
+    uint32_t u = h.pos < 0 ? 0u - (uint32_t)h.pos : (uint32_t)h.pos;
+    if (h.pos < 0) put(n, '-');
+    for (int k = pl - 1; k >= (h.pos < 0 ? 1 : 0); --k) {
+        put(n + k, '0' + u % 10u);
+        u /= 10u;
+    }
+    n += pl;
+    put(n++, ',');
+    const uint32_t L = e[0].x & 0xFFu;
+    const uint32_t w[14] = {e[0].z, e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x,
+                            e[2].y, e[2].z, e[2].w, e[3].x, e[3].y, e[3].z, e[3].w};
+#pragma unroll
+    for (int j = 0; j < SID_LSTR_BYTES - 8; ++j)
+        if ((uint32_t)j < L) put(n + j, (w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+}
+
+__device__ __noinline__ void lynch_put_global(const char* text, uint64_t len, Head h, uint4 e0, uint4 e1, uint4 e2,
+                                              uint4 e3, char* out)
+{
+    Reader R{text, len};
+    const uint4 e[4] = {e0, e1, e2, e3};
+    lynch_record_bytes(R, h, e, [&](uint32_t k, uint32_t ch) { out[k] = (char)ch; });
+}
+
+__device__ __noinline__ void lynch_put_or(const char* text, uint64_t len, Head h, uint4 e0, uint4 e1, uint4 e2,
+                                          uint4 e3, unsigned long long* B, uint32_t q)
+{
+    Reader R{text, len};
+    const uint4 e[4] = {e0, e1, e2, e3};
+    lynch_record_bytes(R, h, e, [&](uint32_t k, uint32_t ch) { lds_or_byte(B, q + k, ch); });
+}
+
+__global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_lynch_put_kernel(const char* __restrict__ text, uint64_t len,
+                                                                          const uint64_t* __restrict__ starts,
+                                                                          const uint64_t* __restrict__ hdr, uint64_t n,
+                                                                          const uint64_t* __restrict__ counts,
+                                                                          sid_lynch_fmt V,
+                                                                          const uint64_t* __restrict__ boff,
+                                                                          const uint64_t* state, unsigned long long* lb,
+                                                                          char* __restrict__ out)
+{
+    constexpr int NQ = (FMT_LDS2 + 64) / 16;   // records, slack
+    __shared__ uint4 buf4[NQ];
+    for (int k = threadIdx.x; k < NQ; k += FTB) buf4[k] = make_uint4(0, 0, 0, 0);
+    unsigned long long* const B = (unsigned long long*)buf4;
+    const uint64_t i = (uint64_t)blockIdx.x * FTB + threadIdx.x;
+    int l = 0;
+    Head h{0, 0, 0, 0};
+    uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0, e2 = e0, e3 = e0;
+    if (i < n && !V.empty) {
+        const uint32_t idx = lynch_class(counts[i], V);
+        if (idx != 0xFFFFFFFFu) {
+            const uint4* e = (const uint4*)(V.lstr + (size_t)idx * SID_LSTR_BYTES);
+            e0 = e[0];
+            e1 = e[1];
+            e2 = e[2];
+            e3 = e[3];
+            Reader R{text, len};
+            h = site_head(R, starts + i, hdr + 2 * i);
+            l = lynch_rec_len(h, e0.x & 0xFFu);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) lb[4] = state[4];
+    uint32_t tot;
+    const uint32_t my = block_exscan<FTB>((uint32_t)l, &tot);   // (its barriers also order the zeroing)
+    char* const dst = out + boff[blockIdx.x];
+    if (tot > FMT_LDS2) {   // long records (long chromosome names): straight to global, byte by byte
+        if (l) lynch_put_global(text, len, h, e0, e1, e2, e3, dst + my);
+        return;
+    }
+    if (l && (h.c8 || h.clen == 0) && h.pos >= 0) {
+        const uint64_t c8[1] = {h.c8};
+        lds_or_run<1>(B, my, c8);
+        const int pl = sid_i32_len(h.pos);
+        uint64_t pv[2];
+        comma_num_comma((uint32_t)h.pos, pl, pv[0], pv[1]);
+        const uint32_t q1 = my + h.clen;
+        lds_or_run<2>(B, q1, pv);
+        const uint64_t tv[7] = {((uint64_t)e0.w << 32) | e0.z, ((uint64_t)e1.y << 32) | e1.x,
+                                ((uint64_t)e1.w << 32) | e1.z, ((uint64_t)e2.y << 32) | e2.x,
+                                ((uint64_t)e2.w << 32) | e2.z, ((uint64_t)e3.y << 32) | e3.x,
+                                ((uint64_t)e3.w << 32) | e3.z};
+        lds_or_run<7>(B, q1 + (uint32_t)pl + 2, tv);
+    } else if (l) {
+        lynch_put_or(text, len, h, e0, e1, e2, e3, B, my);
+    }
+    __syncthreads();
+    block_store<true>((const char*)buf4, tot, dst);
+}
+
+// tails of the U classes (one thread each), then the dense codes' lengths
+__global__ __launch_bounds__(256) void sid_lynch_str_kernel(const uint8_t* __restrict__ pcode,
+                                                           const double* __restrict__ cc, uint32_t U, CType ct,
+                                                           char* __restrict__ lstr, uint32_t* bad)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= U) return;
+    char t[SID_LSTR_BYTES];
+    const uint8_t c = pcode[i];
+    const bool het = c & 0x80;
+    int n = 0;
+    t[n++] = 'h';
+    t[n++] = het ? 'e' : 'o';
+    t[n++] = het ? 't' : 'm';
+    t[n++] = ',';
+    t[n++] = "ACGT"[c & 3];
+    t[n++] = "ACGT"[(c >> 2) & 3];
+    t[n++] = ',';
+    const int a = sid_g6_put(sid_g6_prep(cc[2 * i]), t + n);
+    if (a < 0) atomicExch(bad, 1u);
+    n += a < 0 ? 0 : a;
+    t[n++] = ',';
+    const int b = sid_g6_put(sid_g6_prep(cc[2 * i + 1]), t + n);
+    if (b < 0) atomicExch(bad, 1u);
+    n += b < 0 ? 0 : b;
+    t[n++] = ',';
+    for (int k = 0; k < ct.len; ++k) t[n++] = ct.s[k];
+    t[n++] = '\n';
+    if (n > SID_LSTR_BYTES - 8) atomicExch(bad, 1u);   // (45 at most: never)
+    char* e = lstr + (size_t)i * SID_LSTR_BYTES;
+    for (int k = 0; k < SID_LSTR_BYTES; ++k) e[k] = 0;
+    e[0] = (char)n;
+    for (int k = 0; k < n && k < SID_LSTR_BYTES - 8; ++k) e[8 + k] = t[k];
+}
+
+__global__ __launch_bounds__(256) void sid_lynch_dlen_kernel(const uint32_t* __restrict__ dense_cidx,
+                                                            const char* __restrict__ lstr, uint8_t* __restrict__ dlen)
+{
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= SID_DENSE_N) return;
+    const uint32_t idx = dense_cidx[d];
+    dlen[d] = idx == SID_DENSE_NONE ? 0 : (uint8_t)lstr[(size_t)idx * SID_LSTR_BYTES];
+}
+
 // ------------------------------------------------------------ -m quality --
 // call.cpp:311-369 callQualityBasedSimple, one lane per site, reading the
 // read bases and both quality fields straight from the resident text.  The
@@ -2482,6 +2695,48 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
                                                       W->lb, out);
     WCHECK(hipGetLastError());
     return SID_OK;
+}
+
+int sid_chunk_lynch_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st)
+{
+    sid_lynch_fmt V;
+    if (sid_lynch_fmt_view(ctx, &V) != SID_OK) return SID_ESTATE;
+    if (n > W->site_cap) return SID_EINVAL;
+    WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));   // [1] bytes, [2] range flag
+    const uint64_t nb = (n + FTB - 1) / FTB;
+    if (nb && V.empty) {   // no class: every site dropped (and no length table)
+        WCHECK(hipMemsetAsync(W->bsum, 0, nb * 4, st));
+    } else if (nb) {
+        sid_lynch_len_kernel<<<(unsigned)((nb + LPB - 1) / LPB), FTB, 0, st>>>(base, c1, W->starts, W->hdr, n,
+                                                                                W->counts, V, W->bsum);
+    }
+    WCHECK(hipGetLastError());
+    return fmt_scan(W, nb, st);
+}
+
+int sid_chunk_lynch_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, char* out,
+                        hipStream_t st)
+{
+    sid_lynch_fmt V;
+    if (sid_lynch_fmt_view(ctx, &V) != SID_OK) return SID_ESTATE;
+    const uint64_t nb = (n + FTB - 1) / FTB;
+    if (nb == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
+                            ? SID_OK : SID_EHIP;
+    sid_lynch_put_kernel<<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, V, W->boff,
+                                                      W->state, W->lb, out);
+    WCHECK(hipGetLastError());
+    return SID_OK;
+}
+
+hipError_t sid_launch_lynch_str_build(const uint8_t* pcode, const double* cc, uint32_t U, const char* conf_type,
+                                      const uint32_t* dense_cidx, char* lstr, uint8_t* dlen, uint32_t* bad,
+                                      hipStream_t st)
+{
+    CType ct;
+    if (chunk_ctype(conf_type, &ct)) return hipErrorInvalidValue;
+    if (U) sid_lynch_str_kernel<<<(U + 255) / 256, 256, 0, st>>>(pcode, cc, U, ct, lstr, bad);
+    sid_lynch_dlen_kernel<<<SID_DENSE_N / 256, 256, 0, st>>>(dense_cidx, lstr, dlen);
+    return hipGetLastError();
 }
 
 int sid_chunk_quality(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st)
