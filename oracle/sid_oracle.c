@@ -824,22 +824,14 @@ int oracle_estimate(const oracle_profile* p, size_t u, const double dist[4],
 /* ------------------------------------------------------------------------ */
 /* stats.cpp:58-80 adjustBenjaminiHochberg (tie order provably irrelevant)  */
 /* ------------------------------------------------------------------------ */
-static const double* bh_values;
-static int cmp_desc(const void* a, const void* b)
-{
-    size_t i = *(const size_t*)a, j = *(const size_t*)b;
-    if (bh_values[i] > bh_values[j]) return -1;
-    if (bh_values[j] > bh_values[i]) return 1;
-    return (i > j) - (i < j);
-}
+void oracle_descending_sorted_indices(const double* v, size_t m, size_t* idx);   /* sid_oracle_sort.cpp */
 
+/* stats.cpp:69-80 */
 void oracle_bh(const double* p, size_t m, double* adj)
 {
     if (m == 0) return;
     size_t* sorted = (size_t*)malloc(m * sizeof(size_t));
-    for (size_t i = 0; i < m; ++i) sorted[i] = i;
-    bh_values = p;
-    qsort(sorted, m, sizeof(size_t), cmp_desc);
+    oracle_descending_sorted_indices(p, m, sorted);
     adj[sorted[0]] = p[sorted[0]];
     for (size_t i = 1; i < m; ++i) {
         double cand = p[sorted[i]] * (double)m / (double)(m - i);

@@ -468,6 +468,65 @@ __device__ __forceinline__ void sid_mixture(uint64_t key, const sid_lynch_eval& 
     }
 }
 
+// ---- the mixture as the reference's long doubles, every operation rounded
+// (ld_round: x87 overflow, denormal steps, underflow), in its order of
+// evaluation (lynch.hpp:48-96): for the profiles whose likelihoods leave the
+// normal long double range (coverage in the thousands), where the log-domain
+// sums above lose the reference's denormal quantisation, a 0 * inf = NaN or an
+// inf (multinomialCoefficient over LDBL_MAX).
+__device__ __forceinline__ sid_ld ld_ln(double ln)
+{
+    sid_ld r;
+    r.ln = ln;
+    r.neg = 0;
+    return r;
+}
+// a + b, both >= 0 (NaN propagates)
+__device__ __forceinline__ sid_ld ld_add_pos(sid_ld a, sid_ld b)
+{
+    if (isnan(a.ln) || isnan(b.ln)) return ld_ln(a.ln + b.ln);
+    const double m = fmax(a.ln, b.ln);
+    if (m == -__builtin_inf() || m == __builtin_inf()) return ld_ln(m);
+    return ld_round(ld_ln(m + log1p(exp(fmin(a.ln, b.ln) - m))));
+}
+// d * powl(x, a) * powl(y, b) (lynch.hpp:65-66, :85-86): ld = ln d (a double),
+// lx, ly the bases' logs
+__device__ __forceinline__ sid_ld ld_term(double ld, double lx, uint32_t a, double ly, uint32_t b)
+{
+    const sid_ld px = a ? ld_round(ld_ln((double)a * lx)) : ld_ln(0.0);
+    const sid_ld py = b ? ld_round(ld_ln((double)b * ly)) : ld_ln(0.0);
+    return ld_mul(ld_mul(ld_ln(ld), px), py);
+}
+// homozygousLikelihood / heterozygousLikelihood (lynch.hpp:57-74, :82-90)
+__device__ __noinline__ void sid_mixture_ld(uint64_t key, const sid_lynch_eval& E, double lnM, sid_ld* hom,
+                                            sid_ld* het)
+{
+    const uint32_t n[4] = {(uint32_t)(key >> 48), (uint32_t)((key >> 32) & 0xffff),
+                           (uint32_t)((key >> 16) & 0xffff), (uint32_t)(key & 0xffff)};
+    const uint32_t c = n[0] + n[1] + n[2] + n[3];
+    const sid_ld M = ld_round(ld_ln(lnM));   // expl of the double lnGamma sum
+    sid_ld L = ld_ln(-__builtin_inf());
+    for (int i = 0; i < 4; ++i) L = ld_add_pos(L, ld_term(E.ld[i], E.la, n[i], E.lb, c - n[i]));
+    *hom = ld_mul(M, L);
+    sid_ld H = ld_ln(-__builtin_inf());
+    int k = 0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = i + 1; j < 4; ++j, ++k) H = ld_add_pos(H, ld_term(E.ldd[k], E.lh, n[i] + n[j], E.lb, c - n[i] - n[j]));
+    H = ld_round(ld_ln(H.ln + E.lnorm));     // L /= (1 - s): 0 / 0 = NaN when 1 - s is 0
+    *het = ld_mul(M, H);
+}
+// the log-domain path is exact (to double rounding) while every intermediate
+// of the reference is a normal long double with 64 bits to spare: the sums
+// (the smallest partial result feeding a later operation) above LDBL_MIN *
+// 2^64 and M below LDBL_MAX.  A sum the log-domain path finds empty is not
+// taken as 0: its terms are cut at LDBL_TRUE_MIN, the reference's round to
+// the nearest multiple of it (a term of 0.55 units is 1 unit there).
+__device__ __forceinline__ bool sid_mixture_normal(double sh, double st, double lnM)
+{
+    constexpr double lo = SID_LN_LDBL_MIN + 64.0 * SID_LN2;
+    return lnM < SID_LN_LDBL_MAX - 1.0 && sh > lo && (isnan(st) || st > lo);
+}
+
 __device__ __forceinline__ void sid_two_sum(double a, double b, double& s, double& e)
 {
     s = a + b;
@@ -499,6 +558,13 @@ __device__ __forceinline__ void sid_objective_slice(const uint64_t* __restrict__
         double lhom = sh == -__builtin_inf() ? sh : lnM[i] + sh;
         double lhet = st == -__builtin_inf() ? st : lnM[i] + st;
         double lL = sid_lse2(E.l1p + lhom, E.lp + lhet);
+        constexpr double nlo = SID_LN_LDBL_MIN + 64.0 * SID_LN2;
+        if (!sid_mixture_normal(sh, st, lnM[i]) || (E.l1p + lhom < nlo && lhom != -__builtin_inf()) ||
+            (E.lp + lhet < nlo && lhet != -__builtin_inf())) {
+            sid_ld hm, ht;
+            sid_mixture_ld(keys[i], E, lnM[i], &hm, &ht);
+            lL = ld_add_pos(ld_mul(ld_ln(E.l1p), hm), ld_mul(ld_ln(E.lp), ht)).ln;
+        }
         if (lL > -__builtin_inf() && !isnan(lL)) {   // if (L > 0)
             double v = lL * (double)cnt[i];          // logl(L) * p.count
             double p = fma(lL, (double)cnt[i], -v);  // exact product error
@@ -1059,6 +1125,13 @@ __global__ __launch_bounds__(256) void sid_profile_lik_kernel(const uint64_t* __
          i += (size_t)gridDim.x * blockDim.x) {
         double sh, st;
         sid_mixture(keys[i], E, sh, st);
+        if (!sid_mixture_normal(sh, st, lnM[i])) {
+            sid_ld hm, ht;
+            sid_mixture_ld(keys[i], E, lnM[i], &hm, &ht);
+            lhom[i] = hm.ln;
+            lhet[i] = ht.ln;
+            continue;
+        }
         sid_ld M;
         M.ln = lnM[i];
         M.neg = 0;

@@ -132,7 +132,8 @@ struct sid_chunk_ws {
     uint64_t* starts = nullptr;   // line start offsets (relative to the chunk's base)
     uint64_t* counts = nullptr;   // profile_t per site
     uint64_t* hdr = nullptr;      // per site for the formatter: (chrom / position word, chrom's first 8 bytes)
-    uint32_t* fb = nullptr;       // lines for the general parse routine (count in state[6])
+    uint32_t* fb = nullptr;       // lines left by the parse passes: [0, site_cap) for the per-line fast
+                                  // path (count in state[6]), [site_cap, 2 site_cap) for the general routine ([7])
     uint8_t* code = nullptr;
     double* hom = nullptr;
     double* het = nullptr;
@@ -141,9 +142,11 @@ struct sid_chunk_ws {
     uint32_t* bsum = nullptr;     // per 256-site block record bytes (+ scan workspace)
     uint64_t* boff = nullptr;
     uint16_t* masks = nullptr;    // line-start masks of the index, a u16 per lane per 4 KiB tile
+    uint16_t* lowm = nullptr;     // token-end bytes (< 0x21 or outside the chunk), a u16 per 16 B in text order
+    uint8_t* tflag = nullptr;     // per 16 KiB tile: holds a control byte other than '\t' / '\n'
     unsigned long long* lb = nullptr;   // formatter flags and totals (sid_chunk_fmt_len)
     uint64_t* state = nullptr;    // [0] sites [1..2] parse range [3] CSV bytes [4] first error key [5] range flag
-                                  // [6] fallback lines
+                                  // [6] [7] fallback lines
 };
 int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites);
 void sid_chunk_release(sid_chunk_ws* W);

@@ -28,7 +28,7 @@
 #define SID_LN3 1.09861228866810969140
 #define SID_LN_LDBL_MAX 11356.523406294143949      // ln(LDBL_MAX), x87 80-bit
 #define SID_LN_LDBL_MIN (-11355.137111933024058)   // ln(LDBL_MIN) = -16382 ln 2
-#define SID_LDBL_DENORM_SHIFT 11398.805021138601254 // 16445 ln 2: ln(LDBL_TRUE_MIN) = -shift
+#define SID_LDBL_DENORM_SHIFT 11398.805384308300613 // 16445 ln 2: ln(LDBL_TRUE_MIN) = -shift
 #define SID_FAST_FLOOR (-11000.0)                   // fast path while every ln >= this
 
 struct sid_local_k {

@@ -326,13 +326,41 @@ __device__ __forceinline__ uint32_t ix_mask(const IxWin& w, uint64_t at, uint64_
     return m;
 }
 
+// The window's token-end bytes for the cooperative parse: bit j = byte j is
+// < 0x21 (' ', '\t', '\n', NUL, other control bytes) or outside [c0, c1) (such
+// a byte ends any token); *ctl |= a control byte other than '\t' / '\n' inside
+// [c0, c1) (the parse leaves the lines of such a tile to the per-line routines,
+// which tokenise on ' ' / '\t' only, as parsePileupLine does)
+__device__ __forceinline__ uint32_t ix_low(const IxWin& w, uint64_t at, uint64_t c0, uint64_t c1, uint32_t* ctl)
+{
+    const uint32_t ws[4] = {w.v.x, w.v.y, w.v.z, w.v.w};
+    uint32_t lo[4], cb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = ws[k];
+        lo[k] = low_bytes(x);
+        const uint32_t lt20 = ~(((x & 0x7F7F7F7Fu) + 0x60606060u) | x) & 0x80808080u;   // b < 0x20
+        cb[k] = lt20 & ~eq_bytes(x, 0x09090909u) & ~eq_bytes(x, 0x0A0A0A0Au);
+    }
+    uint32_t inr = 0xFFFFu;   // bytes inside [c0, c1)
+    if (at + 16 > c1) inr = c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
+    if (at < c0) inr &= c0 - at >= 16 ? 0u : (0xFFFFu << (uint32_t)(c0 - at)) & 0xFFFFu;
+    const uint32_t cm = compress8(cb[0], cb[1]) | (compress8(cb[2], cb[3]) << 8);
+    *ctl |= cm & inr;
+    return (compress8(lo[0], lo[1]) | (compress8(lo[2], lo[3]) << 8) | ~inr) & 0xFFFFu;
+}
+
 // Blocks stride over the tiles (a fixed grid of a few per CU), the next
 // tile's four windows per lane in flight while this one is counted; the tile
 // count is a block reduction (two LDS slots alternate: one barrier a tile).
+// With lowm set (the engine's chunk path) it also writes the token-end mask
+// (ix_low: a u16 per 16-B window in text order from tile_base, 1/8 of the
+// text) and tflag[t] = the tile holds a control byte other than '\t' / '\n'.
 __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restrict__ text, uint64_t tile_base,
                                                              uint64_t c0, uint64_t c1, uint64_t ntiles,
                                                              uint16_t* __restrict__ masks,
-                                                             uint32_t* __restrict__ cnt, uint64_t* __restrict__ state)
+                                                             uint32_t* __restrict__ cnt, uint64_t* __restrict__ state,
+                                                             uint16_t* __restrict__ lowm, uint8_t* __restrict__ tflag)
 {
     __shared__ uint32_t red[2][TB / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -358,24 +386,32 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
             for (int k = 0; k < IX_SUB; ++k)
                 w[k] = ix_load(text, tile_base + tn * IX_TILE + (uint64_t)k * TILE + threadIdx.x * 16, c0, c1);
         }
-        uint32_t c = 0;
+        uint32_t c = 0, ctl = 0;
         uint64_t mw = 0;   // the lane's four sub-tile masks in one 8-B word
 #pragma unroll
         for (int k = 0; k < IX_SUB; ++k) {
-            const uint32_t m = ix_mask(cur[k], t0 + (uint64_t)k * TILE + threadIdx.x * 16, c0, c1);
+            const uint64_t at = t0 + (uint64_t)k * TILE + threadIdx.x * 16;
+            const uint32_t m = ix_mask(cur[k], at, c0, c1);
             c += __popc(m);
             mw |= (uint64_t)m << (16 * k);
+            if (lowm) lowm[(t * IX_SUB + k) * TB + threadIdx.x] = (uint16_t)ix_low(cur[k], at, c0, c1, &ctl);
         }
         ((uint64_t*)masks)[t * TB + threadIdx.x] = mw;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-        if (lane == 0) red[par][wid] = c;
+        // (a wave's count is at most 64 x 64 lines: bit 31 carries its control-byte flag)
+        const uint32_t wctl = __ballot(ctl != 0) ? 0x80000000u : 0u;   // (every lane votes)
+        if (lane == 0) red[par][wid] = c | wctl;
         __syncthreads();
         if (threadIdx.x == 0) {
-            uint32_t tot = 0;
+            uint32_t tot = 0, fl = 0;
 #pragma unroll
-            for (int k = 0; k < TB / 64; ++k) tot += red[par][k];
+            for (int k = 0; k < TB / 64; ++k) {
+                tot += red[par][k] & 0x7FFFFFFFu;
+                fl |= red[par][k] >> 31;
+            }
             cnt[t] = tot;
+            if (tflag) tflag[t] = (uint8_t)fl;
         }
     }
 }
@@ -819,27 +855,239 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
 // Pass 1: the fast path over every line; a line it cannot take is appended to
 // the fallback list fb (count in *fbn).  Pass 2 (sid_parse_serial_kernel):
 // the general routine over that list -- or over every line, for -m quality.
+// LIST: over the lines a previous pass listed in (in, *inn) instead of all of
+// [lo, hi) (the cooperative parse's leftovers).
+template <bool LIST>
 __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ text, uint64_t len,
                                                        const uint64_t* __restrict__ starts,
                                                        const uint64_t* __restrict__ range,   // [lo, hi)
                                                        uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
-                                                       uint32_t* __restrict__ fb, unsigned long long* fbn)
+                                                       uint32_t* __restrict__ fb, unsigned long long* fbn,
+                                                       const uint32_t* __restrict__ in, const unsigned long long* inn)
 {
     __shared__ uint8_t cls[256];
     __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
     if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
     __syncthreads();
-    const uint64_t lo = range[0], hi = range[1];
+    const uint64_t lo = range[0], hi = LIST ? *inn : range[1];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t s_next = i < hi ? starts[i] : 0;
-    for (; i < hi; i += stride) {
+    uint64_t k = (LIST ? 0 : lo) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t s_next = k < hi ? starts[LIST ? lo + in[k] : k] : 0;
+    for (; k < hi; k += stride) {
+        const uint64_t i = LIST ? lo + in[k] : k;
         const uint64_t s0 = s_next;
-        if (i + stride < hi) s_next = starts[i + stride];   // the next line's offset in flight
+        if (k + stride < hi) s_next = starts[LIST ? lo + in[k + stride] : k + stride];   // the next line's offset in flight
         uint64_t c = 0, h[2] = {0, 0};
         if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
             counts[i] = c;
             *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h[0], h[1]);
+        } else {
+            fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
+        }
+    }
+}
+
+// ------------------------------------------------------ cooperative parse --
+// The engine's parse (sid_chunk_parse): the same fast path as parse_line_fast,
+// laid out for the block instead of the lane.  A block takes 256 consecutive
+// lines:
+//   H  one lane per line, from the index's token-end mask (ix_low) alone:
+//      token starts 0-4 and the end of token 4 by bit tricks on 64-bit words
+//      (no byte of the header is classified); ref, position and the chrom's
+//      first 8 bytes by three 8-B reads; the line's 16-B windows of token 4
+//   C  the block's windows of token 4 dealt to its lanes in order (window w ->
+//      its line by a binary search of the window prefix in LDS): every lane
+//      counts one 16-B window at a time, so lines of any length keep every
+//      lane busy, and consecutive lanes read consecutive bytes; the counts
+//      meet in the line's LDS accumulator (one 64-bit atomic add a window)
+//   W  one lane per line: the '.'/',' counts to the ref's base, the counts and
+//      the header pair written (as parse_line_fast writes them)
+// A line whose tile holds a control byte other than '\t'/'\n', whose token 4
+// starts 64 or more bytes into it, or that the fast path would leave (indel,
+// '^' run, a ref whose class is not a base) is listed for the per-line passes.
+constexpr int PC_LEN_MAX = 4096;   // token 4 bytes a line may have here (12-bit fields of the accumulator)
+
+// 8 text bytes at any offset: two aligned 8-B reads and a funnel shift
+__device__ __forceinline__ uint64_t text_u64(const char* __restrict__ text, uint64_t off)
+{
+    const uint64_t* p = (const uint64_t*)(text + (off & ~(uint64_t)7));
+    const uint32_t r = (uint32_t)(off & 7);
+    const uint64_t lo = p[0];
+    return r ? (lo >> (8 * r)) | (p[1] << (64 - 8 * r)) : lo;
+}
+// token-end bits of the 64 bytes from byte b (relative to the mask's base)
+__device__ __forceinline__ uint64_t low_bits(const uint64_t* __restrict__ low64, uint64_t b)
+{
+    const uint64_t w = b >> 6;
+    const uint32_t r = (uint32_t)(b & 63);
+    const uint64_t lo = low64[w];
+    return r ? (lo >> r) | (low64[w + 1] << (64 - r)) : lo;
+}
+
+__global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restrict__ text, uint64_t len,
+                                                            uint64_t tbase, const uint64_t* __restrict__ low64,
+                                                            const uint8_t* __restrict__ tflag,
+                                                            const uint64_t* __restrict__ starts,
+                                                            const uint64_t* __restrict__ range,
+                                                            uint64_t* __restrict__ counts,
+                                                            uint64_t* __restrict__ hdr, uint32_t* __restrict__ fb,
+                                                            unsigned long long* fbn)
+{
+    __shared__ uint8_t cls[256];
+    __shared__ uint32_t wpre[TB + 1];            // windows of the lines before each line
+    __shared__ uint64_t q4[TB];                  // first byte of each line's token 4
+    __shared__ uint32_t n4[TB];                  // its length
+    __shared__ unsigned long long acc[TB];       // A, C, G, T, '.'/',' in 12-bit fields
+    __shared__ uint32_t lbad[TB];
+    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    const uint64_t lo = range[0], hi = range[1];
+    const uint64_t i = lo + (uint64_t)blockIdx.x * TB + threadIdx.x;
+    const int tid = threadIdx.x;
+    __syncthreads();
+    // ---- H
+    bool ok = false;
+    uint32_t nw = 0, kd = 0;
+    uint64_t h0 = 0, h1 = 0, q = 0, e4 = 0;
+    if (i < hi) {
+        const uint64_t s0 = starts[i];
+        const uint64_t s1 = i + 1 < hi ? starts[i + 1] : len;   // the next line's start (bytes past it are not this line's)
+        const uint32_t span = (uint32_t)min(s1 - s0, (uint64_t)64);
+        uint64_t S = low_bits(low64, s0 - tbase);
+        if (span < 64) S |= ~0ull << span;
+        const uint64_t N = ~S;
+        uint64_t T = N & ~(N << 1);   // token starts
+        const int t0 = ctz64(T);
+        T &= T - 1;
+        const int t1 = ctz64(T);
+        T &= T - 1;
+        const int t2 = ctz64(T);
+        T &= T - 1;
+        T &= T - 1;
+        const int t4 = ctz64(T);
+        ok = t4 < 64 && ((S >> ((t2 + 1) & 63)) & 1);   // five tokens in the first 64 bytes, token 2 one byte
+        if (ok) {
+            q = s0 + (uint64_t)t4;
+            // end of token 4: the first token-end byte after it (the line's '\n' at the latest)
+            uint64_t m = t4 < 63 ? S >> (t4 + 1) : 0;
+            if (m) {
+                e4 = q + 1 + (uint64_t)ctz64(m);
+            } else {
+                uint64_t b = s0 + 64;
+                for (;;) {
+                    if (b >= s1) {
+                        e4 = s1;
+                        break;
+                    }
+                    if (b - q >= (uint64_t)PC_LEN_MAX) {   // too long for here: the per-line passes take it
+                        e4 = b;
+                        break;
+                    }
+                    const uint64_t wm = low_bits(low64, b - tbase);
+                    if (wm) {
+                        e4 = min(s1, b + (uint64_t)ctz64(wm));
+                        break;
+                    }
+                    b += 64;
+                }
+            }
+            ok = e4 - q < (uint64_t)PC_LEN_MAX;
+            const uint64_t tl = (min(e4, len - 1) - tbase) / IX_TILE;   // the tile of the byte ending token 4
+            for (uint64_t tt = (s0 - tbase) / IX_TILE; ok && tt <= tl; ++tt) ok = !tflag[tt];
+        }
+        if (ok) {
+            const int l0 = ctz64(S >> t0);
+            const int lp = ctz64(S >> t1);
+            const uint32_t ref = (uint32_t)(uint8_t)text[s0 + t2];
+            const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
+            const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
+            kd = cls[up];
+            const uint32_t kc = cls[lw];
+            ok = kd < K_CARET && kc < K_CARET && kd == kc;
+            // the position as in parse_line_fast
+            const uint32_t L8 = min((uint32_t)lp, 8u);
+            const uint64_t p8 = text_u64(text, s0 + t1);
+            const uint32_t plo = (uint32_t)p8, phi = (uint32_t)(p8 >> 32);
+            const uint64_t nd = (uint64_t)not_digit(plo) | ((uint64_t)not_digit(phi) << 32);
+            const uint64_t inl = L8 >= 8 ? ~0ull : ((1ull << (8 * L8)) - 1);
+            const uint32_t d9 = (uint32_t)(uint8_t)text[s0 + t1 + 8] - '0';
+            const bool pos_ok = lp >= 1 && lp <= 9 && (nd & inl) == 0 && (lp < 9 || d9 < 10u);
+            const uint64_t dv = ((uint64_t)(phi - 0x30303030u) << 32) | (plo - 0x30303030u);
+            const uint64_t dz = L8 == 0 ? 0 : dv << ((8 * (8 - L8)) & 63);
+            const uint32_t z0 = (uint32_t)dz, z1 = (uint32_t)(dz >> 32);
+            const uint32_t hh = __umul24(__builtin_amdgcn_udot4(z0, 0x0000010Au, 0u, false), 100u) +
+                                __builtin_amdgcn_udot4(z0, 0x010A0000u, 0u, false);
+            const uint32_t ll = __umul24(__builtin_amdgcn_udot4(z1, 0x0000010Au, 0u, false), 100u) +
+                                __builtin_amdgcn_udot4(z1, 0x010A0000u, 0u, false);
+            uint32_t pos = __umul24(hh, 10000u) + ll;
+            if (lp == 9) pos = pos * 10u + d9;
+            h0 = pos_ok ? (1ull << 63) | ((uint64_t)t0 << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
+            h1 = text_u64(text, s0 + t0) & (l0 >= 8 ? ~0ull : ((1ull << (8 * l0)) - 1));
+            nw = ok ? (uint32_t)(((e4 - 1) >> 4) - (q >> 4) + 1) : 0u;
+        }
+    }
+    uint32_t tot;
+    const uint32_t pre = block_exscan(nw, &tot);
+    wpre[tid] = pre;
+    if (tid == TB - 1) wpre[TB] = tot;
+    q4[tid] = q;
+    n4[tid] = (uint32_t)(e4 - q);
+    acc[tid] = 0;
+    lbad[tid] = 0;
+    __syncthreads();
+    // ---- C
+    for (uint32_t w = tid; w < tot; w += TB) {
+        uint32_t L = 0;
+#pragma unroll
+        for (uint32_t st = TB / 2; st > 0; st >>= 1)
+            if (wpre[L + st] <= w) L += st;
+        const uint64_t qa = q4[L], qe = qa + n4[L];
+        const uint32_t j = w - wpre[L];
+        const uint64_t a = (qa & ~(uint64_t)15) + 16ull * j;
+        const uint4 v = *(const uint4*)(text + a);
+        const uint32_t lead = j == 0 ? (uint32_t)(qa & 15) : 0u;
+        const uint32_t room = (uint32_t)min(qe - a, (uint64_t)16);
+        const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
+        // bit 7: byte 0 is skipped (a '^' ends the window before; a '^' run fails the line wherever it lies)
+        uint32_t carry = (j > 0 && text[a - 1] == '^') ? 0x80u : 0u;
+        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+        uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t x = ws[k];
+            const uint32_t vm = (__umul24((valid >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) << 7;
+            const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
+            const uint32_t skip = ((caret << 8) | carry) & vm;
+            bad = bad || (caret & skip) != 0;
+            carry = caret >> 24;
+            const uint32_t cm = vm & ~skip;
+            bad = bad || (eq_bytes(x | 0x06060606u, 0x2F2F2F2Fu) & cm) != 0;   // '+' '-' (')' '/')
+            const uint32_t f = x | 0x20202020u;
+            nA += __popc(eq_bytes(f, 0x61616161u) & cm);
+            nC += __popc(eq_bytes(f, 0x63636363u) & cm);
+            nG += __popc(eq_bytes(f, 0x67676767u) & cm);
+            nT += __popc(eq_bytes(f, 0x74747474u) & cm);
+            nM += __popc(eq_bytes(x | 0x02020202u, 0x2E2E2E2Eu) & cm);
+        }
+        atomicAdd(&acc[L], (unsigned long long)nA | ((unsigned long long)nC << 12) |
+                               ((unsigned long long)nG << 24) | ((unsigned long long)nT << 36) |
+                               ((unsigned long long)nM << 48));
+        if (bad) lbad[L] = 1;
+    }
+    __syncthreads();
+    // ---- W
+    if (i < hi) {
+        if (ok && !lbad[tid]) {
+            const unsigned long long a = acc[tid];
+            uint32_t nA = (uint32_t)a & 0xFFFu, nC = (uint32_t)(a >> 12) & 0xFFFu;
+            uint32_t nG = (uint32_t)(a >> 24) & 0xFFFu, nT = (uint32_t)(a >> 36) & 0xFFFu;
+            const uint32_t nM = (uint32_t)(a >> 48) & 0xFFFu;
+            nA += kd == K_A ? nM : 0;
+            nC += kd == K_C ? nM : 0;
+            nG += kd == K_G ? nM : 0;
+            nT += kd == K_T ? nM : 0;
+            counts[i] = (uint64_t)nA | ((uint64_t)nC << 16) | ((uint64_t)nG << 32) | ((uint64_t)nT << 48);
+            *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h0, h1);
         } else {
             fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
         }
@@ -904,7 +1152,7 @@ static void launch_parse(const char* text, uint64_t len, const uint64_t* starts,
     }
     const unsigned pgf = env ? pg : line_walk_grid(n, len, pg);
     (void)hipMemsetAsync(fbn, 0, sizeof *fbn, st);
-    sid_parse_kernel<<<pgf, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn);
+    sid_parse_kernel<false><<<pgf, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, nullptr, nullptr);
     sid_parse_serial_kernel<<<256, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, err, 0);
 }
 
@@ -2492,6 +2740,16 @@ static uint64_t chunk_tiles(uint64_t c0, uint64_t c1)
     return std::max<uint64_t>((c1 - t0 + TILE - 1) / TILE, 1);
 }
 
+// the cooperative parse (sid_parse_coop_kernel) instead of the per-line one:
+// SID_PARSE_COOP=1.  Off by default: the token-end mask it needs costs the
+// index more than the parse saves (C2 index 0.92 -> 1.55 ms,
+// parse 1.84 -> 1.95 ms per step; the C5 200x shard's parse 10.6 -> 9.1 ms)
+static bool parse_coop()
+{
+    static const bool on = std::getenv("SID_PARSE_COOP") && std::atoi(std::getenv("SID_PARSE_COOP")) != 0;
+    return on;
+}
+
 int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
 {
     // grow-only; hipFree waits for the device, so buffers still in use by
@@ -2504,13 +2762,21 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         if (W->tcnt) (void)hipFree(W->tcnt);
         if (W->toff) (void)hipFree(W->toff);
         if (W->masks) (void)hipFree(W->masks);
+        if (W->lowm) (void)hipFree(W->lowm);
+        if (W->tflag) (void)hipFree(W->tflag);
         W->tcnt = nullptr;
         W->toff = nullptr;
         W->masks = nullptr;
+        W->lowm = nullptr;
+        W->tflag = nullptr;
         W->tile_cap = 0;
         WCHECK(hipMalloc(&W->tcnt, ((t * 4 + 7) & ~(size_t)7) + scan_ws_bytes(t)));
         WCHECK(hipMalloc(&W->toff, t * 8));
         WCHECK(hipMalloc(&W->masks, t * TB * sizeof(uint16_t)));   // a u16 per lane per 4 KiB tile
+        if (parse_coop()) {
+            WCHECK(hipMalloc(&W->lowm, t * TB * sizeof(uint16_t) + 64));   // (+ the word a 64-bit read may touch past the end)
+            WCHECK(hipMalloc(&W->tflag, t / IX_SUB + 1));
+        }
         W->tile_cap = t;
     }
     if (sites > W->site_cap) {
@@ -2530,7 +2796,7 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         WCHECK(hipMalloc(&W->starts, m * 8));
         WCHECK(hipMalloc(&W->counts, m * 8));
         WCHECK(hipMalloc(&W->hdr, m * 16));
-        WCHECK(hipMalloc(&W->fb, m * 4));
+        WCHECK(hipMalloc(&W->fb, m * 8));
         WCHECK(hipMalloc(&W->code, m));
         WCHECK(hipMalloc(&W->hom, m * 8));
         WCHECK(hipMalloc(&W->het, m * 8));
@@ -2546,7 +2812,7 @@ void sid_chunk_release(sid_chunk_ws* W)
 {
     for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
                     (void*)W->bsum, (void*)W->boff, (void*)W->tcnt, (void*)W->toff, (void*)W->state,
-                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb})
+                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb, (void*)W->lowm, (void*)W->tflag})
         if (p) (void)hipFree(p);
     *W = sid_chunk_ws{};
 }
@@ -2573,12 +2839,16 @@ int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
         return SID_OK;
     }
     const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, ix_grid());
-    sid_index_count_kernel<<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state);
+    const bool coop = parse_coop();
+    sid_index_count_kernel<<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state,
+                                                coop ? W->lowm : nullptr, coop ? W->tflag : nullptr);
     launch_scan(W->tcnt, ntiles, W->toff, W->state, W->state + 1,
                 (uint64_t*)((char*)W->tcnt + ((ntiles * 4 + 7) & ~(size_t)7)), st);
     WCHECK(hipGetLastError());
     return SID_OK;
 }
+
+constexpr unsigned PC_LIST_GRID = 1024;   // blocks of the per-line pass over the cooperative parse's leftovers
 
 // line offsets from the index's masks + the two-pass parse of the n sites;
 // state[4] = min(offset * 8 + kind) over the malformed lines (all ones: none)
@@ -2591,8 +2861,21 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     const uint64_t ntiles = (c1 - t0 + IX_TILE - 1) / IX_TILE;
     sid_index_emit_kernel<<<(unsigned)std::min<uint64_t>(ntiles, ix_grid()), TB, 0, st>>>(W->masks, t0, ntiles,
                                                                                           W->toff, W->starts);
-    launch_parse(base, c1, W->starts, W->state + 1, n, W->counts, W->hdr, W->fb,
-                 (unsigned long long*)(W->state + 6), (unsigned long long*)(W->state + 4), qmode, st);
+    if (qmode || !parse_coop()) {
+        launch_parse(base, c1, W->starts, W->state + 1, n, W->counts, W->hdr, W->fb,
+                     (unsigned long long*)(W->state + 6), (unsigned long long*)(W->state + 4), qmode, st);
+    } else {
+        // the cooperative parse; its leftovers to the per-line fast path, that one's to the general routine
+        unsigned long long* fbn = (unsigned long long*)(W->state + 6);
+        uint32_t* fb2 = W->fb + W->site_cap;
+        WCHECK(hipMemsetAsync(fbn, 0, 2 * sizeof *fbn, st));
+        sid_parse_coop_kernel<<<(unsigned)((n + TB - 1) / TB), TB, 0, st>>>(
+            base, c1, t0, (const uint64_t*)W->lowm, W->tflag, W->starts, W->state + 1, W->counts, W->hdr, W->fb, fbn);
+        sid_parse_kernel<true><<<PC_LIST_GRID, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr,
+                                                            fb2, fbn + 1, W->fb, fbn);
+        sid_parse_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr, fb2,
+                                                    fbn + 1, (unsigned long long*)(W->state + 4), 0);
+    }
     WCHECK(hipGetLastError());
     return SID_OK;
 }

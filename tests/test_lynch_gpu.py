@@ -246,3 +246,52 @@ def test_device_estimate_edge_tables(gpu, sid, oracle, monkeypatch, method, o):
         assert rc == 0 and (e1.heterozygosity, e1.error_rate, e1.iterations) == \
             (rest.heterozygosity, rest.error_rate, rest.iterations)
         assert_parity(c1, h1, t1, rcode, rhom, rhet, what=f"device estimate edge table {method}")
+
+
+def high_coverage_counts(seed, n):
+    """30x sites plus profiles of coverage 500-17000 whose likelihoods fall
+    in the long double's denormal range (a few units of 2^-16445 before M
+    multiplies them), underflow, or meet an M over LDBL_MAX (0 * inf)."""
+    rng = np.random.default_rng(seed)
+    base = np.asarray(__import__("sid_amd").synth_counts_host(seed, n, 30.0)).copy()
+    rows = []
+    for _ in range(3000):
+        c = int(rng.choice([500, 1000, 1500, 2000, 3148, 3150, 5000, 13000]))
+        f = rng.dirichlet(rng.choice([[1, 1, 1, 1], [20, 20, 1, 1], [40, 1, 1, 1], [2, 2, 2, 4]]))
+        p = rng.multinomial(c, f)
+        rows.append(np.minimum(p, 65535))
+    for p in ([630, 630, 629, 1259], [630, 630, 1259, 629], [630, 1260, 629, 629], [1260, 630, 629, 629]):
+        rows += [p] * 5
+    hc = np.asarray(rows, np.uint16)
+    out = np.concatenate([base, hc])
+    return out[rng.permutation(len(out))]
+
+
+def test_objective_in_the_long_double_denormal_range(gpu, sid, oracle):
+    """compoundLikelihood (lynch.cpp:37-61) where lynch.hpp:57-96's long
+    doubles are denormal, zero or infinite: the emulated mixture (every
+    operation rounded as the x87 format rounds it) against the oracle's real
+    long doubles."""
+    counts = high_coverage_counts(21, 50_000)
+    ctx = sid.Context(0, method="likelihood_ratio")
+    d = gpu.to_device(counts)
+    ctx.profile_reset(None)
+    ctx.profile_accumulate(d.data_ptr(), len(counts), None)
+    ctx.lynch_setup()
+    for pi, eps in [(1e-3, 1e-3), (1.1e-3, 1e-3), (1e-3, 1.1e-3), (5e-4, 8e-3), (0.2, 0.05), (1e-3, 1e-2),
+                    (1e-3, 3e-4), (0.0, 1e-3), (1.0, 1e-3)]:
+        g = ctx.lynch_objective(pi, eps)
+        r = oracle.compound_likelihood(counts, pi, eps)
+        assert g == r or abs(g - r) <= 1e-13 * abs(r), (pi, eps, g, r)
+    ctx.close()
+
+
+@pytest.mark.parametrize("method,o", CASES[:2] + CASES[3:], ids=lambda x: str(x))
+def test_method_parity_high_coverage(gpu, sid, oracle, method, o):
+    counts = high_coverage_counts(22, 40_000)
+    code, hom, het, est = gpu.run_method(counts, method, **o)
+    rc, rcode, rhom, rhet, rest, u = oracle.call_method(counts, method, **o)
+    assert rc == 0
+    assert (est.heterozygosity, est.error_rate, est.iterations, est.converged) == \
+        (rest.heterozygosity, rest.error_rate, rest.iterations, rest.converged)
+    assert_parity(code, hom, het, rcode, rhom, rhet, what=f"{method} {o} high coverage")
