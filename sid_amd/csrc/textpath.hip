@@ -356,6 +356,7 @@ __device__ __forceinline__ uint32_t ix_low(const IxWin& w, uint64_t at, uint64_t
 // With lowm set (the engine's chunk path) it also writes the token-end mask
 // (ix_low: a u16 per 16-B window in text order from tile_base, 1/8 of the
 // text) and tflag[t] = the tile holds a control byte other than '\t' / '\n'.
+template <bool LOWM>
 __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restrict__ text, uint64_t tile_base,
                                                              uint64_t c0, uint64_t c1, uint64_t ntiles,
                                                              uint16_t* __restrict__ masks,
@@ -394,13 +395,13 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
             const uint32_t m = ix_mask(cur[k], at, c0, c1);
             c += __popc(m);
             mw |= (uint64_t)m << (16 * k);
-            if (lowm) lowm[(t * IX_SUB + k) * TB + threadIdx.x] = (uint16_t)ix_low(cur[k], at, c0, c1, &ctl);
+            if (LOWM) lowm[(t * IX_SUB + k) * TB + threadIdx.x] = (uint16_t)ix_low(cur[k], at, c0, c1, &ctl);
         }
         ((uint64_t*)masks)[t * TB + threadIdx.x] = mw;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
         // (a wave's count is at most 64 x 64 lines: bit 31 carries its control-byte flag)
-        const uint32_t wctl = __ballot(ctl != 0) ? 0x80000000u : 0u;   // (every lane votes)
+        const uint32_t wctl = LOWM && __ballot(ctl != 0) ? 0x80000000u : 0u;   // (every lane votes)
         if (lane == 0) red[par][wid] = c | wctl;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -411,7 +412,7 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
                 fl |= red[par][k] >> 31;
             }
             cnt[t] = tot;
-            if (tflag) tflag[t] = (uint8_t)fl;
+            if (LOWM) tflag[t] = (uint8_t)fl;
         }
     }
 }
@@ -2840,8 +2841,12 @@ int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     }
     const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, ix_grid());
     const bool coop = parse_coop();
-    sid_index_count_kernel<<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state,
-                                                coop ? W->lowm : nullptr, coop ? W->tflag : nullptr);
+    if (coop)
+        sid_index_count_kernel<true><<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state,
+                                                          W->lowm, W->tflag);
+    else
+        sid_index_count_kernel<false><<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state,
+                                                           nullptr, nullptr);
     launch_scan(W->tcnt, ntiles, W->toff, W->state, W->state + 1,
                 (uint64_t*)((char*)W->tcnt + ((ntiles * 4 + 7) & ~(size_t)7)), st);
     WCHECK(hipGetLastError());
