@@ -403,9 +403,11 @@ def bench_weak(R, a, cfg):
                    "estimate_prior": cfg["R"], "seed": cfg["seed"], "depth": cfg["depth"],
                    "sites_per_gpu": n, "sites_total": sites_all, "text_bytes_rank0": ln,
                    "csv_bytes_rank0": st2.bytes_out,
-                   "parallelism": f"site-range shards x{R.world}" + (" + RCCL histogram all-gather"
-                                                                     if lynch and R.world > 1 else ""),
-                   "ranks": R.world, "oversubscribed": R.oversub,
+                   "parallelism": f"site-range shards x{R.world}" + (
+                       (" + RCCL histogram all-gather" if R.backend == "nccl" else
+                        f" + {R.backend} histogram all-gather (ranks sharing a GPU)")
+                       if lynch and R.world > 1 else ""),
+                   "ranks": R.world, "oversubscribed": R.oversub, "dist_backend": R.backend,
                    "rccl_world": R.world if R.dist is not None and R.backend == "nccl" else None,
                    "numa": R.numa},
         "pcie": pcie,
