@@ -59,7 +59,7 @@ sys.path.insert(0, ROOT)
 # the copy engines (SDMA) for every host<->device copy, set before the HIP
 # runtime starts: with the runtime's default, device->host copies ran at 30
 # GB/s; with SDMA both directions reach ~57 GB/s at the same time
-# (tools/debug/pcie_probe.cpp, profiles/pcie_probe_r03.txt)
+# (tools/debug/pcie_probe.cpp, profiles/pcie_probe_r03.jsonl)
 os.environ.setdefault("HSA_ENABLE_SDMA", "1")
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
