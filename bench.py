@@ -195,11 +195,21 @@ def fmt_kind(cfg):
     return None if os.environ.get("SID_LYNCH_FUSED", "1") == "0" else "lynch"
 
 
+def parse_len(fused):
+    """-m local: the records' lengths computed by the parse (run.cpp,
+    sid_parse_len_kernel; SID_PARSE_LEN=0 keeps the separate length kernel)."""
+    return fused == "local" and os.environ.get("SID_PARSE_LEN", "1") != "0"
+
+
 def stage_bytes(stage, text_per_site, csv_per_site, fused):
     """Algorithmic HBM bytes per site of each engine stage.
     fused: a fmt_kind, the call / lookup fused into the formatter (it reads
-    the 8 B counts instead of the call kernel's 17 B code + confs)."""
+    the 8 B counts instead of the call kernel's 17 B code + confs); with
+    parse_len the length stage has only the fix-up and the block-sum scan
+    left (4 B per 512 sites, read and written)."""
     site_in = 8 if fused else 17
+    if stage == "fmt_len" and parse_len(fused):
+        return 2 * 4 / 512 + 8 / 512
     return {
         "index": text_per_site + text_per_site / 8,    # text read once, line-start masks written
         # text read; line-start masks (1/8 of the text) and offsets read back;
@@ -219,10 +229,13 @@ def stage_bytes(stage, text_per_site, csv_per_site, fused):
 def stage_kernels(stage, fused):
     return {
         "index": ["sid_index_count_kernel", "sid_scan_*"],
-        "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_serial_kernel"],
+        "parse": ["sid_index_emit_kernel"] + (["sid_parse_len_kernel", "sid_parse_serial_kernel",
+                                                 "sid_local_len_list_kernel"] if parse_len(fused)
+                                                else ["sid_parse_kernel", "sid_parse_serial_kernel"]),
         "call": ["sid_lookup_rec_kernel"],
         "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
-        "fmt_len": {"local": ["sid_local_len_kernel", "sid_local_fixlen_kernel"],
+        "fmt_len": {"local": (["sid_local_fixlen_kernel"] if parse_len(fused) else
+                              ["sid_local_len_kernel", "sid_local_fixlen_kernel"]),
                     "lynch": ["sid_lynch_len_kernel"]}.get(fused, ["sid_fmt_blen_kernel"]) + ["sid_scan_*"],
         "fmt_write": {"local": ["sid_local_put_kernel"], "lynch": ["sid_lynch_put_kernel"]}.get(
             fused, ["sid_fmt_put_kernel"]),

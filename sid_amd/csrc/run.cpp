@@ -1003,6 +1003,7 @@ void compute(sid_engine* e, Dev& d, int pass)
         if (L.ev && !pre_indexed) x = hipStreamWaitEvent(d.s_comp, L.ev, 0);
         const bool P = e->prof;
         if (P) d.prof_chunks++;
+        W.lens_ready = false;   // (set by this chunk's parse when it computes the -m local record lengths)
         const uint64_t tbytes = L.c1 - (L.c0 & ~(uint64_t)15);
         if (x == hipSuccess && !pre_indexed) rc = sid_chunk_reserve(&W, tbytes, 0);
         // pass 2 of a Lynch path: the parse kept since pass 1 stands in for the
@@ -1064,7 +1065,16 @@ void compute(sid_engine* e, Dev& d, int pass)
                 }
             }
             pe = d.prof_begin(P);
-            if (rc == SID_OK) rc = sid_chunk_parse(&W, L.base, L.c0, L.c1, n, qmode, d.s_comp);
+            // -m local: the records' lengths come out of the parse when this
+            // pass formats (sid_parse_len_kernel; the length kernel is skipped)
+            // (SID_PARSE_LEN=0: the separate length kernel; A/B)
+            static const bool parse_len = [] {
+                const char* v = std::getenv("SID_PARSE_LEN");
+                return !v || std::atoi(v) != 0;
+            }();
+            const bool lens = parse_len && e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx) && !qmode &&
+                              !(pass == 1 && e->lynch) && (pass == 2 || needs_format_pass1(e));
+            if (rc == SID_OK) rc = sid_chunk_parse(&W, L.base, L.c0, L.c1, n, qmode, d.s_comp, lens ? d.ctx : nullptr);
             d.prof_end(1, pe);
             if (rc != SID_OK) return (void)fail(e, rc);
         }

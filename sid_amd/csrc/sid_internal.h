@@ -132,8 +132,11 @@ struct sid_chunk_ws {
     uint64_t* starts = nullptr;   // line start offsets (relative to the chunk's base)
     uint64_t* counts = nullptr;   // profile_t per site
     uint64_t* hdr = nullptr;      // per site for the formatter: (chrom / position word, chrom's first 8 bytes)
-    uint32_t* fb = nullptr;       // lines left by the parse passes: [0, site_cap) for the per-line fast
-                                  // path (count in state[6]), [site_cap, 2 site_cap) for the general routine ([7])
+    uint32_t* fb = nullptr;       // three site lists of site_cap entries: the lines the first parse pass
+                                  // leaves (count in state[6]); the second pass's leftovers, or the lines the
+                                  // general routine parsed for the fused -m local lengths ([7]); the
+                                  // -m local fix-up's sites (lb[0])
+    bool lens_ready = false;      // the parse computed the -m local record lengths (sid_chunk_parse lctx)
     uint8_t* code = nullptr;
     double* hom = nullptr;
     double* het = nullptr;
@@ -151,8 +154,10 @@ struct sid_chunk_ws {
 int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites);
 void sid_chunk_release(sid_chunk_ws* W);
 int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, hipStream_t st);
+// lctx (optional, -m local with class tables, sid_chunk_local_ok): the
+// records' lengths computed by the parse, for sid_chunk_local_len next
 int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint64_t n, int qmode,
-                    hipStream_t st);
+                    hipStream_t st, const sid_ctx* lctx = nullptr);
 // the formatter: records of the n sites into out, which must hold
 // sid_chunk_fmt_bound(n, text bytes).  _len: record bytes per 512-site block
 // and their offsets; _put: the records.  Afterwards lb[1], lb[2], lb[4] =

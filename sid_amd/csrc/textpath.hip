@@ -1095,6 +1095,8 @@ __global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restri
     }
 }
 
+// late (optional): the lines it parsed, for the -m local record lengths the
+// fused parse computes for its own lines (sid_local_len_list_kernel)
 __global__ __launch_bounds__(TB) void sid_parse_serial_kernel(const char* __restrict__ text, uint64_t len,
                                                               const uint64_t* __restrict__ starts,
                                                               const uint64_t* __restrict__ range,
@@ -1102,7 +1104,9 @@ __global__ __launch_bounds__(TB) void sid_parse_serial_kernel(const char* __rest
                                                               uint64_t* __restrict__ hdr,
                                                               const uint32_t* __restrict__ fb,
                                                               const unsigned long long* fbn,
-                                                              unsigned long long* __restrict__ err, int qmode)
+                                                              unsigned long long* __restrict__ err, int qmode,
+                                                              uint32_t* __restrict__ late = nullptr,
+                                                              unsigned long long* nlate = nullptr)
 {
     __shared__ uint8_t cls[256];
     if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
@@ -1115,6 +1119,7 @@ __global__ __launch_bounds__(TB) void sid_parse_serial_kernel(const char* __rest
         parse_line_serial(text, len, starts[i], cls, &c, err, qmode);
         counts[i] = c;
         hdr[2 * i] = 0;   // the formatter tokenises these lines itself
+        if (late) late[atomicAdd(nlate, 1ull)] = (uint32_t)(i - lo);
     }
 }
 
@@ -1500,6 +1505,106 @@ __device__ __forceinline__ uint32_t local_entry(uint32_t nf, uint32_t ns, uint32
 __device__ __forceinline__ int local_rec_len(const Head& h, uint32_t tail)
 {
     return (int)h.clen + 1 + sid_i32_len(h.pos) + 1 + 7 + (int)tail;
+}
+
+// a site's -m local record length from its counts and header (the call's
+// class-table entry -> the tail length); 0 and the site listed for the
+// fix-up when neither table covers it
+struct LocalLen {
+    const uint8_t* len1;            // tail lengths of the LDS table's entries
+    const uint8_t* len2;            // ... of the second-level table's
+    uint32_t* bsum;                 // per FTB-site block: record bytes (zeroed before)
+    uint32_t* miss;                 // sites for sid_local_fixlen_kernel
+    unsigned long long* nmiss;
+};
+__device__ __forceinline__ int local_site_len(const Head& h, uint64_t c, uint64_t i, const uint8_t* L1,
+                                              const LocalLen& LL)
+{
+    uint32_t f, s, nf, ns, cov;
+    sid_major(c, f, s, nf, ns, cov);
+    const uint32_t k = local_entry(nf, ns, cov - nf - ns);
+    const uint32_t L = k < SID_TAB_N ? L1[k] : k != UINT32_MAX ? LL.len2[k - SID_TAB_N] : 0xFFu;
+    if (L == 0xFFu) {
+        LL.miss[atomicAdd(LL.nmiss, 1ull)] = (uint32_t)i;   // its bytes: the fix-up's
+        return 0;
+    }
+    return local_rec_len(h, L);
+}
+
+// (out of line: its tokeniser would set the parse's register count)
+__device__ __noinline__ int local_site_len_text(const char* text, uint64_t len, uint64_t s0, uint64_t c, uint64_t i,
+                                                LocalLen LL)
+{
+    Reader R{text, len};
+    return local_site_len(site_head(R, &s0, nullptr), c, i, LL.len1, LL);
+}
+
+// The parse with the -m local call's record lengths fused in (the length
+// kernel then only has the fix-up left): the per-line fast path as
+// sid_parse_kernel, then each parsed line's class entry and record length,
+// summed per wave (a wave's 64 lines lie in one FTB-site block) into the
+// block's byte count.  Lines the fast path leaves get theirs after the
+// general routine (sid_local_len_list_kernel).  The tail-length table is read
+// through the caches (an LDS copy would cost the parse a block per CU).
+__global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
+                                                           const uint64_t* __restrict__ starts,
+                                                           const uint64_t* __restrict__ range,
+                                                           uint64_t* __restrict__ counts,
+                                                           uint64_t* __restrict__ hdr, uint32_t* __restrict__ fb,
+                                                           unsigned long long* fbn, LocalLen LL)
+{
+    static_assert(FTB % 64 == 0 && TB % 64 == 0, "a wave's lines lie in one formatter block");
+    __shared__ uint8_t cls[256];
+    __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
+    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    __syncthreads();
+    const uint64_t lo = range[0], hi = range[1];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t w0 = lo + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);   // the wave's first line
+    uint64_t i = w0 + (threadIdx.x & 63u);
+    uint64_t s_next = i < hi ? starts[i] : 0;
+    for (uint64_t wb = w0; wb < hi; wb += stride, i += stride) {   // wave-uniform trip count
+        const uint64_t s0 = s_next;
+        if (i + stride < hi) s_next = starts[i + stride];
+        int l = 0;
+        if (i < hi) {
+            uint64_t c = 0, h[2] = {0, 0};
+            if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
+                counts[i] = c;
+                *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h[0], h[1]);
+                if (h[0] >> 63) {
+                    Head hd;
+                    hd.clen = (uint32_t)(h[0] >> 32) & 0xFFFu;
+                    hd.pos = (int32_t)(uint32_t)h[0];
+                    l = local_site_len(hd, c, i - lo, LL.len1, LL);
+                } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
+                    l = local_site_len_text(text, len, s0, c, i - lo, LL);
+                }
+            } else {
+                fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) l += __shfl_xor(l, off, 64);
+        if ((threadIdx.x & 63u) == 0 && l) atomicAdd(LL.bsum + (wb - lo) / FTB, (uint32_t)l);
+    }
+}
+
+// the record lengths of listed sites (the lines the general routine parsed)
+__global__ __launch_bounds__(TB) void sid_local_len_list_kernel(const char* __restrict__ text, uint64_t len,
+                                                               const uint64_t* __restrict__ starts,
+                                                               const uint64_t* __restrict__ hdr,
+                                                               const uint64_t* __restrict__ counts,
+                                                               const uint32_t* __restrict__ list,
+                                                               const unsigned long long* nlist, LocalLen LL)
+{
+    const uint64_t m = *nlist;
+    for (uint64_t j = (uint64_t)blockIdx.x * TB + threadIdx.x; j < m; j += (uint64_t)gridDim.x * TB) {
+        const uint32_t i = list[j];
+        Reader R{text, len};
+        const int l = local_site_len(site_head(R, starts + i, hdr + 2 * i), counts[i], i, LL.len1, LL);
+        if (l) atomicAdd(LL.bsum + i / FTB, (uint32_t)l);
+    }
 }
 
 __global__ __launch_bounds__(FTB) void sid_local_len_kernel(const char* __restrict__ text, uint64_t len,
@@ -2797,7 +2902,7 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         WCHECK(hipMalloc(&W->starts, m * 8));
         WCHECK(hipMalloc(&W->counts, m * 8));
         WCHECK(hipMalloc(&W->hdr, m * 16));
-        WCHECK(hipMalloc(&W->fb, m * 8));
+        WCHECK(hipMalloc(&W->fb, m * 12));   // three site lists (sid_chunk_ws::fb)
         WCHECK(hipMalloc(&W->code, m));
         WCHECK(hipMalloc(&W->hom, m * 8));
         WCHECK(hipMalloc(&W->het, m * 8));
@@ -2858,15 +2963,33 @@ constexpr unsigned PC_LIST_GRID = 1024;   // blocks of the per-line pass over th
 // line offsets from the index's masks + the two-pass parse of the n sites;
 // state[4] = min(offset * 8 + kind) over the malformed lines (all ones: none)
 int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint64_t n, int qmode,
-                    hipStream_t st)
+                    hipStream_t st, const sid_ctx* lctx)
 {
+    W->lens_ready = false;
     if (n > W->site_cap) return SID_EINVAL;
     if (n == 0) return SID_OK;
     const uint64_t t0 = c0 & ~(uint64_t)15;
     const uint64_t ntiles = (c1 - t0 + IX_TILE - 1) / IX_TILE;
     sid_index_emit_kernel<<<(unsigned)std::min<uint64_t>(ntiles, ix_grid()), TB, 0, st>>>(W->masks, t0, ntiles,
                                                                                           W->toff, W->starts);
-    if (qmode || !parse_coop()) {
+    if (lctx && !qmode && !parse_coop() && n < (1ull << 32)) {
+        // -m local: the record lengths out of the parse (sid_parse_len_kernel);
+        // sid_chunk_local_len then has only the fix-up and the scan left
+        const uint64_t nb = (n + FTB - 1) / FTB;
+        unsigned long long* fbn = (unsigned long long*)(W->state + 6);
+        uint32_t* late = W->fb + W->site_cap;
+        const LocalLen LL{lctx->ws.len1, lctx->ws.len2, W->bsum, W->fb + 2 * W->site_cap, W->lb};
+        WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));   // [0] the miss count, [1] bytes, [2] range flag
+        WCHECK(hipMemsetAsync(W->bsum, 0, nb * 4, st));
+        WCHECK(hipMemsetAsync(fbn, 0, 2 * sizeof *fbn, st));
+        const unsigned pg = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, 16384);
+        sid_parse_len_kernel<<<line_walk_grid(n, c1 - c0, pg), TB, 0, st>>>(base, c1, W->starts, W->state + 1,
+                                                                            W->counts, W->hdr, W->fb, fbn, LL);
+        sid_parse_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr, W->fb,
+                                                    fbn, (unsigned long long*)(W->state + 4), 0, late, fbn + 1);
+        sid_local_len_list_kernel<<<64, TB, 0, st>>>(base, c1, W->starts, W->hdr, W->counts, late, fbn + 1, LL);
+        W->lens_ready = true;
+    } else if (qmode || !parse_coop()) {
         launch_parse(base, c1, W->starts, W->state + 1, n, W->counts, W->hdr, W->fb,
                      (unsigned long long*)(W->state + 6), (unsigned long long*)(W->state + 4), qmode, st);
     } else {
@@ -2957,15 +3080,19 @@ int sid_chunk_local_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
     CType ct;
     if (local_ctype(ctx, conf_type, &ct)) return SID_EINVAL;
     if (n > W->site_cap || n >= (1ull << 32)) return SID_EINVAL;
-    WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));   // [0] the miss count, [1] bytes, [2] range flag
+    // the fix-up's sites in the third list of W->fb
+    uint32_t* miss = W->fb + 2 * W->site_cap;
     const uint64_t nb = (n + FTB - 1) / FTB;
+    if (!W->lens_ready) WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));   // [0] the miss count, [1] bytes, [2] range flag
     if (nb) {
         const unsigned grid = (unsigned)((nb + LPB - 1) / LPB);
-        sid_local_len_kernel<<<grid, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, ctx->ws.len1,
-                                                   ctx->ws.len2, W->bsum, W->fb, W->lb);
-        sid_local_fixlen_kernel<<<64, TB, 0, st>>>(base, c1, W->starts, W->hdr, W->counts, W->fb, W->lb, ctx->K,
+        if (!W->lens_ready)   // (else the parse computed them: sid_parse_len_kernel)
+            sid_local_len_kernel<<<grid, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, ctx->ws.len1,
+                                                       ctx->ws.len2, W->bsum, miss, W->lb);
+        sid_local_fixlen_kernel<<<64, TB, 0, st>>>(base, c1, W->starts, W->hdr, W->counts, miss, W->lb, ctx->K,
                                                    ctx->d_lnt, ct, W->code, W->hom, W->het, W->bsum, W->lb);
     }
+    W->lens_ready = false;
     WCHECK(hipGetLastError());
     return fmt_scan(W, nb, st);
 }

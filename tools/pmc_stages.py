@@ -17,7 +17,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGES = {   # the scan kernels (shared by the index and the formatter, ~20 us) are left out
     "index": ["sid_index_count_kernel"],
-    "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_serial_kernel"],
+    "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_len_kernel", "sid_parse_serial_kernel",
+              "sid_local_len_list_kernel"],
     "call": ["sid_lookup_rec_kernel"],
     "fmt_len": ["sid_local_len_kernel", "sid_local_fixlen_kernel", "sid_fmt_blen_kernel"],
     "fmt_write": ["sid_local_put_kernel", "sid_fmt_put_kernel"],
