@@ -859,99 +859,13 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     return read_bases_fast(text, len, s0 + (uint64_t)t4, kd, out);
 }
 
-// (out of line: the rare long headers of parse_line_fast32)
-__device__ __noinline__ bool parse_line_fast48(const char* __restrict__ text, uint64_t len, uint64_t s0,
-                                               const uint8_t* cls, char* stage, uint64_t* out, uint64_t* hdr)
-{
-    return parse_line_fast(text, len, s0, cls, stage, out, hdr);
-}
-
-// The same fast path with the header read as the 32 bytes from the line's
-// start (two unaligned 16-B loads: 8 words to classify instead of the 12 of
-// three aligned windows, and no shift by the line's phase).  A line whose
-// token 4 starts 32 or more bytes in (with no control byte before that) takes
-// parse_line_fast's 48-byte header instead.
-__device__ __forceinline__ bool parse_line_fast32(const char* __restrict__ text, uint64_t len, uint64_t s0,
-                                                  const uint8_t* cls, char* stage, uint64_t* out, uint64_t* hdr)
-{
-    uint4 v0, v1;
-    __builtin_memcpy(&v0, text + s0, 16);   // (unaligned global loads: one dwordx4 each on gfx950)
-    __builtin_memcpy(&v1, text + s0 + 16, 16);
-    *(uint4*)(stage) = v0;
-    *(uint4*)(stage + 16) = v1;
-    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    uint32_t fbad = 64;   // offset of the first control byte ('\n', NUL, < 0x20 but '\t')
-    uint32_t sp[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        sp[k] = eq_bytes(w[k], 0x20202020u) | eq_bytes(w[k], 0x09090909u);
-        const uint32_t f = (uint32_t)__ffs(low_bytes(w[k]) & ~sp[k]);
-        fbad = min(fbad, f ? 4u * k + ((f - 1u) >> 3) : 64u);
-    }
-    const uint32_t S0 = compress8(sp[0], sp[1]) | (compress8(sp[2], sp[3]) << 8) |
-                        (compress8(sp[4], sp[5]) << 16) | (compress8(sp[6], sp[7]) << 24);
-    const uint64_t avail = len > s0 ? len - s0 : 0;
-    const uint32_t nb = (uint32_t)min((uint64_t)32, avail);
-    const uint64_t valid = nb >= 32 ? 0xFFFFFFFFull : ((1ull << nb) - 1);
-    const uint64_t S = (uint64_t)S0 & valid;
-    const uint64_t N = ~S & valid;
-    uint64_t T = N & ~(N << 1);   // token starts
-    const int t0 = ctz64(T);
-    T &= T - 1;
-    const int t1 = ctz64(T);
-    T &= T - 1;
-    const int t2 = ctz64(T);
-    T &= T - 1;
-    T &= T - 1;
-    const int t4 = ctz64(T);
-    if (t4 >= (int)nb) {   // token 4 not within the 32 bytes: the 48-byte header when nothing stops it earlier
-        if (nb == 32 && fbad >= 32) return parse_line_fast48(text, len, s0, cls, stage, out, hdr);
-        return false;
-    }
-    if (fbad < (uint32_t)t4 || !((S >> ((t2 + 1) & 63)) & 1)) return false;
-    const int l0 = ctz64(S >> t0);
-    const int lp = ctz64(S >> t1);
-    const uint32_t ref = (uint8_t)stage[t2];
-    // the position as in parse_line_fast (staged bytes past the 32: the next
-    // lane's or padding -- garbage, masked)
-    const uint32_t L8 = min((uint32_t)lp, 8u);
-    const uint64_t p8 = stage_u64(stage, t1);
-    const uint32_t plo = (uint32_t)p8, phi = (uint32_t)(p8 >> 32);
-    const uint64_t nd = (uint64_t)not_digit(plo) | ((uint64_t)not_digit(phi) << 32);
-    const uint64_t inl = L8 >= 8 ? ~0ull : ((1ull << (8 * L8)) - 1);
-    const uint32_t d9 = (uint32_t)(uint8_t)stage[t1 + 8] - '0';
-    const bool pos_ok = lp >= 1 && lp <= 9 && (nd & inl) == 0 && (lp < 9 || d9 < 10u);
-    const uint64_t dv = ((uint64_t)(phi - 0x30303030u) << 32) | (plo - 0x30303030u);
-    const uint64_t dz = L8 == 0 ? 0 : dv << ((8 * (8 - L8)) & 63);
-    const uint32_t q0 = (uint32_t)dz, q1 = (uint32_t)(dz >> 32);
-    const uint32_t h4 = __umul24(__builtin_amdgcn_udot4(q0, 0x0000010Au, 0u, false), 100u) +
-                        __builtin_amdgcn_udot4(q0, 0x010A0000u, 0u, false);
-    const uint32_t l4 = __umul24(__builtin_amdgcn_udot4(q1, 0x0000010Au, 0u, false), 100u) +
-                        __builtin_amdgcn_udot4(q1, 0x010A0000u, 0u, false);
-    uint32_t pos = __umul24(h4, 10000u) + l4;
-    if (lp == 9) pos = pos * 10u + d9;
-    hdr[0] = pos_ok ? (1ull << 63) | ((uint64_t)t0 << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
-    hdr[1] = stage_u64(stage, t0) & (l0 >= 8 ? ~0ull : ((1ull << (8 * l0)) - 1));
-    const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
-    const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
-    const uint32_t kd = cls[up], kc = cls[lw];
-    if (kd >= K_CARET || kc >= K_CARET || kd != kc) return false;
-    return read_bases_fast(text, len, s0 + (uint64_t)t4, kd, out);
-}
-
 // Pass 1: the fast path over every line; a line it cannot take is appended to
 // the fallback list fb (count in *fbn).  Pass 2 (sid_parse_serial_kernel):
 // the general routine over that list -- or over every line, for -m quality.
 // LIST: over the lines a previous pass listed in (in, *inn) instead of all of
 // [lo, hi) (the cooperative parse's leftovers).
-#ifndef SID_PARSE_WAVES
-#define SID_PARSE_WAVES 8   // the per-line parse's min waves per SIMD (its register cap: 512 / this)
-#endif
-#ifdef SID_HDR48            // A/B: the 48-byte aligned header everywhere
-#define parse_line_fast32 parse_line_fast
-#endif
 template <bool LIST>
-__global__ __launch_bounds__(TB, SID_PARSE_WAVES) void sid_parse_kernel(const char* __restrict__ text, uint64_t len,
+__global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ text, uint64_t len,
                                                        const uint64_t* __restrict__ starts,
                                                        const uint64_t* __restrict__ range,   // [lo, hi)
                                                        uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
@@ -971,7 +885,7 @@ __global__ __launch_bounds__(TB, SID_PARSE_WAVES) void sid_parse_kernel(const ch
         const uint64_t s0 = s_next;
         if (k + stride < hi) s_next = starts[LIST ? lo + in[k + stride] : k + stride];   // the next line's offset in flight
         uint64_t c = 0, h[2] = {0, 0};
-        if (parse_line_fast32(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
+        if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
             counts[i] = c;
             *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h[0], h[1]);
         } else {
@@ -1638,7 +1552,7 @@ __device__ __noinline__ int local_site_len_text(const char* text, uint64_t len, 
 // block's byte count.  Lines the fast path leaves get theirs after the
 // general routine (sid_local_len_list_kernel).  The tail-length table is read
 // through the caches (an LDS copy would cost the parse a block per CU).
-__global__ __launch_bounds__(TB, SID_PARSE_WAVES) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
+__global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
                                                            const uint64_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ range,
                                                            uint64_t* __restrict__ counts,
@@ -1661,7 +1575,7 @@ __global__ __launch_bounds__(TB, SID_PARSE_WAVES) void sid_parse_len_kernel(cons
         int l = 0;
         if (i < hi) {
             uint64_t c = 0, h[2] = {0, 0};
-            if (parse_line_fast32(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
+            if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
                 counts[i] = c;
                 *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h[0], h[1]);
                 if (h[0] >> 63) {
