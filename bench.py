@@ -393,6 +393,7 @@ def bench_weak(R, a, cfg):
             "GBps_h2d": ln / (elapsed / a.steps) / 1e9, "GBps_d2h": st2.bytes_out / (elapsed / a.steps) / 1e9,
             "chunks": st.chunks, "chunks_held_in_host_arena": st.chunks_held, "ingest_s": st.ingest_s,
             "emit_s": st2.emit_s}
+    pcie["ceiling"] = pcie_ceiling(ln, st2.bytes_out, lynch, elapsed / a.steps)
     eng.close()
     del host
 
@@ -599,6 +600,27 @@ def generate_resident(torch, sid_amd, dev, gpu, cfg, first, n):
 
 VALU_ISSUE_PER_S = 256 * 4 / 2 * 2.4e9   # wave64 VALU instructions/s: 1024 SIMDs, one per 2 cycles, 2.4 GHz
 PMC_ROUND = os.environ.get("SID_PMC_ROUND", "r03")
+
+
+def pcie_ceiling(text_bytes, csv_bytes, lynch, step_s):
+    """The step's PCIe floor from the committed probe of these boxes
+    (profiles/pcie_probe_r03.jsonl, tools/debug/pcie_probe.cpp): -m local
+    overlaps the records' D2H with the upload (full duplex: the H2D at its
+    duplex rate), the Lynch paths format after the estimate (H2D, then D2H)."""
+    try:
+        rows = [json.loads(l) for l in open(os.path.join(ROOT, "profiles", "pcie_probe_r03.jsonl")) if l.strip()]
+    except OSError:
+        return None
+    best = {}
+    for r in rows:
+        best[r["probe"]] = max(best.get(r["probe"], 0.0), r["GBps"])
+    h2d_duplex, h2d, d2h = best.get("duplex_h2d_part"), best.get("h2d_128MiB_pieces"), best.get("d2h_one_2GiB")
+    if not (h2d_duplex and h2d and d2h):
+        return None
+    floor = (text_bytes / (h2d * 1e9) + csv_bytes / (d2h * 1e9)) if lynch else \
+        max(text_bytes / (h2d_duplex * 1e9), csv_bytes / (d2h * 1e9))
+    return {"floor_ms": floor * 1e3, "frac": floor / step_s, "GBps_h2d": h2d, "GBps_h2d_duplex": h2d_duplex,
+            "GBps_d2h": d2h, "source": "profiles/pcie_probe_r03.jsonl (pinned copies, best of the probe's runs)"}
 
 
 def pmc_file(stage):
