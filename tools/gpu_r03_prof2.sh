@@ -7,8 +7,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 200 python3 -u bench.py --device-only --steps 10 --device-steps 10 > $O/dev_c2.json 2> $O/dev_c2.err || { echo dev bench failed; tail $O/dev_c2.err; exit 1; }
-python3 -c "import json; d=json.load(open('$O/dev_c2.json'))['device_path']; print('C2 device', round(d['ms_per_step'],3), {k: round(v,3) for k,v in d['stages_ms'].items()})"
+timeout -k 10 400 python3 -u bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { echo bench failed; tail $O/bench_c2.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench_c2.json')); print('C2', d['value'], d['ms_per_step'], d['pcie']['ceiling']['frac'], d['device_path']['ms_per_step'], {k: round(v,3) for k,v in d['device_path']['stages_ms'].items()}, d['roofline']['frac'], d['cpu_baseline']['value'])"
 ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/r03trace -o trace -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 5 --no-cpu > $O/r03trace.json 2> $O/r03trace.log ) || { echo trace failed; tail $O/r03trace.log; exit 1; }
 python3 - <<'PY'
 import csv, os
