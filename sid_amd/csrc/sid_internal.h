@@ -146,7 +146,6 @@ struct sid_chunk_ws {
     uint64_t* boff = nullptr;
     uint16_t* masks = nullptr;    // line-start masks of the index, a u16 per lane per 4 KiB tile
     uint16_t* lowm = nullptr;     // token-end bytes (< 0x21 or outside the chunk), a u16 per 16 B in text order
-    uint8_t* tflag = nullptr;     // per 16 KiB tile: holds a control byte other than '\t' / '\n'
     unsigned long long* lb = nullptr;   // formatter flags and totals (sid_chunk_fmt_len)
     uint64_t* state = nullptr;    // [0] sites [1..2] parse range [3] CSV bytes [4] first error key [5] range flag
                                   // [6] [7] fallback lines

@@ -327,41 +327,29 @@ __device__ __forceinline__ uint32_t ix_mask(const IxWin& w, uint64_t at, uint64_
 }
 
 // The window's token-end bytes for the cooperative parse: bit j = byte j is
-// < 0x21 (' ', '\t', '\n', NUL, other control bytes) or outside [c0, c1) (such
-// a byte ends any token); *ctl |= a control byte other than '\t' / '\n' inside
-// [c0, c1) (the parse leaves the lines of such a tile to the per-line routines,
-// which tokenise on ' ' / '\t' only, as parsePileupLine does)
-__device__ __forceinline__ uint32_t ix_low(const IxWin& w, uint64_t at, uint64_t c0, uint64_t c1, uint32_t* ctl)
+// < 0x21 (' ', '\t', '\n', NUL, other control bytes) or outside [c0, c1)
+// (such a byte ends any token).  Which of them a line's separators are is
+// checked per line by the parse (only ' ' and '\t' separate tokens there).
+__device__ __forceinline__ uint32_t ix_low(const IxWin& w, uint64_t at, uint64_t c0, uint64_t c1)
 {
-    const uint32_t ws[4] = {w.v.x, w.v.y, w.v.z, w.v.w};
-    uint32_t lo[4], cb[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t x = ws[k];
-        lo[k] = low_bytes(x);
-        const uint32_t lt20 = ~(((x & 0x7F7F7F7Fu) + 0x60606060u) | x) & 0x80808080u;   // b < 0x20
-        cb[k] = lt20 & ~eq_bytes(x, 0x09090909u) & ~eq_bytes(x, 0x0A0A0A0Au);
-    }
     uint32_t inr = 0xFFFFu;   // bytes inside [c0, c1)
     if (at + 16 > c1) inr = c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
     if (at < c0) inr &= c0 - at >= 16 ? 0u : (0xFFFFu << (uint32_t)(c0 - at)) & 0xFFFFu;
-    const uint32_t cm = compress8(cb[0], cb[1]) | (compress8(cb[2], cb[3]) << 8);
-    *ctl |= cm & inr;
-    return (compress8(lo[0], lo[1]) | (compress8(lo[2], lo[3]) << 8) | ~inr) & 0xFFFFu;
+    return (compress8(low_bytes(w.v.x), low_bytes(w.v.y)) | (compress8(low_bytes(w.v.z), low_bytes(w.v.w)) << 8) |
+            ~inr) & 0xFFFFu;
 }
 
 // Blocks stride over the tiles (a fixed grid of a few per CU), the next
 // tile's four windows per lane in flight while this one is counted; the tile
 // count is a block reduction (two LDS slots alternate: one barrier a tile).
-// With lowm set (the engine's chunk path) it also writes the token-end mask
-// (ix_low: a u16 per 16-B window in text order from tile_base, 1/8 of the
-// text) and tflag[t] = the tile holds a control byte other than '\t' / '\n'.
+// LOWM (the cooperative parse) also writes the token-end mask (ix_low: a u16
+// per 16-B window in text order from tile_base, 1/8 of the text).
 template <bool LOWM>
 __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restrict__ text, uint64_t tile_base,
                                                              uint64_t c0, uint64_t c1, uint64_t ntiles,
                                                              uint16_t* __restrict__ masks,
                                                              uint32_t* __restrict__ cnt, uint64_t* __restrict__ state,
-                                                             uint16_t* __restrict__ lowm, uint8_t* __restrict__ tflag)
+                                                             uint16_t* __restrict__ lowm)
 {
     __shared__ uint32_t red[2][TB / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -387,7 +375,7 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
             for (int k = 0; k < IX_SUB; ++k)
                 w[k] = ix_load(text, tile_base + tn * IX_TILE + (uint64_t)k * TILE + threadIdx.x * 16, c0, c1);
         }
-        uint32_t c = 0, ctl = 0;
+        uint32_t c = 0;
         uint64_t mw = 0;   // the lane's four sub-tile masks in one 8-B word
 #pragma unroll
         for (int k = 0; k < IX_SUB; ++k) {
@@ -395,24 +383,18 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
             const uint32_t m = ix_mask(cur[k], at, c0, c1);
             c += __popc(m);
             mw |= (uint64_t)m << (16 * k);
-            if (LOWM) lowm[(t * IX_SUB + k) * TB + threadIdx.x] = (uint16_t)ix_low(cur[k], at, c0, c1, &ctl);
+            if (LOWM) lowm[(t * IX_SUB + k) * TB + threadIdx.x] = (uint16_t)ix_low(cur[k], at, c0, c1);
         }
         ((uint64_t*)masks)[t * TB + threadIdx.x] = mw;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-        // (a wave's count is at most 64 x 64 lines: bit 31 carries its control-byte flag)
-        const uint32_t wctl = LOWM && __ballot(ctl != 0) ? 0x80000000u : 0u;   // (every lane votes)
-        if (lane == 0) red[par][wid] = c | wctl;
+        if (lane == 0) red[par][wid] = c;
         __syncthreads();
         if (threadIdx.x == 0) {
-            uint32_t tot = 0, fl = 0;
+            uint32_t tot = 0;
 #pragma unroll
-            for (int k = 0; k < TB / 64; ++k) {
-                tot += red[par][k] & 0x7FFFFFFFu;
-                fl |= red[par][k] >> 31;
-            }
+            for (int k = 0; k < TB / 64; ++k) tot += red[par][k];
             cnt[t] = tot;
-            if (LOWM) tflag[t] = (uint8_t)fl;
         }
     }
 }
@@ -909,9 +891,10 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
 //      meet in the line's LDS accumulator (one 64-bit atomic add a window)
 //   W  one lane per line: the '.'/',' counts to the ref's base, the counts and
 //      the header pair written (as parse_line_fast writes them)
-// A line whose tile holds a control byte other than '\t'/'\n', whose token 4
-// starts 64 or more bytes into it, or that the fast path would leave (indel,
-// '^' run, a ref whose class is not a base) is listed for the per-line passes.
+// A line with a token-end byte other than ' '/'\t' before its token 4 (or one
+// other than those and '\n' ending it), whose token 4 starts 64 or more bytes
+// into it, or that the fast path would leave (indel, '^' run, a ref whose
+// class is not a base) is listed for the per-line passes.
 constexpr int PC_LEN_MAX = 4096;   // token 4 bytes a line may have here (12-bit fields of the accumulator)
 
 // 8 text bytes at any offset: two aligned 8-B reads and a funnel shift
@@ -931,9 +914,36 @@ __device__ __forceinline__ uint64_t low_bits(const uint64_t* __restrict__ low64,
     return r ? (lo >> r) | (low64[w + 1] << (64 - r)) : lo;
 }
 
+// the 16-B window counts of token 4: valid = the window's bytes inside the
+// token, carry = bit 7 when its byte 0 follows a '^' (is skipped); returns A,
+// C, G, T and '.'/',' in 12-bit fields; *bad: an indel or a '^' run
+__device__ __forceinline__ unsigned long long window_counts(uint4 v, uint32_t valid, uint32_t& carry, bool& bad)
+{
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+    uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = ws[k];
+        const uint32_t vm = (__umul24((valid >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) << 7;
+        const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
+        const uint32_t skip = ((caret << 8) | carry) & vm;
+        bad = bad || (caret & skip) != 0;
+        carry = caret >> 24;
+        const uint32_t cm = vm & ~skip;
+        bad = bad || (eq_bytes(x | 0x06060606u, 0x2F2F2F2Fu) & cm) != 0;   // '+' '-' (')' '/')
+        const uint32_t f = x | 0x20202020u;
+        nA += __popc(eq_bytes(f, 0x61616161u) & cm);
+        nC += __popc(eq_bytes(f, 0x63636363u) & cm);
+        nG += __popc(eq_bytes(f, 0x67676767u) & cm);
+        nT += __popc(eq_bytes(f, 0x74747474u) & cm);
+        nM += __popc(eq_bytes(x | 0x02020202u, 0x2E2E2E2Eu) & cm);
+    }
+    return (unsigned long long)nA | ((unsigned long long)nC << 12) | ((unsigned long long)nG << 24) |
+           ((unsigned long long)nT << 36) | ((unsigned long long)nM << 48);
+}
+
 __global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restrict__ text, uint64_t len,
                                                             uint64_t tbase, const uint64_t* __restrict__ low64,
-                                                            const uint8_t* __restrict__ tflag,
                                                             const uint64_t* __restrict__ starts,
                                                             const uint64_t* __restrict__ range,
                                                             uint64_t* __restrict__ counts,
@@ -973,6 +983,14 @@ __global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restri
         const int t4 = ctz64(T);
         ok = t4 < 64 && ((S >> ((t2 + 1) & 63)) & 1);   // five tokens in the first 64 bytes, token 2 one byte
         if (ok) {
+            // the token-end bytes before token 4 must be ' ' or '\t' (parsePileupLine
+            // splits on those two only; a NUL or other control byte: the per-line passes)
+            for (uint64_t m = S & ((1ull << t4) - 1); ok && m; m &= m - 1) {
+                const uint32_t b = (uint8_t)text[s0 + (uint64_t)ctz64(m)];
+                ok = b == ' ' || b == '\t';
+            }
+        }
+        if (ok) {
             q = s0 + (uint64_t)t4;
             // end of token 4: the first token-end byte after it (the line's '\n' at the latest)
             uint64_t m = t4 < 63 ? S >> (t4 + 1) : 0;
@@ -998,8 +1016,10 @@ __global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restri
                 }
             }
             ok = e4 - q < (uint64_t)PC_LEN_MAX;
-            const uint64_t tl = (min(e4, len - 1) - tbase) / IX_TILE;   // the tile of the byte ending token 4
-            for (uint64_t tt = (s0 - tbase) / IX_TILE; ok && tt <= tl; ++tt) ok = !tflag[tt];
+            if (ok && e4 < len) {   // the byte that ends token 4: a separator or the line's end
+                const uint32_t b = (uint8_t)text[e4];
+                ok = b == ' ' || b == '\t' || b == '\n';
+            }
         }
         if (ok) {
             const int l0 = ctz64(S >> t0);
@@ -1041,7 +1061,8 @@ __global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restri
     acc[tid] = 0;
     lbad[tid] = 0;
     __syncthreads();
-    // ---- C
+    // ---- C: window w on lane w mod 256 (a wave's loads cover 1 KiB of
+    // consecutive windows; 64-B runs per lane measured 40% slower)
     for (uint32_t w = tid; w < tot; w += TB) {
         uint32_t L = 0;
 #pragma unroll
@@ -1056,29 +1077,8 @@ __global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restri
         const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
         // bit 7: byte 0 is skipped (a '^' ends the window before; a '^' run fails the line wherever it lies)
         uint32_t carry = (j > 0 && text[a - 1] == '^') ? 0x80u : 0u;
-        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-        uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
         bool bad = false;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t x = ws[k];
-            const uint32_t vm = (__umul24((valid >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) << 7;
-            const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
-            const uint32_t skip = ((caret << 8) | carry) & vm;
-            bad = bad || (caret & skip) != 0;
-            carry = caret >> 24;
-            const uint32_t cm = vm & ~skip;
-            bad = bad || (eq_bytes(x | 0x06060606u, 0x2F2F2F2Fu) & cm) != 0;   // '+' '-' (')' '/')
-            const uint32_t f = x | 0x20202020u;
-            nA += __popc(eq_bytes(f, 0x61616161u) & cm);
-            nC += __popc(eq_bytes(f, 0x63636363u) & cm);
-            nG += __popc(eq_bytes(f, 0x67676767u) & cm);
-            nT += __popc(eq_bytes(f, 0x74747474u) & cm);
-            nM += __popc(eq_bytes(x | 0x02020202u, 0x2E2E2E2Eu) & cm);
-        }
-        atomicAdd(&acc[L], (unsigned long long)nA | ((unsigned long long)nC << 12) |
-                               ((unsigned long long)nG << 24) | ((unsigned long long)nT << 36) |
-                               ((unsigned long long)nM << 48));
+        atomicAdd(&acc[L], window_counts(v, valid, carry, bad));
         if (bad) lbad[L] = 1;
     }
     __syncthreads();
@@ -2875,19 +2875,16 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         if (W->toff) (void)hipFree(W->toff);
         if (W->masks) (void)hipFree(W->masks);
         if (W->lowm) (void)hipFree(W->lowm);
-        if (W->tflag) (void)hipFree(W->tflag);
         W->tcnt = nullptr;
         W->toff = nullptr;
         W->masks = nullptr;
         W->lowm = nullptr;
-        W->tflag = nullptr;
         W->tile_cap = 0;
         WCHECK(hipMalloc(&W->tcnt, ((t * 4 + 7) & ~(size_t)7) + scan_ws_bytes(t)));
         WCHECK(hipMalloc(&W->toff, t * 8));
         WCHECK(hipMalloc(&W->masks, t * TB * sizeof(uint16_t)));   // a u16 per lane per 4 KiB tile
         if (parse_coop()) {
             WCHECK(hipMalloc(&W->lowm, t * TB * sizeof(uint16_t) + 64));   // (+ the word a 64-bit read may touch past the end)
-            WCHECK(hipMalloc(&W->tflag, t / IX_SUB + 1));
         }
         W->tile_cap = t;
     }
@@ -2924,7 +2921,7 @@ void sid_chunk_release(sid_chunk_ws* W)
 {
     for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
                     (void*)W->bsum, (void*)W->boff, (void*)W->tcnt, (void*)W->toff, (void*)W->state,
-                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb, (void*)W->lowm, (void*)W->tflag})
+                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb, (void*)W->lowm})
         if (p) (void)hipFree(p);
     *W = sid_chunk_ws{};
 }
@@ -2954,10 +2951,10 @@ int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     const bool coop = parse_coop();
     if (coop)
         sid_index_count_kernel<true><<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state,
-                                                          W->lowm, W->tflag);
+                                                          W->lowm);
     else
         sid_index_count_kernel<false><<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state,
-                                                           nullptr, nullptr);
+                                                           nullptr);
     launch_scan(W->tcnt, ntiles, W->toff, W->state, W->state + 1,
                 (uint64_t*)((char*)W->tcnt + ((ntiles * 4 + 7) & ~(size_t)7)), st);
     WCHECK(hipGetLastError());
@@ -3004,7 +3001,7 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
         uint32_t* fb2 = W->fb + W->site_cap;
         WCHECK(hipMemsetAsync(fbn, 0, 2 * sizeof *fbn, st));
         sid_parse_coop_kernel<<<(unsigned)((n + TB - 1) / TB), TB, 0, st>>>(
-            base, c1, t0, (const uint64_t*)W->lowm, W->tflag, W->starts, W->state + 1, W->counts, W->hdr, W->fb, fbn);
+            base, c1, t0, (const uint64_t*)W->lowm, W->starts, W->state + 1, W->counts, W->hdr, W->fb, fbn);
         sid_parse_kernel<true><<<PC_LIST_GRID, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr,
                                                             fb2, fbn + 1, W->fb, fbn);
         sid_parse_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr, fb2,

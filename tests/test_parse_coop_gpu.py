@@ -115,6 +115,10 @@ def test_stress_text_equals_oracle(sid, oracle, tmp_path, seed, depth):
                   ["--chunk-bytes", "20000"]):
         same_as_oracle(sid, oracle, p, [], extra)
     same_as_oracle(sid, oracle, p, ["-R", "-m", "likelihood_ratio"], ["--chunk-bytes", "300000"])
+    if seed == 41:   # the other Lynch-path methods on the same profiles (NaN p-values, denormal likelihoods)
+        same_as_oracle(sid, oracle, p, ["-m", "bayes"], ["--chunk-bytes", "300000"])
+        same_as_oracle(sid, oracle, p, ["-R", "-m", "local"], ["--chunk-bytes", "300000", "--devices", "2"])
+        same_as_oracle(sid, oracle, p, ["-m", "likelihood_ratio", "-p", "0.2"], ["--chunk-bytes", "1000000"])
 
 
 @pytest.mark.parametrize("seed", [4, 5, 6, 9])
