@@ -1629,6 +1629,31 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
         e->ingested = false;
         return ok ? SID_OK : SID_EIO;
     }
+    // the device sink with every chunk's records held in HBM since pass 1: no
+    // pass 2 for the devices (the ingest synchronised their streams), only the
+    // byte count -- no threads to start for a run that has nothing left to do
+    bool all_held = sink == 1 && !e->recs.empty();
+    for (const auto& r : e->recs) all_held = all_held && r.held;
+    if (all_held) {
+        uint64_t out = 0;
+        for (auto& r : e->recs) {
+            Dev& d = *e->devs[r.dev];
+            out += r.held_len;
+            d.pool.put(r.held, r.held_cap, nullptr);
+            if (r.kept) d.pool.put(r.kept, r.kept_cap, nullptr);
+            if (r.pre) d.pool.put(r.pre, r.pre_cap, nullptr);
+            r.held = r.kept = r.pre = nullptr;
+        }
+        e->sink_bytes = out;
+        if (st) {
+            st->chunks_reloaded = 0;
+            st->bytes_out = out;
+            st->emit_s = wall() - t0;
+        }
+        timing_report(e, "emit", wall() - t0);
+        e->ingested = false;
+        return SID_OK;
+    }
     start_queues(e);
     const int D = (int)e->devs.size();
     // pinned ring per device: 4 x 16 MiB (pinned once, reused by every run)

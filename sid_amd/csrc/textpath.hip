@@ -399,10 +399,18 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
     }
 }
 
+// Zeroes on the way (for the kernels behind it, instead of memset launches):
+// z32[0, n32), z64a[0, 8), z64b[0, 2) when set.
 __global__ __launch_bounds__(TB) void sid_index_emit_kernel(const uint16_t* __restrict__ masks, uint64_t tile_base,
                                                             uint64_t ntiles, const uint64_t* __restrict__ toff,
-                                                            uint64_t* __restrict__ starts)
+                                                            uint64_t* __restrict__ starts,
+                                                            uint32_t* __restrict__ z32 = nullptr, uint64_t n32 = 0,
+                                                            unsigned long long* __restrict__ z64a = nullptr,
+                                                            unsigned long long* __restrict__ z64b = nullptr)
 {
+    for (uint64_t k = (uint64_t)blockIdx.x * TB + threadIdx.x; k < n32; k += (uint64_t)gridDim.x * TB) z32[k] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 8 && z64a) z64a[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 2 && z64b) z64b[threadIdx.x] = 0;
     // blocks stride over the tiles as in the count kernel, the next tile's
     // masks loaded ahead (measured the same as a block per tile: 137 vs 140 us
     // per 2 GiB chunk; the scattered 8-B offset stores set its pace)
@@ -2973,18 +2981,20 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     if (n == 0) return SID_OK;
     const uint64_t t0 = c0 & ~(uint64_t)15;
     const uint64_t ntiles = (c1 - t0 + IX_TILE - 1) / IX_TILE;
-    sid_index_emit_kernel<<<(unsigned)std::min<uint64_t>(ntiles, ix_grid()), TB, 0, st>>>(W->masks, t0, ntiles,
-                                                                                          W->toff, W->starts);
-    if (lctx && !qmode && !parse_coop() && n < (1ull << 32)) {
+    const bool lens = lctx && !qmode && !parse_coop() && n < (1ull << 32);
+    const uint64_t nb = (n + FTB - 1) / FTB;
+    unsigned long long* fbn = (unsigned long long*)(W->state + 6);
+    // (with lens the emit kernel also zeroes the formatter's block sums and
+    // flags and the fallback counts: three memset launches fewer)
+    sid_index_emit_kernel<<<(unsigned)std::min<uint64_t>(ntiles, ix_grid()), TB, 0, st>>>(
+        W->masks, t0, ntiles, W->toff, W->starts, lens ? W->bsum : nullptr, lens ? nb : 0, lens ? W->lb : nullptr,
+        lens ? fbn : nullptr);
+    if (lens) {
         // -m local: the record lengths out of the parse (sid_parse_len_kernel);
         // sid_chunk_local_len then has only the fix-up and the scan left
-        const uint64_t nb = (n + FTB - 1) / FTB;
-        unsigned long long* fbn = (unsigned long long*)(W->state + 6);
+        // (lb: [0] the miss count, [1] bytes, [2] range flag; zeroed above)
         uint32_t* late = W->fb + W->site_cap;
         const LocalLen LL{lctx->ws.len1, lctx->ws.len2, W->bsum, W->fb + 2 * W->site_cap, W->lb};
-        WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));   // [0] the miss count, [1] bytes, [2] range flag
-        WCHECK(hipMemsetAsync(W->bsum, 0, nb * 4, st));
-        WCHECK(hipMemsetAsync(fbn, 0, 2 * sizeof *fbn, st));
         const unsigned pg = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, 16384);
         sid_parse_len_kernel<<<line_walk_grid(n, c1 - c0, pg), TB, 0, st>>>(base, c1, W->starts, W->state + 1,
                                                                             W->counts, W->hdr, W->fb, fbn, LL);
