@@ -1418,7 +1418,13 @@ __device__ __forceinline__ void block_store(const char* buf, uint32_t tot, char*
             v.y = __builtin_amdgcn_alignbyte(x2, x1, r);
             v.z = __builtin_amdgcn_alignbyte(x3, x2, r);
             v.w = __builtin_amdgcn_alignbyte(x4, x3, r);
+#ifdef SID_NT_STORE   // A/B: streaming (non-temporal) stores for the records
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 nv = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(nv, (u32x4*)(dst + k));
+#else
             *(uint4*)(dst + k) = v;
+#endif
         } else {
             for (uint32_t j = k; j < k + 16 && j < span; ++j)
                 if (j >= phase) dst[j] = buf[quad((j - phase) >> 4) * 16 + ((j - phase) & 15u)];
