@@ -228,6 +228,11 @@ __device__ __forceinline__ uint32_t compress8(uint32_t a, uint32_t b)
 }
 // a 16-B load marked non-temporal (streamed data read once: kept out of the
 // caches the data read again needs)
+// the intermediate arrays (line-start masks, line offsets, counts, header
+// pairs: hundreds of MB a chunk, read back once by the next kernel, from HBM
+// in any case) stored non-temporal, out of the way of the text the kernels
+// read (index 0.896 -> 0.877, parse 2.015 -> 2.003 ms per C2 step, A/B)
+#define ST_MID(ptr, val) __builtin_nontemporal_store((val), (ptr))
 __device__ __forceinline__ uint4 ld_nt(const void* p)
 {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -395,7 +400,7 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
             mw |= (uint64_t)m << (16 * k);
             if (LOWM) lowm[(t * IX_SUB + k) * TB + threadIdx.x] = (uint16_t)ix_low(cur[k], at, c0, c1);
         }
-        ((uint64_t*)masks)[t * TB + threadIdx.x] = mw;
+        ST_MID((uint64_t*)masks + t * TB + threadIdx.x, mw);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
         if (lane == 0) red[par][wid] = c;
@@ -447,7 +452,8 @@ __global__ __launch_bounds__(TB) void sid_index_emit_kernel(const uint16_t* __re
             uint32_t mk = m[k];
             while (mk) {
                 const int j = __ffs(mk) - 1;
-                starts[q++] = at + j;
+                ST_MID(starts + q, at + j);
+                ++q;
                 mk &= mk - 1;
             }
             o += (tot >> (16 * k)) & 0xFFFF;
@@ -1600,8 +1606,9 @@ __global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __rest
         if (i < hi) {
             uint64_t c = 0, h[2] = {0, 0};
             if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
-                counts[i] = c;
-                *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h[0], h[1]);
+                ST_MID(counts + i, c);
+                ST_MID(hdr + 2 * i, h[0]);
+                ST_MID(hdr + 2 * i + 1, h[1]);
                 if (h[0] >> 63) {
                     Head hd;
                     hd.clen = (uint32_t)(h[0] >> 32) & 0xFFFu;

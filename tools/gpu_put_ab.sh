@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B: current (build), more single-use reads non-temporal (build_b: masks, read-bases windows)
+# A/B: current (build), intermediate arrays stored non-temporal (build_b)
 
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
