@@ -195,10 +195,11 @@ def fmt_kind(cfg):
     return None if os.environ.get("SID_LYNCH_FUSED", "1") == "0" else "lynch"
 
 
-def parse_len(fused):
+def parse_len(fused, text_per_site=81.0):
     """-m local: the records' lengths computed by the parse (run.cpp,
-    sid_parse_len_kernel; SID_PARSE_LEN=0 keeps the separate length kernel)."""
-    return fused == "local" and os.environ.get("SID_PARSE_LEN", "1") != "0"
+    sid_parse_len_kernel; SID_PARSE_LEN=0 keeps the separate length kernel),
+    for lines of up to 256 bytes (textpath.hip sid_chunk_parse)."""
+    return fused == "local" and os.environ.get("SID_PARSE_LEN", "1") != "0" and text_per_site <= 256
 
 
 def stage_bytes(stage, text_per_site, csv_per_site, fused):
@@ -208,7 +209,7 @@ def stage_bytes(stage, text_per_site, csv_per_site, fused):
     parse_len the length stage has only the fix-up and the block-sum scan
     left (4 B per 512 sites, read and written)."""
     site_in = 8 if fused else 17
-    if stage == "fmt_len" and parse_len(fused):
+    if stage == "fmt_len" and parse_len(fused, text_per_site):
         return 2 * 4 / 512 + 8 / 512
     return {
         "index": text_per_site + text_per_site / 8,    # text read once, line-start masks written
@@ -226,15 +227,16 @@ def stage_bytes(stage, text_per_site, csv_per_site, fused):
     }[stage]
 
 
-def stage_kernels(stage, fused):
+def stage_kernels(stage, fused, text_per_site=81.0):
+    pl = parse_len(fused, text_per_site)
     return {
         "index": ["sid_index_count_kernel", "sid_scan_*"],
         "parse": ["sid_index_emit_kernel"] + (["sid_parse_len_kernel", "sid_parse_serial_kernel",
-                                                 "sid_local_len_list_kernel"] if parse_len(fused)
+                                                 "sid_local_len_list_kernel"] if pl
                                                 else ["sid_parse_kernel", "sid_parse_serial_kernel"]),
         "call": ["sid_lookup_rec_kernel"],
         "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
-        "fmt_len": {"local": (["sid_local_fixlen_kernel"] if parse_len(fused) else
+        "fmt_len": {"local": (["sid_local_fixlen_kernel"] if pl else
                               ["sid_local_len_kernel", "sid_local_fixlen_kernel"]),
                     "lynch": ["sid_lynch_len_kernel"]}.get(fused, ["sid_fmt_blen_kernel"]) + ["sid_scan_*"],
         "fmt_write": {"local": ["sid_local_put_kernel"], "lynch": ["sid_lynch_put_kernel"]}.get(
@@ -489,9 +491,9 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
     d = roofs[dom]
     roofline = {"bound": "hbm", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": d["frac"], "traffic": pmc_traffic(dom, per_launch_sites),
-                "kernel": f"engine stage '{dom}'", "stage_kernels": stage_kernels(dom, fused),
+                "kernel": f"engine stage '{dom}'", "stage_kernels": stage_kernels(dom, fused, tps),
                 "launch_ms": d["launch_ms"], "sites_per_launch": per_launch_sites, "bytes_per_site": d["bytes_per_site"],
-                "valu": valu_issue(dom, per_launch_sites, d["launch_ms"], stage_kernels(dom, fused)),
+                "valu": valu_issue(dom, per_launch_sites, d["launch_ms"], stage_kernels(dom, fused, tps)),
                 "source": "device_path: HIP event pairs around each engine stage on the compute stream"}
     return {"sites_per_s": sites_all * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
             "stages_ms": stages, "stage_roofline": roofs, "roofline": roofline,

@@ -3004,7 +3004,10 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     if (n == 0) return SID_OK;
     const uint64_t t0 = c0 & ~(uint64_t)15;
     const uint64_t ntiles = (c1 - t0 + IX_TILE - 1) / IX_TILE;
-    const bool lens = lctx && !qmode && !parse_coop() && n < (1ull << 32);
+    // (not for long lines: at 200x the parse runs on a small grid (line_walk_grid),
+    // where the fused kernel's register cap costs more than the length kernel:
+    // C5 parse + lengths 145 vs 141 ms)
+    const bool lens = lctx && !qmode && !parse_coop() && n < (1ull << 32) && (c1 - c0) <= 256 * n;
     const uint64_t nb = (n + FTB - 1) / FTB;
     unsigned long long* fbn = (unsigned long long*)(W->state + 6);
     // (with lens the emit kernel also zeroes the formatter's block sums and
