@@ -728,21 +728,27 @@ def bench_cli(cfg, text, ln, n):
         cli_runs = []
         for _ in range(3):
             with open(os.devnull, "wb") as dn:
+                u0 = time.time()
                 t0 = time.perf_counter()
                 r = subprocess.run([cli, "--stats"] + flags + [path], stdout=dn, stderr=subprocess.PIPE)
                 dt = time.perf_counter() - t0
+                u1 = time.time()
             if r.returncode != 0:
                 return {"error": r.returncode, "stderr": r.stderr.decode()[-400:]}
             try:
                 stt = json.loads(r.stderr.decode().strip().splitlines()[-1])
             except Exception:
                 stt = {}
+            if "main_entry_unix" in stt:   # the process's start-up (exec, loading) and teardown, apart
+                stt["startup_s"] = stt["main_entry_unix"] - u0
+                stt["teardown_s"] = u1 - stt["main_exit_unix"]
             cli_runs.append((dt, stt))
         dt, stt = min(cli_runs[1:], key=lambda x: x[0])
         return {"wall_s": dt, "sites_per_s_wall": n / dt, "sites_per_s_cli_clock": stt.get("sites_per_s"),
                 "wall_s_runs": [x[0] for x in cli_runs], "cli_stats": stt,
                 "note": "build/sid FILE > /dev/null, one GPU: wall = process start + HIP init + mmap + "
-                        "H2D + parse/call/format + D2H + write; cli_clock = input mapping to last write"}
+                        "H2D + parse/call/format + D2H + write; cli_clock = input mapping to last write; "
+                        "startup_s = exec to main(), teardown_s = main's last line to the exit seen here"}
 
 
 def write_text_file(text, ln, path):

@@ -107,6 +107,26 @@ double now()
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// wall-clock seconds (--stats: main's entry and exit, so a caller timing the
+// process can split off the start-up and the teardown)
+double unix_now()
+{
+    return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+// The end of a successful run: stdout and stderr flushed, then the process
+// ends without the HIP runtime's teardown (the kernel driver releases the
+// HBM, the pinned pages and the mapping with the process either way).
+// SID_EXIT=normal: exit() with the runtime's static destructors instead (A/B).
+[[noreturn]] void finish(int code)
+{
+    std::fflush(stdout);
+    std::fflush(stderr);
+    static const char* mode = std::getenv("SID_EXIT");
+    if (mode && std::strcmp(mode, "normal") == 0) std::exit(code);
+    ::_exit(code);
+}
+
 struct Input {
     const char* data = nullptr;   // the text in memory (pipes, or mapped for --host-parse)
     size_t len = 0;
@@ -177,6 +197,7 @@ struct Shard {
 
 int main(int argc, char** argv)
 {
+    const double t_entry = unix_now();
     // host<->device copies on the copy engines (set before the HIP runtime
     // starts; an explicit setting in the environment wins): with the
     // runtime's default, device->host ran at 30 GB/s, with SDMA at ~57 GB/s
@@ -353,14 +374,14 @@ int main(int argc, char** argv)
                          "\"create_s\": %.6f, \"parse_s\": %.6f, \"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, "
                          "\"sites_per_s\": %.1f, \"chunks\": %llu, \"chunks_held\": %llu, "
                          "\"chunks_retained\": %llu, \"chunks_reloaded\": %llu, \"bytes_in\": %llu, "
-                         "\"bytes_out\": %llu}\n",
+                         "\"bytes_out\": %llu, \"main_entry_unix\": %.6f, \"main_exit_unix\": %.6f}\n",
                          (unsigned long long)st.sites, D, T, tc - t0, t1 - t0, t2 - t1, t3 - t2, t3 - t0,
                          st.sites / std::max(1e-9, t3 - t0), (unsigned long long)st.chunks,
                          (unsigned long long)st.chunks_held, (unsigned long long)st.chunks_retained,
                          (unsigned long long)st.chunks_reloaded, (unsigned long long)st.bytes_in,
-                         (unsigned long long)st.bytes_out);
+                         (unsigned long long)st.bytes_out, t_entry, unix_now());
         // device memory, pinned staging and the mapping go with the process
-        return 0;
+        finish(0);
     }
 
     // ------------------------------------------------------ host-parse path --
@@ -521,11 +542,12 @@ int main(int argc, char** argv)
     if (opt.stats) {
         std::fprintf(stderr,
                      "{\"sites\": %zu, \"devices\": %d, \"threads\": %d, \"path\": \"%s\", \"parse_s\": %.6f, "
-                     "\"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, \"sites_per_s\": %.1f}\n",
+                     "\"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, \"sites_per_s\": %.1f, "
+                     "\"main_entry_unix\": %.6f, \"main_exit_unix\": %.6f}\n",
                      n, D, T, "host", t1 - t0, t2 - t1, t3 - t2, t3 - t0,
-                     n / std::max(1e-9, t3 - t0));
+                     n / std::max(1e-9, t3 - t0), t_entry, unix_now());
     }
     // device memory, pinned staging and mappings go with the process: freeing
     // gigabytes of HBM and pinned host memory one by one only delays the exit
-    return 0;
+    finish(0);
 }
