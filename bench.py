@@ -209,8 +209,14 @@ def stage_bytes(stage, text_per_site, csv_per_site, fused):
     parse_len the length stage has only the fix-up and the block-sum scan
     left (4 B per 512 sites, read and written)."""
     site_in = 8 if fused else 17
-    if stage == "fmt_len" and parse_len(fused, text_per_site):
+    pl = parse_len(fused, text_per_site)
+    if stage == "fmt_len" and pl:
         return 2 * 4 / 512 + 8 / 512
+    if pl and stage in ("parse", "fmt_write"):
+        # the fused parse writes each site's 4 B class word instead of its 8 B
+        # counts (textpath.hip local_word), which the writer reads instead
+        return {"parse": text_per_site + text_per_site / 8 + 8 + 4 + 16,
+                "fmt_write": 4 + 16 + csv_per_site}[stage]
     return {
         "index": text_per_site + text_per_site / 8,    # text read once, line-start masks written
         # text read; line-start masks (1/8 of the text) and offsets read back;

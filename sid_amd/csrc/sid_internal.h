@@ -137,6 +137,10 @@ struct sid_chunk_ws {
                                   // general routine parsed for the fused -m local lengths ([7]); the
                                   // -m local fix-up's sites (lb[0])
     bool lens_ready = false;      // the parse computed the -m local record lengths (sid_chunk_parse lctx)
+    uint32_t* cls = nullptr;      // with lens_ready: per site its -m local class word (the table entry and the
+                                  // major / minor bases, or SID_CLS_MISS); the counts are then written only for
+                                  // the fix-up's sites
+    bool cls_ready = false;       // cls holds this chunk's words (set by the parse, read by sid_chunk_local_put)
     uint8_t* code = nullptr;
     double* hom = nullptr;
     double* het = nullptr;

@@ -1552,7 +1552,26 @@ struct LocalLen {
     uint32_t* bsum;                 // per FTB-site block: record bytes (zeroed before)
     uint32_t* miss;                 // sites for sid_local_fixlen_kernel
     unsigned long long* nmiss;
+    uint32_t* cls;                  // per site its class word (sid_local_word)
 };
+
+// The -m local class word of a tabulated site, for the writer: the class-
+// table entry (< 2^20) in bits 0-19, the major base in bits 28-29, the minor
+// in 30-31.  SID_CLS_MISS (bits 20-27 set: no entry has them): the fix-up's
+// site, whose record comes from its code and confidences.  The writer then
+// reads 4 B a site instead of the 8 B counts, and skips getMajorAlleleIndices.
+constexpr uint32_t SID_CLS_MISS = 0xFFFFFFFFu;
+#ifndef SID_CLS_NT
+#define SID_CLS_NT 0   // 1: the class words stored non-temporal, as the counts were (A/B)
+#endif
+static_assert(SID_TAB_N + SID_TAB2_N <= (1u << 20), "class entries fit the word's 20 bits");
+__device__ __forceinline__ uint32_t local_word(uint32_t k, uint32_t f, uint32_t s)
+{
+    return k | (f << 28) | (s << 30);
+}
+
+// The site's record length (0: a fix-up site, listed in LL.miss; a record
+// is never empty) and its class word into LL.cls[i]
 __device__ __forceinline__ int local_site_len(const Head& h, uint64_t c, uint64_t i, const uint8_t* L1,
                                               const LocalLen& LL)
 {
@@ -1560,7 +1579,13 @@ __device__ __forceinline__ int local_site_len(const Head& h, uint64_t c, uint64_
     sid_major(c, f, s, nf, ns, cov);
     const uint32_t k = local_entry(nf, ns, cov - nf - ns);
     const uint32_t L = k < SID_TAB_N ? L1[k] : k != UINT32_MAX ? LL.len2[k - SID_TAB_N] : 0xFFu;
-    if (L == 0xFFu) {
+    const bool miss = L == 0xFFu;
+#if SID_CLS_NT
+    ST_MID(LL.cls + i, miss ? SID_CLS_MISS : local_word(k, f, s));
+#else
+    LL.cls[i] = miss ? SID_CLS_MISS : local_word(k, f, s);   // (read back by the writer soon: through the caches)
+#endif
+    if (miss) {
         LL.miss[atomicAdd(LL.nmiss, 1ull)] = (uint32_t)i;   // its bytes: the fix-up's
         return 0;
     }
@@ -1606,7 +1631,6 @@ __global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __rest
         if (i < hi) {
             uint64_t c = 0, h[2] = {0, 0};
             if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
-                ST_MID(counts + i, c);
                 ST_MID(hdr + 2 * i, h[0]);
                 ST_MID(hdr + 2 * i + 1, h[1]);
                 if (h[0] >> 63) {
@@ -1617,6 +1641,7 @@ __global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __rest
                 } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
                     l = local_site_len_text(text, len, s0, c, i - lo, LL);
                 }
+                if (l == 0) counts[i] = c;   // a fix-up site: the fix-up reads its counts (the writer, the class word)
             } else {
                 fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
             }
@@ -1880,10 +1905,14 @@ __device__ __noinline__ void miss_put(const char* text, uint64_t len, Head h, ui
     record_put(R, h, c, sid_g6_prep(hm), sid_g6_prep(ht), ct, out);
 }
 
+// CLS: the sites' class words from the fused parse (W->cls) stand in for
+// their counts (the entry and the bases come with the word)
+template <bool CLS>
 __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const char* __restrict__ text, uint64_t len,
                                                            const uint64_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ hdr, uint64_t n,
                                                            const uint64_t* __restrict__ counts,
+                                                           const uint32_t* __restrict__ cwords,
                                                            const char* __restrict__ str1,
                                                            const char* __restrict__ str2,
                                                            const uint8_t* __restrict__ code,
@@ -1904,9 +1933,17 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     bool tab = false;
     uint8_t c = 0;
     if (i < n) {
-        uint32_t nf, ns, cov;
-        sid_major(counts[i], f, s, nf, ns, cov);
-        const uint32_t k = local_entry(nf, ns, cov - nf - ns);
+        uint32_t k;
+        if (CLS) {
+            const uint32_t w = cwords[i];
+            k = w == SID_CLS_MISS ? UINT32_MAX : w & 0xFFFFFu;
+            f = (w >> 28) & 3u;
+            s = w >> 30;
+        } else {
+            uint32_t nf, ns, cov;
+            sid_major(counts[i], f, s, nf, ns, cov);
+            k = local_entry(nf, ns, cov - nf - ns);
+        }
         {
             Reader R{text, len};
             h = site_head(R, starts + i, hdr + 2 * i);
@@ -2922,9 +2959,10 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
     if (sites > W->site_cap) {
         const uint64_t m = std::max<uint64_t>(sites, W->site_cap + W->site_cap / 2);
         for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
-                        (void*)W->bsum, (void*)W->boff, (void*)W->hdr, (void*)W->fb, (void*)W->lb})
+                        (void*)W->bsum, (void*)W->boff, (void*)W->hdr, (void*)W->fb, (void*)W->lb, (void*)W->cls})
             if (p) (void)hipFree(p);
         W->lb = nullptr;
+        W->cls = nullptr;
         W->starts = W->counts = W->hdr = nullptr;
         W->fb = nullptr;
         W->code = nullptr;
@@ -2935,6 +2973,7 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         const uint64_t nb = (m + TB - 1) / TB + 1;
         WCHECK(hipMalloc(&W->starts, m * 8));
         WCHECK(hipMalloc(&W->counts, m * 8));
+        WCHECK(hipMalloc(&W->cls, m * 4));
         WCHECK(hipMalloc(&W->hdr, m * 16));
         WCHECK(hipMalloc(&W->fb, m * 12));   // three site lists (sid_chunk_ws::fb)
         WCHECK(hipMalloc(&W->code, m));
@@ -2952,7 +2991,7 @@ void sid_chunk_release(sid_chunk_ws* W)
 {
     for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
                     (void*)W->bsum, (void*)W->boff, (void*)W->tcnt, (void*)W->toff, (void*)W->state,
-                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb, (void*)W->lowm})
+                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb, (void*)W->lowm, (void*)W->cls})
         if (p) (void)hipFree(p);
     *W = sid_chunk_ws{};
 }
@@ -3000,6 +3039,7 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
                     hipStream_t st, const sid_ctx* lctx)
 {
     W->lens_ready = false;
+    W->cls_ready = false;
     if (n > W->site_cap) return SID_EINVAL;
     if (n == 0) return SID_OK;
     const uint64_t t0 = c0 & ~(uint64_t)15;
@@ -3020,7 +3060,7 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
         // sid_chunk_local_len then has only the fix-up and the scan left
         // (lb: [0] the miss count, [1] bytes, [2] range flag; zeroed above)
         uint32_t* late = W->fb + W->site_cap;
-        const LocalLen LL{lctx->ws.len1, lctx->ws.len2, W->bsum, W->fb + 2 * W->site_cap, W->lb};
+        const LocalLen LL{lctx->ws.len1, lctx->ws.len2, W->bsum, W->fb + 2 * W->site_cap, W->lb, W->cls};
         const unsigned pg = (unsigned)std::min<uint64_t>((n + TB - 1) / TB, 16384);
         sid_parse_len_kernel<<<line_walk_grid(n, c1 - c0, pg), TB, 0, st>>>(base, c1, W->starts, W->state + 1,
                                                                             W->counts, W->hdr, W->fb, fbn, LL);
@@ -3028,6 +3068,7 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
                                                     fbn, (unsigned long long*)(W->state + 4), 0, late, fbn + 1);
         sid_local_len_list_kernel<<<64, TB, 0, st>>>(base, c1, W->starts, W->hdr, W->counts, late, fbn + 1, LL);
         W->lens_ready = true;
+        W->cls_ready = true;
     } else if (qmode || !parse_coop()) {
         launch_parse(base, c1, W->starts, W->state + 1, n, W->counts, W->hdr, W->fb,
                      (unsigned long long*)(W->state + 6), (unsigned long long*)(W->state + 4), qmode, st);
@@ -3144,9 +3185,14 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
     const uint64_t nb = (n + FTB - 1) / FTB;
     if (nb == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
                             ? SID_OK : SID_EHIP;
-    sid_local_put_kernel<<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, ctx->ws.str1,
-                                                      ctx->ws.str2, W->code, W->hom, W->het, ct, W->boff, W->state,
-                                                      W->lb, out);
+    if (W->cls_ready)
+        sid_local_put_kernel<true><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, W->cls,
+                                                                ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
+                                                                ct, W->boff, W->state, W->lb, out);
+    else
+        sid_local_put_kernel<false><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, nullptr,
+                                                                 ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
+                                                                 ct, W->boff, W->state, W->lb, out);
     WCHECK(hipGetLastError());
     return SID_OK;
 }
