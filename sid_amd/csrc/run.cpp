@@ -779,21 +779,6 @@ namespace {
 
 bool needs_format_pass1(const sid_engine* e) { return !e->lynch; }
 
-// The records' device -> pinned host copies.  hipMemcpyDeviceToHost is
-// carried out by a blit kernel on the CUs (rocprofv3: __amd_rocclr_copyBuffer,
-// 1.4 ms per 128 MiB chunk's records), which slowed the compute kernels
-// beside it (the line index's emit 0.1 -> 1.2 ms a chunk); the pinned host
-// arena is mapped for the device, so the copy can go as a device-to-device
-// copy without compute units (a copy engine).  SID_D2H_NOCU=0/1 (A/B).
-hipMemcpyKind d2h_kind()
-{
-    static const hipMemcpyKind k = [] {
-        const char* v = std::getenv("SID_D2H_NOCU");
-        return v && std::atoi(v) != 0 ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToHost;
-    }();
-    return k;
-}
-
 // the uploader of device d: the chunks of `list` into device buffers, in order
 void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass)
 {
@@ -1225,7 +1210,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                 x = hipEventRecord(ev, d.s_comp);
                 if (x == hipSuccess) x = hipStreamWaitEvent(d.s_d2h, ev, 0);
                 d.give_event(ev);
-                if (x == hipSuccess && bytes) x = hipMemcpyAsync(hp, out, bytes, d2h_kind(), d.s_d2h);
+                if (x == hipSuccess && bytes) x = hipMemcpyAsync(hp, out, bytes, hipMemcpyDeviceToHost, d.s_d2h);
                 if (x != hipSuccess) return (void)hipfail(e, x);
                 d.pool.put(out, cap, d.s_d2h);   // reusable once the copy is done
                 r.host = hp;
@@ -1302,7 +1287,7 @@ void drain(sid_engine* e, Dev& d)
         if (char* hp = d.hh_take(it.len)) {   // the whole chunk into the host arena, one copy
             hipEvent_t ev = d.take_event();
             if (!ev) return (void)fail(e, SID_EHIP);
-            x = hipMemcpyAsync(hp, it.buf, it.len, d2h_kind(), d.s_d2h);
+            x = hipMemcpyAsync(hp, it.buf, it.len, hipMemcpyDeviceToHost, d.s_d2h);
             if (x == hipSuccess) x = hipEventRecord(ev, d.s_d2h);
             if (x != hipSuccess) return (void)hipfail(e, x);
             e->recs[it.j].host = hp;
@@ -1322,7 +1307,7 @@ void drain(sid_engine* e, Dev& d)
             int ps;
             if (!d.free_pinned.pop(ps)) return;
             const uint64_t m = std::min<uint64_t>(d.pinned_cap, it.len - o);
-            x = hipMemcpyAsync(d.pinned[ps], it.buf + o, m, d2h_kind(), d.s_d2h);
+            x = hipMemcpyAsync(d.pinned[ps], it.buf + o, m, hipMemcpyDeviceToHost, d.s_d2h);
             if (x == hipSuccess) x = hipEventRecord(d.pinned_ev[ps], d.s_d2h);
             if (x != hipSuccess) return (void)hipfail(e, x);
             o += m;
