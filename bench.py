@@ -98,6 +98,10 @@ def parse_args(argv=None):
     p.add_argument("--allow-shared-gpu", action="store_true",
                    help="rehearsal: more ranks than GPUs share them round-robin")
     p.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL)")
+    p.add_argument("--dump-records", default=None, metavar="DIR",
+                   help="after the timed PCIe leg (C2/C3): each rank writes its records (file order) to "
+                        "DIR/rank<r>.csv and its estimate to DIR/rank<r>.json (parity tests)")
+    p.add_argument("--no-node-cli", action="store_true", help="N > 1: skip the whole-node CLI leg")
     p.add_argument("--stream", action="store_true",
                    help="C4/C5: generate the text on the device chunk by chunk inside the step, even when the "
                         "rank's shard would fit in HBM")
@@ -269,6 +273,7 @@ class Rank:
         self.gpu = self.local_rank % ndev
         torch.cuda.set_device(self.gpu)
         self.dev = torch.device("cuda", self.gpu)
+        self.cpus0 = os.sched_getaffinity(0)   # before the NUMA binding (the node CLI leg runs unbound)
         self.numa = numa_bind(torch, self.gpu)
         self.dist = None
         self.backend = None
@@ -394,9 +399,24 @@ def bench_weak(R, a, cfg):
     elapsed, (st, st2, est) = R.timed(lambda: R.run_step(eng, lynch), a.steps, a.warmup)
     elapsed = R.max_over_ranks([elapsed])[0]
     sites_all = R.sum_over_ranks(st.sites)
-    # the same records in host memory as the CLI writes (spot check)
     if st2.bytes_out == 0 and st.sites:
         raise SystemExit("bench.py: no records came back")
+    # the first chunk's records from the host arena, for the cpu_baseline
+    # leg's spot check against the oracle (-m local: the records of a prefix
+    # of the text do not depend on the rest)
+    spot = eng.records_bytes(1) if not lynch else None
+    if a.dump_records:
+        os.makedirs(a.dump_records, exist_ok=True)
+        with open(os.path.join(a.dump_records, f"rank{R.rank}.csv"), "wb") as f:
+            for j in range(st.chunks):
+                p, m = eng.records(j)
+                if m:
+                    f.write(__import__("ctypes").string_at(p, m))
+        with open(os.path.join(a.dump_records, f"rank{R.rank}.json"), "w") as f:
+            json.dump({"rank": R.rank, "world": R.world, "sites": st.sites, "first_site": first,
+                       "pi": est.heterozygosity if lynch else None, "eps": est.error_rate if lynch else None,
+                       "iterations": est.iterations if lynch else None,
+                       "n_unique": est.n_unique if lynch else None}, f)
     pcie = {"text_bytes": ln, "csv_bytes": st2.bytes_out,
             "GBps_h2d": ln / (elapsed / a.steps) / 1e9, "GBps_d2h": st2.bytes_out / (elapsed / a.steps) / 1e9,
             "chunks": st.chunks, "chunks_held_in_host_arena": st.chunks_held, "ingest_s": st.ingest_s,
@@ -406,6 +426,11 @@ def bench_weak(R, a, cfg):
     del host
 
     dp = device_path(R, a, cfg, text, ln, lynch)
+    node_cli = None
+    if R.world > 1 and not a.no_extras and not a.no_node_cli:
+        holder = [text]
+        text = None   # the rank's text is freed before the CLI takes the GPUs (the N = 1 extras do not run)
+        node_cli = bench_cli_node(R, cfg, holder, ln, n)
     out = {
         "metric": METRIC,
         "value": sites_all * a.steps / elapsed,
@@ -439,22 +464,37 @@ def bench_weak(R, a, cfg):
     if lynch:
         out["estimate"] = {"pi": est.heterozygosity, "eps": est.error_rate, "iterations": est.iterations,
                            "n_unique": est.n_unique}
+    if node_cli is not None:
+        out["cli"] = node_cli
     if R.world == 1 and not a.no_extras:
         out["kernel_local"] = bench_kernel_local(torch, R.dev, cfg, n)
         out["cli"] = bench_cli(cfg, text, ln, n)
         if not a.no_cpu:
-            out["cpu_baseline"] = bench_cpu(cfg, text, ln, n)
+            out["cpu_baseline"] = bench_cpu(cfg, text, ln, n, spot=spot)
     return out, []
+
+
+# C4 / C5 with the rank's shard resident in HBM: 1 GiB chunks (2 GiB chunks'
+# record bounds and hold arena overran the HBM the text leaves on one GPU)
+STRONG_RESIDENT_CHUNK_MIB = 1024
+
+
+def device_engine(cfg, gpu, chunk_mib, device_sink=1, **kw):
+    """The engine of the device path (text in HBM): one device, chunk_mib MiB
+    chunks (0 = the engine's 2 GiB default for resident text), records left in
+    HBM (device_sink 1).  tests/test_benchpath_gpu.py builds the same engine
+    with device_sink 0 to read the records back."""
+    import sid_amd
+    return sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=gpu,
+                          chunk_bytes=chunk_mib << 20, device_sink=device_sink, **kw)
 
 
 def device_path(R, a, cfg, text, ln, lynch, gen=None):
     """The same sid run over text resident in HBM, records left in HBM, with
     HIP event pairs around every engine stage on the compute stream: the
     kernels' own rate and the roofline of the dominant stage."""
-    import sid_amd
     steps = a.device_steps or max(a.steps, 10)
-    eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=R.gpu,
-                         chunk_bytes=a.chunk_mib << 20, device_sink=1)
+    eng = device_engine(cfg, R.gpu, a.chunk_mib)
     if gen is None:
         eng.source_device_text(text.data_ptr(), ln, keep=text)
     else:
@@ -528,8 +568,8 @@ def bench_strong(R, a, cfg):
         t0 = time.perf_counter()
         text, ln = generate_resident(torch, sid_amd, R.dev, R.gpu, cfg, first, n)
         gen_ms = (time.perf_counter() - t0) * 1e3
-        if not a.chunk_mib:   # 2 GiB chunks' record bounds and hold arena overran the HBM the text leaves (C4, 1 GPU)
-            a.chunk_mib = 1024
+        if not a.chunk_mib:
+            a.chunk_mib = STRONG_RESIDENT_CHUNK_MIB
         dp = device_path(R, a, cfg, text, ln, False)
     else:
         dp = device_path(R, a, cfg, None, None, False, gen=(first, n))
@@ -732,7 +772,7 @@ def bench_cli(cfg, text, ln, n):
         write_text_file(text, ln, path)
         flags = [] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) + ["-m", cfg["method"]]
         cli_runs = []
-        for _ in range(3):
+        for _ in range(6):   # the first warms the page cache and the code objects; the median of the other 5
             with open(os.devnull, "wb") as dn:
                 u0 = time.time()
                 t0 = time.perf_counter()
@@ -749,12 +789,106 @@ def bench_cli(cfg, text, ln, n):
                 stt["startup_s"] = stt["main_entry_unix"] - u0
                 stt["teardown_s"] = u1 - stt["main_exit_unix"]
             cli_runs.append((dt, stt))
-        dt, stt = min(cli_runs[1:], key=lambda x: x[0])
-        return {"wall_s": dt, "sites_per_s_wall": n / dt, "sites_per_s_cli_clock": stt.get("sites_per_s"),
+        dt, stt = sorted(cli_runs[1:], key=lambda x: x[0])[len(cli_runs[1:]) // 2]
+        return {"wall_s": dt, "wall_s_is": "median of 5 runs after one warm-up",
+                "sites_per_s_wall": n / dt, "sites_per_s_cli_clock": stt.get("sites_per_s"),
                 "wall_s_runs": [x[0] for x in cli_runs], "cli_stats": stt,
                 "note": "build/sid FILE > /dev/null, one GPU: wall = process start + HIP init + mmap + "
                         "H2D + parse/call/format + D2H + write; cli_clock = input mapping to last write; "
                         "startup_s = exec to main(), teardown_s = main's last line to the exit seen here"}
+
+
+def bench_cli_node(R, cfg, holder, ln, n):
+    """N > 1: the drop-in over the whole node.  Every rank writes its text
+    into one file (the shards in rank order, each at its byte offset), frees
+    its GPU memory and waits on the store (no collective runs on the GPUs
+    meanwhile); rank 0 runs `build/sid --devices N --stats FILE > /dev/null`
+    (one mapping, one uploader per device, chunks dealt round robin, one
+    ordered writer: main.cpp, run.cpp) -- one warm-up, then the median of 3.
+    The reference's whole-node shape is one sid process per chromosome
+    (scripts/sid-pipeline/parallel-run-sid.sh:2); this is one process over
+    every GPU."""
+    import shutil
+    from datetime import timedelta
+    torch, dist = R.torch, R.dist
+    cli = os.path.join(ROOT, "build", "sid")
+    lens = [None] * R.world
+    dist.all_gather_object(lens, int(ln))
+    total = sum(lens)
+    info = [None]
+    if R.rank == 0 and os.path.exists(cli):
+        for cand in (tempfile.gettempdir(), "/dev/shm"):
+            try:
+                if shutil.disk_usage(cand).free > total + (8 << 30):
+                    d = tempfile.mkdtemp(prefix="sid_node_", dir=cand)
+                    path = os.path.join(d, "node.plp")
+                    with open(path, "wb") as f:
+                        f.truncate(total)
+                    info = [path]
+                    break
+            except OSError:
+                pass
+    dist.broadcast_object_list(info, 0)
+    path = info[0]
+    text = holder.pop()
+    if path is not None:
+        t0 = time.perf_counter()
+        fd = os.open(path, os.O_WRONLY)
+        off, step = sum(lens[:R.rank]), 256 << 20
+        for lo in range(0, ln, step):
+            os.pwrite(fd, text[lo:min(ln, lo + step)].cpu().numpy().tobytes(), off + lo)
+        os.close(fd)
+        write_s = time.perf_counter() - t0
+    del text
+    torch.cuda.synchronize(R.dev)
+    torch.cuda.empty_cache()
+    torch._C._host_emptyCache()
+    dist.barrier()
+    if path is None:
+        return {"skipped": f"build/sid missing or no directory with {total / 1e9:.1f} GB free"}
+    store = dist.distributed_c10d._get_default_store()
+    res = None
+    if R.rank == 0:
+        try:
+            env = dict(os.environ)
+            runs = []
+            for _ in range(4):
+                with open(os.devnull, "wb") as dn:
+                    t0 = time.perf_counter()
+                    r = subprocess.run([cli, "--stats", "--devices", str(R.world)] +
+                                       ([] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) +
+                                        ["-m", cfg["method"]]) + [path],
+                                       stdout=dn, stderr=subprocess.PIPE, env=env,
+                                       preexec_fn=lambda: os.sched_setaffinity(0, R.cpus0))
+                    dt = time.perf_counter() - t0
+                if r.returncode != 0:
+                    res = {"error": r.returncode, "stderr": r.stderr.decode()[-400:]}
+                    break
+                try:
+                    stt = json.loads(r.stderr.decode().strip().splitlines()[-1])
+                except Exception:
+                    stt = {}
+                runs.append((dt, stt))
+            if res is None:
+                dt, stt = sorted(runs[1:], key=lambda x: x[0])[len(runs[1:]) // 2]
+                sites = n * R.world
+                res = {"devices": R.world, "sites": sites, "text_bytes": total, "wall_s": dt,
+                       "wall_s_is": "median of 3 runs after one warm-up", "sites_per_s_wall": sites / dt,
+                       "sites_per_s_cli_clock": stt.get("sites_per_s"), "wall_s_runs": [x[0] for x in runs],
+                       "cli_stats": stt, "file_write_s_rank0": write_s,
+                       "note": f"build/sid --devices {R.world} FILE > /dev/null on one file holding every "
+                               "rank's shard (the whole node's drop-in: one process, every GPU); wall = "
+                               "process start + HIP init + mapping + H2D + kernels + D2H + write"}
+        finally:
+            store.set("sid_node_cli_done", "1")
+            try:
+                shutil.rmtree(os.path.dirname(path))
+            except OSError:
+                pass
+    else:
+        store.wait(["sid_node_cli_done"], timedelta(minutes=15))
+    dist.barrier()
+    return res
 
 
 def write_text_file(text, ln, path):
@@ -778,11 +912,33 @@ def cpu_model():
     return None
 
 
-def bench_cpu(cfg, text, ln, n):
+def cut_after_lines(host, m):
+    """Byte offset just past the first m lines of host (a uint8 array)."""
+    cut, need = 0, m
+    while need > 0:
+        seg = host[cut:cut + (64 << 20)].tobytes()
+        nl = seg.count(b"\n")
+        if nl < need:
+            cut += len(seg)
+            need -= nl
+            if not seg:
+                break
+        else:
+            idx = -1
+            for _ in range(need):
+                idx = seg.find(b"\n", idx + 1)
+            cut += idx + 1
+            need = 0
+    return cut
+
+
+def bench_cpu(cfg, text, ln, n, spot=None):
     """The oracle CLI (reference sid.cpp/call.cpp/lynch/stats restated in C,
     single-threaded) on the same text: 16 line-aligned shard processes over
     all n sites (-m local: sites are independent; the GPU box's CPU share is
-    16 cores), and one process on the first 4M sites."""
+    16 cores), and one process on the first 4M sites.  spot: the timed PCIe
+    leg's first chunk of records (from the engine's host arena), checked
+    byte for byte against the oracle's CSV of the same lines (untimed)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     if not os.path.exists(oracle.CLI):
@@ -816,20 +972,7 @@ def bench_cpu(cfg, text, ln, n):
                                   f"shards, one oracle/_build/sid_oracle process each, CSV to /dev/null, wall"})
         # one core on the first 4M sites
         m = min(n, 4_000_000)
-        cut = 0
-        need = m
-        while need > 0:
-            nl = host[cut:cut + (64 << 20)].tobytes().count(b"\n")
-            if nl <= need:
-                cut += 64 << 20
-                need -= nl
-            else:
-                seg = host[cut:cut + (64 << 20)].tobytes()
-                idx = -1
-                for _ in range(need):
-                    idx = seg.find(b"\n", idx + 1)
-                cut += idx + 1
-                need = 0
+        cut = cut_after_lines(host, m)
         one = os.path.join(td, "one.plp")
         with open(one, "wb") as f:
             f.write(host[:cut].tobytes())
@@ -844,6 +987,19 @@ def bench_cpu(cfg, text, ln, n):
             res["sample"] = single["sample"]
         else:
             res["single_core"] = single
+        if spot is not None:   # the checker: the value's own records against the oracle's
+            k = spot.count(b"\n")
+            pre = os.path.join(td, "spot.plp")
+            with open(pre, "wb") as f:
+                f.write(host[:cut_after_lines(host, k)].tobytes())
+            r = subprocess.run([oracle.CLI] + flags + [pre], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+            want = r.stdout
+            got = b"chrom,pos,label,gt,hom_conf,het_conf,conf_type\n" + spot
+            res["spot_check"] = {"sites": k, "bytes": len(spot), "equal": r.returncode == 0 and got == want,
+                                 "what": "the timed PCIe leg's first chunk of records (engine host arena) vs "
+                                         "the oracle CLI over the same lines"}
+            if not res["spot_check"]["equal"]:
+                raise SystemExit("bench.py: the value's records differ from the oracle's (spot check)")
     return res
 
 

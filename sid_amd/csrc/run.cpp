@@ -130,7 +130,13 @@ public:
         }
         const uint64_t c = (need + PAD + (4u << 20) - 1) & ~(uint64_t)((4u << 20) - 1);
         char* p = nullptr;
-        if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+        if (hipMalloc(&p, c) != hipSuccess) {
+            // the caller falls back (ring slot, pass 2, arena): clear the
+            // runtime's sticky last error, or the next launch check on this
+            // thread (hipGetLastError) reports this failed allocation
+            (void)hipGetLastError();
+            return nullptr;
+        }
         all_.push_back(p);
         bytes_ += c;
         *cap = c;
@@ -269,7 +275,10 @@ struct Dev {
             const uint64_t want = std::min<uint64_t>(4ull << 30, std::max(need, left));
             const uint64_t c = (std::max(need, want) + (2u << 20) - 1) & ~(uint64_t)((2u << 20) - 1);
             char* p = nullptr;
-            if (hipMalloc(&p, c) != hipSuccess) return nullptr;
+            if (hipMalloc(&p, c) != hipSuccess) {
+                (void)hipGetLastError();   // not an error: the chunk is formatted in pass 2 (see DevPool::get)
+                return nullptr;
+            }
             arena.push_back({p, c});
             arena_off = 0;
         }

@@ -127,6 +127,15 @@ struct sid_ctx {
 // textpath.hip: one line-aligned chunk of text resident on the device,
 // processed in place by the streaming engine (run.cpp).  Grow-only device
 // workspace; every function is asynchronous on `st`.
+//
+// Invariant: the chunk is the bytes [c0, c1) of `base`, and every kernel
+// bounds what it USES by c1.  The bytes past c1 (at least 256 readable, for
+// whole 16-B windows) are NOT zero: a ring slot keeps a previous, longer
+// chunk's text there, and resident text has the next chunk there.  A kernel
+// may load them but must mask them (as the index's line-start masks, the
+// parse's token scans and the formatters do); a kernel that needs NUL
+// padding must write it itself (tests/test_engine_gpu.py
+// test_stale_ring_slot_behind_a_last_line_without_newline).
 struct sid_chunk_ws {
     uint64_t site_cap = 0, tile_cap = 0;
     uint64_t* starts = nullptr;   // line start offsets (relative to the chunk's base)

@@ -57,3 +57,66 @@ def test_shared_gpu_rehearsal_reports_every_rank():
     assert d["n_gpus"] == 1
     assert d["config"]["sites_total"] == 2 * 200000
     assert d["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_two_rank_lynch_exchange_equals_one_process(sid, oracle, gpu, tmp_path):
+    """C3's one collective (bench.py Rank.lynch_step_exchange): two ranks, each
+    with 2M sites of seed 3, all-gather their unique-profile tables as device
+    tensors, rank 0 runs the one Nelder-Mead estimate and broadcasts (pi, eps).
+    The rank-ordered concatenation of both ranks' records (the timed PCIe
+    leg's, from the engines' host arenas) must be the one-process oracle's CSV
+    over the same 4M sites (call.cpp:62-143: the estimate is global), and both
+    ranks' (pi, eps, iterations) the oracle's, bit for bit.  On one GPU the
+    ranks share it over gloo (RCCL takes one rank per GPU); the exchange code
+    and its device tensors are the same for either backend (sid_amd/dist.py)."""
+    n = 2_000_000
+    dump = tmp_path / "dump"
+    r = run_bench(["--gpus", "2", "--allow-shared-gpu", "--config", "C3", "--sites", str(n), "--steps", "1",
+                   "--warmup", "0", "--device-steps", "1", "--no-extras", "--dump-records", str(dump)], 600)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    d = json.loads([ln for ln in r.stdout.decode().splitlines() if ln.startswith('{"metric"')][0])
+    assert d["config"]["ranks"] == 2 and d["config"]["sites_total"] == 2 * n
+    text, ln = gpu.synth_text_hbm(3, 30.0, 0, 2 * n)
+    host = text[:ln].cpu().numpy().tobytes()
+    del text
+    p = tmp_path / "c3_4m.plp"
+    p.write_bytes(host)
+    ref = oracle.run_cli(["-R", "-m", "likelihood_ratio", str(p)])
+    assert ref.returncode == 0
+    got = sid.HEADER + b"".join((dump / f"rank{k}.csv").read_bytes() for k in range(2))
+    if got != ref.stdout:
+        import numpy as np
+        m = min(len(got), len(ref.stdout))
+        i = int(np.argmax(np.frombuffer(got[:m], np.uint8) != np.frombuffer(ref.stdout[:m], np.uint8)))
+        raise AssertionError(f"first difference at byte {i}: {got[i - 80:i + 80]!r} vs {ref.stdout[i - 80:i + 80]!r}")
+    s = sid.parse_text(host)
+    rc, _, _, _, est, u = oracle.call_method(s.counts, "likelihood_ratio", estimate_prior=True)
+    assert rc == 0
+    for k in range(2):
+        j = json.loads((dump / f"rank{k}.json").read_text())
+        assert j["first_site"] == k * n and j["sites"] == n
+        assert (j["pi"], j["eps"], j["iterations"]) == (est.heterozygosity, est.error_rate, est.iterations)
+        assert j["n_unique"] == u
+    assert d["estimate"]["pi"] == est.heterozygosity and d["estimate"]["eps"] == est.error_rate
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_shared_gpu_rehearsal_runs_the_node_cli():
+    """N > 1 (bench.py bench_cli_node): after the timed legs the ranks write
+    their texts into one file and free their GPUs; rank 0 runs build/sid
+    --devices N over it (the whole node's drop-in) and the line carries it."""
+    if visible_gpus() != 1:
+        pytest.skip("the rehearsal case: one visible GPU")
+    args = ["--gpus", "2", "--allow-shared-gpu", "--sites", "300000", "--steps", "1", "--warmup", "0",
+            "--device-steps", "1"]
+    r = run_bench(args, 500)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    d = json.loads([ln for ln in r.stdout.decode().splitlines() if ln.startswith('{"metric"')][0])
+    cli = d["cli"]
+    assert "error" not in cli and "skipped" not in cli, cli
+    assert cli["devices"] == 2 and cli["sites"] == 600_000
+    assert cli["cli_stats"]["sites"] == 600_000
+    assert cli["sites_per_s_wall"] > 0

@@ -146,3 +146,80 @@ def test_c3_pcie_path_equals_oracle(sid, c3):
     got = eng.records_bytes(st.chunks)
     eng.close()
     assert_same(sid.HEADER + got, ref.stdout, "C3 PCIe path (pinned host text, host arena in pass 2)")
+
+
+# ---- C4 / C5 (configs[3], configs[4]): the strong-scaling device path ----
+# bench.py bench_strong: the rank's shard generated into HBM by
+# generate_resident, then device_path's engine (device_engine) with 1 GiB
+# chunks (STRONG_RESIDENT_CHUNK_MIB).  Here the same engine with device_sink
+# 0, so the records come back, at sizes that span several chunks.
+
+@pytest.fixture(scope="module")
+def bench_mod():
+    import bench
+    return bench
+
+
+def resident_shard(bench_mod, sid, cfg, first, n):
+    import torch
+    return bench_mod.generate_resident(torch, sid, torch.device("cuda", 0), 0, cfg, first, n)
+
+
+@pytest.fixture(scope="module")
+def c5(sid, gpu, oracle, bench_mod, tmp_path_factory):
+    """12M sites of C5 (seed 5, 200x, 125M-site chromosomes): ~6.8 GB of text,
+    7 chunks of 1 GiB or 4 of 2 GiB; lines of ~560 B, so the parse runs on the
+    line-length-sized grid with the separate -m local length kernel
+    (textpath.hip sid_chunk_parse: lines over 256 B)."""
+    cfg = bench_mod.CONFIGS["C5"]
+    n = 12_000_000
+    text, ln = resident_shard(bench_mod, sid, cfg, 0, n)
+    assert ln / n > 256
+    ref = oracle_local_sharded(oracle, text[:ln].cpu().numpy(), str(tmp_path_factory.mktemp("c5")))
+    return cfg, text, ln, n, ref
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("chunk_mib", [1024, 0], ids=["bench-1GiB", "engine-default-2GiB"])
+def test_c5_device_path_equals_oracle(sid, bench_mod, c5, chunk_mib):
+    cfg, text, ln, n, ref = c5
+    if chunk_mib == 1024:
+        assert bench_mod.STRONG_RESIDENT_CHUNK_MIB == 1024   # the chunking bench_strong uses
+    eng = bench_mod.device_engine(cfg, 0, chunk_mib, device_sink=0)
+    eng.source_device_text(text.data_ptr(), ln, keep=text)
+    out, st = eng.run()
+    eng.close()
+    assert st.sites == n
+    assert st.chunks >= (7 if chunk_mib else 4)
+    assert_same(out, ref, f"C5 device path ({chunk_mib or 2048} MiB chunks)")
+
+
+@pytest.fixture(scope="module")
+def c4(sid, gpu, oracle, bench_mod, tmp_path_factory):
+    """40M sites of C4 (seed 4, 30x, 24 x 125M-site chromosomes) from site
+    110M: the slice crosses the chr1/chr2 boundary; ~3.3 GB of text."""
+    cfg = bench_mod.CONFIGS["C4"]
+    first, n = 110_000_000, 40_000_000
+    text, ln = resident_shard(bench_mod, sid, cfg, first, n)
+    ref = oracle_local_sharded(oracle, text[:ln].cpu().numpy(), str(tmp_path_factory.mktemp("c4")))
+    assert b"\nchr1,125000000," in ref and b"\nchr2,1," in ref
+    return cfg, text, ln, n, ref
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("hold", [0, 5 << 29], ids=["held", "hold-budget-spent"])
+def test_c4_device_path_equals_oracle(sid, bench_mod, c4, hold):
+    """hold-budget-spent: as at C4's full size on one GPU (131 GB of records
+    against a hold budget of 40% of the HBM the text leaves), the chunks past
+    the budget are formatted in pass 2 from the resident text."""
+    cfg, text, ln, n, ref = c4
+    eng = bench_mod.device_engine(cfg, 0, bench_mod.STRONG_RESIDENT_CHUNK_MIB, device_sink=0, hold_bytes=hold)
+    eng.source_device_text(text.data_ptr(), ln, keep=text)
+    out, st = eng.run()
+    eng.close()
+    assert st.sites == n and st.chunks >= 4
+    if hold:
+        assert 0 < st.chunks_held < st.chunks
+    else:
+        assert st.chunks_held == st.chunks
+    assert_same(out, ref, f"C4 device path (1 GiB chunks, hold {hold})")

@@ -376,3 +376,58 @@ def test_source_file_range_past_eof(sid, tmp_path):
         with pytest.raises(sid.SidError):
             eng.source_file(f.fileno(), 0, 1 << 20)
     eng.close()
+
+
+@pytest.mark.parametrize("method", ["local", "quality"])
+def test_stale_ring_slot_behind_a_last_line_without_newline(sid, oracle, tmp_path, method):
+    """One ring slot (every chunk uploads into the same device buffer): the
+    short last chunk, whose last line has no trailing newline, sits in front
+    of the previous, longer chunk's stale lines.  Every kernel bounds its reads
+    by the chunk's end (sid_internal.h), so no stale line is indexed or parsed
+    and no stale byte joins the last line's fields (call.cpp:11-20 reads the
+    last line without its newline)."""
+    n = 40_000
+    text = sid.synth_text(41, n, 30.0, sites_per_chrom=15_000, mapq=method == "quality")
+    C = len(text) * 10 // 43   # 4.3 chunks: the last one ~0.3 of the others
+    text = text.rstrip(b"\n")
+    p = tmp_path / "nonl.plp"
+    p.write_bytes(text)
+    flags = ["-m", method] if method != "local" else []
+    ref = oracle.run_cli(flags + [str(p)])
+    assert ref.returncode == 0
+    eng = sid.Engine(method=method, slots=1, chunk_bytes=C)
+    eng.source_text(text)
+    for _ in range(2):
+        out, st = eng.run()
+        assert st.sites == n and st.chunks == 5
+        assert out == ref.stdout
+    eng.close()
+
+
+def test_arena_allocation_failure_falls_back(sid, oracle, tmp_path):
+    """The hold arena's allocation failing (HBM taken by another allocation,
+    a hold budget the GPU cannot meet) is not an error: the chunks are
+    formatted in pass 2.  The failed hipMalloc must not leave the runtime's
+    sticky last error behind for the next launch check on the compute thread
+    (run.cpp DevPool::get / Dev::arena_reserve); the CSV equals the oracle's."""
+    import torch
+    n = 300_000
+    text = sid.synth_text(43, n, 30.0, sites_per_chrom=100_000)
+    p = tmp_path / "oom.plp"
+    p.write_bytes(text)
+    ref = oracle.run_cli([str(p)])
+    assert ref.returncode == 0
+    eng = sid.Engine(method="local", chunk_bytes=1 << 20, hold_bytes=64 << 30)
+    eng.source_text(text)
+    free, _ = torch.cuda.mem_get_info()
+    leave = 2 << 30   # the arena asks for a 4 GiB segment: it cannot get one
+    filler = torch.empty(max(0, free - leave), dtype=torch.uint8, device="cuda")
+    try:
+        out, st = eng.run()
+    finally:
+        del filler
+        torch.cuda.empty_cache()
+    eng.close()
+    assert st.sites == n and st.chunks > 10
+    assert st.chunks_held == 0   # every chunk formatted in pass 2
+    assert out == ref.stdout

@@ -118,6 +118,31 @@ def test_lngamma_against_scipy(oracle):
     assert oracle.lngamma(1.0) == 0.0 and oracle.lngamma(2.0) == 0.0
 
 
+def catch_approx(got, want):
+    """Catch v1.9.4's default `== Approx(want)` (test/catch.hpp:2766-2806):
+    |got - want| < 100 FLT_EPSILON (1 + max(|got|, |want|))."""
+    eps = float(np.finfo(np.float32).eps) * 100
+    return abs(got - want) < eps * (1.0 + max(abs(got), abs(want)))
+
+
+@pytest.mark.parametrize("k", KAT["binomial_pmf"], ids=lambda k: f"n{k['n']}k{k['k']}")
+def test_lngamma_binomial_pmf_reference_vectors(oracle, k):
+    """The reference's one held set of lnGamma-dependent numbers: 30 binomial
+    pmf values (scipy-computed, test/test-likelihoods.cpp:22-49), rebuilt from
+    the oracle's restated gsl_sf_lngamma as -m quality's log-binomial does
+    (call.cpp:344-349: lnG(n+1) - lnG(n-k+1) - lnG(k+1)), where lnG does not
+    cancel.  Checked at Catch's default Approx, and tighter (1e-9 relative)
+    wherever the expected value is a normal double."""
+    n, kk, p, want = k["n"], k["k"], k["p"], k["pmf"]
+    lb = oracle.lngamma(n + 1) - oracle.lngamma(n - kk + 1) - oracle.lngamma(kk + 1)
+    got = math.exp(lb + kk * math.log(p) + (n - kk) * math.log(1 - p))
+    assert catch_approx(got, want), (got, want)
+    if want > 1e-300:
+        assert abs(got - want) <= 1e-9 * want, (got, want)
+    else:   # the pmf underflows a double (exponent below -745)
+        assert got == 0.0 and lb + kk * math.log(p) + (n - kk) * math.log(1 - p) < -745
+
+
 # ---- outputs the survey observed from the reference build (SURVEY.md §8(c)) ----
 EDGE = (b"c1\t1\tA\t0\t*\t*\n"
         b"c1\t2\tA\t4\tAACC\tIIII\n"
