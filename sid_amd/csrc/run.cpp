@@ -203,6 +203,7 @@ struct ChunkRec {
     const char* host = nullptr;      // its records in the host arena (host_hold_bytes), or null
     uint64_t host_len = 0;
     bool host1 = false;              // copied there during pass 1 (the emit only writes them)
+    bool sunk = false;               // device sink: formatted in pass 1 and dropped (held_len bytes)
 };
 
 enum SrcKind { SRC_NONE, SRC_HOST, SRC_FILE, SRC_DEVICE, SRC_SYNTH_HOST, SRC_SYNTH_DEVICE };
@@ -788,6 +789,16 @@ namespace {
 
 bool needs_format_pass1(const sid_engine* e) { return !e->lynch; }
 
+// The device sink (cfg.device_sink 1: records formatted into HBM and dropped)
+// formats every -m local / quality chunk in pass 1: within the hold budget
+// into the hold arena (counted at the emit), past it into a pooled scratch
+// buffer whose bytes are counted and dropped at once.  Nothing is written
+// anywhere, so the all-or-nothing output that makes the other sinks hold
+// records until every chunk is validated does not apply, and no chunk is
+// indexed and parsed a second time in pass 2 (C4 on one GPU: 131 GB of
+// records against a hold budget of ~16 GB).
+bool sink_all_pass1(const sid_engine* e) { return e->cfg.device_sink == 1 && needs_format_pass1(e); }
+
 // the uploader of device d: the chunks of `list` into device buffers, in order
 void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass)
 {
@@ -798,7 +809,7 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
         ChunkRec& r = e->recs[j];
         Loaded L;
         L.j = j;
-        if (pass == 2 && r.host1) continue;   // already in host memory: the writer takes it from there
+        if (pass == 2 && (r.host1 || r.sunk)) continue;   // in host memory already (the writer takes it), or sunk
         if (pass == 2 && r.held) {
             L.kind = 1;
             if (!d.loaded.push(L)) break;
@@ -823,7 +834,9 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
         uint64_t need = e->src == SRC_SYNTH_HOST || e->src == SRC_SYNTH_DEVICE ? e->per_chunk_cap : r.len;
         // keep it for pass 2?  Lynch always needs a second pass; local and
         // quality only once the hold budget ran out
-        bool want_keep = pass == 1 && (e->lynch || d.hold_full.load()) &&
+        // (the device sink formats every -m local / quality chunk in pass 1:
+        // nothing to keep for a second pass)
+        bool want_keep = pass == 1 && (e->lynch || (d.hold_full.load() && !sink_all_pass1(e))) &&
                          d.retain_used.load() + need + PAD <= d.retain_budget;
         char* dst = nullptr;
         uint64_t dcap = 0;
@@ -1089,7 +1102,7 @@ void compute(sid_engine* e, Dev& d, int pass)
             if (rc != SID_OK) return (void)fail(e, rc);
         }
         const bool lynch_hist = pass == 1 && e->lynch;
-        const bool format = pass == 2 || (needs_format_pass1(e) && !d.hold_full.load());
+        const bool format = pass == 2 || (needs_format_pass1(e) && (!d.hold_full.load() || sink_all_pass1(e)));
         if (lynch_hist) {
             x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
             if (x != hipSuccess) return (void)hipfail(e, x);
@@ -1107,6 +1120,7 @@ void compute(sid_engine* e, Dev& d, int pass)
         char* out = nullptr;
         uint64_t cap = 0;   // 0: arena memory (never returned to the pool)
         bool via_host = false;   // pass 1: records go on to the host arena (a pooled device buffer meanwhile)
+        bool sunk = false;       // pass 1, device sink past the hold budget: a scratch buffer, dropped
         // -m local: the call fused into the formatter (sid_chunk_local_*)
         const bool fused = e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx);
         // likelihood_ratio / bayes pass 2: the class lookup fused into the
@@ -1132,6 +1146,12 @@ void compute(sid_engine* e, Dev& d, int pass)
                 if (!out) cap = 0;
             }
             if (n == 0 || via_host) {
+            } else if (pass == 1 && sink_all_pass1(e) &&
+                       (d.hold_full.load() || d.hold_used.load() + bound > d.hold_budget)) {
+                d.hold_full = true;
+                out = d.pool.get(bound, &cap, d.s_comp);
+                sunk = out != nullptr;   // (no HBM for it: formatted in pass 2 instead)
+                if (!out) cap = 0;
             } else if (pass == 1 && d.hold_used.load() + bound > d.hold_budget) {
                 d.hold_full = true;   // this chunk and the rest: formatted in pass 2
             } else if (pass == 1) {
@@ -1210,6 +1230,12 @@ void compute(sid_engine* e, Dev& d, int pass)
         if (pass == 2 && r.pre) {
             d.pool.put(r.pre, r.pre_cap, d.s_comp);
             r.pre = nullptr;
+        }
+        if (pass == 1 && sunk) {
+            r.sunk = true;
+            r.held_len = bytes;
+            d.pool.put(out, cap, d.s_comp);   // reused on this stream only: ordered
+            continue;
         }
         if (pass == 1 && via_host) {
             char* hp = d.hh_take(bytes);
@@ -1366,6 +1392,7 @@ static void reset_run(sid_engine* e)
         r.host = nullptr;
         r.host_len = 0;
         r.host1 = false;
+        r.sunk = false;
         r.err = ~0ull;
         r.parsed = 0;
     }
@@ -1472,7 +1499,7 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
     for (auto& r : e->recs) {
         sites += r.parsed;
         bytes += r.len;
-        held += r.held != nullptr || r.host1;
+        held += r.held != nullptr || r.host1 || r.sunk;
         kept += r.kept != nullptr;
     }
     if (st) {
@@ -1619,6 +1646,8 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
     e->rc = SID_OK;
     e->reloaded = 0;
     e->sink_bytes = 0;
+    for (const auto& r : e->recs)
+        if (r.sunk) e->sink_bytes += r.held_len;   // formatted and dropped in pass 1
     // every chunk's records already in the host arena (-m local / quality
     // with host_hold_bytes): nothing left for the devices, only the writes
     bool all_host = sink != 1;
@@ -1643,13 +1672,13 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
     // pass 2 for the devices (the ingest synchronised their streams), only the
     // byte count -- no threads to start for a run that has nothing left to do
     bool all_held = sink == 1 && !e->recs.empty();
-    for (const auto& r : e->recs) all_held = all_held && r.held;
+    for (const auto& r : e->recs) all_held = all_held && (r.held || r.sunk);
     if (all_held) {
         uint64_t out = 0;
         for (auto& r : e->recs) {
             Dev& d = *e->devs[r.dev];
             out += r.held_len;
-            d.pool.put(r.held, r.held_cap, nullptr);
+            if (r.held) d.pool.put(r.held, r.held_cap, nullptr);
             if (r.kept) d.pool.put(r.kept, r.kept_cap, nullptr);
             if (r.pre) d.pool.put(r.pre, r.pre_cap, nullptr);
             r.held = r.kept = r.pre = nullptr;

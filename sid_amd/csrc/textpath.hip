@@ -686,6 +686,12 @@ __device__ __noinline__ void parse_line_serial(const char* __restrict__ text, ui
 __device__ __forceinline__ int ctz64(uint64_t x) { return x ? __builtin_ctzll(x) : 64; }
 
 constexpr int HDR_BYTES = 48;   // bytes staged per lane for the header (3 aligned windows)
+// 1: the header's token starts from the low-byte mask alone (3 instructions a
+// word; lines with single ' '/'\t' gaps); 0: separator and control-byte masks
+// per word (strtok_r's separator runs in the fast path too; A/B)
+#ifndef SID_PARSE_HDR
+#define SID_PARSE_HDR 1
+#endif
 
 // 8 bytes from a lane's staged header at any offset < HDR_BYTES + 16: two
 // aligned 8-B LDS reads and a funnel shift (past the lane's 48 bytes: the next
@@ -763,6 +769,98 @@ __device__ __forceinline__ bool read_bases_fast(const char* __restrict__ text, u
     return true;
 }
 
+// 1: the read-bases counts by an LDS table, one lookup a byte (below); 0:
+// five SWAR equality masks and popcounts a word (A/B)
+#ifndef SID_PARSE_LUT
+#define SID_PARSE_LUT 1
+#endif
+
+// The LDS table of the read-bases counts (pileup.cpp:76-150): a byte's
+// increments in 5-bit fields -- a 16-byte window adds at most 16 to a field:
+// bits 0-4 A/a, 5-9 C/c, 10-14 G/g, 15-19 T/t, 20-24 '.'/',' (the ref's,
+// added to its base at the end), 25-29 '+'/'-' (an indel: the line takes the
+// general routine); every other byte 0.  Bytes not to count are zeroed before
+// the lookup (NUL's entry is 0).
+constexpr uint32_t RB_M_SHIFT = 20, RB_INDEL_SHIFT = 25;
+__device__ __forceinline__ uint32_t rb_entry(uint32_t c)
+{
+    switch (c) {
+    case 'A': case 'a': return 1u;
+    case 'C': case 'c': return 1u << 5;
+    case 'G': case 'g': return 1u << 10;
+    case 'T': case 't': return 1u << 15;
+    case '.': case ',': return 1u << RB_M_SHIFT;
+    case '+': case '-': return 1u << RB_INDEL_SHIFT;
+    default: return 0;
+    }
+}
+
+// the four bytes of x through the table (byte b at LDS word b)
+__device__ __forceinline__ uint32_t rb_word(const uint32_t* lut, uint32_t x)
+{
+    return lut[x & 0xFFu] + lut[(x >> 8) & 0xFFu] + lut[(x >> 16) & 0xFFu] + lut[x >> 24];
+}
+
+// read_bases_fast with the table: the same byte masks per word (the token's
+// end, the '^' skip, the window's bytes inside [q, len)), the counted bytes
+// kept and the others zeroed, four lookups a word; the token's end byte is
+// checked once, after the loop
+__device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, uint64_t len, uint64_t q, uint32_t kd,
+                                               const uint32_t* lut, uint64_t* out)
+{
+    uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
+    uint64_t a = q & ~(uint64_t)15;
+    uint32_t lead = (uint32_t)(q & 15);
+    uint32_t carry = 0;   // bit 7: byte 0 of the next word is skipped
+    uint32_t tend = 0;    // the token's end byte in bits 0-7 (0: the text's end)
+    bool done = false, bad = false;
+    uint4 vn = *(const uint4*)(text + a);
+    do {
+        const uint4 v = vn;
+        vn = *(const uint4*)(text + a + 16);
+        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t room = len > a ? (uint32_t)min(len - a, (uint64_t)16) : 0u;
+        const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t x = ws[k];
+            const int b0 = 4 * k;
+            uint32_t vm = (__umul24((valid >> b0) & 15u, 0x00204081u) & 0x01010101u) << 7;
+            const int hi_b = (int)room - b0;
+            vm = done ? 0u : vm;
+            const uint32_t lo = low_bytes(x) & vm;
+            const uint32_t first = lo & (0u - lo);               // the token's end, if in this word
+            tend = first ? x >> ((__builtin_ctz(first) - 7) & 31) : tend;
+            vm &= first - 1u;                                    // bytes before it (all if none)
+            done = done || first != 0 || hi_b < 4;
+            const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
+            const uint32_t skip = ((caret << 8) | carry) & vm;
+            bad = bad || (caret & skip) != 0;                    // '^' run
+            carry = caret >> 24;
+            const uint32_t cm = vm & ~skip;                      // bit 7 of the counted bytes
+            acc += rb_word(lut, x & (cm | (cm - (cm >> 7))));    // (0xFF for each of them)
+        }
+        bad = bad || (acc >> RB_INDEL_SHIFT) != 0;
+        nA += acc & 31u;
+        nC += (acc >> 5) & 31u;
+        nG += (acc >> 10) & 31u;
+        nT += (acc >> 15) & 31u;
+        nM += (acc >> RB_M_SHIFT) & 31u;
+        lead = 0;
+        a += 16;
+    } while (!done);
+    const uint32_t tb = tend & 0xFFu;
+    if (bad || (tb != ' ' && tb != '\t' && tb != '\n' && tb != 0)) return false;
+    nA += kd == K_A ? nM : 0;
+    nC += kd == K_C ? nM : 0;
+    nG += kd == K_G ? nM : 0;
+    nT += kd == K_T ? nM : 0;
+    *out = (uint64_t)(uint16_t)nA | ((uint64_t)(uint16_t)nC << 16) | ((uint64_t)(uint16_t)nG << 32) |
+           ((uint64_t)(uint16_t)nT << 48);
+    return true;
+}
+
 // The fast path of one line (pileup.cpp:13-46 + :70-153 for the lines that
 // need none of the general routine's cases), branch-free over SWAR byte masks:
 //   header   the 48 bytes from the line's 16-B window: separator (' ', '\t')
@@ -780,7 +878,8 @@ __device__ __forceinline__ bool read_bases_fast(const char* __restrict__ text, u
 //                                       '\t', '\n' or NUL, else fail
 // Returns false when the line needs the general routine.
 __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, uint64_t len, uint64_t s0,
-                                                const uint8_t* cls, char* stage, uint64_t* out, uint64_t* hdr)
+                                                const uint8_t* cls, char* stage, uint64_t* out, uint64_t* hdr,
+                                                const uint32_t* rbl)
 {
     const uint64_t a0 = s0 & ~(uint64_t)15;
     const uint32_t sh = (uint32_t)(s0 & 15);
@@ -790,6 +889,47 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     *(uint4*)(stage) = v0;
     *(uint4*)(stage + 16) = v1;
     *(uint4*)(stage + 32) = v2;
+#if SID_PARSE_HDR
+    // low bytes (< 0x21: the separators, '\n', NUL, every other control byte)
+    // of the 48 staged bytes as a 48-bit mask: 3 instructions a word
+    const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
+    uint32_t lowb[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) lowb[k] = low_bytes(w[k]);
+    const uint32_t l_lo = compress8(lowb[0], lowb[1]) | (compress8(lowb[2], lowb[3]) << 8) |
+                          (compress8(lowb[4], lowb[5]) << 16) | (compress8(lowb[6], lowb[7]) << 24);
+    const uint32_t l_hi = compress8(lowb[8], lowb[9]) | (compress8(lowb[10], lowb[11]) << 8);
+    // bit j = byte s0 + j, for the bytes inside the text and the 48 staged
+    const uint64_t avail = len > s0 ? len - s0 : 0;
+    const uint32_t nb = (uint32_t)min((uint64_t)(HDR_BYTES - sh), avail);
+    const uint64_t valid = (1ull << nb) - 1;   // (nb <= 48)
+    const uint64_t L = ((((uint64_t)l_hi << 32) | l_lo) >> sh) & valid;
+    const uint64_t N = ~L & valid;
+    uint64_t T = N & ~(N << 1) & ~1ull;   // starts of tokens 1, 2, ...
+    const int t1 = ctz64(T);
+    T &= T - 1;
+    const int t2 = ctz64(T);
+    T &= T - 1;
+    const int t3 = ctz64(T);
+    T &= T - 1;
+    const int t4 = ctz64(T);
+    // The fast path's lines (the rest take the general routine, which has
+    // strtok_r's semantics): token 0 at the line start, and exactly one
+    // separator byte before each of tokens 1-4 -- the low bytes before token
+    // 4 are then the four gaps, which must be ' ' or '\t' (a '\n', NUL or
+    // other control byte there ends or splits a token differently) -- and a
+    // one-byte token 2 (the reference base)
+    bool ok = (N & 1) && t4 < (int)nb && t3 == t2 + 2;
+    ok = ok && __popcll(L & ((1ull << t4) - 1)) == 4;
+    if (!ok) return false;
+    const uint32_t gaps = (uint32_t)(uint8_t)stage[sh + t1 - 1] | ((uint32_t)(uint8_t)stage[sh + t2 - 1] << 8) |
+                          ((uint32_t)(uint8_t)stage[sh + t2 + 1] << 16) | ((uint32_t)(uint8_t)stage[sh + t4 - 1] << 24);
+    if ((eq_bytes(gaps, 0x20202020u) | eq_bytes(gaps, 0x09090909u)) != 0x80808080u) return false;
+    const int t0 = 0;
+    const int l0 = t1 - 1;
+    const int lp = t2 - 1 - t1;
+    const uint32_t ref = (uint8_t)stage[sh + t2];
+#else
     const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
     // S: separator bytes as a 48-bit mask; fbad: window offset of the first
     // control byte ('\n', NUL, < 0x20 but '\t') at or after the line's start
@@ -831,6 +971,7 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     const int l0 = ctz64(S >> t0);
     const int lp = ctz64(S >> t1);
     const uint32_t ref = (uint8_t)stage[sh + t2];
+#endif
     // the position: its first 8 bytes by two aligned 8-B LDS reads and a
     // funnel shift, digit-checked in SWAR, left-padded with zero digits and
     // summed by v_dot4 pairs (10, 1) and two 24-bit multiply-adds; a 9th digit
@@ -862,7 +1003,11 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
     const uint32_t kd = cls[up], kc = cls[lw];
     if (kd >= K_CARET || kc >= K_CARET || kd != kc) return false;
+#if SID_PARSE_LUT
+    return read_bases_lut(text, len, s0 + (uint64_t)t4, kd, rbl, out);
+#else
     return read_bases_fast(text, len, s0 + (uint64_t)t4, kd, out);
+#endif
 }
 
 // Pass 1: the fast path over every line; a line it cannot take is appended to
@@ -879,8 +1024,12 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
                                                        const uint32_t* __restrict__ in, const unsigned long long* inn)
 {
     __shared__ uint8_t cls[256];
+    __shared__ uint32_t rbl[256];
     __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
-    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    if (threadIdx.x < 256) {
+        cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+        rbl[threadIdx.x] = rb_entry(threadIdx.x);
+    }
     __syncthreads();
     const uint64_t lo = range[0], hi = LIST ? *inn : range[1];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -891,7 +1040,7 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
         const uint64_t s0 = s_next;
         if (k + stride < hi) s_next = starts[LIST ? lo + in[k + stride] : k + stride];   // the next line's offset in flight
         uint64_t c = 0, h[2] = {0, 0};
-        if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
+        if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h, rbl)) {
             counts[i] = c;
             *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h[0], h[1]);
         } else {
@@ -1616,8 +1765,12 @@ __global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __rest
 {
     static_assert(FTB % 64 == 0 && TB % 64 == 0, "a wave's lines lie in one formatter block");
     __shared__ uint8_t cls[256];
+    __shared__ uint32_t rbl[256];
     __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
-    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    if (threadIdx.x < 256) {
+        cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+        rbl[threadIdx.x] = rb_entry(threadIdx.x);
+    }
     __syncthreads();
     const uint64_t lo = range[0], hi = range[1];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1630,7 +1783,7 @@ __global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __rest
         int l = 0;
         if (i < hi) {
             uint64_t c = 0, h[2] = {0, 0};
-            if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h)) {
+            if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h, rbl)) {
                 ST_MID(hdr + 2 * i, h[0]);
                 ST_MID(hdr + 2 * i + 1, h[1]);
                 if (h[0] >> 63) {

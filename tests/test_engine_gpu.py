@@ -431,3 +431,38 @@ def test_arena_allocation_failure_falls_back(sid, oracle, tmp_path):
     assert st.sites == n and st.chunks > 10
     assert st.chunks_held == 0   # every chunk formatted in pass 2
     assert out == ref.stdout
+
+
+@pytest.mark.parametrize("source", ["text", "device", "synth_device"])
+def test_device_sink_formats_past_the_hold_budget_once(sid, source):
+    """The device sink (records formatted into HBM and dropped) formats every
+    -m local chunk in pass 1: past the hold budget into a scratch buffer,
+    counted and dropped (run.cpp sink_all_pass1), so no chunk is indexed and
+    parsed a second time.  Its byte count equals the CSV the same engine
+    writes with a real sink, whose chunks past the budget take pass 2."""
+    import torch
+    n = 200_000
+    text = sid.synth_text(47, n, 30.0, sites_per_chrom=70_000)
+    kw = dict(chunk_bytes=1 << 20, hold_bytes=3 << 20)
+    ref, st_ref = engine_csv(sid, "local", source, text, n=n, seed=47, spc=70_000, **kw)
+    assert 0 < st_ref.chunks_held < st_ref.chunks   # the written run: chunks past the budget in pass 2
+    eng = sid.Engine(device_sink=True, **kw)
+    if source == "text":
+        eng.source_text(text)
+    elif source == "device":
+        buf = torch.zeros(len(text) + 512, dtype=torch.uint8, device="cuda")
+        buf[: len(text)] = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
+        eng.source_device_text(buf.data_ptr(), len(text), keep=buf)
+    else:
+        eng.source_synth(47, n, 30.0, sites_per_chrom=70_000, on_device=True)
+    eng.profile(True)
+    for _ in range(2):
+        st = eng.ingest()
+        eng.estimate()
+        out, st2 = eng.emit()
+        assert out == b"" and st.sites == n
+        assert st.chunks_held == st.chunks and st2.chunks_reloaded == 0
+        assert st2.bytes_out == len(ref) - len(sid.HEADER)
+    prof = eng.profile_read()
+    assert prof["chunks"] == 2 * st.chunks   # one index + parse per chunk and run
+    eng.close()
