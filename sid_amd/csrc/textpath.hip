@@ -779,9 +779,11 @@ __device__ __forceinline__ bool read_bases_fast(const char* __restrict__ text, u
 // increments in 5-bit fields -- a 16-byte window adds at most 16 to a field:
 // bits 0-4 A/a, 5-9 C/c, 10-14 G/g, 15-19 T/t, 20-24 '.'/',' (the ref's,
 // added to its base at the end), 25-29 '+'/'-' (an indel: the line takes the
-// general routine); every other byte 0.  Bytes not to count are zeroed before
-// the lookup (NUL's entry is 0).
-constexpr uint32_t RB_M_SHIFT = 20, RB_INDEL_SHIFT = 25;
+// general routine), bit 30 a control byte other than '\t' / '\n' ending the
+// token (only the token's end byte is looked up among the low bytes: the
+// general routine then has strtok_r's view of it); every other byte 0.
+// Bytes not to count are zeroed before the lookup (NUL's entry is 0).
+constexpr uint32_t RB_M_SHIFT = 20, RB_BAD_SHIFT = 25;
 __device__ __forceinline__ uint32_t rb_entry(uint32_t c)
 {
     switch (c) {
@@ -790,8 +792,9 @@ __device__ __forceinline__ uint32_t rb_entry(uint32_t c)
     case 'G': case 'g': return 1u << 10;
     case 'T': case 't': return 1u << 15;
     case '.': case ',': return 1u << RB_M_SHIFT;
-    case '+': case '-': return 1u << RB_INDEL_SHIFT;
-    default: return 0;
+    case '+': case '-': return 1u << RB_BAD_SHIFT;
+    case ' ': case '\t': case '\n': case 0: return 0;
+    default: return c < 0x21 ? 1u << 30 : 0;
     }
 }
 
@@ -801,57 +804,75 @@ __device__ __forceinline__ uint32_t rb_word(const uint32_t* lut, uint32_t x)
     return lut[x & 0xFFu] + lut[(x >> 8) & 0xFFu] + lut[(x >> 16) & 0xFFu] + lut[x >> 24];
 }
 
-// read_bases_fast with the table: the same byte masks per word (the token's
-// end, the '^' skip, the window's bytes inside [q, len)), the counted bytes
-// kept and the others zeroed, four lookups a word; the token's end byte is
-// checked once, after the loop
+// One 16-B window of token 4: per word, the bytes before the token's end
+// (the first byte < 0x21; `done` from then on), the '^' skip (carried into
+// the next word), the counted bytes kept and the others zeroed, then four
+// table lookups; the token's end byte is looked up too (its entry flags a
+// control byte).  MASKED: only the bytes `valid` (the window's bytes at or
+// after the token's start and before the text's end, room = bytes before
+// the end) count; else the whole window lies inside the text.
+template <bool MASKED>
+__device__ __forceinline__ uint32_t rb_window(const uint4 v, uint32_t valid, int room, const uint32_t* lut, bool& done,
+                                              uint32_t& carry, bool& bad)
+{
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = ws[k];
+        uint32_t vm = MASKED ? (__umul24((valid >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) << 7 : 0x80808080u;
+        vm = done ? 0u : vm;
+        const uint32_t lo = low_bytes(x) & vm;
+        const uint32_t first = lo & (0u - lo);               // the token's end, if in this word
+        vm &= first - 1u;                                    // bytes before it (all if none)
+        done = done || first != 0 || (MASKED && room - 4 * k < 4);
+        const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
+        const uint32_t skip = ((caret << 8) | carry) & vm;
+        bad = bad || (caret & skip) != 0;                    // '^' run
+        carry = caret >> 24;
+        const uint32_t cm = (vm | first) & ~skip;            // bit 7 of the bytes looked up
+        acc += rb_word(lut, x & (cm | (cm - (cm >> 7))));    // (0xFF for each of them)
+    }
+    return acc;
+}
+
+// read_bases_fast with the table: the first window (the token's start inside
+// it) masked, then whole windows while they lie inside the text
 __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, uint64_t len, uint64_t q, uint32_t kd,
                                                const uint32_t* lut, uint64_t* out)
 {
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
     uint64_t a = q & ~(uint64_t)15;
-    uint32_t lead = (uint32_t)(q & 15);
     uint32_t carry = 0;   // bit 7: byte 0 of the next word is skipped
-    uint32_t tend = 0;    // the token's end byte in bits 0-7 (0: the text's end)
     bool done = false, bad = false;
     uint4 vn = *(const uint4*)(text + a);
-    do {
+    uint32_t acc = 0;
+    auto masked = [&](const uint4& v, uint32_t lead) {
+        const int room = len > a ? (int)min(len - a, (uint64_t)16) : 0;
+        const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
+        return rb_window<true>(v, valid, room, lut, done, carry, bad);
+    };
+    auto add = [&](uint32_t w) {
+        nA += w & 31u;
+        nC += (w >> 5) & 31u;
+        nG += (w >> 10) & 31u;
+        nT += (w >> 15) & 31u;
+        nM += (w >> RB_M_SHIFT) & 31u;
+        acc |= w;
+    };
+    {
+        const uint4 v = vn;
+        vn = *(const uint4*)(text + a + 16);   // the next window in flight while this one is counted
+        add(masked(v, (uint32_t)(q & 15)));
+        a += 16;
+    }
+    while (!done) {
         const uint4 v = vn;
         vn = *(const uint4*)(text + a + 16);
-        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-        const uint32_t room = len > a ? (uint32_t)min(len - a, (uint64_t)16) : 0u;
-        const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t x = ws[k];
-            const int b0 = 4 * k;
-            uint32_t vm = (__umul24((valid >> b0) & 15u, 0x00204081u) & 0x01010101u) << 7;
-            const int hi_b = (int)room - b0;
-            vm = done ? 0u : vm;
-            const uint32_t lo = low_bytes(x) & vm;
-            const uint32_t first = lo & (0u - lo);               // the token's end, if in this word
-            tend = first ? x >> ((__builtin_ctz(first) - 7) & 31) : tend;
-            vm &= first - 1u;                                    // bytes before it (all if none)
-            done = done || first != 0 || hi_b < 4;
-            const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
-            const uint32_t skip = ((caret << 8) | carry) & vm;
-            bad = bad || (caret & skip) != 0;                    // '^' run
-            carry = caret >> 24;
-            const uint32_t cm = vm & ~skip;                      // bit 7 of the counted bytes
-            acc += rb_word(lut, x & (cm | (cm - (cm >> 7))));    // (0xFF for each of them)
-        }
-        bad = bad || (acc >> RB_INDEL_SHIFT) != 0;
-        nA += acc & 31u;
-        nC += (acc >> 5) & 31u;
-        nG += (acc >> 10) & 31u;
-        nT += (acc >> 15) & 31u;
-        nM += (acc >> RB_M_SHIFT) & 31u;
-        lead = 0;
+        add(a + 16 <= len ? rb_window<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u));
         a += 16;
-    } while (!done);
-    const uint32_t tb = tend & 0xFFu;
-    if (bad || (tb != ' ' && tb != '\t' && tb != '\n' && tb != 0)) return false;
+    }
+    if (bad || (acc >> RB_BAD_SHIFT) != 0) return false;
     nA += kd == K_A ? nM : 0;
     nC += kd == K_C ? nM : 0;
     nG += kd == K_G ? nM : 0;

@@ -1,6 +1,8 @@
 // The CLI's start-up, piece by piece (measurement only): HIP runtime init
-// (hipGetDeviceCount), the first and a second sid_create (class tables, lazy
-// code-object loads), sid_engine_create, and a hipMalloc / hipFree pair.
+// (hipInit, then hipGetDeviceCount), the device's context (hipSetDevice +
+// hipFree(0)), the first and a second sid_create (class tables, lazy
+// code-object loads), the engine's pieces (streams, events, a pinned word),
+// sid_engine_create, and a hipMalloc / hipFree pair.
 // Build: hipcc -O2 -Iinclude tools/debug/startup_probe.cpp -Lbuild -lsid -Wl,-rpath,$PWD/build -o build/startup_probe
 #include <hip/hip_runtime.h>
 
@@ -14,35 +16,56 @@ static double now()
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+static double t_last;
+static void step(const char* name, int rc = 0)
+{
+    const double t = now();
+    std::printf("{\"step\": \"%s\", \"ms\": %.2f, \"rc\": %d}\n", name, (t - t_last) * 1e3, rc);
+    std::fflush(stdout);
+    t_last = now();
+}
+
 int main()
 {
-    double t = now();
+    const double t0 = now();
+    t_last = t0;
+    int rc = (int)hipInit(0);
+    step("hipInit", rc);
     int n = 0;
-    sid_device_count(&n);
-    double t1 = now();
-    std::printf("{\"step\": \"hipGetDeviceCount\", \"ms\": %.2f, \"devices\": %d}\n", (t1 - t) * 1e3, n);
+    rc = sid_device_count(&n);
+    step("hipGetDeviceCount", rc);
+    rc = (int)hipSetDevice(0);
+    step("hipSetDevice", rc);
+    rc = (int)hipFree(nullptr);
+    step("hipFree(0) (context)", rc);
     sid_opts o;
     sid_opts_default(&o);
     for (int k = 0; k < 2; ++k) {
-        t = now();
         sid_ctx* c = nullptr;
-        int rc = sid_create(0, &o, &c);
-        t1 = now();
-        std::printf("{\"step\": \"sid_create %d\", \"ms\": %.2f, \"rc\": %d}\n", k, (t1 - t) * 1e3, rc);
+        rc = sid_create(0, &o, &c);
+        step(k ? "sid_create 1" : "sid_create 0", rc);
     }
-    t = now();
+    hipStream_t s[3];
+    for (int k = 0; k < 3; ++k) {
+        rc = (int)hipStreamCreateWithFlags(&s[k], hipStreamNonBlocking);
+        step("hipStreamCreateWithFlags", rc);
+    }
+    hipEvent_t ev[8];
+    for (auto& e : ev) rc |= (int)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    step("8 x hipEventCreateWithFlags", rc);
+    void* h = nullptr;
+    rc = (int)hipHostMalloc(&h, 128, hipHostMallocDefault);
+    step("hipHostMalloc 128 B", rc);
     void* p = nullptr;
-    (void)hipMalloc(&p, 1ull << 30);
-    (void)hipFree(p);
-    t1 = now();
-    std::printf("{\"step\": \"hipMalloc+hipFree 1 GiB\", \"ms\": %.2f}\n", (t1 - t) * 1e3);
+    rc = (int)hipMalloc(&p, 1ull << 30);
+    rc |= (int)hipFree(p);
+    step("hipMalloc+hipFree 1 GiB", rc);
     sid_engine_cfg cfg;
     sid_engine_cfg_default(&cfg);
     cfg.devices = 1;
-    t = now();
     sid_engine* e = nullptr;
-    int rc = sid_engine_create(&o, &cfg, &e);
-    t1 = now();
-    std::printf("{\"step\": \"sid_engine_create\", \"ms\": %.2f, \"rc\": %d}\n", (t1 - t) * 1e3, rc);
+    rc = sid_engine_create(&o, &cfg, &e);
+    step("sid_engine_create", rc);
+    std::printf("{\"step\": \"total\", \"ms\": %.2f}\n", (now() - t0) * 1e3);
     return 0;
 }
