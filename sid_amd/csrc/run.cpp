@@ -198,7 +198,7 @@ struct ChunkRec {
     char* kept = nullptr;            // text kept for pass 2 (device)
     uint64_t kept_cap = 0, kept_len = 0;
     char* pre = nullptr;             // Lynch paths: the pass-1 parse (line offsets, counts, formatter
-    uint64_t pre_cap = 0;            // header pairs: n x 32 B) kept for pass 2, which skips index + parse
+    uint64_t pre_cap = 0;            // header pairs: n x 28 B) kept for pass 2, which skips index + parse
     uint64_t err = ~0ull;            // min(offset * 8 + kind) of the chunk's malformed lines
     const char* host = nullptr;      // its records in the host arena (host_hold_bytes), or null
     uint64_t host_len = 0;
@@ -435,7 +435,8 @@ const uint64_t CHUNK_SYNTH = 512ull << 20;
 
 uint64_t chunk_bytes(const sid_engine* e)
 {
-    if (e->cfg.chunk_bytes) return e->cfg.chunk_bytes;
+    // (32-bit line offsets: a chunk spans less than 4 GiB, sid_off_t)
+    if (e->cfg.chunk_bytes) return std::min<uint64_t>(e->cfg.chunk_bytes, SID_CHUNK_MAX - (64ull << 20));
     return e->src == SRC_DEVICE ? CHUNK_DEVICE : e->src == SRC_SYNTH_DEVICE ? CHUNK_SYNTH : CHUNK_HOST;
 }
 
@@ -1033,7 +1034,8 @@ void compute(sid_engine* e, Dev& d, int pass)
         // workspace's line offsets, counts and header pairs (restored below)
         struct View {
             sid_chunk_ws& W;
-            uint64_t *starts, *counts, *hdr;
+            sid_off_t* starts;
+            uint64_t *counts, *hdr;
             bool on = false;
             ~View()
             {
@@ -1042,13 +1044,14 @@ void compute(sid_engine* e, Dev& d, int pass)
         } view{W, W.starts, W.counts, W.hdr};
         hipEvent_t pe = nullptr;
         uint64_t n = 0;
-        // the kept parse's layout: starts, counts, header pairs, each at a
-        // 16-B aligned offset (the lookup reads counts as 16-B site pairs)
+        // the kept parse's layout: starts (4 B), counts (8 B), header pairs
+        // (16 B), each at a 16-B aligned offset (the lookup reads counts as
+        // 16-B site pairs)
         auto use_pre = [&](char* pre, uint64_t m) {
             view.starts = W.starts, view.counts = W.counts, view.hdr = W.hdr, view.on = true;
-            const uint64_t m2 = (m + 1) & ~(uint64_t)1;
-            W.starts = (uint64_t*)pre;
-            W.counts = W.starts + m2;
+            const uint64_t m2 = (m + 1) & ~(uint64_t)1, m4 = (m + 3) & ~(uint64_t)3;
+            W.starts = (sid_off_t*)pre;
+            W.counts = (uint64_t*)(pre + 4 * m4);
             W.hdr = W.counts + m2;
         };
         if (pass == 2 && r.pre) {
@@ -1074,9 +1077,9 @@ void compute(sid_engine* e, Dev& d, int pass)
             r.parsed = n;
             // Lynch paths: the parse goes straight into a buffer kept for
             // pass 2 (which then skips index and parse) while the retain
-            // budget allows: 32 B a site, cheaper than indexing and parsing
+            // budget allows: 28 B a site, cheaper than indexing and parsing
             // the text again
-            const uint64_t pre_bytes = 32 * ((n + 1) & ~(uint64_t)1);
+            const uint64_t pre_bytes = 4 * ((n + 3) & ~(uint64_t)3) + 24 * ((n + 1) & ~(uint64_t)1);
             if (pass == 1 && e->lynch && n && !qmode && d.retain_used.load() + pre_bytes <= d.retain_budget) {
                 uint64_t pc = 0;
                 char* pre = d.pool.get(pre_bytes, &pc, d.s_comp);

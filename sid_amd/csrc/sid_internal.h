@@ -136,9 +136,17 @@ struct sid_ctx {
 // parse's token scans and the formatters do); a kernel that needs NUL
 // padding must write it itself (tests/test_engine_gpu.py
 // test_stale_ring_slot_behind_a_last_line_without_newline).
+//
+// Line offsets of a chunk, relative to its 16-B aligned base: 32 bits (a
+// chunk spans less than 4 GiB; sid_chunk_index refuses a longer one), 4 B a
+// site written by the index and read by the parse (the whole-text sid_dtext_*
+// path keeps 64-bit offsets)
+typedef uint32_t sid_off_t;
+constexpr uint64_t SID_CHUNK_MAX = (4ull << 30) - (1ull << 20);   // bytes a chunk may span
+
 struct sid_chunk_ws {
     uint64_t site_cap = 0, tile_cap = 0;
-    uint64_t* starts = nullptr;   // line start offsets (relative to the chunk's base)
+    sid_off_t* starts = nullptr;  // line start offsets (relative to the chunk's base)
     uint64_t* counts = nullptr;   // profile_t per site
     uint64_t* hdr = nullptr;      // per site for the formatter: (chrom / position word, chrom's first 8 bytes)
     uint32_t* fb = nullptr;       // three site lists of site_cap entries: the lines the first parse pass

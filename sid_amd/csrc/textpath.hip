@@ -418,7 +418,7 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
 // z32[0, n32), z64a[0, 8), z64b[0, 2) when set.
 __global__ __launch_bounds__(TB) void sid_index_emit_kernel(const uint16_t* __restrict__ masks, uint64_t tile_base,
                                                             uint64_t ntiles, const uint64_t* __restrict__ toff,
-                                                            uint64_t* __restrict__ starts,
+                                                            sid_off_t* __restrict__ starts,
                                                             uint32_t* __restrict__ z32 = nullptr, uint64_t n32 = 0,
                                                             unsigned long long* __restrict__ z64a = nullptr,
                                                             unsigned long long* __restrict__ z64b = nullptr)
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(TB) void sid_index_emit_kernel(const uint16_t* __re
             uint32_t mk = m[k];
             while (mk) {
                 const int j = __ffs(mk) - 1;
-                ST_MID(starts + q, at + j);
+                ST_MID(starts + q, (sid_off_t)(at + j));
                 ++q;
                 mk &= mk - 1;
             }
@@ -837,15 +837,17 @@ __device__ __forceinline__ uint32_t rb_window(const uint4 v, uint32_t valid, int
 }
 
 // read_bases_fast with the table: the first window (the token's start inside
-// it) masked, then whole windows while they lie inside the text
+// it) masked, then whole windows while they lie inside the text.  first: the
+// first window's 16 bytes, in the header's LDS stage (no second global load
+// of bytes the header already read)
 __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, uint64_t len, uint64_t q, uint32_t kd,
-                                               const uint32_t* lut, uint64_t* out)
+                                               const uint32_t* lut, const uint4* first, uint64_t* out)
 {
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
     uint64_t a = q & ~(uint64_t)15;
     uint32_t carry = 0;   // bit 7: byte 0 of the next word is skipped
     bool done = false, bad = false;
-    uint4 vn = *(const uint4*)(text + a);
+    uint4 vn = *(const uint4*)(text + a + 16);   // the next window in flight while the first is counted
     uint32_t acc = 0;
     auto masked = [&](const uint4& v, uint32_t lead) {
         const int room = len > a ? (int)min(len - a, (uint64_t)16) : 0;
@@ -860,12 +862,8 @@ __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, ui
         nM += (w >> RB_M_SHIFT) & 31u;
         acc |= w;
     };
-    {
-        const uint4 v = vn;
-        vn = *(const uint4*)(text + a + 16);   // the next window in flight while this one is counted
-        add(masked(v, (uint32_t)(q & 15)));
-        a += 16;
-    }
+    add(masked(*first, (uint32_t)(q & 15)));
+    a += 16;
     while (!done) {
         const uint4 v = vn;
         vn = *(const uint4*)(text + a + 16);
@@ -1025,7 +1023,7 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     const uint32_t kd = cls[up], kc = cls[lw];
     if (kd >= K_CARET || kc >= K_CARET || kd != kc) return false;
 #if SID_PARSE_LUT
-    return read_bases_lut(text, len, s0 + (uint64_t)t4, kd, rbl, out);
+    return read_bases_lut(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out);
 #else
     return read_bases_fast(text, len, s0 + (uint64_t)t4, kd, out);
 #endif
@@ -1036,9 +1034,9 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
 // the general routine over that list -- or over every line, for -m quality.
 // LIST: over the lines a previous pass listed in (in, *inn) instead of all of
 // [lo, hi) (the cooperative parse's leftovers).
-template <bool LIST>
+template <bool LIST, class Off>
 __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ text, uint64_t len,
-                                                       const uint64_t* __restrict__ starts,
+                                                       const Off* __restrict__ starts,
                                                        const uint64_t* __restrict__ range,   // [lo, hi)
                                                        uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
                                                        uint32_t* __restrict__ fb, unsigned long long* fbn,
@@ -1138,7 +1136,7 @@ __device__ __forceinline__ unsigned long long window_counts(uint4 v, uint32_t va
 
 __global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restrict__ text, uint64_t len,
                                                             uint64_t tbase, const uint64_t* __restrict__ low64,
-                                                            const uint64_t* __restrict__ starts,
+                                                            const sid_off_t* __restrict__ starts,
                                                             const uint64_t* __restrict__ range,
                                                             uint64_t* __restrict__ counts,
                                                             uint64_t* __restrict__ hdr, uint32_t* __restrict__ fb,
@@ -1297,8 +1295,9 @@ __global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restri
 
 // late (optional): the lines it parsed, for the -m local record lengths the
 // fused parse computes for its own lines (sid_local_len_list_kernel)
+template <class Off>
 __global__ __launch_bounds__(TB) void sid_parse_serial_kernel(const char* __restrict__ text, uint64_t len,
-                                                              const uint64_t* __restrict__ starts,
+                                                              const Off* __restrict__ starts,
                                                               const uint64_t* __restrict__ range,
                                                               uint64_t* __restrict__ counts,
                                                               uint64_t* __restrict__ hdr,
@@ -1345,7 +1344,8 @@ static unsigned line_walk_grid(uint64_t n, uint64_t len, unsigned cap)
 }
 
 // the two passes over sites [range[0], range[1]) (the range lives on the device)
-static void launch_parse(const char* text, uint64_t len, const uint64_t* starts, const uint64_t* range, uint64_t n,
+template <class Off>
+static void launch_parse(const char* text, uint64_t len, const Off* starts, const uint64_t* range, uint64_t n,
                          uint64_t* counts, uint64_t* hdr, uint32_t* fb, unsigned long long* fbn,
                          unsigned long long* err, int qmode, hipStream_t st)
 {
@@ -1358,7 +1358,7 @@ static void launch_parse(const char* text, uint64_t len, const uint64_t* starts,
     }
     const unsigned pgf = env ? pg : line_walk_grid(n, len, pg);
     (void)hipMemsetAsync(fbn, 0, sizeof *fbn, st);
-    sid_parse_kernel<false><<<pgf, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, nullptr, nullptr);
+    sid_parse_kernel<false, Off><<<pgf, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, nullptr, nullptr);
     sid_parse_serial_kernel<<<256, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, err, 0);
 }
 
@@ -1385,7 +1385,8 @@ struct Head {
 // hdr: the parse's (header word, chrom's first 8 bytes) of the site, or null;
 // the line's offset (*startp) is read only when the text is (a chrom longer
 // than 8 bytes, or no valid header word)
-__device__ __forceinline__ Head site_head(Reader& R, const uint64_t* startp, const uint64_t* hdr)
+template <class Off>
+__device__ __forceinline__ Head site_head(Reader& R, const Off* startp, const uint64_t* hdr)
 {
     Head h;
     h.c8 = 0;
@@ -1620,7 +1621,7 @@ __device__ __forceinline__ void block_store(const char* buf, uint32_t tot, char*
 
 // ---- any method: code / hom_conf / het_conf per site (call kernels) ----
 __global__ __launch_bounds__(FTB) void sid_fmt_blen_kernel(const char* __restrict__ text, uint64_t len,
-                                                          const uint64_t* __restrict__ starts,
+                                                          const sid_off_t* __restrict__ starts,
                                                           const uint64_t* __restrict__ hdr, uint64_t n,
                                                           const uint8_t* __restrict__ code,
                                                           const double* __restrict__ hom,
@@ -1648,7 +1649,7 @@ __global__ __launch_bounds__(FTB) void sid_fmt_blen_kernel(const char* __restric
 }
 
 __global__ __launch_bounds__(FTB) void sid_fmt_put_kernel(const char* __restrict__ text, uint64_t len,
-                                                         const uint64_t* __restrict__ starts,
+                                                         const sid_off_t* __restrict__ starts,
                                                          const uint64_t* __restrict__ hdr, uint64_t n,
                                                          const uint8_t* __restrict__ code,
                                                          const double* __restrict__ hom,
@@ -1778,7 +1779,7 @@ __device__ __noinline__ int local_site_len_text(const char* text, uint64_t len, 
 // general routine (sid_local_len_list_kernel).  The tail-length table is read
 // through the caches (an LDS copy would cost the parse a block per CU).
 __global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
-                                                           const uint64_t* __restrict__ starts,
+                                                           const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ range,
                                                            uint64_t* __restrict__ counts,
                                                            uint64_t* __restrict__ hdr, uint32_t* __restrict__ fb,
@@ -1828,7 +1829,7 @@ __global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __rest
 
 // the record lengths of listed sites (the lines the general routine parsed)
 __global__ __launch_bounds__(TB) void sid_local_len_list_kernel(const char* __restrict__ text, uint64_t len,
-                                                               const uint64_t* __restrict__ starts,
+                                                               const sid_off_t* __restrict__ starts,
                                                                const uint64_t* __restrict__ hdr,
                                                                const uint64_t* __restrict__ counts,
                                                                const uint32_t* __restrict__ list,
@@ -1844,7 +1845,7 @@ __global__ __launch_bounds__(TB) void sid_local_len_list_kernel(const char* __re
 }
 
 __global__ __launch_bounds__(FTB) void sid_local_len_kernel(const char* __restrict__ text, uint64_t len,
-                                                           const uint64_t* __restrict__ starts,
+                                                           const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ hdr, uint64_t n,
                                                            const uint64_t* __restrict__ counts,
                                                            const uint8_t* __restrict__ len1,
@@ -1880,7 +1881,7 @@ __global__ __launch_bounds__(FTB) void sid_local_len_kernel(const char* __restri
 }
 
 __global__ __launch_bounds__(TB) void sid_local_fixlen_kernel(const char* __restrict__ text, uint64_t len,
-                                                             const uint64_t* __restrict__ starts,
+                                                             const sid_off_t* __restrict__ starts,
                                                              const uint64_t* __restrict__ hdr,
                                                              const uint64_t* __restrict__ counts,
                                                              const uint32_t* __restrict__ miss,
@@ -2083,7 +2084,7 @@ __device__ __noinline__ void miss_put(const char* text, uint64_t len, Head h, ui
 // their counts (the entry and the bases come with the word)
 template <bool CLS>
 __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const char* __restrict__ text, uint64_t len,
-                                                           const uint64_t* __restrict__ starts,
+                                                           const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ hdr, uint64_t n,
                                                            const uint64_t* __restrict__ counts,
                                                            const uint32_t* __restrict__ cwords,
@@ -2204,7 +2205,7 @@ __device__ __forceinline__ int lynch_rec_len(const Head& h, uint32_t tail)
 }
 
 __global__ __launch_bounds__(FTB) void sid_lynch_len_kernel(const char* __restrict__ text, uint64_t len,
-                                                           const uint64_t* __restrict__ starts,
+                                                           const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ hdr, uint64_t n,
                                                            const uint64_t* __restrict__ counts, sid_lynch_fmt V,
                                                            uint32_t* __restrict__ bsum)
@@ -2287,7 +2288,7 @@ __device__ __noinline__ void lynch_put_or(const char* text, uint64_t len, Head h
 }
 
 __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_lynch_put_kernel(const char* __restrict__ text, uint64_t len,
-                                                                          const uint64_t* __restrict__ starts,
+                                                                          const sid_off_t* __restrict__ starts,
                                                                           const uint64_t* __restrict__ hdr, uint64_t n,
                                                                           const uint64_t* __restrict__ counts,
                                                                           sid_lynch_fmt V,
@@ -2421,8 +2422,9 @@ __device__ __forceinline__ void dd_acc(sid_dd& a, double t)
 // waves per SIMD) and the latency-bound walk ran at that occupancy.
 // Phase 1 stores the two per-read sums as double-double: the hi parts in
 // hom/het (phase 2 overwrites them), the lo parts in lo2.
+template <class Off>
 __global__ __launch_bounds__(TB) void sid_quality_sum_kernel(const char* __restrict__ text, uint64_t len,
-                                                             const uint64_t* __restrict__ starts,
+                                                             const Off* __restrict__ starts,
                                                              const uint64_t* __restrict__ counts, uint64_t n,
                                                              const double* __restrict__ g_qtab,
                                                              double* __restrict__ hom, double* __restrict__ het,
@@ -2990,7 +2992,8 @@ extern "C" int sid_format_g6_device(sid_ctx* ctx, const double* d_v, size_t n, c
 // Host tables: the four per-quality terms (glibc pow/log through volatile
 // pointers, so no compiler rewrite of pow(10, x)) and log_gamma up to the
 // largest n = count[ref0] + count[ref1] of the sites.
-static int quality_run(sid_ctx* ctx, const char* text, uint64_t len, const uint64_t* starts, const uint64_t* counts,
+template <class Off>
+static int quality_run(sid_ctx* ctx, const char* text, uint64_t len, const Off* starts, const uint64_t* counts,
                        uint64_t n, uint8_t* code, double* hom_conf, double* het_conf, hipStream_t st)
 {
     if (n == 0) return SID_OK;
@@ -3137,7 +3140,8 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
             if (p) (void)hipFree(p);
         W->lb = nullptr;
         W->cls = nullptr;
-        W->starts = W->counts = W->hdr = nullptr;
+        W->starts = nullptr;
+        W->counts = W->hdr = nullptr;
         W->fb = nullptr;
         W->code = nullptr;
         W->hom = W->het = nullptr;
@@ -3145,7 +3149,7 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         W->boff = nullptr;
         W->site_cap = 0;
         const uint64_t nb = (m + TB - 1) / TB + 1;
-        WCHECK(hipMalloc(&W->starts, m * 8));
+        WCHECK(hipMalloc(&W->starts, m * sizeof(sid_off_t)));
         WCHECK(hipMalloc(&W->counts, m * 8));
         WCHECK(hipMalloc(&W->cls, m * 4));
         WCHECK(hipMalloc(&W->hdr, m * 16));
@@ -3186,6 +3190,7 @@ int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     const uint64_t t0 = c0 & ~(uint64_t)15;
     const uint64_t ntiles = c1 > c0 ? (c1 - t0 + IX_TILE - 1) / IX_TILE : 0;
     if (ntiles * IX_SUB > W->tile_cap) return SID_EINVAL;
+    if (c1 > UINT32_MAX) return SID_ERANGE;   // line offsets are 32-bit (sid_off_t)
     if (ntiles == 0) {
         WCHECK(hipMemsetAsync(W->state, 0, 4 * sizeof(uint64_t), st));
         WCHECK(hipMemsetAsync(W->state + 4, 0xFF, sizeof(uint64_t), st));
@@ -3253,7 +3258,7 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
         WCHECK(hipMemsetAsync(fbn, 0, 2 * sizeof *fbn, st));
         sid_parse_coop_kernel<<<(unsigned)((n + TB - 1) / TB), TB, 0, st>>>(
             base, c1, t0, (const uint64_t*)W->lowm, W->starts, W->state + 1, W->counts, W->hdr, W->fb, fbn);
-        sid_parse_kernel<true><<<PC_LIST_GRID, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr,
+        sid_parse_kernel<true, sid_off_t><<<PC_LIST_GRID, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr,
                                                             fb2, fbn + 1, W->fb, fbn);
         sid_parse_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr, fb2,
                                                     fbn + 1, (unsigned long long*)(W->state + 4), 0);
