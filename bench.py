@@ -710,7 +710,7 @@ def valu_issue(stage, sites, launch_ms, kernels):
 
 def pmc_traffic(stage, sites):
     """HBM bytes per launch of the stage from the committed PMC summary
-    (tools/pmc_traffic.py over separate FETCH_SIZE / WRITE_SIZE passes), scaled
+    (tools/pmc_stages.py over separate FETCH_SIZE / WRITE_SIZE passes), scaled
     to this launch's sites; None when absent."""
     p = pmc_file(stage)
     try:

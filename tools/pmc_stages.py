@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-stage HBM traffic of the engine from the rocprofv3 --pmc passes of
-tools/gpu_pmc_c2.sh, written as profiles/pmc_<stage>_<tag>.json for bench.py's
+tools/gpu/profile.sh, written as profiles/pmc_<stage>_<tag>.json for bench.py's
 roofline.traffic (bytes per site x the sites of a launch).
 
 Bytes per launch of a kernel: FETCH_SIZE x 1024 x 2 (gfx950 reports half the
