@@ -218,14 +218,16 @@ def stage_bytes(stage, text_per_site, csv_per_site, fused):
         return 2 * 4 / 512 + 8 / 512
     if pl and stage in ("parse", "fmt_write"):
         # the fused parse writes each site's 4 B class word instead of its 8 B
-        # counts (textpath.hip local_word), which the writer reads instead
-        return {"parse": text_per_site + text_per_site / 8 + 8 + 4 + 16,
+        # counts (textpath.hip local_word), which the writer reads instead;
+        # line offsets 4 B (sid_off_t), written by the emit, read by the parse
+        return {"parse": text_per_site + text_per_site / 8 + 4 + 4 + 4 + 16,
                 "fmt_write": 4 + 16 + csv_per_site}[stage]
     return {
         "index": text_per_site + text_per_site / 8,    # text read once, line-start masks written
-        # text read; line-start masks (1/8 of the text) and offsets read back;
-        # counts (8) and the formatter's header pair (16) written
-        "parse": text_per_site + text_per_site / 8 + 8 + 8 + 16,
+        # text read; line-start masks (1/8 of the text) read back, 4 B line
+        # offsets written and read; counts (8) and the formatter's header pair
+        # (16) written
+        "parse": text_per_site + text_per_site / 8 + 4 + 4 + 8 + 16,
         "call": 8 + 17,                                # counts in, code + confs out (Lynch lookup, quality)
         "hist": 8,                                     # counts read
         # formatter: the site's counts (or code + confs) and header pair read
@@ -647,7 +649,7 @@ def generate_resident(torch, sid_amd, dev, gpu, cfg, first, n):
 
 
 VALU_ISSUE_PER_S = 256 * 4 / 2 * 2.4e9   # wave64 VALU instructions/s: 1024 SIMDs, one per 2 cycles, 2.4 GHz
-PMC_ROUND = os.environ.get("SID_PMC_ROUND", "r03")
+PMC_ROUND = os.environ.get("SID_PMC_ROUND", "r04")
 
 
 def pcie_ceiling(text_bytes, csv_bytes, lynch, step_s):
@@ -681,7 +683,7 @@ def pmc_file(stage):
 
 def valu_issue(stage, sites, launch_ms, kernels):
     """The stage's VALU work against the chip's VALU issue rate: SQ_INSTS_VALU
-    per site of its kernels (the committed PMC pass, tools/gpu_pmc_c2.sh) x
+    per site of its kernels (the committed PMC pass, tools/gpu/profile.sh) x
     the sites of a launch, at one wave64 instruction per SIMD per 2 cycles
     (MI355X_MICROARCH.md); None when absent."""
     try:

@@ -564,10 +564,21 @@ extern "C" int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg
         d->index = i;
         d->device = (e->cfg.first_device + i / lanes) % nvis;
         d->pool.device = d->device;
-        int rc = sid_create(d->device, &e->opts, &d->ctx);
+        e->devs.push_back(std::move(d));
+    }
+    // every pipeline's context (class tables, the first kernel launches on
+    // its GPU), streams and events: one thread per GPU, its pipelines in
+    // order -- the GPUs' start-up costs (tens of ms each) overlap instead of
+    // adding up on a whole node
+    std::vector<int> rcs(D, SID_OK);
+    // (the streams -- a hardware queue each, ~8 ms apiece -- are created on a
+    // second thread while sid_create builds the class tables)
+    auto make = [&](int i) {
+        Dev* d = e->devs[i].get();
         hipError_t x = hipSuccess;
-        if (rc == SID_OK) {
-            x = hipStreamCreateWithFlags(&d->s_up, hipStreamNonBlocking);
+        std::thread qs([&] {
+            x = hipSetDevice(d->device);
+            if (x == hipSuccess) x = hipStreamCreateWithFlags(&d->s_up, hipStreamNonBlocking);
             if (x == hipSuccess) x = hipStreamCreateWithFlags(&d->s_comp, hipStreamNonBlocking);
             if (x == hipSuccess) x = hipStreamCreateWithFlags(&d->s_d2h, hipStreamNonBlocking);
             if (x == hipSuccess) x = hipHostMalloc((void**)&d->h_small, 128, hipHostMallocDefault);
@@ -576,14 +587,27 @@ extern "C" int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg
                 if (x == hipSuccess) x = hipEventCreateWithFlags(&s.ev_up, hipEventDisableTiming);
                 if (x == hipSuccess) x = hipEventCreateWithFlags(&s.ev_free, hipEventDisableTiming);
             }
-            if (x != hipSuccess) rc = sid_set_hip_error(x);
-        }
-        e->devs.push_back(std::move(d));
+        });
+        int rc = sid_create(d->device, &e->opts, &d->ctx);
+        qs.join();
+        if (rc == SID_OK && x != hipSuccess) rc = sid_set_hip_error(x);
+        rcs[i] = rc;
+    };
+    auto per_gpu = [&](int g) {
+        for (int i = g * lanes; i < std::min(D, (g + 1) * lanes); ++i) make(i);
+    };
+    {
+        std::vector<std::thread> th;
+        for (int g = 1; g < G; ++g) th.emplace_back(per_gpu, g);
+        per_gpu(0);
+        for (auto& t : th) t.join();
+    }
+    (void)hipSetDevice(e->devs[0]->device);
+    for (int rc : rcs)
         if (rc != SID_OK) {
             sid_engine_destroy(e);
             return rc;
         }
-    }
     *out = e;
     return SID_OK;
 }

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -155,6 +156,21 @@ int main(int argc, char** argv)
             std::fprintf(stderr, "host_bw_probe: hipHostMalloc failed\n");
             return 1;
         }
+    // the NUMA node of each buffer's first page (move_pages with no target
+    // nodes reports where a page lives)
+    {
+        std::string nodes_of = "[";
+        for (int t = 0; t < T; ++t) {
+            void* pg = buf[t];
+            int status = -1;
+            if (syscall(SYS_move_pages, 0, 1UL, &pg, nullptr, &status, 0) != 0) status = -1;
+            nodes_of += (t ? ", " : "") + std::to_string(status);
+        }
+        std::printf("{\"probe\": \"buffer_nodes\", \"first_page_node\": %s], \"reader_cpus\": [", nodes_of.c_str());
+        for (int t = 0; t < T; ++t) std::printf("%s%d", t ? ", " : "", order[t]);
+        std::printf("]}\n");
+        std::fflush(stdout);
+    }
     std::atomic<uint64_t> sink{0};
     auto cpu_read = [&](int n, double* secs) {
         std::atomic<int> ready{0};
@@ -208,21 +224,32 @@ int main(int argc, char** argv)
         std::atomic<bool> stop{false};
         std::vector<std::thread> th;
         std::atomic<uint64_t> bytes{0};
+        // the readers' bytes between the DMA's start and end: each reader
+        // times its passes; a pass counts by the part of it inside the window
+        std::vector<std::vector<std::pair<double, double>>> passes(n + 1);
         for (int t = 1; t <= n; ++t)
             th.emplace_back([&, t] {
                 pin(order[t]);
                 while (!stop.load()) {
+                    const double p0 = now();
                     sink ^= stream_read(buf[t], B / 8);
-                    bytes += B;
+                    passes[t].emplace_back(p0, now());
                 }
             });
         const double a = now();
         const double g = dma(2 * R);
-        const double el = now() - a;
+        const double b = now();
         stop = true;
         for (auto& x : th) x.join();
+        double in = 0;
+        for (auto& v : passes)
+            for (auto& pr : v) {
+                const double lo = std::max(pr.first, a), hi = std::min(pr.second, b);
+                if (hi > lo) in += (double)B * (hi - lo) / (pr.second - pr.first);
+            }
+        (void)bytes;
         std::printf("{\"probe\": \"dma_h2d\", \"cpu_readers\": %d, \"GBps\": %.1f, \"cpu_GBps_beside\": %.1f}\n", n, g,
-                    bytes.load() / el / 1e9);
+                    in / (b - a) / 1e9);
         std::fflush(stdout);
     }
     std::fprintf(stderr, "(sink %llu)\n", (unsigned long long)sink.load());

@@ -45,7 +45,7 @@ def main():
             continue
         out = {"stage": stage, "hbm_bytes_per_launch": tot, "sites_per_launch": sites,
                "hbm_bytes_per_site": tot / sites, "kernels": parts,
-               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/gpu_pmc_c2.sh); "
+               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/gpu/profile.sh); "
                          "FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 per launch, averaged over launches",
                "bench": os.path.basename(bench)}
         with open(os.path.join(ROOT, "profiles", f"pmc_{stage}_{tag}.json"), "w") as f:
