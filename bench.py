@@ -476,9 +476,11 @@ def bench_weak(R, a, cfg):
     return out, []
 
 
-# C4 / C5 with the rank's shard resident in HBM: 1 GiB chunks (2 GiB chunks'
-# record bounds and hold arena overran the HBM the text leaves on one GPU)
-STRONG_RESIDENT_CHUNK_MIB = 1024
+# C4 / C5 with the rank's shard resident in HBM: 2 GiB chunks, the engine's
+# default for resident text (C4 on one GPU: 1.50e10 sites/s against 1.41e10
+# with 1 GiB chunks, profiles/bench_c4_r04.json; the device sink formats into
+# a pooled buffer, so the records need no hold arena beside the text)
+STRONG_RESIDENT_CHUNK_MIB = 2048
 
 
 def device_engine(cfg, gpu, chunk_mib, device_sink=1, **kw):

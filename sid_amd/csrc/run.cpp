@@ -815,9 +815,10 @@ namespace {
 bool needs_format_pass1(const sid_engine* e) { return !e->lynch; }
 
 // The device sink (cfg.device_sink 1: records formatted into HBM and dropped)
-// formats every -m local / quality chunk in pass 1: within the hold budget
-// into the hold arena (counted at the emit), past it into a pooled scratch
-// buffer whose bytes are counted and dropped at once.  Nothing is written
+// formats every -m local / quality chunk in pass 1 into a pooled scratch
+// buffer whose bytes are counted and dropped at once (no hold arena, whose
+// HBM a 2 GiB chunk's record bound then lacked beside C4's 244 GB of
+// resident text: SID_ENOMEM, profiles/bench_c4_2gib_chunks_r04.err).  Nothing is written
 // anywhere, so the all-or-nothing output that makes the other sinks hold
 // records until every chunk is validated does not apply, and no chunk is
 // indexed and parsed a second time in pass 2 (C4 on one GPU: 131 GB of
@@ -1147,7 +1148,7 @@ void compute(sid_engine* e, Dev& d, int pass)
         char* out = nullptr;
         uint64_t cap = 0;   // 0: arena memory (never returned to the pool)
         bool via_host = false;   // pass 1: records go on to the host arena (a pooled device buffer meanwhile)
-        bool sunk = false;       // pass 1, device sink past the hold budget: a scratch buffer, dropped
+        bool sunk = false;       // pass 1, device sink: a scratch buffer, dropped
         // -m local: the call fused into the formatter (sid_chunk_local_*)
         const bool fused = e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx);
         // likelihood_ratio / bayes pass 2: the class lookup fused into the
@@ -1173,12 +1174,12 @@ void compute(sid_engine* e, Dev& d, int pass)
                 if (!out) cap = 0;
             }
             if (n == 0 || via_host) {
-            } else if (pass == 1 && sink_all_pass1(e) &&
-                       (d.hold_full.load() || d.hold_used.load() + bound > d.hold_budget)) {
-                d.hold_full = true;
+            } else if (pass == 1 && sink_all_pass1(e)) {
+                // (no hold arena: nothing is emitted, so no record need wait
+                // in HBM; the pooled buffer is reused chunk after chunk)
                 out = d.pool.get(bound, &cap, d.s_comp);
                 sunk = out != nullptr;   // (no HBM for it: formatted in pass 2 instead)
-                if (!out) cap = 0;
+                if (!out) cap = 0, d.hold_full = true;
             } else if (pass == 1 && d.hold_used.load() + bound > d.hold_budget) {
                 d.hold_full = true;   // this chunk and the rest: formatted in pass 2
             } else if (pass == 1) {
