@@ -701,9 +701,16 @@ def valu_issue(stage, sites, launch_ms, kernels):
         return None
     insts = 0.0
     for k in kernels:
+        found = False
         for name, r in pm.items():
             if name.startswith(k.rstrip("*")) and "SQ_INSTS_VALU" in r:
                 insts += r["SQ_INSTS_VALU"] / sites_pmc
+                found = True
+        # a stage kernel the committed counters do not cover (another config's
+        # kernels): no figure rather than a partial one (the rare-path helpers
+        # excepted)
+        if not found and not k.endswith("*") and not any(x in k for x in ("serial", "list", "fixlen")):
+            return None
     if not insts:
         return None
     per_launch = insts * sites

@@ -299,6 +299,22 @@ struct Dev {
     char* hh = nullptr;
     uint64_t hh_cap = 0, hh_off = 0;
     bool hh_full = false;
+    bool hh_alloc(uint64_t bytes)
+    {
+        if (hipHostMalloc((void**)&hh, bytes, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            hh = nullptr;
+            return false;
+        }
+        hh_cap = bytes;
+        return true;
+    }
+    void hh_free()
+    {
+        if (hh) (void)hipHostFree(hh);
+        hh = nullptr;
+        hh_cap = 0;
+    }
     char* hh_take(uint64_t bytes)
     {
         if (!hh || hh_off + bytes > hh_cap) return nullptr;
@@ -363,6 +379,7 @@ struct sid_engine {
     int src = SRC_NONE;
     const char* text = nullptr;     // SRC_HOST / SRC_FILE (mapping) / SRC_DEVICE
     uint64_t text_len = 0;
+    bool reg_upload = false;        // SRC_HOST / SRC_FILE pageable: chunks registered for DMA (upload_register)
     void* map = nullptr;
     uint64_t map_len = 0, map_skew = 0;
     uint64_t synth_seed = 0, synth_first = 0, synth_n = 0, synth_spc = 0, synth_per = 0;
@@ -383,6 +400,7 @@ struct sid_engine {
     // SID_ENGINE_TIMING: host time (ns) spent in compute-stream syncs and in
     // the writer's waits for D2H pieces, printed per phase
     std::atomic<uint64_t> t_comp_sync{0}, t_write_wait{0};
+    std::atomic<uint64_t> reg_chunks{0};   // chunks uploaded from registered pages (upload_register)
     // host-generated input: pinned buffers
     std::vector<char*> gen_buf;
     std::vector<uint64_t> gen_cap;
@@ -643,7 +661,7 @@ extern "C" int sid_engine_destroy(sid_engine* e)
             if (s.ev_free) (void)hipEventDestroy(s.ev_free);
         }
         for (char* p : d->pinned) (void)hipHostFree(p);
-        if (d->hh) (void)hipHostFree(d->hh);
+        d->hh_free();
         for (hipEvent_t ev : d->pinned_ev) (void)hipEventDestroy(ev);
         for (hipEvent_t ev : d->ev_cache) (void)hipEventDestroy(ev);
         for (auto& pr : d->prof_pending) (void)hipEventDestroy(pr.second.first), (void)hipEventDestroy(pr.second.second);
@@ -683,6 +701,33 @@ static void assign_devices(sid_engine* e)
     for (size_t j = 0; j < e->recs.size(); ++j) e->recs[j].dev = (int)(j % D);
 }
 
+// Pageable host text (a file's mapping, or host memory the caller did not
+// pin) is uploaded chunk by chunk from registered pages: each chunk's page-
+// aligned body is pinned (hipHostRegister, read-only) by the uploader while
+// the previous chunk's DMA runs, copied straight from the page cache, and
+// released once its copy is done; the partial pages at its ends (shared with
+// the neighbouring chunks) take the runtime's pageable path.  Without it the
+// runtime copies every byte through its own pinned staging buffers first
+// (a CPU copy per byte: at a whole node's N uploads, host memory traffic).
+// SID_UPLOAD_REGISTER=0: the pageable path for everything (A/B).
+static bool upload_register()
+{
+    static const bool on = [] {
+        const char* v = std::getenv("SID_UPLOAD_REGISTER");
+        return !v || std::atoi(v) != 0;
+    }();
+    return on;
+}
+
+// host memory the runtime already maps for the device (pinned or registered)
+static bool host_pinned(const char* p)
+{
+    hipPointerAttribute_t a;
+    const bool pinned = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+    (void)hipGetLastError();   // (pageable memory: an error to clear, not to report)
+    return pinned;
+}
+
 extern "C" int sid_engine_source_text(sid_engine* e, const char* text, uint64_t len)
 {
     if (!e || (!text && len)) return SID_EINVAL;
@@ -690,6 +735,7 @@ extern "C" int sid_engine_source_text(sid_engine* e, const char* text, uint64_t 
     e->src = SRC_HOST;
     e->text = text;
     e->text_len = len;
+    e->reg_upload = upload_register() && len && !host_pinned(text);
     split_host_text(e, text, len);
     assign_devices(e);
     return SID_OK;
@@ -723,6 +769,7 @@ extern "C" int sid_engine_source_file(sid_engine* e, int fd, uint64_t offset, ui
     e->src = SRC_FILE;
     e->text = (const char*)m + e->map_skew;
     e->text_len = len;
+    e->reg_upload = upload_register();
     split_host_text(e, e->text, len);
     assign_devices(e);
     return SID_OK;
@@ -825,10 +872,122 @@ bool needs_format_pass1(const sid_engine* e) { return !e->lynch; }
 // records against a hold budget of ~16 GB).
 bool sink_all_pass1(const sid_engine* e) { return e->cfg.device_sink == 1 && needs_format_pass1(e); }
 
+// An uploader's registered chunk bodies (upload_register): at most the one
+// being copied and the next, each released once its copy's event is done.
+struct UploadReg {
+    struct Reg {
+        uint64_t j = UINT64_MAX;
+        char* p = nullptr;          // page-aligned body, registered
+        uint64_t n = 0;
+        hipEvent_t ev = nullptr;    // its copy done
+        bool copied = false;
+    };
+    sid_engine* e;
+    bool on;
+    std::deque<Reg> regs;
+    std::vector<hipEvent_t> evs;
+    UploadReg(sid_engine* e_, int pass) : e(e_), on(e_->reg_upload && (pass == 1 || e_->src == SRC_FILE)) {}
+    ~UploadReg()
+    {
+        for (auto& r : regs) {
+            if (r.ev) (void)hipEventSynchronize(r.ev);
+            (void)hipHostUnregister(r.p);
+        }
+        for (auto& r : regs)
+            if (r.ev) (void)hipEventDestroy(r.ev);
+        for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
+    }
+    Reg* find(uint64_t j)
+    {
+        for (auto& r : regs)
+            if (r.j == j) return &r;
+        return nullptr;
+    }
+    // pin chunk j's whole pages (bodies of at least 1 MiB; smaller chunks
+    // take the pageable path, and so does every chunk after a registration
+    // fails)
+    void pin(uint64_t j)
+    {
+        if (!on || j == UINT64_MAX || find(j)) return;
+        const ChunkRec& r = e->recs[j];
+        const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
+        const uintptr_t s = (uintptr_t)(e->text + r.off), t = s + r.len;
+        const uintptr_t a = (s + pg - 1) & ~(uintptr_t)(pg - 1), b = t & ~(uintptr_t)(pg - 1);
+        if (b <= a || b - a < (1u << 20)) return;
+        if (hipHostRegister((void*)a, b - a, hipHostRegisterReadOnly) != hipSuccess &&
+            ((void)hipGetLastError(), hipHostRegister((void*)a, b - a, hipHostRegisterDefault) != hipSuccess)) {
+            (void)hipGetLastError();   // not an error: the pageable path from now on
+            on = false;
+            return;
+        }
+        Reg g;
+        g.j = j;
+        g.p = (char*)a;
+        g.n = b - a;
+        regs.push_back(g);
+    }
+    void ahead(uint64_t j)
+    {
+        release_done();
+        pin(j);
+    }
+    // chunk j (pinned now if it is not yet) into dst on stream st
+    hipError_t copy(char* dst, uint64_t j, hipStream_t st)
+    {
+        const ChunkRec& r = e->recs[j];
+        const char* src = e->text + r.off;
+        pin(j);
+        Reg* g = find(j);
+        if (!g) return hipMemcpyAsync(dst, src, r.len, hipMemcpyHostToDevice, st);
+        const uint64_t head = (uint64_t)(g->p - src), body = g->n, tail = r.len - head - body;
+        hipError_t x = hipSuccess;
+        if (head) x = hipMemcpyAsync(dst, src, head, hipMemcpyHostToDevice, st);
+        if (x == hipSuccess) x = hipMemcpyAsync(dst + head, g->p, body, hipMemcpyHostToDevice, st);
+        if (x == hipSuccess) e->reg_chunks++;
+        if (x == hipSuccess && tail) x = hipMemcpyAsync(dst + head + body, g->p + body, tail, hipMemcpyHostToDevice, st);
+        if (x == hipSuccess) {
+            if (evs.empty()) {
+                hipEvent_t ev = nullptr;
+                x = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+                if (x == hipSuccess) evs.push_back(ev);
+            }
+            if (x == hipSuccess) {
+                g->ev = evs.back();
+                evs.pop_back();
+                x = hipEventRecord(g->ev, st);
+                g->copied = true;
+            }
+        }
+        return x;
+    }
+    // unregister the bodies whose copies are done (in copy order)
+    void release_done()
+    {
+        while (!regs.empty() && regs.front().copied && hipEventQuery(regs.front().ev) == hipSuccess) {
+            (void)hipHostUnregister(regs.front().p);
+            evs.push_back(regs.front().ev);
+            regs.pop_front();
+        }
+        (void)hipGetLastError();   // (hipEventQuery's "not ready")
+    }
+};
+
 // the uploader of device d: the chunks of `list` into device buffers, in order
 void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass)
 {
     if (hipSetDevice(d.device) != hipSuccess) return (void)fail(e, SID_EHIP);
+    UploadReg reg(e, pass);
+    // the chunk this uploader copies after j from the host (UINT64_MAX: none)
+    size_t at = 0;
+    auto next_of = [&](uint64_t j) -> uint64_t {
+        while (at < list.size() && list[at] != j) ++at;
+        for (size_t k = at + 1; k < list.size(); ++k) {
+            const ChunkRec& q = e->recs[list[k]];
+            if (pass == 2 && (q.host1 || q.sunk || q.held || q.kept)) continue;
+            return list[k];
+        }
+        return UINT64_MAX;
+    };
     for (uint64_t j : list) {
         if (e->rc.load() != SID_OK) break;
         if (pass == 1 && j > e->first_err.load()) break;
@@ -898,11 +1057,15 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
         }
         uint64_t len = r.len;
         if (e->src == SRC_HOST || e->src == SRC_FILE) {
-            if (len) x = hipMemcpyAsync(dst, e->text + r.off, len, hipMemcpyHostToDevice, d.s_up);
+            if (len) x = reg.copy(dst, j, d.s_up);
+            // the next chunk's pages pinned while this copy runs; the ones
+            // whose copies are done released
+            if (x == hipSuccess) reg.ahead(next_of(j));
             if (e->src == SRC_FILE && x == hipSuccess && e->text_len > (8ull << 30)) {
                 // large mapped inputs: drop the chunk's page-table entries once
                 // copied (the page cache keeps the data; RSS stays bounded)
                 x = hipStreamSynchronize(d.s_up);
+                reg.release_done();
                 const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE);
                 const uint64_t a = (e->map_skew + r.off + pg - 1) & ~(pg - 1);
                 const uint64_t b = (e->map_skew + r.off + len) & ~(pg - 1);
@@ -1397,9 +1560,12 @@ static void timing_report(sid_engine* e, const char* phase, double s)
     static const bool on = std::getenv("SID_ENGINE_TIMING") != nullptr;
     if (on)
         std::fprintf(stderr,
-                     "{\"engine_phase\": \"%s\", \"s\": %.6f, \"compute_sync_s\": %.6f, \"writer_wait_s\": %.6f}\n",
-                     phase, s, e->t_comp_sync.load() * 1e-9, e->t_write_wait.load() * 1e-9);
+                     "{\"engine_phase\": \"%s\", \"s\": %.6f, \"compute_sync_s\": %.6f, \"writer_wait_s\": %.6f, "
+                     "\"chunks_registered\": %llu}\n",
+                     phase, s, e->t_comp_sync.load() * 1e-9, e->t_write_wait.load() * 1e-9,
+                     (unsigned long long)e->reg_chunks.load());
     e->t_comp_sync = e->t_write_wait = 0;
+    e->reg_chunks = 0;
 }
 
 static void reset_run(sid_engine* e)
@@ -1465,11 +1631,8 @@ static int setup_budgets(sid_engine* e)
         // the host arena: pinned (and so populated) once, reused by every run
         const uint64_t hb = e->cfg.device_sink == 1 ? 0 : e->cfg.host_hold_bytes;
         if (hb && d.hh_cap < hb) {
-            if (d.hh) (void)hipHostFree(d.hh);
-            d.hh = nullptr;
-            d.hh_cap = 0;
-            if (hipHostMalloc((void**)&d.hh, hb, hipHostMallocDefault) != hipSuccess) return SID_ENOMEM;
-            d.hh_cap = hb;
+            d.hh_free();
+            if (!d.hh_alloc(hb)) return SID_ENOMEM;
         }
     }
     return SID_OK;

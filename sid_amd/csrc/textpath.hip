@@ -1385,12 +1385,12 @@ struct Head {
 // hdr: the parse's (header word, chrom's first 8 bytes) of the site, or null;
 // the line's offset (*startp) is read only when the text is (a chrom longer
 // than 8 bytes, or no valid header word)
+// (hw: the header pair, loaded by the caller)
 template <class Off>
-__device__ __forceinline__ Head site_head(Reader& R, const Off* startp, const uint64_t* hdr)
+__device__ __forceinline__ Head site_head_hw(Reader& R, const Off* startp, const ulonglong2 hw)
 {
     Head h;
     h.c8 = 0;
-    const ulonglong2 hw = hdr ? *(const ulonglong2*)hdr : make_ulonglong2(0, 0);
     if (hw.x >> 63) {
         h.clen = (uint32_t)(hw.x >> 32) & 0xFFFu;
         h.pos = (int32_t)(uint32_t)hw.x;
@@ -1410,6 +1410,12 @@ __device__ __forceinline__ Head site_head(Reader& R, const Off* startp, const ui
     }
     h.pos = atoi_like(R, pb, q);
     return h;
+}
+
+template <class Off>
+__device__ __forceinline__ Head site_head(Reader& R, const Off* startp, const uint64_t* hdr)
+{
+    return site_head_hw(R, startp, hdr ? *(const ulonglong2*)hdr : make_ulonglong2(0, 0));
 }
 
 // record length of a site (call.hpp:29-38): 0 for a filtered profile (no
@@ -1865,14 +1871,16 @@ __global__ __launch_bounds__(FTB) void sid_local_len_kernel(const char* __restri
         int l = 0;
         if (i < n) {
             uint32_t f, s, nf, ns, cov;
-            sid_major(counts[i], f, s, nf, ns, cov);
+            const uint64_t w = counts[i];
+            const ulonglong2 hw = *(const ulonglong2*)(hdr + 2 * i);   // in flight beside the class lookup
+            sid_major(w, f, s, nf, ns, cov);
             const uint32_t k = local_entry(nf, ns, cov - nf - ns);
             const uint32_t L = k < SID_TAB_N ? L1[k] : k != UINT32_MAX ? len2[k - SID_TAB_N] : 0xFFu;
             if (L == 0xFFu) {
                 miss[atomicAdd(nmiss, 1ull)] = (uint32_t)i;   // its bytes: the fix-up's
             } else {
                 Reader R{text, len};
-                l = local_rec_len(site_head(R, starts + i, hdr + 2 * i), L);
+                l = local_rec_len(site_head_hw(R, starts + i, hw), L);
             }
         }
         const uint32_t tot = block_sum<FTB>((uint32_t)l);
@@ -2119,6 +2127,9 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
             sid_major(counts[i], f, s, nf, ns, cov);
             k = local_entry(nf, ns, cov - nf - ns);
         }
+        // (the record tail's load issued before the header pair's was
+        // measured slower here: 0.88-0.89 vs 0.86-0.87 ms per C2 step; in
+        // the Lynch writer, which looks the class up first, it pays)
         {
             Reader R{text, len};
             h = site_head(R, starts + i, hdr + 2 * i);
@@ -2223,6 +2234,7 @@ __global__ __launch_bounds__(FTB) void sid_lynch_len_kernel(const char* __restri
         int l = 0;
         if (i < n && !V.empty) {
             const uint64_t w = counts[i];
+            const ulonglong2 hw = *(const ulonglong2*)(hdr + 2 * i);   // in flight beside the class lookup
             const uint32_t d = sid_dense_code(w);
             uint32_t L = 0;
             if (d != SID_DENSE_NONE) {
@@ -2233,7 +2245,7 @@ __global__ __launch_bounds__(FTB) void sid_lynch_len_kernel(const char* __restri
             }
             if (L) {
                 Reader R{text, len};
-                l = lynch_rec_len(site_head(R, starts + i, hdr + 2 * i), L);
+                l = lynch_rec_len(site_head_hw(R, starts + i, hw), L);
             }
         }
         const uint32_t tot = block_sum<FTB>((uint32_t)l);
@@ -2305,7 +2317,9 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_lynch_put_kernel(const
     Head h{0, 0, 0, 0};
     uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0, e2 = e0, e3 = e0;
     if (i < n && !V.empty) {
-        const uint32_t idx = lynch_class(counts[i], V);
+        const uint64_t w = counts[i];
+        const ulonglong2 hw = *(const ulonglong2*)(hdr + 2 * i);   // in flight beside the class lookup
+        const uint32_t idx = lynch_class(w, V);
         if (idx != 0xFFFFFFFFu) {
             const uint4* e = (const uint4*)(V.lstr + (size_t)idx * SID_LSTR_BYTES);
             e0 = e[0];
@@ -2313,7 +2327,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_lynch_put_kernel(const
             e2 = e[2];
             e3 = e[3];
             Reader R{text, len};
-            h = site_head(R, starts + i, hdr + 2 * i);
+            h = site_head_hw(R, starts + i, hw);
             l = lynch_rec_len(h, e0.x & 0xFFu);
         }
     }
@@ -2842,7 +2856,7 @@ extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, 
     // and the allocation holds up the device work: 1 Mi-site pieces cost
     // 33-41 ms before the first write at 50M sites, 256 Ki-site pieces 14-16
     // ms with the same D2H rate; 64 Ki-site pieces D2H slower
-    // (tools/e2e_probe.sh; SID_FMT_PIECE_BLOCKS overrides, measurement)
+    // (round-1 measurement; SID_FMT_PIECE_BLOCKS overrides)
     size_t PB = 1024;
     if (const char* e = std::getenv("SID_FMT_PIECE_BLOCKS")) PB = std::max(1, std::atoi(e));
     const size_t nb = (n + TB - 1) / TB;

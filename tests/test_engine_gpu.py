@@ -109,6 +109,26 @@ def test_first_error_in_a_late_chunk(sid, oracle, tmp_path):
             assert a.stderr == bb.stderr, (tag, extra)
 
 
+def test_dense_short_lines(sid, oracle, tmp_path):
+    """More than 2048 line starts in a 16 KiB index tile (lines of a few bytes,
+    all malformed): the offset emit stores them directly instead of through
+    its LDS buffer (textpath.hip EMIT_CAP), and the first malformed line is
+    still the first of them."""
+    good = b"".join(b"chr1\t%d\tA\t3\t.,.\tIII\n" % i for i in range(1, 2000))
+    cases = {"x": good * 2 + b"x\n" * 9000 + good, "tabs": good + b"1\t2\n" * 5000 + good * 2,
+             "short_first": b"ab\n" * 6000 + good}
+    for tag, text in cases.items():
+        p = tmp_path / f"{tag}.plp"
+        p.write_bytes(text)
+        for extra, flags in (([], []), (["--chunk-bytes", "20000", "--devices", "2"], []),
+                             (["--chunk-bytes", "20000"], ["-R", "-m", "likelihood_ratio"])):
+            b = oracle.run_cli(flags + [str(p)])
+            a = run(sid.CLI_PATH, extra + flags + [str(p)])
+            assert a.returncode == b.returncode != 0, (tag, extra, a.returncode, b.returncode)
+            assert a.stdout == b.stdout, (tag, extra)
+            assert a.stderr == b.stderr, (tag, extra)
+
+
 def test_bayes_without_coverage_prints_the_header(sid, oracle, tmp_path):
     """callBayes on a file where no profile reaches coverage 4: the estimate
     runs on an empty table, no record survives, exit 0 (call.cpp:145-211)."""

@@ -46,10 +46,15 @@ def main():
                 if p.returncode != 0:
                     print(spec, "failed", p.returncode, p.stderr.decode()[-300:])
                     sys.exit(1)
-                st = json.loads(p.stderr.decode().strip().splitlines()[-1])
+                lines = p.stderr.decode().strip().splitlines()
+                st = json.loads(lines[-1])
+                # SID_ENGINE_TIMING=1: the engine's phase lines before it
+                eng = [json.loads(x) for x in lines[:-1] if x.startswith('{"engine_phase"')]
                 rec = {"bin": spec, "round": r, "wall_s": dt, "create_s": st.get("create_s"),
                        "total_s": st.get("total_s"), "emit_s": st.get("emit_s"), "parse_s": st.get("parse_s"),
-                       "main_s": st["main_exit_unix"] - st["main_entry_unix"]}
+                       "main_s": st["main_exit_unix"] - st["main_entry_unix"],
+                       "chunks": st.get("chunks"),
+                       "chunks_registered": sum(x.get("chunks_registered", 0) for x in eng) if eng else None}
                 fo.write(json.dumps(rec) + "\n")
                 fo.flush()
                 if r:   # the first round warms the page cache and the code objects

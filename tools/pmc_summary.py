@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 --pmc passes of tools/gpu_pmc_c2.sh: per kernel, the
+"""Summarise the rocprofv3 --pmc passes of tools/gpu/profile.sh: per kernel, the
 average per launch of every counter collected, HBM bytes per launch
 (FETCH_SIZE x 1024 x 2 -- gfx950 reports half the bytes of wide coalesced
 reads, MI355X_MICROARCH.md §HBM -- + WRITE_SIZE x 1024) and the wave
