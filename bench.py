@@ -540,10 +540,11 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
     dom = max(roofs, key=lambda k: roofs[k]["ms_per_step"])
     d = roofs[dom]
     roofline = {"bound": "hbm", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": d["frac"], "traffic": pmc_traffic(dom, per_launch_sites),
+                "frac": d["frac"],
+                "traffic": pmc_traffic(dom, per_launch_sites, stage_kernels(dom, fused, tps), a.config),
                 "kernel": f"engine stage '{dom}'", "stage_kernels": stage_kernels(dom, fused, tps),
                 "launch_ms": d["launch_ms"], "sites_per_launch": per_launch_sites, "bytes_per_site": d["bytes_per_site"],
-                "valu": valu_issue(dom, per_launch_sites, d["launch_ms"], stage_kernels(dom, fused, tps)),
+                "valu": valu_issue(dom, per_launch_sites, d["launch_ms"], stage_kernels(dom, fused, tps), a.config),
                 "source": "device_path: HIP event pairs around each engine stage on the compute stream"}
     return {"sites_per_s": sites_all * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
             "stages_ms": stages, "stage_roofline": roofs, "roofline": roofline,
@@ -675,28 +676,33 @@ def pcie_ceiling(text_bytes, csv_bytes, lynch, step_s):
             "GBps_d2h": d2h, "source": "profiles/pcie_probe_r03.jsonl (pinned copies, best of the probe's runs)"}
 
 
-def pmc_file(stage):
-    for r in (PMC_ROUND, "r02"):
-        p = os.path.join(ROOT, "profiles", f"pmc_{stage}_{r}.json")
+def pmc_file(stage, config="C2"):
+    """The committed per-stage PMC file: the config's own (pmc_<stage>_<round>_<config>.json)
+    before the C2 one."""
+    names = ([f"pmc_{stage}_{PMC_ROUND}_{config.lower()}.json"] if config != "C2" else []) + \
+        [f"pmc_{stage}_{r}.json" for r in (PMC_ROUND, "r02")]
+    for n in names:
+        p = os.path.join(ROOT, "profiles", n)
         if os.path.exists(p):
             return p
     return None
 
 
-def valu_issue(stage, sites, launch_ms, kernels):
+def valu_issue(stage, sites, launch_ms, kernels, config="C2"):
     """The stage's VALU work against the chip's VALU issue rate: SQ_INSTS_VALU
     per site of its kernels (the committed PMC pass, tools/gpu/profile.sh) x
     the sites of a launch, at one wave64 instruction per SIMD per 2 cycles
     (MI355X_MICROARCH.md); None when absent."""
     try:
         summ = None
-        for r in (PMC_ROUND, "r02"):
-            p = os.path.join(ROOT, "profiles", f"pmc_c2_{r}_summary.json")
+        for n in [f"pmc_{config.lower()}_{PMC_ROUND}_summary.json"] + [f"pmc_c2_{r}_summary.json"
+                                                                     for r in (PMC_ROUND, "r02")]:
+            p = os.path.join(ROOT, "profiles", n)
             if os.path.exists(p):
                 summ = p
                 break
         pm = json.load(open(summ))
-        sites_pmc = json.load(open(pmc_file(stage)))["sites_per_launch"]
+        sites_pmc = json.load(open(pmc_file(stage, config)))["sites_per_launch"]
     except Exception:
         return None
     insts = 0.0
@@ -719,13 +725,22 @@ def valu_issue(stage, sites, launch_ms, kernels):
             "note": "VALU instructions of the stage's kernels (PMC) at the chip's issue rate vs the measured launch"}
 
 
-def pmc_traffic(stage, sites):
+def pmc_traffic(stage, sites, kernels=None, config="C2"):
     """HBM bytes per launch of the stage from the committed PMC summary
     (tools/pmc_stages.py over separate FETCH_SIZE / WRITE_SIZE passes), scaled
-    to this launch's sites; None when absent."""
-    p = pmc_file(stage)
+    to this launch's sites; None when absent, or when the committed pass
+    measured other kernels for this stage (the counters are C2's: a C3 line's
+    parse stage runs sid_parse_kernel, not sid_parse_len_kernel)."""
+    p = pmc_file(stage, config)
     try:
-        return json.load(open(p))["hbm_bytes_per_site"] * sites
+        d = json.load(open(p))
+        measured = d.get("kernels", {})
+        for k in kernels or []:
+            if k.endswith("*") or any(x in k for x in ("serial", "list", "fixlen")):
+                continue
+            if not measured.get(k):
+                return None
+        return d["hbm_bytes_per_site"] * sites
     except Exception:
         return None
 

@@ -1213,7 +1213,7 @@ void compute(sid_engine* e, Dev& d, int pass)
         hipError_t x = hipSuccess;
         if (L.ev && !pre_indexed) x = hipStreamWaitEvent(d.s_comp, L.ev, 0);
         const bool P = e->prof;
-        if (P) d.prof_chunks++;
+        if (P && pass == 1) d.prof_chunks++;   // chunks, not passes: a Lynch run formats each chunk again in pass 2
         W.lens_ready = false;   // (set by this chunk's parse when it computes the -m local record lengths)
         W.cls_ready = false;    // (... and the class words)
         const uint64_t tbytes = L.c1 - (L.c0 & ~(uint64_t)15);

@@ -20,8 +20,9 @@ STAGES = {   # the scan kernels (shared by the index and the formatter, ~20 us) 
     "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_len_kernel", "sid_parse_serial_kernel",
               "sid_local_len_list_kernel"],
     "call": ["sid_lookup_rec_kernel"],
-    "fmt_len": ["sid_local_len_kernel", "sid_local_fixlen_kernel", "sid_fmt_blen_kernel"],
-    "fmt_write": ["sid_local_put_kernel", "sid_fmt_put_kernel"],
+    "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel", "sid_hist_list_kernel"],
+    "fmt_len": ["sid_local_len_kernel", "sid_local_fixlen_kernel", "sid_fmt_blen_kernel", "sid_lynch_len_kernel"],
+    "fmt_write": ["sid_local_put_kernel", "sid_fmt_put_kernel", "sid_lynch_put_kernel"],
 }
 
 
