@@ -880,6 +880,71 @@ __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, ui
     return true;
 }
 
+// read_bases_lut for a line worked by a quad of 4 lanes (long lines, the
+// quad parse below): window k of token 4 (16-B aligned, from q's window) goes
+// to lane k mod 4, so a quad reads 64 consecutive bytes a step and a line
+// needs a quarter of the steps.  A window's '^' carry-in is whether the byte
+// before it is a '^' (the previous window's lane; a '^' that is itself
+// skipped is a '^' run, which fails in that lane); the token ends in the
+// quad's first window holding its end, and the windows after it are dropped.
+// Every lane of the quad returns the same result.
+__device__ __forceinline__ bool read_bases_quad(const char* __restrict__ text, uint64_t len, uint64_t q, uint32_t kd,
+                                                const uint32_t* lut, const uint4* first, uint64_t* out)
+{
+    const uint32_t j = threadIdx.x & 3u;
+    const uint64_t a0 = q & ~(uint64_t)15;
+    uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0, acc = 0;
+    bool bad = false;
+    uint32_t prev3 = 0;   // lane 3's last byte was a '^' (the previous step's window 4(it-1)+3)
+    for (uint32_t it = 0;; ++it) {   // uniform across the quad
+        const uint32_t k = 4u * it + j;
+        const uint64_t a = a0 + 16ull * k;
+        const uint4 v = k == 0 ? *first : *(const uint4*)(text + a);   // (past the line's end: the readable padding)
+        const int room = len > a ? (int)min(len - a, (uint64_t)16) : 0;
+        const uint32_t lead = k == 0 ? (uint32_t)(q & 15) : 0u;
+        const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
+        const uint32_t last_caret = (v.w >> 24) == 0x5Eu ? 1u : 0u;
+        const uint32_t from_left = (uint32_t)__shfl((int)last_caret, (int)((j + 3u) & 3u), 4);
+        const uint32_t cin = k == 0 ? 0u : (j ? from_left : prev3);
+        prev3 = (uint32_t)__shfl((int)last_caret, 3, 4);
+        bool done = false, wbad = false;
+        uint32_t carry = cin << 7;
+        const uint32_t w = rb_window<true>(v, valid, room, lut, done, carry, wbad);
+        // the quad's first window that ends the token (or the text)
+        const uint64_t bal = __ballot(done);
+        const uint32_t qb = (uint32_t)(bal >> (threadIdx.x & 60u)) & 15u;
+        const bool keep = qb == 0 || j <= (uint32_t)__builtin_ctz(qb);
+        if (keep) {
+            nA += w & 31u;
+            nC += (w >> 5) & 31u;
+            nG += (w >> 10) & 31u;
+            nT += (w >> 15) & 31u;
+            nM += (w >> RB_M_SHIFT) & 31u;
+            acc |= w;
+            bad = bad || wbad;
+        }
+        if (qb) break;
+    }
+#pragma unroll
+    for (int m = 1; m < 4; m <<= 1) {
+        nA += (uint32_t)__shfl_xor((int)nA, m, 4);
+        nC += (uint32_t)__shfl_xor((int)nC, m, 4);
+        nG += (uint32_t)__shfl_xor((int)nG, m, 4);
+        nT += (uint32_t)__shfl_xor((int)nT, m, 4);
+        nM += (uint32_t)__shfl_xor((int)nM, m, 4);
+        acc |= (uint32_t)__shfl_xor((int)acc, m, 4);
+        bad = __shfl_xor((int)bad, m, 4) != 0 || bad;
+    }
+    if (bad || (acc >> RB_BAD_SHIFT) != 0) return false;
+    nA += kd == K_A ? nM : 0;
+    nC += kd == K_C ? nM : 0;
+    nG += kd == K_G ? nM : 0;
+    nT += kd == K_T ? nM : 0;
+    *out = (uint64_t)(uint16_t)nA | ((uint64_t)(uint16_t)nC << 16) | ((uint64_t)(uint16_t)nG << 32) |
+           ((uint64_t)(uint16_t)nT << 48);
+    return true;
+}
+
 // The fast path of one line (pileup.cpp:13-46 + :70-153 for the lines that
 // need none of the general routine's cases), branch-free over SWAR byte masks:
 //   header   the 48 bytes from the line's 16-B window: separator (' ', '\t')
@@ -896,6 +961,10 @@ __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, ui
 //            first byte < 0x21       -> end of the token, which must be ' ',
 //                                       '\t', '\n' or NUL, else fail
 // Returns false when the line needs the general routine.
+// QUAD: the read bases counted by the line's quad of lanes (read_bases_quad;
+// every lane of the quad parses the same line, so its header is the same in
+// all four)
+template <bool QUAD = false>
 __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, uint64_t len, uint64_t s0,
                                                 const uint8_t* cls, char* stage, uint64_t* out, uint64_t* hdr,
                                                 const uint32_t* rbl)
@@ -1023,6 +1092,8 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     const uint32_t kd = cls[up], kc = cls[lw];
     if (kd >= K_CARET || kc >= K_CARET || kd != kc) return false;
 #if SID_PARSE_LUT
+    if (QUAD)
+        return read_bases_quad(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out);
     return read_bases_lut(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out);
 #else
     return read_bases_fast(text, len, s0 + (uint64_t)t4, kd, out);
@@ -1064,6 +1135,45 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
             *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h[0], h[1]);
         } else {
             fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
+        }
+    }
+}
+
+// sid_parse_kernel for long lines (> 256 B on average: 200x) with a quad of
+// lanes per line (parse_line_fast<true>): 16 lines a wave, each quad reading
+// 64 consecutive bytes of its line a step, instead of 64 lanes walking 64
+// lines 16 bytes at a time (whose in-flight lines are a cache working set
+// the 200x lines overflow, line_walk_grid).  SID_PARSE_QUAD=0: the per-lane
+// kernel on the reduced grid (A/B).
+template <class Off>
+__global__ __launch_bounds__(TB) void sid_parse_quad_kernel(const char* __restrict__ text, uint64_t len,
+                                                            const Off* __restrict__ starts,
+                                                            const uint64_t* __restrict__ range,   // [lo, hi)
+                                                            uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
+                                                            uint32_t* __restrict__ fb, unsigned long long* fbn)
+{
+    __shared__ uint8_t cls[256];
+    __shared__ uint32_t rbl[256];
+    __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
+    if (threadIdx.x < 256) {
+        cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+        rbl[threadIdx.x] = rb_entry(threadIdx.x);
+    }
+    __syncthreads();
+    constexpr uint32_t LPB = TB / 4;   // lines per block step
+    const uint64_t lo = range[0], hi = range[1];
+    const uint64_t stride = (uint64_t)gridDim.x * LPB;
+    for (uint64_t i = lo + (uint64_t)blockIdx.x * LPB + (threadIdx.x >> 2); i < hi; i += stride) {
+        uint64_t c = 0, h[2] = {0, 0};
+        const bool ok = parse_line_fast<true>(text, len, starts[i], cls, stage + threadIdx.x * HDR_BYTES, &c, h, rbl);
+        if ((threadIdx.x & 3u) == 0) {
+            if (ok) {
+                ST_MID(counts + i, c);
+                ST_MID(hdr + 2 * i, h[0]);
+                ST_MID(hdr + 2 * i + 1, h[1]);
+            } else {
+                fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
+            }
         }
     }
 }
@@ -1356,9 +1466,16 @@ static void launch_parse(const char* text, uint64_t len, const Off* starts, cons
         sid_parse_serial_kernel<<<pg, TB, 0, st>>>(text, len, starts, range, counts, hdr, nullptr, nullptr, err, 1);
         return;
     }
-    const unsigned pgf = env ? pg : line_walk_grid(n, len, pg);
+    static const bool quad = !std::getenv("SID_PARSE_QUAD") || std::atoi(std::getenv("SID_PARSE_QUAD")) != 0;
     (void)hipMemsetAsync(fbn, 0, sizeof *fbn, st);
-    sid_parse_kernel<false, Off><<<pgf, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, nullptr, nullptr);
+    if (quad && n && len > 256 * n) {   // long lines: a quad of lanes per line, the full grid
+        const unsigned pq = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + TB / 4 - 1) / (TB / 4), 1), PG);
+        sid_parse_quad_kernel<Off><<<pq, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn);
+    } else {
+        const unsigned pgf = env ? pg : line_walk_grid(n, len, pg);
+        sid_parse_kernel<false, Off><<<pgf, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, nullptr,
+                                                         nullptr);
+    }
     sid_parse_serial_kernel<<<256, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, err, 0);
 }
 

@@ -166,3 +166,22 @@ def test_caret_at_every_window_offset(sid, oracle, tmp_path):
     p.write_bytes(b"\n".join(out) + b"\n")
     for extra in (["--chunk-bytes", str(1 << 20)], ["--chunk-bytes", "7777"]):
         same_as_oracle(sid, oracle, p, [], extra)
+
+
+def test_caret_at_every_window_offset_long_lines(sid, oracle, tmp_path):
+    """The same '^' placements in 200x-long lines (over 256 B on average: the
+    quad parse, textpath.hip sid_parse_quad_kernel): a '^' at a window's last
+    byte skips the first byte of the next window, which another lane of the
+    quad counts; '^^' across that boundary fails in the right lane."""
+    out = []
+    for lead in range(16):
+        for off in range(0, 96):
+            for mq in (b"I", b"^", b"$", b"A"):
+                bases = b"..,,AC.,gt" * 36
+                bases = bases[:off] + b"^" + mq + bases[off:]
+                chrom = b"c" * (1 + lead)
+                out.append(b"\t".join([chrom, str(100 + off).encode(), b"A", b"370", bases, b"I" * 370]))
+    p = tmp_path / "caret_long.plp"
+    p.write_bytes(b"\n".join(out) + b"\n")
+    for extra in (["--chunk-bytes", str(1 << 20)], ["--chunk-bytes", "77777", "--devices", "2"]):
+        same_as_oracle(sid, oracle, p, [], extra)
