@@ -199,6 +199,13 @@ def fmt_kind(cfg):
     return None if os.environ.get("SID_LYNCH_FUSED", "1") == "0" else "lynch"
 
 
+def parse_quad(text_per_site):
+    """Lines over 256 B on average are parsed by a quad of lanes each
+    (textpath.hip sid_parse_quad_kernel;
+    SID_PARSE_QUAD=0: one lane per line)."""
+    return text_per_site > 256 and os.environ.get("SID_PARSE_QUAD", "1") != "0"
+
+
 def parse_len(fused, text_per_site=81.0):
     """-m local: the records' lengths computed by the parse (run.cpp,
     sid_parse_len_kernel; SID_PARSE_LEN=0 keeps the separate length kernel),
@@ -243,9 +250,10 @@ def stage_kernels(stage, fused, text_per_site=81.0):
     pl = parse_len(fused, text_per_site)
     return {
         "index": ["sid_index_count_kernel", "sid_scan_*"],
-        "parse": ["sid_index_emit_kernel"] + (["sid_parse_len_kernel", "sid_parse_serial_kernel",
-                                                 "sid_local_len_list_kernel"] if pl
-                                                else ["sid_parse_kernel", "sid_parse_serial_kernel"]),
+        "parse": ["sid_index_emit_kernel"] + (
+            ["sid_parse_len_kernel", "sid_parse_serial_kernel", "sid_local_len_list_kernel"] if pl
+            else [("sid_parse_quad_kernel" if parse_quad(text_per_site) else "sid_parse_kernel"),
+                  "sid_parse_serial_kernel"]),
         "call": ["sid_lookup_rec_kernel"],
         "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
         "fmt_len": {"local": (["sid_local_fixlen_kernel"] if pl else

@@ -1453,6 +1453,15 @@ static unsigned line_walk_grid(uint64_t n, uint64_t len, unsigned cap)
     return (unsigned)std::min<uint64_t>(cap, (uint64_t)std::max(1L, bpc) * (uint64_t)ncu);
 }
 
+// lines over 256 B on average are parsed by a quad of lanes each
+// (sid_parse_quad_kernel); SID_PARSE_QUAD=0: one lane per line on the
+// reduced grid (A/B)
+static bool parse_quad()
+{
+    static const bool on = !std::getenv("SID_PARSE_QUAD") || std::atoi(std::getenv("SID_PARSE_QUAD")) != 0;
+    return on;
+}
+
 // the two passes over sites [range[0], range[1]) (the range lives on the device)
 template <class Off>
 static void launch_parse(const char* text, uint64_t len, const Off* starts, const uint64_t* range, uint64_t n,
@@ -1466,9 +1475,8 @@ static void launch_parse(const char* text, uint64_t len, const Off* starts, cons
         sid_parse_serial_kernel<<<pg, TB, 0, st>>>(text, len, starts, range, counts, hdr, nullptr, nullptr, err, 1);
         return;
     }
-    static const bool quad = !std::getenv("SID_PARSE_QUAD") || std::atoi(std::getenv("SID_PARSE_QUAD")) != 0;
     (void)hipMemsetAsync(fbn, 0, sizeof *fbn, st);
-    if (quad && n && len > 256 * n) {   // long lines: a quad of lanes per line, the full grid
+    if (parse_quad() && n && len > 256 * n) {   // long lines: a quad of lanes per line, the full grid
         const unsigned pq = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + TB / 4 - 1) / (TB / 4), 1), PG);
         sid_parse_quad_kernel<Off><<<pq, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn);
     } else {
@@ -3357,6 +3365,10 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     // (not for long lines: at 200x the parse runs on a small grid (line_walk_grid),
     // where the fused kernel's register cap costs more than the length kernel:
     // C5 parse + lengths 145 vs 141 ms)
+    // (not for long lines: at 200x the fused kernel's extra registers and work
+    // cost the parse more than the length kernel costs (C5: the per-lane parse
+    // on the reduced grid, parse + lengths 145 vs 141 ms; the quad parse with
+    // the lengths fused, 71.4 + 1.8 vs 65.9 + 5.4 ms per step)
     const bool lens = lctx && !qmode && !parse_coop() && n < (1ull << 32) && (c1 - c0) <= 256 * n;
     const uint64_t nb = (n + FTB - 1) / FTB;
     unsigned long long* fbn = (unsigned long long*)(W->state + 6);

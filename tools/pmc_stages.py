@@ -17,7 +17,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGES = {   # the scan kernels (shared by the index and the formatter, ~20 us) are left out
     "index": ["sid_index_count_kernel"],
-    "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_len_kernel", "sid_parse_serial_kernel",
+    "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_len_kernel", "sid_parse_quad_kernel",
+              "sid_parse_serial_kernel",
               "sid_local_len_list_kernel"],
     "call": ["sid_lookup_rec_kernel"],
     "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel", "sid_hist_list_kernel"],
