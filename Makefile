@@ -48,5 +48,6 @@ probes: $(BUILD)/libsid.so
 	$(HIPCC) -O3 -march=x86-64-v3 -o tools/debug/host_bw_probe tools/debug/host_bw_probe.cpp -lpthread
 	$(HIPCC) -O3 -o tools/debug/pcie_probe tools/debug/pcie_probe.cpp -lpthread
 	$(HIPCC) -O2 -Iinclude tools/debug/startup_probe.cpp -L$(BUILD) -lsid -Wl,-rpath,'$$ORIGIN' -o $(BUILD)/startup_probe
+	$(HIPCC) -O2 -Iinclude tools/debug/exit_probe.cpp -L$(BUILD) -lsid -Wl,-rpath,'$$ORIGIN' -o $(BUILD)/exit_probe
 
 .PHONY: probes

@@ -49,6 +49,7 @@ import argparse
 import json
 import os
 import socket
+import statistics
 import subprocess
 import sys
 import tempfile
@@ -827,6 +828,11 @@ def bench_cli(cfg, text, ln, n):
         return {"wall_s": dt, "wall_s_is": "median of 5 runs after one warm-up",
                 "sites_per_s_wall": n / dt, "sites_per_s_cli_clock": stt.get("sites_per_s"),
                 "wall_s_runs": [x[0] for x in cli_runs], "cli_stats": stt,
+                # main() entry to its last line, and its last line to the exit seen here (the
+                # driver's teardown of a GPU process: 1 ms or 0.1-0.15 s, run to run)
+                "main_s_median": statistics.median(x[1]["main_exit_unix"] - x[1]["main_entry_unix"]
+                                                   for x in cli_runs[1:]) if all("main_entry_unix" in x[1] for x in cli_runs[1:]) else None,
+                "teardown_s_runs": [x[1].get("teardown_s") for x in cli_runs],
                 "note": "build/sid FILE > /dev/null, one GPU: wall = process start + HIP init + mmap + "
                         "H2D + parse/call/format + D2H + write; cli_clock = input mapping to last write; "
                         "startup_s = exec to main(), teardown_s = main's last line to the exit seen here"}

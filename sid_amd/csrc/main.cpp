@@ -417,18 +417,31 @@ int main(int argc, char** argv)
         if (rc == SID_EIO) std::exit(EXIT_FAILURE);
         CHECK(rc, "emit");
         const double t3 = now();
+        // SID_CLI_TEARDOWN=1 (a probe): the mapping and the engine released
+        // here, each timed, instead of with the process
+        double unmap_s = -1, destroy_s = -1;
+        const char* td = std::getenv("SID_CLI_TEARDOWN");
+        if (td && std::strcmp(td, "1") == 0) {
+            const double u0 = now();
+            if (pre_map) munmap((void*)pre_map, in.len);
+            const double u1 = now();
+            sid_engine_destroy(eng);
+            unmap_s = u1 - u0;
+            destroy_s = now() - u1;
+        }
         if (opt.stats)
             std::fprintf(stderr,
                          "{\"sites\": %llu, \"devices\": %d, \"threads\": %d, \"path\": \"stream\", "
                          "\"create_s\": %.6f, \"parse_s\": %.6f, \"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, "
                          "\"sites_per_s\": %.1f, \"chunks\": %llu, \"chunks_held\": %llu, "
                          "\"chunks_retained\": %llu, \"chunks_reloaded\": %llu, \"bytes_in\": %llu, "
-                         "\"bytes_out\": %llu, \"main_entry_unix\": %.6f, \"main_exit_unix\": %.6f}\n",
+                         "\"bytes_out\": %llu, \"unmap_s\": %.6f, \"destroy_s\": %.6f, "
+                         "\"main_entry_unix\": %.6f, \"main_exit_unix\": %.6f}\n",
                          (unsigned long long)st.sites, D, T, tc - t0, t1 - t0, t2 - t1, t3 - t2, t3 - t0,
                          st.sites / std::max(1e-9, t3 - t0), (unsigned long long)st.chunks,
                          (unsigned long long)st.chunks_held, (unsigned long long)st.chunks_retained,
                          (unsigned long long)st.chunks_reloaded, (unsigned long long)st.bytes_in,
-                         (unsigned long long)st.bytes_out, t_entry, unix_now());
+                         (unsigned long long)st.bytes_out, unmap_s, destroy_s, t_entry, unix_now());
         // device memory, pinned staging and the mapping go with the process
         finish(0);
     }

@@ -1654,6 +1654,38 @@ static int setup_generator(sid_engine* e)
     return SID_OK;
 }
 
+// The emit's pinned ring per device: 4 x 16 MiB (pinned once, reused by
+// every run; 8 x 16, 4 x 64 and 16 x 8 MiB measured slower while the pinning
+// was on the emit's path)
+constexpr uint64_t EMIT_RING_BYTES = 16ull << 20;
+constexpr int EMIT_RING_N = 4;
+static int alloc_ring(Dev& d)
+{
+    if (hipSetDevice(d.device) != hipSuccess) return SID_EHIP;
+    while ((int)d.pinned.size() < EMIT_RING_N) {
+        char* p = nullptr;
+        hipEvent_t ev;
+        if (hipHostMalloc((void**)&p, EMIT_RING_BYTES, hipHostMallocDefault) != hipSuccess) return SID_ENOMEM;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipHostFree(p);
+            return SID_EHIP;
+        }
+        d.pinned.push_back(p);
+        d.pinned_ev.push_back(ev);
+    }
+    d.pinned_cap = EMIT_RING_BYTES;
+    return SID_OK;
+}
+
+// SID_EMIT_RING_EARLY=0: the emit's ring pinned by the emit itself (A/B);
+// default: pinned on a thread of its own during the ingest of a run that
+// writes its records through it (no host arena, no device sink)
+static bool ring_early()
+{
+    static const char* v = std::getenv("SID_EMIT_RING_EARLY");
+    return !(v && std::strcmp(v, "0") == 0);
+}
+
 extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
 {
     if (!e || e->src == SRC_NONE) return SID_EINVAL;
@@ -1674,6 +1706,11 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         th.emplace_back(uploader, e, std::ref(*e->devs[i]), std::cref(lists[i]), 1);
         th.emplace_back(compute, e, std::ref(*e->devs[i]), 1);
     }
+    // (a failure here leaves the ring to the emit, which reports it)
+    if (e->cfg.device_sink == 0 && e->cfg.host_hold_bytes == 0 && ring_early())
+        th.emplace_back([e] {
+            for (auto& dp : e->devs) (void)alloc_ring(*dp);
+        });
     for (auto& t : th) t.join();
     if (e->rc.load() != SID_OK) {
         close_all(e);
@@ -1886,24 +1923,12 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
     }
     start_queues(e);
     const int D = (int)e->devs.size();
-    // pinned ring per device: 4 x 16 MiB (pinned once, reused by every run)
-    // (8 x 16, 4 x 64 and 16 x 8 MiB measured slower: the pinning costs more)
-    const uint64_t PC = 16ull << 20;
-    const int NP = 4;
     if (sink != 1)
         for (auto& dp : e->devs) {
             Dev& d = *dp;
-            if (hipSetDevice(d.device) != hipSuccess) return SID_EHIP;
-            while ((int)d.pinned.size() < NP) {
-                char* p = nullptr;
-                hipEvent_t ev;
-                if (hipHostMalloc((void**)&p, PC, hipHostMallocDefault) != hipSuccess) return SID_ENOMEM;
-                if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return SID_EHIP;
-                d.pinned.push_back(p);
-                d.pinned_ev.push_back(ev);
-            }
-            d.pinned_cap = PC;
-            for (int i = 0; i < NP; ++i) d.free_pinned.push(i);
+            const int rc = alloc_ring(d);
+            if (rc != SID_OK) return rc;
+            for (int i = 0; i < EMIT_RING_N; ++i) d.free_pinned.push(i);
         }
     std::vector<std::vector<uint64_t>> lists(D);
     for (uint64_t j = 0; j < e->recs.size(); ++j) lists[e->recs[j].dev].push_back(j);

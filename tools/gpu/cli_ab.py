@@ -39,10 +39,12 @@ def main():
                     k, v = kv.split("=", 1)
                     env[k] = v
                 with open(os.devnull, "wb") as dn:
+                    u0 = time.time()
                     t0 = time.perf_counter()
                     p = subprocess.run([os.path.join(ROOT, b), "--stats", path], stdout=dn, stderr=subprocess.PIPE,
                                        env=env, timeout=120)
                     dt = time.perf_counter() - t0
+                    u1 = time.time()
                 if p.returncode != 0:
                     print(spec, "failed", p.returncode, p.stderr.decode()[-300:])
                     sys.exit(1)
@@ -53,6 +55,9 @@ def main():
                 rec = {"bin": spec, "round": r, "wall_s": dt, "create_s": st.get("create_s"),
                        "total_s": st.get("total_s"), "emit_s": st.get("emit_s"), "parse_s": st.get("parse_s"),
                        "main_s": st["main_exit_unix"] - st["main_entry_unix"],
+                       # process start to main, main's end to the parent's wait
+                       "pre_s": st["main_entry_unix"] - u0, "post_s": u1 - st["main_exit_unix"],
+                       "unmap_s": st.get("unmap_s"), "destroy_s": st.get("destroy_s"),
                        "chunks": st.get("chunks"),
                        "chunks_registered": sum(x.get("chunks_registered", 0) for x in eng) if eng else None}
                 fo.write(json.dumps(rec) + "\n")
