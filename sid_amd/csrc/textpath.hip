@@ -840,14 +840,25 @@ __device__ __forceinline__ uint32_t rb_window(const uint4 v, uint32_t valid, int
 // it) masked, then whole windows while they lie inside the text.  first: the
 // first window's 16 bytes, in the header's LDS stage (no second global load
 // of bytes the header already read)
+// SID_RB_STAGED=1: the windows after the first that the header's 48 staged
+// bytes also hold come from the stage too (nst of them: 2, 1 or 0); A/B
+#ifndef SID_RB_STAGED
+#define SID_RB_STAGED 0
+#endif
 __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, uint64_t len, uint64_t q, uint32_t kd,
-                                               const uint32_t* lut, const uint4* first, uint64_t* out)
+                                               const uint32_t* lut, const uint4* first, uint64_t* out, int nst = 0)
 {
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
     uint64_t a = q & ~(uint64_t)15;
     uint32_t carry = 0;   // bit 7: byte 0 of the next word is skipped
     bool done = false, bad = false;
+#if SID_RB_STAGED
+    uint4 vn = nst >= 1 ? first[1] : *(const uint4*)(text + a + 16);
+    int k = 1;
+#else
+    (void)nst;
     uint4 vn = *(const uint4*)(text + a + 16);   // the next window in flight while the first is counted
+#endif
     uint32_t acc = 0;
     auto masked = [&](const uint4& v, uint32_t lead) {
         const int room = len > a ? (int)min(len - a, (uint64_t)16) : 0;
@@ -866,7 +877,12 @@ __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, ui
     a += 16;
     while (!done) {
         const uint4 v = vn;
+#if SID_RB_STAGED
+        ++k;
+        vn = k <= nst ? first[k] : *(const uint4*)(text + a + 16);
+#else
         vn = *(const uint4*)(text + a + 16);
+#endif
         add(a + 16 <= len ? rb_window<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u));
         a += 16;
     }
@@ -1094,7 +1110,8 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
 #if SID_PARSE_LUT
     if (QUAD)
         return read_bases_quad(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out);
-    return read_bases_lut(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out);
+    return read_bases_lut(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out,
+                          2 - (int)((sh + t4) >> 4));
 #else
     return read_bases_fast(text, len, s0 + (uint64_t)t4, kd, out);
 #endif
@@ -1909,7 +1926,10 @@ __device__ __noinline__ int local_site_len_text(const char* text, uint64_t len, 
 // block's byte count.  Lines the fast path leaves get theirs after the
 // general routine (sid_local_len_list_kernel).  The tail-length table is read
 // through the caches (an LDS copy would cost the parse a block per CU).
-__global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
+#ifndef SID_PARSE_LEN_WAVES
+#define SID_PARSE_LEN_WAVES 8
+#endif
+__global__ __launch_bounds__(TB, SID_PARSE_LEN_WAVES) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
                                                            const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ range,
                                                            uint64_t* __restrict__ counts,
