@@ -1657,15 +1657,25 @@ static int setup_generator(sid_engine* e)
 // The emit's pinned ring per device: 4 x 16 MiB (pinned once, reused by
 // every run; 8 x 16, 4 x 64 and 16 x 8 MiB measured slower while the pinning
 // was on the emit's path)
-constexpr uint64_t EMIT_RING_BYTES = 16ull << 20;
+// (SID_EMIT_RING_MIB: the piece size, 1-256 MiB; A/B)
 constexpr int EMIT_RING_N = 4;
+static uint64_t emit_ring_bytes()
+{
+    static const uint64_t b = [] {
+        const char* v = std::getenv("SID_EMIT_RING_MIB");
+        const long m = v ? std::atol(v) : 16;
+        return (uint64_t)std::min(256L, std::max(1L, m)) << 20;
+    }();
+    return b;
+}
 static int alloc_ring(Dev& d)
 {
     if (hipSetDevice(d.device) != hipSuccess) return SID_EHIP;
+    const uint64_t bytes = emit_ring_bytes();
     while ((int)d.pinned.size() < EMIT_RING_N) {
         char* p = nullptr;
         hipEvent_t ev;
-        if (hipHostMalloc((void**)&p, EMIT_RING_BYTES, hipHostMallocDefault) != hipSuccess) return SID_ENOMEM;
+        if (hipHostMalloc((void**)&p, bytes, hipHostMallocDefault) != hipSuccess) return SID_ENOMEM;
         if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
             (void)hipHostFree(p);
             return SID_EHIP;
@@ -1673,7 +1683,7 @@ static int alloc_ring(Dev& d)
         d.pinned.push_back(p);
         d.pinned_ev.push_back(ev);
     }
-    d.pinned_cap = EMIT_RING_BYTES;
+    d.pinned_cap = bytes;
     return SID_OK;
 }
 
