@@ -2005,6 +2005,19 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
         (void)hipSetDevice(dp->device);
         if (hipDeviceSynchronize() != hipSuccess) fail(e, SID_EHIP);
     }
+    // SID_EMIT_FREE_RING=1: the pinned ring released after the run (a
+    // one-run process: the driver's teardown of pinned pages at exit)
+    static const char* fr = std::getenv("SID_EMIT_FREE_RING");
+    if (fr && std::strcmp(fr, "1") == 0)
+        for (auto& dp : e->devs) {
+            Dev& d = *dp;
+            (void)hipSetDevice(d.device);
+            for (char* p : d.pinned) (void)hipHostFree(p);
+            for (hipEvent_t ev : d.pinned_ev) (void)hipEventDestroy(ev);
+            d.pinned.clear();
+            d.pinned_ev.clear();
+            d.free_pinned.reset();
+        }
     if (st) {
         st->chunks_reloaded = e->reloaded.load();
         st->bytes_out = sink == 1 ? e->sink_bytes.load() : out_bytes.load();
