@@ -31,11 +31,12 @@ Configs (--config):
       the profile histogram; N>1 all-gathers it over RCCL (device tensors,
       backend "nccl"), rank 0 runs the one Nelder-Mead estimate and broadcasts
       (pi, eps) over RCCL; then every rank formats its records
-  C4  -m local, seed 4, 3G sites in total = 24 chromosomes x 125M (strong
-      scaling: rank r takes sites [r*3G/N, (r+1)*3G/N)); device path: the
-      shard's text generated into HBM before the timed region when it fits
-      (--stream: generated chunk by chunk inside the step, never stored)
-  C5  -m local, seed 5, 200x, 500M sites in total (strong), as C4
+  C4  -m local, seed 4, 3G sites in total = 24 chromosomes x 125M, quoted on
+      8 GPUs: rank r takes the eighth [r*3G/8, (r+1)*3G/8) (375M sites, 30.4
+      GB of text), so N = 8 runs the whole genome; the same step as C2 (host
+      text -> CSV in host memory), device_path on the shard resident in HBM
+  C5  -m local, seed 5, 200x, 500M sites in total, as C4 (62.5M sites, 26.6
+      GB of text per eighth)
 
 Multi-GPU: one rank per GPU.  Under torchrun (WORLD_SIZE set) each process is
 a rank; without it, `--gpus N` (N > 1) starts N rank processes itself (before
@@ -103,9 +104,6 @@ def parse_args(argv=None):
                    help="after the timed PCIe leg (C2/C3): each rank writes its records (file order) to "
                         "DIR/rank<r>.csv and its estimate to DIR/rank<r>.json (parity tests)")
     p.add_argument("--no-node-cli", action="store_true", help="N > 1: skip the whole-node CLI leg")
-    p.add_argument("--stream", action="store_true",
-                   help="C4/C5: generate the text on the device chunk by chunk inside the step, even when the "
-                        "rank's shard would fit in HBM")
     a = p.parse_args(argv)
     if a.config is None:
         a.config = "C3" if a.method == "likelihood_ratio" else "C2"
@@ -192,26 +190,22 @@ def numa_bind(torch, gpu):
 # ----------------------------------------------------------------- ranks ----
 def fmt_kind(cfg):
     """The formatter the engine runs: "local" (-m local, the call fused into
-    it), "lynch" (likelihood_ratio / bayes pass 2, the class lookup fused into
-    it; SID_LYNCH_FUSED=0 turns that off) or None (the generic one, after the
-    call / lookup kernel)."""
-    if cfg["method"] == "local":
-        return "local"
-    return None if os.environ.get("SID_LYNCH_FUSED", "1") == "0" else "lynch"
+    it) or "lynch" (likelihood_ratio / bayes pass 2, the class lookup fused
+    into it)."""
+    return "local" if cfg["method"] == "local" else "lynch"
 
 
 def parse_quad(text_per_site):
     """Lines over 256 B on average are parsed by a quad of lanes each
-    (textpath.hip sid_parse_quad_kernel;
-    SID_PARSE_QUAD=0: one lane per line)."""
-    return text_per_site > 256 and os.environ.get("SID_PARSE_QUAD", "1") != "0"
+    (textpath.hip sid_parse_quad_kernel)."""
+    return text_per_site > 256
 
 
 def parse_len(fused, text_per_site=81.0):
     """-m local: the records' lengths computed by the parse (run.cpp,
-    sid_parse_len_kernel; SID_PARSE_LEN=0 keeps the separate length kernel),
-    for lines of up to 256 bytes (textpath.hip sid_chunk_parse)."""
-    return fused == "local" and os.environ.get("SID_PARSE_LEN", "1") != "0" and text_per_site <= 256
+    sid_parse_len_kernel), for lines of up to 256 bytes (textpath.hip
+    sid_chunk_parse)."""
+    return fused == "local" and text_per_site <= 256
 
 
 def stage_bytes(stage, text_per_site, csv_per_site, fused):
@@ -402,16 +396,8 @@ def bench_weak(R, a, cfg):
                 "steps": dp["steps"], "ms_per_step": dp["ms_per_step"], "roofline": dp.pop("roofline"),
                 "device_path": dp, "note": "--device-only (profiling): value is the device path's"}, []
     host = text[:ln].cpu().pin_memory()     # the rank's input, in host memory (its GPU's NUMA node)
-    # the CSV is ~0.53 of the text at 30x: the arena never runs out
-    hh = int(ln * 0.6) + (64 << 20)
-    eng = sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=R.gpu,
-                         chunk_bytes=a.pcie_chunk_mib << 20, slots=a.slots, device_sink=2, host_hold_bytes=hh)
-    eng.source_host_ptr(host.data_ptr(), ln, keep=host)
-    elapsed, (st, st2, est) = R.timed(lambda: R.run_step(eng, lynch), a.steps, a.warmup)
-    elapsed = R.max_over_ranks([elapsed])[0]
+    elapsed, st, st2, est, eng = pcie_leg(R, a, cfg, host, ln, n, lynch)
     sites_all = R.sum_over_ranks(st.sites)
-    if st2.bytes_out == 0 and st.sites:
-        raise SystemExit("bench.py: no records came back")
     # the first chunk's records from the host arena, for the cpu_baseline
     # leg's spot check against the oracle (-m local: the records of a prefix
     # of the text do not depend on the rest)
@@ -428,20 +414,16 @@ def bench_weak(R, a, cfg):
                        "pi": est.heterozygosity if lynch else None, "eps": est.error_rate if lynch else None,
                        "iterations": est.iterations if lynch else None,
                        "n_unique": est.n_unique if lynch else None}, f)
-    pcie = {"text_bytes": ln, "csv_bytes": st2.bytes_out,
-            "GBps_h2d": ln / (elapsed / a.steps) / 1e9, "GBps_d2h": st2.bytes_out / (elapsed / a.steps) / 1e9,
-            "chunks": st.chunks, "chunks_held_in_host_arena": st.chunks_held, "ingest_s": st.ingest_s,
-            "emit_s": st2.emit_s}
-    pcie["ceiling"] = pcie_ceiling(ln, st2.bytes_out, lynch, elapsed / a.steps)
+    pcie = pcie_stats(a, ln, st, st2, elapsed, lynch)
     eng.close()
     del host
 
     dp = device_path(R, a, cfg, text, ln, lynch)
-    node_cli = None
+    node_cli, node_cpu = None, None
     if R.world > 1 and not a.no_extras and not a.no_node_cli:
         holder = [text]
         text = None   # the rank's text is freed before the CLI takes the GPUs (the N = 1 extras do not run)
-        node_cli = bench_cli_node(R, cfg, holder, ln, n)
+        node_cli, node_cpu = bench_cli_node(R, cfg, holder, ln, n)
     out = {
         "metric": METRIC,
         "value": sites_all * a.steps / elapsed,
@@ -477,11 +459,13 @@ def bench_weak(R, a, cfg):
                            "n_unique": est.n_unique}
     if node_cli is not None:
         out["cli"] = node_cli
+    if node_cpu is not None and not a.no_cpu:
+        out["cpu_baseline"] = node_cpu
     if R.world == 1 and not a.no_extras:
         out["kernel_local"] = bench_kernel_local(torch, R.dev, cfg, n)
         out["cli"] = bench_cli(cfg, text, ln, n)
         if not a.no_cpu:
-            out["cpu_baseline"] = bench_cpu(cfg, text, ln, n, spot=spot)
+            out["cpu_baseline"] = bench_cpu(cfg, text, ln, n, R.cpus0, spot=spot)
     return out, []
 
 
@@ -564,78 +548,117 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
             "note": "text resident in HBM before the timed region, records formatted into HBM (device_sink 1)"}
 
 
-def bench_strong(R, a, cfg):
-    """C4 / C5: a fixed total split by site range; the device path (text in
-    HBM, or generated inside the step with --stream / when it does not fit).
-    The generator's time is reported apart from sid's stages."""
+STRONG_PARTS = 8   # C4 / C5 are quoted on 8 GPUs: a rank's shard is 1/8 of the config's sites
+
+
+def host_hold_bytes(n):
+    """The PCIe path's host arena for n sites: every chunk's records fit (the
+    CSV is ~42.7 B/site at 30x and at 200x)."""
+    return int(n * 48) + (64 << 20)
+
+
+def pcie_engine(cfg, gpu, n, ln, chunk_mib=0, slots=0):
+    """The engine of the `value` leg (C2 - C5): one device, host text in
+    chunk_mib MiB chunks (0 = the engine's 128 MiB), each chunk's records
+    copied into the pinned host arena during the ingest (device_sink 2: not
+    written anywhere else; sid_engine_records reads them).
+    tests/test_benchpath_gpu.py builds the same engine."""
     import sid_amd
+    return sid_amd.Engine(method=cfg["method"], estimate_prior=cfg["R"], devices=1, first_device=gpu,
+                          chunk_bytes=chunk_mib << 20, slots=slots, device_sink=2,
+                          host_hold_bytes=host_hold_bytes(n))
+
+
+def pcie_leg(R, a, cfg, host, ln, n, lynch):
+    """The timed value leg over pinned host text of n sites: (elapsed, ingest
+    stats, emit stats, estimate, engine) -- the engine still open, its
+    records in its host arena."""
+    eng = pcie_engine(cfg, R.gpu, n, ln, a.pcie_chunk_mib, a.slots)
+    eng.source_host_ptr(host.data_ptr(), ln, keep=host)
+    elapsed, (st, st2, est) = R.timed(lambda: R.run_step(eng, lynch), a.steps, a.warmup)
+    elapsed = R.max_over_ranks([elapsed])[0]
+    if st2.bytes_out == 0 and st.sites:
+        raise SystemExit("bench.py: no records came back")
+    return elapsed, st, st2, est, eng
+
+
+def pcie_stats(a, ln, st, st2, elapsed, lynch):
+    pcie = {"text_bytes": ln, "csv_bytes": st2.bytes_out,
+            "GBps_h2d": ln / (elapsed / a.steps) / 1e9, "GBps_d2h": st2.bytes_out / (elapsed / a.steps) / 1e9,
+            "chunks": st.chunks, "chunks_held_in_host_arena": st.chunks_held, "ingest_s": st.ingest_s,
+            "emit_s": st2.emit_s, "h2d_s_last_step": st.h2d_s,
+            "h2d_GBps_last_step": st.h2d_bytes / st.h2d_s / 1e9 if st.h2d_s else None}
+    pcie["ceiling"] = pcie_ceiling(ln, st2.bytes_out, lynch, elapsed / a.steps)
+    return pcie
+
+
+def bench_strong(R, a, cfg):
+    """C4 / C5 on the metric's footing (in-memory pileup text
+    -> CSV): each rank takes 1/8 of the config's sites (C4: 375M sites, 30.4 GB
+    of text; C5: 62.5M sites at 200x, 26.6 GB), so N = 8 ranks run the whole
+    config (3G / 500M sites) and N = 1 its first eighth.  The value leg is
+    C2's step: the shard's text in pinned host memory on the GPU's NUMA node
+    when the timed region starts -> H2D, index, parse, call, format -> the
+    CSV records in the pinned host arena (sid.cpp:85-105, call.cpp:213-289).
+    Beside it, device_path: the same shard resident in HBM (generated there
+    before the timed region), records formatted into HBM -- the kernels'
+    own rate."""
     torch = R.torch
+    import sid_amd
     total = a.sites or cfg["total"]
-    first, hi = total * R.rank // R.world, total * (R.rank + 1) // R.world
-    n = hi - first
-    need = int(n * (2.72 * cfg["depth"] + 2))
-    free, _ = torch.cuda.mem_get_info(R.dev)
-    resident = not a.stream and need + (24 << 30) < free
-    gen_ms = None
-    text, ln = None, None
-    if resident:
-        t0 = time.perf_counter()
-        text, ln = generate_resident(torch, sid_amd, R.dev, R.gpu, cfg, first, n)
-        gen_ms = (time.perf_counter() - t0) * 1e3
-        if not a.chunk_mib:
-            a.chunk_mib = STRONG_RESIDENT_CHUNK_MIB
-        dp = device_path(R, a, cfg, text, ln, False)
-    else:
-        dp = device_path(R, a, cfg, None, None, False, gen=(first, n))
-        gen_ms = generator_probe(R, cfg, first, n)
+    if R.world > STRONG_PARTS:
+        raise SystemExit(f"bench.py: {a.config} is split into {STRONG_PARTS} shards; {R.world} ranks")
+    per = total // STRONG_PARTS
+    first, n = R.rank * per, per
+    t0 = time.perf_counter()
+    text, ln = generate_resident(torch, sid_amd, R.dev, R.gpu, cfg, first, n)
+    gen_ms = (time.perf_counter() - t0) * 1e3
+    lynch = cfg["method"] != "local" or cfg["R"]
+    host = torch.empty(ln, dtype=torch.uint8, pin_memory=True)   # on the GPU's NUMA node (numa_bind)
+    host.copy_(text[:ln])
+    torch.cuda.synchronize(R.dev)
+    elapsed, st, st2, est, eng = pcie_leg(R, a, cfg, host, ln, n, lynch)
+    sites_all = R.sum_over_ranks(st.sites)
+    spot = eng.records_bytes(1) if not lynch else None
+    pcie = pcie_stats(a, ln, st, st2, elapsed, lynch)
+    eng.close()
+    del host
+    if not a.chunk_mib:
+        a.chunk_mib = STRONG_RESIDENT_CHUNK_MIB
+    dp = device_path(R, a, cfg, text, ln, lynch)
     out = {
         "metric": METRIC,
-        "value": dp["sites_per_s"],
+        "value": sites_all * a.steps / elapsed,
         "unit": "sites/s",
         "n_gpus": R.n_gpus,
-        "steps": dp["steps"],
-        "warmup": 2,
-        "ms_per_step": dp["ms_per_step"],
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic (counter-based pileup generator, BASELINE.md): "
-                 + ("the rank's shard of text generated into HBM before the timed region"
-                    if resident else "text generated on the device chunk by chunk inside the step (never stored)")
-                 + "; CSV records formatted into HBM (device path; C2 is the PCIe-inclusive headline)"),
-        "config": {"workload": f"{a.config}: {cfg['desc']}", "method": cfg["method"], "seed": cfg["seed"],
-                   "depth": cfg["depth"], "sites_total": total, "sites_rank0": n, "sites_per_chrom": cfg["spc"],
-                   "resident": resident, "parallelism": f"site-range shards x{R.world}", "ranks": R.world,
+        "data": ("synthetic (counter-based pileup generator, BASELINE.md): each rank's 1/8 shard of the config's "
+                 "text in pinned host memory when the timed region starts, the CSV records in pinned host memory "
+                 "when it ends (H2D, index, parse, call, format, D2H inside every step)"),
+        "config": {"workload": f"{a.config}: {cfg['desc']}; 1/{STRONG_PARTS} of its {total:,} sites per GPU "
+                               f"({per:,} sites; {STRONG_PARTS} GPUs run the whole config)",
+                   "method": cfg["method"], "seed": cfg["seed"], "depth": cfg["depth"], "sites_total": total,
+                   "sites_per_gpu": per, "sites_all_ranks": sites_all, "first_site_rank0": 0,
+                   "sites_per_chrom": cfg["spc"], "text_bytes_rank0": ln, "csv_bytes_rank0": st2.bytes_out,
+                   "parallelism": f"site-range shards x{R.world}", "ranks": R.world,
                    "oversubscribed": R.oversub, "numa": R.numa},
+        "pcie": pcie,
         "roofline": dp.pop("roofline"),
         "device_path": dp,
-        "generator": {"ms": gen_ms, "inside_step": not resident,
-                      "note": ("generating the shard's text into HBM, before the timed region" if resident else
-                               "the device generator alone over the rank's sites (no sid stage), measured apart; "
-                               "inside the step it runs on the upload stream beside sid's kernels")},
+        "generator": {"ms": gen_ms, "inside_step": False,
+                      "note": "the shard's text generated into HBM (then copied to pinned host memory), before "
+                              "the timed region"},
     }
+    if R.world == 1 and not a.no_extras and not a.no_cpu:
+        out["cpu_baseline"] = bench_cpu(cfg, text, ln, n, R.cpus0, spot=spot,
+                                        sample_sites=50_000_000 if cfg["depth"] < 100 else 10_000_000)
     return out, []
-
-
-def generator_probe(R, cfg, first, n):
-    """Device time of the generator alone over the rank's sites, in 50M-site
-    pieces into one reusable buffer (the inside-the-step generator's work)."""
-    import sid_amd
-    torch = R.torch
-    piece = min(n, 20_000_000)
-    cap = int(piece * (24 + 2.9 * cfg["depth"])) + (64 << 20)
-    buf = torch.empty(cap + 512, dtype=torch.uint8, device=R.dev)
-    ctx = sid_amd.Context(R.gpu)
-    torch.cuda.synchronize(R.dev)
-    t0 = time.perf_counter()
-    for lo in range(0, n, piece):
-        ctx.synth_text_device(cfg["seed"], cfg["depth"], first + lo, min(piece, n - lo), buf.data_ptr(), cap,
-                              sites_per_chrom=cfg["spc"])
-    torch.cuda.synchronize(R.dev)
-    ms = (time.perf_counter() - t0) * 1e3
-    ctx.close()
-    return ms
 
 
 def generate_resident(torch, sid_amd, dev, gpu, cfg, first, n):
@@ -885,22 +908,29 @@ def bench_cli_node(R, cfg, holder, ln, n):
     torch._C._host_emptyCache()
     dist.barrier()
     if path is None:
-        return {"skipped": f"build/sid missing or no directory with {total / 1e9:.1f} GB free"}
+        return {"skipped": f"build/sid missing or no directory with {total / 1e9:.1f} GB free"}, None
     store = dist.distributed_c10d._get_default_store()
-    res = None
+    res, cpu = None, None
     if R.rank == 0:
         try:
             env = dict(os.environ)
             runs = []
+            # the CLI runs unbound (it places its own threads per GPU): this
+            # thread's mask widened for the fork, which the child inherits, and
+            # restored after (no preexec_fn: this process runs other threads)
+            mask = os.sched_getaffinity(0)
             for _ in range(4):
                 with open(os.devnull, "wb") as dn:
-                    t0 = time.perf_counter()
-                    r = subprocess.run([cli, "--stats", "--devices", str(R.world)] +
-                                       ([] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) +
-                                        ["-m", cfg["method"]]) + [path],
-                                       stdout=dn, stderr=subprocess.PIPE, env=env,
-                                       preexec_fn=lambda: os.sched_setaffinity(0, R.cpus0))
-                    dt = time.perf_counter() - t0
+                    os.sched_setaffinity(0, R.cpus0)
+                    try:
+                        t0 = time.perf_counter()
+                        r = subprocess.run([cli, "--stats", "--devices", str(R.world)] +
+                                           ([] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) +
+                                            ["-m", cfg["method"]]) + [path],
+                                           stdout=dn, stderr=subprocess.PIPE, env=env)
+                        dt = time.perf_counter() - t0
+                    finally:
+                        os.sched_setaffinity(0, mask)
                 if r.returncode != 0:
                     res = {"error": r.returncode, "stderr": r.stderr.decode()[-400:]}
                     break
@@ -919,6 +949,16 @@ def bench_cli_node(R, cfg, holder, ln, n):
                        "note": f"build/sid --devices {R.world} FILE > /dev/null on one file holding every "
                                "rank's shard (the whole node's drop-in: one process, every GPU); wall = "
                                "process start + HIP init + mapping + H2D + kernels + D2H + write"}
+                if cfg["method"] == "local":
+                    # the whole node's CPU path beside it: the oracle over the same file, one
+                    # line-aligned shard process per CPU the job may use
+                    P, share = cpu_share(R.cpus0)
+                    dtc = oracle_shards(path, total, P, method_flags(cfg), R.cpus0)
+                    cpu = {"value": sites / dtc if dtc else None, "unit": "sites/s", "cores": P, "kind": "port",
+                           "seconds": dtc, "cpu_model": cpu_model(), "cpu_share": share,
+                           "sample": f"the node file ({sites:,} sites, every rank's shard, {total / 1e9:.2f} GB), "
+                                     f"{P} line-aligned byte ranges, one oracle/_build/sid_oracle process each, "
+                                     "CSV to /dev/null, wall"}
         finally:
             store.set("sid_node_cli_done", "1")
             try:
@@ -928,7 +968,7 @@ def bench_cli_node(R, cfg, holder, ln, n):
     else:
         store.wait(["sid_node_cli_done"], timedelta(minutes=15))
     dist.barrier()
-    return res
+    return res, cpu
 
 
 def write_text_file(text, ln, path):
@@ -952,73 +992,120 @@ def cpu_model():
     return None
 
 
-def cut_after_lines(host, m):
-    """Byte offset just past the first m lines of host (a uint8 array)."""
-    cut, need = 0, m
-    while need > 0:
-        seg = host[cut:cut + (64 << 20)].tobytes()
-        nl = seg.count(b"\n")
-        if nl < need:
-            cut += len(seg)
-            need -= nl
-            if not seg:
-                break
-        else:
-            idx = -1
-            for _ in range(need):
-                idx = seg.find(b"\n", idx + 1)
-            cut += idx + 1
-            need = 0
-    return cut
+def cpu_share(cpus):
+    """The CPUs this job may use: its affinity mask (before the rank's NUMA
+    binding), capped by its cgroup's CPU quota (a GPU box's share of a larger
+    machine: os.cpu_count() shows the whole machine there)."""
+    n = len(cpus)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+            n = min(n, quota)
+    except (OSError, ValueError):
+        pass
+    return n, {"affinity_cpus": len(cpus), "cgroup_quota_cpus": quota, "nproc": os.cpu_count()}
 
 
-def bench_cpu(cfg, text, ln, n, spot=None):
-    """The oracle CLI (reference sid.cpp/call.cpp/lynch/stats restated in C,
-    single-threaded) on the same text: 16 line-aligned shard processes over
-    all n sites (-m local: sites are independent; the GPU box's CPU share is
-    16 cores), and one process on the first 4M sites.  spot: the timed PCIe
-    leg's first chunk of records (from the engine's host arena), checked
-    byte for byte against the oracle's CSV of the same lines (untimed)."""
+def line_cuts(path, ln, P):
+    """P line-aligned byte ranges covering the file's first ln bytes."""
+    cuts = [0]
+    with open(path, "rb") as f:
+        for k in range(1, P):
+            c = max(cuts[-1], ln * k // P)
+            f.seek(c)
+            w = f.read(1 << 20)
+            nl = w.find(b"\n")
+            cuts.append(min(ln, c + nl + 1) if nl >= 0 else ln)
+    cuts.append(ln)
+    return [(cuts[k], cuts[k + 1] - cuts[k]) for k in range(P) if cuts[k + 1] > cuts[k]]
+
+
+def oracle_shards(path, ln, P, flags, cpus):
+    """The oracle CLI in P processes over line-aligned byte ranges of one file
+    (ORACLE_RANGE: the harness's byte range), CSV to /dev/null: wall seconds,
+    or None when a process failed.  -m local only: its sites are independent
+    (the reference's whole-node shape, one sid per chromosome,
+    scripts/sid-pipeline/parallel-run-sid.sh:2, is the same split)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     if not os.path.exists(oracle.CLI):
         oracle.build()
-    flags = [] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) + ["-m", cfg["method"]]
-    P = 16
-    host = text[:ln].cpu().numpy()
-    with tempfile.TemporaryDirectory() as td:
-        cuts = [0]
-        for k in range(1, P):
-            c = ln * k // P
-            nl = host[c:c + (1 << 20)].tobytes().find(b"\n")
-            cuts.append(c + nl + 1)
-        cuts.append(ln)
-        paths = []
-        for k in range(P):
-            pth = os.path.join(td, f"s{k}.plp")
-            with open(pth, "wb") as f:
-                f.write(host[cuts[k]:cuts[k + 1]].tobytes())
-            paths.append(pth)
-        res = {"unit": "sites/s", "kind": "port", "cpu_model": cpu_model()}
-        if cfg["method"] == "local":
-            with open(os.devnull, "wb") as dn:
-                t0 = time.perf_counter()
-                procs = [subprocess.Popen([oracle.CLI] + flags + [p], stdout=dn, stderr=subprocess.DEVNULL)
-                         for p in paths]
-                rcs = [p.wait() for p in procs]
-                dt = time.perf_counter() - t0
-            res.update({"value": n / dt if not any(rcs) else None, "cores": P, "seconds": dt,
-                        "sample": f"the same {n:,}-site {cfg['desc']} text ({ln / 1e9:.2f} GB), {P} line-aligned "
-                                  f"shards, one oracle/_build/sid_oracle process each, CSV to /dev/null, wall"})
-        # one core on the first 4M sites
-        m = min(n, 4_000_000)
-        cut = cut_after_lines(host, m)
-        one = os.path.join(td, "one.plp")
-        with open(one, "wb") as f:
-            f.write(host[:cut].tobytes())
+    ranges = line_cuts(path, ln, P)
+    # the processes run on every CPU of the job (this thread's mask, which
+    # they inherit, widened from the rank's NUMA binding for the forks)
+    mask = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, cpus)
+    try:
         with open(os.devnull, "wb") as dn:
             t0 = time.perf_counter()
-            r = subprocess.run([oracle.CLI] + flags + [one], stdout=dn, stderr=subprocess.DEVNULL)
+            procs = [subprocess.Popen([oracle.CLI] + flags + [path], stdout=dn, stderr=subprocess.DEVNULL,
+                                      env=dict(os.environ, ORACLE_RANGE=f"{o}:{m}")) for o, m in ranges]
+            rcs = [p.wait() for p in procs]
+            dt = time.perf_counter() - t0
+    finally:
+        os.sched_setaffinity(0, mask)
+    return None if any(rcs) else dt
+
+
+def method_flags(cfg):
+    return [] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) + ["-m", cfg["method"]]
+
+
+def bench_cpu(cfg, text, ln, n, cpus, spot=None, sample_sites=None):
+    """The oracle CLI (reference sid.cpp/call.cpp/lynch/stats restated in C,
+    single-threaded) on the same text, bounded to sample_sites (default: all
+    n): one line-aligned shard process per CPU this job may use (-m local:
+    sites are independent), and one process on the first 4M sites.  spot:
+    the timed PCIe leg's first chunk of records (from the engine's host
+    arena), checked byte for byte against the oracle's CSV of the same lines
+    (untimed)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    if not os.path.exists(oracle.CLI):
+        oracle.build()
+    flags = method_flags(cfg)
+    P, share = cpu_share(cpus)
+    m_all = min(n, sample_sites or n)
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "sample.plp")
+        # the sample as one file (256 MiB pieces from HBM), its cut after m_all lines
+        step, cut = 256 << 20, 0
+        with open(path, "wb") as f:
+            need = m_all
+            for lo in range(0, ln, step):
+                seg = text[lo:min(ln, lo + step)].cpu().numpy().tobytes()
+                k = seg.count(b"\n")
+                if k >= need:
+                    idx = -1
+                    for _ in range(need):
+                        idx = seg.find(b"\n", idx + 1)
+                    f.write(seg[:idx + 1])
+                    cut += idx + 1
+                    need = 0
+                    break
+                f.write(seg)
+                cut += len(seg)
+                need -= k
+        res = {"unit": "sites/s", "kind": "port", "cpu_model": cpu_model(), "cpu_share": share}
+        if cfg["method"] == "local":
+            dt = oracle_shards(path, cut, P, flags, cpus)
+            res.update({"value": m_all / dt if dt else None, "cores": P, "seconds": dt,
+                        "sample": f"{m_all:,} sites of the {cfg['desc']} text ({cut / 1e9:.2f} GB), {P} line-aligned "
+                                  f"byte ranges of one file (one per CPU this job may use), one "
+                                  f"oracle/_build/sid_oracle process each, CSV to /dev/null, wall"})
+        # one core on the first 4M sites
+        m = min(m_all, 4_000_000)
+        with open(path, "rb") as f:
+            head = f.read(min(cut, 1 << 31))
+        c1 = 0
+        for _ in range(m):
+            c1 = head.find(b"\n", c1) + 1
+        with open(os.devnull, "wb") as dn:
+            t0 = time.perf_counter()
+            r = subprocess.run([oracle.CLI] + flags + [path], stdout=dn, stderr=subprocess.DEVNULL,
+                               env=dict(os.environ, ORACLE_RANGE=f"0:{c1}"))
             dt = time.perf_counter() - t0
         single = {"value": m / dt if r.returncode == 0 else None, "cores": 1, "seconds": dt,
                   "sample": f"the first {m:,} sites of the same text, one process"}
@@ -1029,10 +1116,11 @@ def bench_cpu(cfg, text, ln, n, spot=None):
             res["single_core"] = single
         if spot is not None:   # the checker: the value's own records against the oracle's
             k = spot.count(b"\n")
-            pre = os.path.join(td, "spot.plp")
-            with open(pre, "wb") as f:
-                f.write(host[:cut_after_lines(host, k)].tobytes())
-            r = subprocess.run([oracle.CLI] + flags + [pre], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+            c2 = 0
+            for _ in range(k):
+                c2 = head.find(b"\n", c2) + 1
+            r = subprocess.run([oracle.CLI] + flags + [path], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                               env=dict(os.environ, ORACLE_RANGE=f"0:{c2}"))
             want = r.stdout
             got = b"chrom,pos,label,gt,hom_conf,het_conf,conf_type\n" + spot
             res["spot_check"] = {"sites": k, "bytes": len(spot), "equal": r.returncode == 0 and got == want,

@@ -59,6 +59,8 @@ enum {
                             (|v| >= 2^63; p-values and posteriors never are)        */
     SID_ENOBQ = 12,      /* -m quality, no base-quality field: parseQualities(NULL)
                             dereferences NULL (pileup.cpp:54,158): SIGSEGV          */
+    SID_ELINE = 13,      /* a line that makes a chunk span 4 GiB or more (line
+                            offsets on the device are 32-bit)                      */
 };
 const char* sid_strerror(int status);
 int sid_last_hip_error(void);
@@ -326,6 +328,16 @@ typedef struct {
     uint64_t err_offset;         /* its input byte offset                            */
     double ingest_s, estimate_s, emit_s;
     sid_estimate estimate;       /* Lynch paths                                      */
+    /* the ingest's uploads of host text (host memory or a file's mapping):     */
+    uint64_t chunks_registered;  /* copied from pages registered for DMA (the
+                                    others: the runtime's pageable path, or the
+                                    source was pinned already)                     */
+    double register_s;           /* host time in hipHostRegister / Unregister,
+                                    summed over the uploaders                      */
+    double h2d_s;                /* device time of the host-to-device copies (HIP
+                                    events on the upload streams), summed over
+                                    the devices                                    */
+    uint64_t h2d_bytes;          /* bytes those copies moved                       */
 } sid_run_stats;
 void sid_engine_cfg_default(sid_engine_cfg* cfg);
 int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg, sid_engine** out);

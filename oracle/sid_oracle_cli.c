@@ -68,13 +68,15 @@ static void push_site(sites_t* s, const oracle_line* l)
     s->n++;
 }
 
-/* call.cpp:11-20 readFile */
-static void read_file(FILE* in, sites_t* s)
+/* call.cpp:11-20 readFile; limit: the bytes to read (harness: ORACLE_RANGE) */
+static void read_file(FILE* in, sites_t* s, unsigned long long limit)
 {
     char* line = NULL;
     size_t cap = 0;
     ssize_t len;
-    while ((len = getline(&line, &cap, in)) >= 0) {
+    unsigned long long used = 0;
+    while (used < limit && (len = getline(&line, &cap, in)) >= 0) {
+        used += (unsigned long long)len;
         if (len > 0 && line[len - 1] == '\n') line[--len] = '\0';
         if (len > 0) {
             oracle_line l;
@@ -127,6 +129,15 @@ int main(int argc, char** argv)
         fprintf(stderr, "Could not open file: %s\n", path);
         exit(EXIT_FAILURE);
     }
+    /* test/bench harness, not a reference option: ORACLE_RANGE=OFF:LEN reads
+       only the (line-aligned) bytes [OFF, OFF + LEN) of the file -- the CPU
+       baseline's shard processes over one file (bench.py) */
+    unsigned long long limit = ~0ull;
+    if (getenv("ORACLE_RANGE")) {
+        unsigned long long off = 0, n = 0;
+        if (sscanf(getenv("ORACLE_RANGE"), "%llu:%llu", &off, &n) == 2 && fseeko(in, (off_t)off, SEEK_SET) == 0)
+            limit = n;
+    }
     int method = -1;
     if (strcmp(o.method, "local") == 0) method = ORACLE_LOCAL;
     else if (strcmp(o.method, "bayes") == 0) method = ORACLE_BAYES;
@@ -173,10 +184,10 @@ int main(int argc, char** argv)
         oracle_call_quality_text(text, len, o.estimate_prior, o.snp_prior, o.significance_level, code, h, t, nq,
                                  &nq, 0);
         rewind(in);
-        read_file(in, &s);   /* chrom and pos; cannot fail after the quality parse */
+        read_file(in, &s, limit);   /* chrom and pos; cannot fail after the quality parse */
         free(text);
     } else if (method >= 0) {
-        read_file(in, &s);
+        read_file(in, &s, limit);
         code = (uint8_t*)malloc(s.n ? s.n : 1);
         h = (double*)malloc((s.n ? s.n : 1) * sizeof(double));
         t = (double*)malloc((s.n ? s.n : 1) * sizeof(double));

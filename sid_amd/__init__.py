@@ -30,7 +30,7 @@ METHODS = {"local": METHOD_LOCAL, "likelihood_ratio": METHOD_LIKELIHOOD_RATIO,
 SID_OK = 0
 STATUS = {0: "SID_OK", 1: "SID_EINVAL", 2: "SID_EHIP", 3: "SID_ENOMEM", 4: "SID_EMALFORMED",
           5: "SID_EMISSING_MQ", 6: "SID_ENULLCHROM", 7: "SID_ESTATE", 8: "SID_EBADFUNC",
-          9: "SID_EEMPTY", 10: "SID_EIO", 11: "SID_ERANGE", 12: "SID_ENOBQ"}
+          9: "SID_EEMPTY", 10: "SID_EIO", 11: "SID_ERANGE", 12: "SID_ENOBQ", 13: "SID_ELINE"}
 
 CODE_HET = 0x80
 CODE_DROPPED = 0x40
@@ -70,7 +70,8 @@ class RunStats(C.Structure):
                 ("bytes_out", C.c_uint64), ("chunks_held", C.c_uint64), ("chunks_retained", C.c_uint64),
                 ("chunks_reloaded", C.c_uint64), ("devices", C.c_int), ("status_kind", C.c_int),
                 ("err_offset", C.c_uint64), ("ingest_s", C.c_double), ("estimate_s", C.c_double),
-                ("emit_s", C.c_double), ("estimate", Estimate)]
+                ("emit_s", C.c_double), ("estimate", Estimate), ("chunks_registered", C.c_uint64),
+                ("register_s", C.c_double), ("h2d_s", C.c_double), ("h2d_bytes", C.c_uint64)]
 
 
 class EngineProf(C.Structure):

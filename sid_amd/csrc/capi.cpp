@@ -43,6 +43,7 @@ extern "C" const char* sid_strerror(int status)
     case SID_EIO: return "output write failed";
     case SID_ERANGE: return "value outside the device formatter's range";
     case SID_ENOBQ: return "no base-quality field";
+    case SID_ELINE: return "a pileup line too long for one chunk (4 GiB)";
     default: return "unknown status";
     }
 }
@@ -130,13 +131,8 @@ extern "C" int sid_create(int device, const sid_opts* opts, sid_ctx** out)
     c->device = device;
     if (opts) c->opts = *opts; else sid_opts_default(&c->opts);
     sid_build_local_k(c->opts, &c->K);
-    if (const char* g = std::getenv("SID_GRID_CAP")) c->grid_cap = std::max(1, std::atoi(g));
-
-    if (const char* g = std::getenv("SID_TABLE_GRID")) c->ws.table_grid = std::max(1, std::atoi(g));
-    if (const char* g = std::getenv("SID_LOCAL_DIRECT")) c->ws.direct = std::atoi(g) != 0;
-    if (const char* g = std::getenv("SID_TABLE_UNROLL")) c->ws.unroll = std::atoi(g);
-    if (const char* g = std::getenv("SID_TABLE_NT")) c->ws.nt = std::atoi(g) != 0;
-    if (const char* g = std::getenv("SID_TABLE_CHUNK")) c->ws.chunk = std::atoi(g) != 0;
+    // SID_TABLE_TAIL=0: the second-level class table off, its sites through
+    // the fix-up (tests/test_local_gpu.py covers both)
     if (const char* g = std::getenv("SID_TABLE_TAIL")) c->ws.tail = std::atoi(g) != 0;
 
     std::vector<double> lnt(SID_LUTN);

@@ -92,30 +92,24 @@ __global__ __launch_bounds__(256) void sid_local_table_build(sid_local_k K, cons
     table[swz ? sid_tab_slot(nf, ns, r2) : i] = v;
 }
 
-// Sites are processed in pairs (one 16-B profile_t load per lane), U pairs
-// per thread per tile, lanes contiguous in every wave instruction: loads and
-// the 16-B conf stores move 1 KiB per instruction, the 2-B code stores 128 B
-// (one full L2 line).  Misses go to an LDS list (one LDS atomic per missed
-// site), flushed with one global atomic per block.
+// Sites are processed in pairs (one 16-B profile_t load per lane), blocks
+// striding over 1024-pair tiles, lanes contiguous in every wave instruction:
+// loads and the 16-B conf stores move 1 KiB per instruction, the 2-B code
+// stores 128 B (one full L2 line).  Misses go to an LDS list (one LDS atomic
+// per missed site), flushed with one global atomic per block.  (Measured and
+// not kept: 2 or 4 pairs per thread, non-temporal stores, one contiguous tile
+// range per block)
 #define SID_LMISS 2048
 
 typedef double sid_dvec2 __attribute__((ext_vector_type(2)));
 
-template <typename T>
-__device__ __forceinline__ void st_stream(T* p, T v, bool nt)
-{
-    if (nt) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
-template <int U, bool NT>
 __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __restrict__ pairs, size_t npairs,
                                                            uint16_t* __restrict__ code2, sid_dvec2* __restrict__ hom,
                                                            sid_dvec2* __restrict__ het,
                                                            const double* __restrict__ g_table, double sig,
                                                            const double* __restrict__ T2,
                                                            uint32_t* __restrict__ miss, uint32_t cap,
-                                                           uint32_t* __restrict__ ctr, bool chunk)
+                                                           uint32_t* __restrict__ ctr)
 {
     __shared__ double T[SID_TAB_N];
     __shared__ uint32_t lmiss[SID_LMISS];
@@ -127,52 +121,32 @@ __global__ __launch_bounds__(1024) void sid_local_table_p2(const ulonglong2* __r
     }
     if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
-    const size_t tile = (size_t)blockDim.x * U;
-    // tiles of this block: grid-stride, or (chunk) one contiguous range
-    const size_t ntiles = (npairs + tile - 1) / tile;
-    size_t tb = blockIdx.x, te = ntiles, ts = gridDim.x;
-    if (chunk) {
-        tb = ntiles * blockIdx.x / gridDim.x;
-        te = ntiles * (blockIdx.x + 1) / gridDim.x;
-        ts = 1;
-    }
-    for (size_t t = tb; t < te; t += ts) {
-        const size_t base = t * tile;
-        ulonglong2 c[U];
-#pragma unroll
-        for (int j = 0; j < U; ++j) {
-            const size_t p = base + (size_t)j * blockDim.x + threadIdx.x;
-            if (p < npairs) c[j] = pairs[p];
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += stride) {
+        const ulonglong2 c = pairs[p];
+        double h0, h1, t0, t1;
+        uint32_t a = table_site(c.x, T, sig, h0, t0);
+        uint32_t b = table_site(c.y, T, sig, h1, t1);
+        // LDS misses (30x het sites, 200x sites with r2 >= 4) through the
+        // second-level table before the stores: an L2 hit the other waves
+        // hide, instead of a scattered rewrite later
+        if (T2 && (a == 0xFFu || b == 0xFFu)) {
+            if (a == 0xFFu) a = table2_site(c.x, T2, sig, h0, t0);
+            if (b == 0xFFu) b = table2_site(c.y, T2, sig, h1, t1);
         }
-#pragma unroll
-        for (int j = 0; j < U; ++j) {
-            const size_t p = base + (size_t)j * blockDim.x + threadIdx.x;
-            if (p < npairs) {
-                double h0, h1, t0, t1;
-                uint32_t a = table_site(c[j].x, T, sig, h0, t0);
-                uint32_t b = table_site(c[j].y, T, sig, h1, t1);
-                // LDS misses (30x het sites, 200x sites with r2 >= 4) through
-                // the second-level table before the stores: an L2 hit the
-                // other waves hide, instead of a scattered rewrite later
-                if (T2 && (a == 0xFFu || b == 0xFFu)) {
-                    if (a == 0xFFu) a = table2_site(c[j].x, T2, sig, h0, t0);
-                    if (b == 0xFFu) b = table2_site(c[j].y, T2, sig, h1, t1);
-                }
-                st_stream(code2 + p, (uint16_t)(a | (b << 8)), NT);
-                st_stream(hom + p, sid_dvec2{h0, h1}, NT);
-                st_stream(het + p, sid_dvec2{t0, t1}, NT);
-                if (a == 0xFFu || b == 0xFFu) {
-                    for (int k = 0; k < 2; ++k) {
-                        if ((k ? b : a) != 0xFFu) continue;
-                        const uint32_t idx = (uint32_t)(2 * p + k);
-                        const uint32_t slot = atomicAdd(&lcnt, 1u);
-                        if (slot < SID_LMISS) {
-                            lmiss[slot] = idx;
-                        } else {
-                            const uint32_t g = atomicAdd(ctr, 1u);
-                            if (g < cap) miss[g] = idx;
-                        }
-                    }
+        code2[p] = (uint16_t)(a | (b << 8));
+        hom[p] = sid_dvec2{h0, h1};
+        het[p] = sid_dvec2{t0, t1};
+        if (a == 0xFFu || b == 0xFFu) {
+            for (int k = 0; k < 2; ++k) {
+                if ((k ? b : a) != 0xFFu) continue;
+                const uint32_t idx = (uint32_t)(2 * p + k);
+                const uint32_t slot = atomicAdd(&lcnt, 1u);
+                if (slot < SID_LMISS) {
+                    lmiss[slot] = idx;
+                } else {
+                    const uint32_t g = atomicAdd(ctr, 1u);
+                    if (g < cap) miss[g] = idx;
                 }
             }
         }
@@ -318,7 +292,7 @@ extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t
     if (n == 0) return hipSuccess;
     const bool aligned = (((uintptr_t)counts | (uintptr_t)hom | (uintptr_t)het) & 15u) == 0 &&
                          (((uintptr_t)code) & 3u) == 0;
-    if (!K->general && ws && ws->table && !ws->direct) {
+    if (!K->general && ws && ws->table) {
         const uint32_t cap = n < 0xFFFFFFFFull ? ws->cap : 0u;   // u32 site indices
         uint32_t* ctr = ws->ctr + ws->parity;
         const int tb = 1024;
@@ -327,20 +301,12 @@ extern "C" hipError_t sid_launch_local(const uint16_t* counts, size_t n, uint8_t
                               (((uintptr_t)code) & 1u) == 0;
         if (aligned2 && n >= 2) {
             const size_t npairs = n / 2;
-            const int U = ws->unroll;
-            size_t want = (npairs + (size_t)tb * U - 1) / ((size_t)tb * U);
+            size_t want = (npairs + (size_t)tb - 1) / (size_t)tb;
             int grid = (int)(want < (size_t)ws->table_grid ? want : (size_t)ws->table_grid);
-            auto* P = (const ulonglong2*)counts;
-            auto* C2 = (uint16_t*)code;
-            auto* H = (sid_dvec2*)hom;
-            auto* Q = (sid_dvec2*)het;
             const double* T2 = ws->tail ? ws->table2 : nullptr;
-            if (U == 1 && !ws->nt) sid_local_table_p2<1, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
-            else if (U == 1) sid_local_table_p2<1, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
-            else if (U == 4 && !ws->nt) sid_local_table_p2<4, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
-            else if (U == 4) sid_local_table_p2<4, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
-            else if (!ws->nt) sid_local_table_p2<2, false><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
-            else sid_local_table_p2<2, true><<<grid, tb, 0, stream>>>(P, npairs, C2, H, Q, ws->table, K->sig, T2, ws->miss, cap, ctr, ws->chunk != 0);
+            sid_local_table_p2<<<grid, tb, 0, stream>>>((const ulonglong2*)counts, npairs, (uint16_t*)code,
+                                                        (sid_dvec2*)hom, (sid_dvec2*)het, ws->table, K->sig, T2,
+                                                        ws->miss, cap, ctr);
             done = npairs * 2;
         }
         if (done < n) {

@@ -1867,33 +1867,15 @@ hipError_t sid_launch_lookup(const uint16_t* counts, size_t n, const unsigned lo
                          (((uintptr_t)code) & 1u) == 0;
     if (rec && rcode && cc && aligned && n >= 2) {
         const size_t npairs = n / 2;
-        // SID_LOOKUP_UNROLL (1, 2) / SID_LOOKUP_GRID: launch shape (A/B knobs).
-        // U = 1, 1024 blocks measured best (C3: 246 us vs 257 us for U = 2)
-        static const int U = [] {
-            const char* e = std::getenv("SID_LOOKUP_UNROLL");
-            return e && std::atoi(e) == 2 ? 2 : 1;
-        }();
-        static const size_t gmax = [] {
-            const char* e = std::getenv("SID_LOOKUP_GRID");
-            return (size_t)(e && std::atoi(e) > 0 ? std::atoi(e) : 1024);
-        }();
-        size_t want = (npairs + (size_t)1024 * U - 1) / ((size_t)1024 * U);
-        const unsigned grid = (unsigned)(want < gmax ? want : gmax);
-        // SID_LOOKUP_INLINE=0: defer every non-record site to the block tail (A/B)
-        static const bool dense_inline = [] {
-            const char* e = std::getenv("SID_LOOKUP_INLINE");
-            return !e || std::atoi(e) != 0;
-        }();
-        if (U == 2)
-            sid_lookup_rec_kernel<2><<<grid, 1024, 0, st>>>((const ulonglong2*)counts, npairs, (const sid_dvec2*)rec,
-                                                            rcode, ckeys, cidx, cmask, special_idx, pcode,
-                                                            (const sid_dvec2*)cc, (uint16_t*)code, (sid_dvec2*)hom,
-                                                            (sid_dvec2*)het, dense_inline);
-        else
-            sid_lookup_rec_kernel<1><<<grid, 1024, 0, st>>>((const ulonglong2*)counts, npairs, (const sid_dvec2*)rec,
-                                                            rcode, ckeys, cidx, cmask, special_idx, pcode,
-                                                            (const sid_dvec2*)cc, (uint16_t*)code, (sid_dvec2*)hom,
-                                                            (sid_dvec2*)het, dense_inline);
+        // one pair per thread, at most 1024 blocks, the dense profiles' records
+        // looked up inline (measured best: C3 246 us vs 257 us with two pairs
+        // per thread)
+        size_t want = (npairs + (size_t)1024 - 1) / (size_t)1024;
+        const unsigned grid = (unsigned)(want < 1024 ? want : 1024);
+        sid_lookup_rec_kernel<1><<<grid, 1024, 0, st>>>((const ulonglong2*)counts, npairs, (const sid_dvec2*)rec,
+                                                        rcode, ckeys, cidx, cmask, special_idx, pcode,
+                                                        (const sid_dvec2*)cc, (uint16_t*)code, (sid_dvec2*)hom,
+                                                        (sid_dvec2*)het, true);
         done = 2 * npairs;
     }
     if (done < n) {

@@ -86,6 +86,13 @@ static void dfree(T*& p)
     p = nullptr;
 }
 
+// SID_LYNCH_TIMING=1: the estimate's phase times (ms) on stderr, measurement only
+static bool lynch_timing()
+{
+    static const bool on = std::getenv("SID_LYNCH_TIMING") != nullptr;
+    return on;
+}
+
 struct sid_lynch_dev {
     // accumulation hash (device)
     unsigned long long* gkeys = nullptr;
@@ -97,7 +104,7 @@ struct sid_lynch_dev {
     // profiles' keys go through the fallback list into the hash
     unsigned long long* dense = nullptr;   // [SID_DENSE_ROWS][SID_DENSE_N]
     uint32_t* part = nullptr;              // per-block rows of the dense pass
-    int hist_grid = 256;                   // SID_HIST_GRID (measurement knob); 256: 89 us vs 95 us at 512 (hist_probe)
+    int hist_grid = 256;                   // blocks of the dense pass: 89 us vs 95 us at 512 (hist_probe)
     unsigned long long* list = nullptr;
     uint64_t list_cap = 0;
     hipStream_t acc_stream = nullptr;      // stream of the last accumulate
@@ -292,7 +299,6 @@ extern "C" int sid_profile_reset(sid_ctx* c, void* stream)
     if (!L->stats) HIPCHECK(hipMalloc(&L->stats, 3 * sizeof(unsigned long long)));
     if (!L->dense) {
         HIPCHECK(hipMalloc(&L->dense, SID_DENSE_ROWS * SID_DENSE_N * sizeof(unsigned long long)));
-        if (const char* e = std::getenv("SID_HIST_GRID")) L->hist_grid = std::max(1, std::min(512, std::atoi(e)));
         HIPCHECK(hipMalloc(&L->part, (size_t)L->hist_grid * SID_DENSE_N * sizeof(uint32_t)));
     }
     HIPCHECK(hipMemsetAsync(L->stats, 0, 3 * sizeof(unsigned long long), st));
@@ -939,7 +945,7 @@ static int run_estimate_device(sid_ctx* c, int verbose, sid_estimate* est, bool*
     const sid_nm_result r = *L->h_nmres;
     L->nm_rounds = (uint64_t)r.rounds;
     L->nm_points = r.points;
-    if (std::getenv("SID_LYNCH_TIMING"))
+    if (lynch_timing())
         std::fprintf(stderr, "{\"nm_ticks\": [%lld, %lld, %lld, %lld]}\n", r.ticks[0], r.ticks[1], r.ticks[2],
                      r.ticks[3]);
     L->launches = 1;
@@ -979,8 +985,7 @@ extern "C" int sid_lynch_prepare_given(sid_ctx* c, int verbose, const sid_estima
     sid_lynch_dev* L;
     int rc = lynch_of(c, &L);
     if (rc) return rc;
-    // SID_LYNCH_TIMING=1: phase times (ms) on stderr, measurement only
-    static const bool timing = std::getenv("SID_LYNCH_TIMING") != nullptr;
+    const bool timing = lynch_timing();
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();

@@ -117,8 +117,8 @@ double unix_now()
 // The end of a successful run: stdout and stderr flushed, then the process
 // ends without the HIP runtime's teardown (the kernel driver releases the
 // HBM, the pinned pages and the mapping with the process either way).
-// SID_EXIT=normal: exit() with the runtime's static destructors instead (A/B).
-// Under the profiler (ROCPROF* / ROCP_* in the environment: rocprofv3 sets
+// (exit() with the runtime's static destructors measured 0.06-0.18 s slower;
+// DESIGN.md §6.)  Under the profiler (ROCPROF* / ROCP_* in the environment: rocprofv3 sets
 // them for its preloaded tool, which writes its buffers from atexit
 // handlers) exit() is used too, so traces of this binary are complete.
 bool tool_attached()
@@ -133,8 +133,7 @@ bool tool_attached()
 {
     std::fflush(stdout);
     std::fflush(stderr);
-    static const char* mode = std::getenv("SID_EXIT");
-    if ((mode && std::strcmp(mode, "normal") == 0) || tool_attached()) std::exit(code);
+    if (tool_attached()) std::exit(code);
     ::_exit(code);
 }
 
@@ -282,11 +281,8 @@ int main(int argc, char** argv)
     // start-up and the engine's creation (60-240 ms: the runtime's
     // initialisation, the contexts' class tables, the streams' hardware
     // queues) on a second thread while this one maps the file and populates
-    // its page tables (~30 ms for 4 GB).  SID_CLI_OVERLAP=0: one after the
-    // other (A/B).
-    const char* ov = std::getenv("SID_CLI_OVERLAP");
-    const bool overlap = !opt.host_parse && in.fd >= 0 && !in.data && in.len && in.len <= (8ull << 30) &&
-                         !(ov && std::strcmp(ov, "0") == 0);
+    // its page tables (~30 ms for 4 GB).
+    const bool overlap = !opt.host_parse && in.fd >= 0 && !in.data && in.len && in.len <= (8ull << 30);
     int ndev = 0, D = 0;
     sid_engine* eng = nullptr;
     sid_engine_cfg cfg;
@@ -417,31 +413,21 @@ int main(int argc, char** argv)
         if (rc == SID_EIO) std::exit(EXIT_FAILURE);
         CHECK(rc, "emit");
         const double t3 = now();
-        // SID_CLI_TEARDOWN=1 (a probe): the mapping and the engine released
-        // here, each timed, instead of with the process
-        double unmap_s = -1, destroy_s = -1;
-        const char* td = std::getenv("SID_CLI_TEARDOWN");
-        if (td && std::strcmp(td, "1") == 0) {
-            const double u0 = now();
-            if (pre_map) munmap((void*)pre_map, in.len);
-            const double u1 = now();
-            sid_engine_destroy(eng);
-            unmap_s = u1 - u0;
-            destroy_s = now() - u1;
-        }
         if (opt.stats)
             std::fprintf(stderr,
                          "{\"sites\": %llu, \"devices\": %d, \"threads\": %d, \"path\": \"stream\", "
                          "\"create_s\": %.6f, \"parse_s\": %.6f, \"device_s\": %.6f, \"emit_s\": %.6f, \"total_s\": %.6f, "
                          "\"sites_per_s\": %.1f, \"chunks\": %llu, \"chunks_held\": %llu, "
                          "\"chunks_retained\": %llu, \"chunks_reloaded\": %llu, \"bytes_in\": %llu, "
-                         "\"bytes_out\": %llu, \"unmap_s\": %.6f, \"destroy_s\": %.6f, "
+                         "\"bytes_out\": %llu, \"ingest_s\": %.6f, \"chunks_registered\": %llu, "
+                         "\"register_s\": %.6f, \"h2d_s\": %.6f, \"h2d_bytes\": %llu, "
                          "\"main_entry_unix\": %.6f, \"main_exit_unix\": %.6f}\n",
                          (unsigned long long)st.sites, D, T, tc - t0, t1 - t0, t2 - t1, t3 - t2, t3 - t0,
                          st.sites / std::max(1e-9, t3 - t0), (unsigned long long)st.chunks,
                          (unsigned long long)st.chunks_held, (unsigned long long)st.chunks_retained,
                          (unsigned long long)st.chunks_reloaded, (unsigned long long)st.bytes_in,
-                         (unsigned long long)st.bytes_out, unmap_s, destroy_s, t_entry, unix_now());
+                         (unsigned long long)st.bytes_out, st.ingest_s, (unsigned long long)st.chunks_registered,
+                         st.register_s, st.h2d_s, (unsigned long long)st.h2d_bytes, t_entry, unix_now());
         // device memory, pinned staging and the mapping go with the process
         finish(0);
     }

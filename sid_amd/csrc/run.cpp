@@ -325,6 +325,37 @@ struct Dev {
     uint64_t hold_budget = 0, retain_budget = 0;
     std::atomic<uint64_t> hold_used{0}, retain_used{0};
     std::atomic<bool> hold_full{false};
+    // the ingest's host-to-device copies, timed on the upload stream (pairs
+    // of timing events, summed after the ingest's sync)
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> h2d_pending;
+    std::vector<hipEvent_t> h2d_free;
+    uint64_t h2d_bytes = 0;
+    hipEvent_t h2d_event()
+    {
+        hipEvent_t ev = nullptr;
+        if (!h2d_free.empty()) {
+            ev = h2d_free.back();
+            h2d_free.pop_back();
+        } else if (hipEventCreate(&ev) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        return ev;
+    }
+    // device time of the copies timed since the last call (the stream drained)
+    double h2d_collect()
+    {
+        double s = 0;
+        for (auto& pr : h2d_pending) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) s += ms * 1e-3;
+            h2d_free.push_back(pr.first);
+            h2d_free.push_back(pr.second);
+        }
+        (void)hipGetLastError();
+        h2d_pending.clear();
+        return s;
+    }
     std::mutex ev_m;
     std::vector<hipEvent_t> ev_cache;   // events marking a chunk's records written (compute -> drain)
     // sid_engine_profile: (stage, start, end) per stage and chunk, read after a sync
@@ -401,6 +432,7 @@ struct sid_engine {
     // the writer's waits for D2H pieces, printed per phase
     std::atomic<uint64_t> t_comp_sync{0}, t_write_wait{0};
     std::atomic<uint64_t> reg_chunks{0};   // chunks uploaded from registered pages (upload_register)
+    std::atomic<uint64_t> t_register{0};   // ns in hipHostRegister / hipHostUnregister (the uploaders)
     // host-generated input: pinned buffers
     std::vector<char*> gen_buf;
     std::vector<uint64_t> gen_cap;
@@ -666,6 +698,8 @@ extern "C" int sid_engine_destroy(sid_engine* e)
         for (hipEvent_t ev : d->ev_cache) (void)hipEventDestroy(ev);
         for (auto& pr : d->prof_pending) (void)hipEventDestroy(pr.second.first), (void)hipEventDestroy(pr.second.second);
         for (hipEvent_t ev : d->prof_free) (void)hipEventDestroy(ev);
+        for (auto& pr : d->h2d_pending) (void)hipEventDestroy(pr.first), (void)hipEventDestroy(pr.second);
+        for (hipEvent_t ev : d->h2d_free) (void)hipEventDestroy(ev);
         sid_chunk_release(&d->ws);
         if (d->h_small) (void)hipHostFree(d->h_small);
         for (hipStream_t s : {d->s_up, d->s_comp, d->s_d2h})
@@ -891,7 +925,7 @@ struct UploadReg {
     {
         for (auto& r : regs) {
             if (r.ev) (void)hipEventSynchronize(r.ev);
-            (void)hipHostUnregister(r.p);
+            unregister(r.p);
         }
         for (auto& r : regs)
             if (r.ev) (void)hipEventDestroy(r.ev);
@@ -914,8 +948,11 @@ struct UploadReg {
         const uintptr_t s = (uintptr_t)(e->text + r.off), t = s + r.len;
         const uintptr_t a = (s + pg - 1) & ~(uintptr_t)(pg - 1), b = t & ~(uintptr_t)(pg - 1);
         if (b <= a || b - a < (1u << 20)) return;
-        if (hipHostRegister((void*)a, b - a, hipHostRegisterReadOnly) != hipSuccess &&
-            ((void)hipGetLastError(), hipHostRegister((void*)a, b - a, hipHostRegisterDefault) != hipSuccess)) {
+        const double t0 = wall();
+        const bool ok = hipHostRegister((void*)a, b - a, hipHostRegisterReadOnly) == hipSuccess ||
+                        ((void)hipGetLastError(), hipHostRegister((void*)a, b - a, hipHostRegisterDefault) == hipSuccess);
+        e->t_register += (uint64_t)((wall() - t0) * 1e9);
+        if (!ok) {
             (void)hipGetLastError();   // not an error: the pageable path from now on
             on = false;
             return;
@@ -960,11 +997,17 @@ struct UploadReg {
         }
         return x;
     }
+    void unregister(char* p)
+    {
+        const double t0 = wall();
+        (void)hipHostUnregister(p);
+        e->t_register += (uint64_t)((wall() - t0) * 1e9);
+    }
     // unregister the bodies whose copies are done (in copy order)
     void release_done()
     {
         while (!regs.empty() && regs.front().copied && hipEventQuery(regs.front().ev) == hipSuccess) {
-            (void)hipHostUnregister(regs.front().p);
+            unregister(regs.front().p);
             evs.push_back(regs.front().ev);
             regs.pop_front();
         }
@@ -1057,7 +1100,17 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
         }
         uint64_t len = r.len;
         if (e->src == SRC_HOST || e->src == SRC_FILE) {
-            if (len) x = reg.copy(dst, j, d.s_up);
+            hipEvent_t h0 = pass == 1 && len ? d.h2d_event() : nullptr, h1 = h0 ? d.h2d_event() : nullptr;
+            if (h0 && h1) x = hipEventRecord(h0, d.s_up);
+            if (len && x == hipSuccess) x = reg.copy(dst, j, d.s_up);
+            if (h0 && h1 && x == hipSuccess) {
+                x = hipEventRecord(h1, d.s_up);
+                d.h2d_pending.push_back({h0, h1});
+                d.h2d_bytes += len;
+            } else {
+                if (h0) d.h2d_free.push_back(h0);
+                if (h1) d.h2d_free.push_back(h1);
+            }
             // the next chunk's pages pinned while this copy runs; the ones
             // whose copies are done released
             if (x == hipSuccess) reg.ahead(next_of(j));
@@ -1281,12 +1334,7 @@ void compute(sid_engine* e, Dev& d, int pass)
             pe = d.prof_begin(P);
             // -m local: the records' lengths come out of the parse when this
             // pass formats (sid_parse_len_kernel; the length kernel is skipped)
-            // (SID_PARSE_LEN=0: the separate length kernel; A/B)
-            static const bool parse_len = [] {
-                const char* v = std::getenv("SID_PARSE_LEN");
-                return !v || std::atoi(v) != 0;
-            }();
-            const bool lens = parse_len && e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx) && !qmode &&
+            const bool lens = e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx) && !qmode &&
                               !(pass == 1 && e->lynch) && (pass == 2 || needs_format_pass1(e));
             if (rc == SID_OK) rc = sid_chunk_parse(&W, L.base, L.c0, L.c1, n, qmode, d.s_comp, lens ? d.ctx : nullptr);
             d.prof_end(1, pe);
@@ -1316,13 +1364,8 @@ void compute(sid_engine* e, Dev& d, int pass)
         const bool fused = e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx);
         // likelihood_ratio / bayes pass 2: the class lookup fused into the
         // formatter (sid_chunk_lynch_*; the records' tails prebuilt per class)
-        // (SID_LYNCH_FUSED=0: lookup, then the generic formatter; A/B)
-        static const bool lynch_fused = [] {
-            const char* v = std::getenv("SID_LYNCH_FUSED");
-            return !v || std::atoi(v) != 0;
-        }();
         sid_lynch_fmt lv;
-        const bool lfused = lynch_fused && pass == 2 && !fused && sid_lynch_fmt_view(d.ctx, &lv) == SID_OK;
+        const bool lfused = pass == 2 && !fused && sid_lynch_fmt_view(d.ctx, &lv) == SID_OK;
         if (format && !lynch_hist) {
             if (!fused && !lfused) {
                 pe = d.prof_begin(P);
@@ -1406,6 +1449,19 @@ void compute(sid_engine* e, Dev& d, int pass)
             release_slot();
             if (pass == 2) return (void)fail(e, SID_EMALFORMED);   // cannot happen: pass 1 validated
             continue;
+        }
+        if (pass == 1 && n == 0 && format && !lynch_hist) {
+            // a chunk without sites has no records: done in pass 1 for the
+            // sinks that take records then (else the emit would start its
+            // threads and a second pass for it)
+            if (sink_all_pass1(e)) {
+                r.sunk = true;
+                r.held_len = 0;
+            } else if (d.hh) {
+                r.host = d.hh;
+                r.host_len = 0;
+                r.host1 = true;
+            }
         }
         if (!format || lynch_hist || (pass == 1 && !out)) {
             release_slot();
@@ -1566,6 +1622,7 @@ static void timing_report(sid_engine* e, const char* phase, double s)
                      (unsigned long long)e->reg_chunks.load());
     e->t_comp_sync = e->t_write_wait = 0;
     e->reg_chunks = 0;
+    e->t_register = 0;
 }
 
 static void reset_run(sid_engine* e)
@@ -1599,6 +1656,8 @@ static void reset_run(sid_engine* e)
         d.arena_off = 0;
         d.hh_off = 0;
         d.hh_full = false;
+        (void)d.h2d_collect();   // (a failed run's copies: its devices were synchronised)
+        d.h2d_bytes = 0;
     }
     e->hist_merged = false;
 }
@@ -1655,23 +1714,14 @@ static int setup_generator(sid_engine* e)
 }
 
 // The emit's pinned ring per device: 4 x 16 MiB (pinned once, reused by
-// every run; 8 x 16, 4 x 64 and 16 x 8 MiB measured slower while the pinning
-// was on the emit's path)
-// (SID_EMIT_RING_MIB: the piece size, 1-256 MiB; A/B)
+// every run; 8 x 16, 4 x 64, 4 x 128 and 16 x 8 MiB measured slower: the
+// pinning slows the ingest beside it and the exit tail grows with it)
 constexpr int EMIT_RING_N = 4;
-static uint64_t emit_ring_bytes()
-{
-    static const uint64_t b = [] {
-        const char* v = std::getenv("SID_EMIT_RING_MIB");
-        const long m = v ? std::atol(v) : 16;
-        return (uint64_t)std::min(256L, std::max(1L, m)) << 20;
-    }();
-    return b;
-}
+constexpr uint64_t EMIT_RING_BYTES = 16ull << 20;
 static int alloc_ring(Dev& d)
 {
     if (hipSetDevice(d.device) != hipSuccess) return SID_EHIP;
-    const uint64_t bytes = emit_ring_bytes();
+    const uint64_t bytes = EMIT_RING_BYTES;
     while ((int)d.pinned.size() < EMIT_RING_N) {
         char* p = nullptr;
         hipEvent_t ev;
@@ -1685,15 +1735,6 @@ static int alloc_ring(Dev& d)
     }
     d.pinned_cap = bytes;
     return SID_OK;
-}
-
-// SID_EMIT_RING_EARLY=0: the emit's ring pinned by the emit itself (A/B);
-// default: pinned on a thread of its own during the ingest of a run that
-// writes its records through it (no host arena, no device sink)
-static bool ring_early()
-{
-    static const char* v = std::getenv("SID_EMIT_RING_EARLY");
-    return !(v && std::strcmp(v, "0") == 0);
 }
 
 extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
@@ -1716,8 +1757,10 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         th.emplace_back(uploader, e, std::ref(*e->devs[i]), std::cref(lists[i]), 1);
         th.emplace_back(compute, e, std::ref(*e->devs[i]), 1);
     }
-    // (a failure here leaves the ring to the emit, which reports it)
-    if (e->cfg.device_sink == 0 && e->cfg.host_hold_bytes == 0 && ring_early())
+    // the emit's pinned ring, pinned on a thread of its own during the ingest
+    // of a run that writes its records through it (no host arena, no device
+    // sink); a failure here leaves the ring to the emit, which reports it
+    if (e->cfg.device_sink == 0 && e->cfg.host_hold_bytes == 0)
         th.emplace_back([e] {
             for (auto& dp : e->devs) (void)alloc_ring(*dp);
         });
@@ -1727,11 +1770,16 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         for (auto& dp : e->devs) (void)hipSetDevice(dp->device), (void)hipDeviceSynchronize();
         return e->rc.load();
     }
+    double h2d_s = 0;
+    uint64_t h2d_bytes = 0;
     for (auto& dp : e->devs) {
         (void)hipSetDevice(dp->device);
         if (hipStreamSynchronize(dp->s_comp) != hipSuccess || hipStreamSynchronize(dp->s_up) != hipSuccess ||
             hipStreamSynchronize(dp->s_d2h) != hipSuccess)
             return SID_EHIP;
+        h2d_s += dp->h2d_collect();
+        h2d_bytes += dp->h2d_bytes;
+        dp->h2d_bytes = 0;
     }
     uint64_t sites = 0, bytes = 0, held = 0, kept = 0;
     for (auto& r : e->recs) {
@@ -1750,6 +1798,10 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         st->status_kind = 0;
         st->err_offset = 0;
         st->ingest_s = wall() - t0;
+        st->chunks_registered = e->reg_chunks.load();
+        st->register_s = e->t_register.load() * 1e-9;
+        st->h2d_s = h2d_s;
+        st->h2d_bytes = h2d_bytes;
     }
     timing_report(e, "ingest", wall() - t0);
     const uint64_t fe = e->first_err.load();
@@ -2005,19 +2057,6 @@ extern "C" int sid_engine_emit(sid_engine* e, const char* header, sid_write_fn w
         (void)hipSetDevice(dp->device);
         if (hipDeviceSynchronize() != hipSuccess) fail(e, SID_EHIP);
     }
-    // SID_EMIT_FREE_RING=1: the pinned ring released after the run (a
-    // one-run process: the driver's teardown of pinned pages at exit)
-    static const char* fr = std::getenv("SID_EMIT_FREE_RING");
-    if (fr && std::strcmp(fr, "1") == 0)
-        for (auto& dp : e->devs) {
-            Dev& d = *dp;
-            (void)hipSetDevice(d.device);
-            for (char* p : d.pinned) (void)hipHostFree(p);
-            for (hipEvent_t ev : d.pinned_ev) (void)hipEventDestroy(ev);
-            d.pinned.clear();
-            d.pinned_ev.clear();
-            d.free_pinned.reset();
-        }
     if (st) {
         st->chunks_reloaded = e->reloaded.load();
         st->bytes_out = sink == 1 ? e->sink_bytes.load() : out_bytes.load();

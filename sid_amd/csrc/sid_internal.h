@@ -26,11 +26,7 @@ struct sid_local_ws {
     uint32_t* ctr = nullptr;     // [2] miss counters, alternating per call
     int parity = 0;
     int table_grid = 4096;       // blocks of the table kernel (2 resident per CU; 8 rounds)
-    int direct = 0;              // SID_LOCAL_DIRECT=1: bypass the table (A/B)
-    int unroll = 1;              // SID_TABLE_UNROLL: pairs per thread per tile (1, 2, 4)
-    int nt = 0;                  // SID_TABLE_NT=1: non-temporal output stores
-    int chunk = 0;               // SID_TABLE_CHUNK=1: one contiguous tile range per block
-    int tail = 1;                // SID_TABLE_TAIL=0: no inline second-level lookup, every miss to the fix-up (A/B)
+    int tail = 1;                // SID_TABLE_TAIL=0: no inline second-level lookup, every miss to the fix-up
     hipEvent_t ev_mid = nullptr; // set only while timing: recorded between main and fix-up
     // the record tails per class entry (the engine's -m local formatter):
     // SID_STR_BYTES per entry of table / table2 (local.hip), and their lengths
@@ -166,7 +162,6 @@ struct sid_chunk_ws {
     uint32_t* bsum = nullptr;     // per 256-site block record bytes (+ scan workspace)
     uint64_t* boff = nullptr;
     uint16_t* masks = nullptr;    // line-start masks of the index, a u16 per lane per 4 KiB tile
-    uint16_t* lowm = nullptr;     // token-end bytes (< 0x21 or outside the chunk), a u16 per 16 B in text order
     unsigned long long* lb = nullptr;   // formatter flags and totals (sid_chunk_fmt_len)
     uint64_t* state = nullptr;    // [0] sites [1..2] parse range [3] CSV bytes [4] first error key [5] range flag
                                   // [6] [7] fallback lines

@@ -341,30 +341,13 @@ __device__ __forceinline__ uint32_t ix_mask(const IxWin& w, uint64_t at, uint64_
     return m;
 }
 
-// The window's token-end bytes for the cooperative parse: bit j = byte j is
-// < 0x21 (' ', '\t', '\n', NUL, other control bytes) or outside [c0, c1)
-// (such a byte ends any token).  Which of them a line's separators are is
-// checked per line by the parse (only ' ' and '\t' separate tokens there).
-__device__ __forceinline__ uint32_t ix_low(const IxWin& w, uint64_t at, uint64_t c0, uint64_t c1)
-{
-    uint32_t inr = 0xFFFFu;   // bytes inside [c0, c1)
-    if (at + 16 > c1) inr = c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
-    if (at < c0) inr &= c0 - at >= 16 ? 0u : (0xFFFFu << (uint32_t)(c0 - at)) & 0xFFFFu;
-    return (compress8(low_bytes(w.v.x), low_bytes(w.v.y)) | (compress8(low_bytes(w.v.z), low_bytes(w.v.w)) << 8) |
-            ~inr) & 0xFFFFu;
-}
-
 // Blocks stride over the tiles (a fixed grid of a few per CU), the next
 // tile's four windows per lane in flight while this one is counted; the tile
 // count is a block reduction (two LDS slots alternate: one barrier a tile).
-// LOWM (the cooperative parse) also writes the token-end mask (ix_low: a u16
-// per 16-B window in text order from tile_base, 1/8 of the text).
-template <bool LOWM>
 __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restrict__ text, uint64_t tile_base,
                                                              uint64_t c0, uint64_t c1, uint64_t ntiles,
                                                              uint16_t* __restrict__ masks,
-                                                             uint32_t* __restrict__ cnt, uint64_t* __restrict__ state,
-                                                             uint16_t* __restrict__ lowm)
+                                                             uint32_t* __restrict__ cnt, uint64_t* __restrict__ state)
 {
     __shared__ uint32_t red[2][TB / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -398,7 +381,6 @@ __global__ __launch_bounds__(TB) void sid_index_count_kernel(const char* __restr
             const uint32_t m = ix_mask(cur[k], at, c0, c1);
             c += __popc(m);
             mw |= (uint64_t)m << (16 * k);
-            if (LOWM) lowm[(t * IX_SUB + k) * TB + threadIdx.x] = (uint16_t)ix_low(cur[k], at, c0, c1);
         }
         ST_MID((uint64_t*)masks + t * TB + threadIdx.x, mw);
 #pragma unroll
@@ -686,12 +668,6 @@ __device__ __noinline__ void parse_line_serial(const char* __restrict__ text, ui
 __device__ __forceinline__ int ctz64(uint64_t x) { return x ? __builtin_ctzll(x) : 64; }
 
 constexpr int HDR_BYTES = 48;   // bytes staged per lane for the header (3 aligned windows)
-// 1: the header's token starts from the low-byte mask alone (3 instructions a
-// word; lines with single ' '/'\t' gaps); 0: separator and control-byte masks
-// per word (strtok_r's separator runs in the fast path too; A/B)
-#ifndef SID_PARSE_HDR
-#define SID_PARSE_HDR 1
-#endif
 
 // 8 bytes from a lane's staged header at any offset < HDR_BYTES + 16: two
 // aligned 8-B LDS reads and a funnel shift (past the lane's 48 bytes: the next
@@ -709,71 +685,6 @@ __device__ __forceinline__ uint32_t not_digit(uint32_t x)
     const uint32_t lt3a = ~(((x & 0x7F7F7F7Fu) + 0x46464646u) | x) & 0x80808080u;   // b < ':'
     return lt30 | (~lt3a & 0x80808080u);
 }
-
-// token 4 from q, in aligned 16-B windows (the fast path's read-bases count,
-// pileup.cpp:70-153); kd = the class '.' and ',' stand for
-__device__ __forceinline__ bool read_bases_fast(const char* __restrict__ text, uint64_t len, uint64_t q, uint32_t kd,
-                                                uint64_t* out)
-{
-    uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
-    uint64_t a = q & ~(uint64_t)15;
-    uint32_t lead = (uint32_t)(q & 15);   // bytes of the first window before the token
-    uint32_t carry = 0;                   // bit 7: byte 0 of the next word is skipped
-    bool done = false, bad = false;
-    uint4 vn = *(const uint4*)(text + a);
-    do {
-        const uint4 v = vn;
-        vn = *(const uint4*)(text + a + 16);   // the next window in flight while this one is processed
-        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-        // bytes of this window inside [q, len) as 16 bits, once per window
-        const uint32_t room = len > a ? (uint32_t)min(len - a, (uint64_t)16) : 0u;
-        const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t x = ws[k];
-            const int b0 = 4 * k;
-            // the word's 4 valid bits as bit 7 of its bytes (24-bit multiply;
-            // the partial products are disjoint: no carries)
-            uint32_t vm = (__umul24((valid >> b0) & 15u, 0x00204081u) & 0x01010101u) << 7;
-            const int hi_b = (int)room - b0;   // bytes of this word before the end of the text (< 4: the last)
-            vm = done ? 0u : vm;
-            const uint32_t lo = low_bytes(x) & vm;
-            const uint32_t first = lo & (0u - lo);                  // the token's end, if in this word
-            const uint32_t tb = (x >> (first ? (__builtin_ctz(first) - 7) : 0)) & 0xFFu;
-            bad = bad || (first && tb != ' ' && tb != '\t' && tb != '\n' && tb != 0);
-            vm &= first - 1u;                                       // bytes before it (all if none)
-            done = done || first != 0 || hi_b < 4;
-            const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
-            const uint32_t skip = ((caret << 8) | carry) & vm;
-            bad = bad || (caret & skip) != 0;                        // '^' run
-            carry = caret >> 24;                                     // bit 31 -> bit 7
-            const uint32_t cm = vm & ~skip;
-            bad = bad || (eq_bytes(x | 0x06060606u, 0x2F2F2F2Fu) & cm) != 0;   // '+' '-' (')' '/')
-            const uint32_t f = x | 0x20202020u;
-            nA += __popc(eq_bytes(f, 0x61616161u) & cm);
-            nC += __popc(eq_bytes(f, 0x63636363u) & cm);
-            nG += __popc(eq_bytes(f, 0x67676767u) & cm);
-            nT += __popc(eq_bytes(f, 0x74747474u) & cm);
-            nM += __popc(eq_bytes(x | 0x02020202u, 0x2E2E2E2Eu) & cm);
-        }
-        lead = 0;
-        a += 16;
-    } while (!done);
-    if (bad) return false;
-    nA += kd == K_A ? nM : 0;
-    nC += kd == K_C ? nM : 0;
-    nG += kd == K_G ? nM : 0;
-    nT += kd == K_T ? nM : 0;
-    *out = (uint64_t)(uint16_t)nA | ((uint64_t)(uint16_t)nC << 16) | ((uint64_t)(uint16_t)nG << 32) |
-           ((uint64_t)(uint16_t)nT << 48);
-    return true;
-}
-
-// 1: the read-bases counts by an LDS table, one lookup a byte (below); 0:
-// five SWAR equality masks and popcounts a word (A/B)
-#ifndef SID_PARSE_LUT
-#define SID_PARSE_LUT 1
-#endif
 
 // The LDS table of the read-bases counts (pileup.cpp:76-150): a byte's
 // increments in 5-bit fields -- a 16-byte window adds at most 16 to a field:
@@ -836,29 +747,20 @@ __device__ __forceinline__ uint32_t rb_window(const uint4 v, uint32_t valid, int
     return acc;
 }
 
-// read_bases_fast with the table: the first window (the token's start inside
-// it) masked, then whole windows while they lie inside the text.  first: the
-// first window's 16 bytes, in the header's LDS stage (no second global load
-// of bytes the header already read)
-// SID_RB_STAGED=1: the windows after the first that the header's 48 staged
-// bytes also hold come from the stage too (nst of them: 2, 1 or 0); A/B
-#ifndef SID_RB_STAGED
-#define SID_RB_STAGED 0
-#endif
+// The read-bases count by the table: the first window (the token's start
+// inside it) masked, then whole windows while they lie inside the text.
+// first: the first window's 16 bytes, in the header's LDS stage (no second
+// global load of bytes the header already read).  (The next windows from the
+// stage too, where the 48 staged bytes hold them, measured slower: the loads
+// hit the caches already)
 __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, uint64_t len, uint64_t q, uint32_t kd,
-                                               const uint32_t* lut, const uint4* first, uint64_t* out, int nst = 0)
+                                               const uint32_t* lut, const uint4* first, uint64_t* out)
 {
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
     uint64_t a = q & ~(uint64_t)15;
     uint32_t carry = 0;   // bit 7: byte 0 of the next word is skipped
     bool done = false, bad = false;
-#if SID_RB_STAGED
-    uint4 vn = nst >= 1 ? first[1] : *(const uint4*)(text + a + 16);
-    int k = 1;
-#else
-    (void)nst;
     uint4 vn = *(const uint4*)(text + a + 16);   // the next window in flight while the first is counted
-#endif
     uint32_t acc = 0;
     auto masked = [&](const uint4& v, uint32_t lead) {
         const int room = len > a ? (int)min(len - a, (uint64_t)16) : 0;
@@ -877,12 +779,7 @@ __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, ui
     a += 16;
     while (!done) {
         const uint4 v = vn;
-#if SID_RB_STAGED
-        ++k;
-        vn = k <= nst ? first[k] : *(const uint4*)(text + a + 16);
-#else
         vn = *(const uint4*)(text + a + 16);
-#endif
         add(a + 16 <= len ? rb_window<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u));
         a += 16;
     }
@@ -993,7 +890,6 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     *(uint4*)(stage) = v0;
     *(uint4*)(stage + 16) = v1;
     *(uint4*)(stage + 32) = v2;
-#if SID_PARSE_HDR
     // low bytes (< 0x21: the separators, '\n', NUL, every other control byte)
     // of the 48 staged bytes as a 48-bit mask: 3 instructions a word
     const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
@@ -1033,49 +929,6 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     const int l0 = t1 - 1;
     const int lp = t2 - 1 - t1;
     const uint32_t ref = (uint8_t)stage[sh + t2];
-#else
-    const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
-    // S: separator bytes as a 48-bit mask; fbad: window offset of the first
-    // control byte ('\n', NUL, < 0x20 but '\t') at or after the line's start
-    // (per word, no second compressed mask)
-    uint32_t fbad = 64;
-    const uint32_t from = (0xFFFFu << sh) & 0xFFFFu;   // the line's bytes among the first 16
-    uint32_t sp[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        sp[k] = eq_bytes(w[k], 0x20202020u) | eq_bytes(w[k], 0x09090909u);
-        uint32_t bl = low_bytes(w[k]) & ~sp[k];
-        if (k < 4) bl &= (__umul24((from >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) << 7;
-        const uint32_t f = (uint32_t)__ffs(bl);
-        fbad = min(fbad, f ? 4u * k + ((f - 1u) >> 3) : 64u);
-    }
-    const uint32_t s_lo = compress8(sp[0], sp[1]) | (compress8(sp[2], sp[3]) << 8) |
-                          (compress8(sp[4], sp[5]) << 16) | (compress8(sp[6], sp[7]) << 24);
-    const uint32_t s_hi = compress8(sp[8], sp[9]) | (compress8(sp[10], sp[11]) << 8);
-    uint64_t S = ((uint64_t)s_hi << 32) | s_lo;
-    // bit j = byte s0 + j, for the bytes inside the text and the 48 staged
-    const uint64_t avail = len > s0 ? len - s0 : 0;
-    const uint32_t nb = (uint32_t)min((uint64_t)(HDR_BYTES - sh), avail);
-    const uint64_t valid = nb >= 64 ? ~0ull : ((1ull << nb) - 1);
-    S = (S >> sh) & valid;
-    const uint64_t N = ~S & valid;
-    uint64_t T = N & ~(N << 1);   // token starts
-    const int t0 = ctz64(T);
-    T &= T - 1;
-    const int t1 = ctz64(T);
-    T &= T - 1;
-    const int t2 = ctz64(T);
-    T &= T - 1;
-    T &= T - 1;
-    const int t4 = ctz64(T);
-    bool ok = t4 < (int)nb;                                          // token 4 starts inside the staged bytes
-    ok = ok && fbad - sh >= (uint32_t)t4;                            // no '\n', NUL, control byte before it
-    ok = ok && ((S >> ((t2 + 1) & 63)) & 1);                         // token 2 is one byte
-    if (!ok) return false;
-    const int l0 = ctz64(S >> t0);
-    const int lp = ctz64(S >> t1);
-    const uint32_t ref = (uint8_t)stage[sh + t2];
-#endif
     // the position: its first 8 bytes by two aligned 8-B LDS reads and a
     // funnel shift, digit-checked in SWAR, left-padded with zero digits and
     // summed by v_dot4 pairs (10, 1) and two 24-bit multiply-adds; a 9th digit
@@ -1107,28 +960,20 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
     const uint32_t kd = cls[up], kc = cls[lw];
     if (kd >= K_CARET || kc >= K_CARET || kd != kc) return false;
-#if SID_PARSE_LUT
     if (QUAD)
         return read_bases_quad(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out);
-    return read_bases_lut(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out,
-                          2 - (int)((sh + t4) >> 4));
-#else
-    return read_bases_fast(text, len, s0 + (uint64_t)t4, kd, out);
-#endif
+    return read_bases_lut(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out);
 }
 
 // Pass 1: the fast path over every line; a line it cannot take is appended to
 // the fallback list fb (count in *fbn).  Pass 2 (sid_parse_serial_kernel):
 // the general routine over that list -- or over every line, for -m quality.
-// LIST: over the lines a previous pass listed in (in, *inn) instead of all of
-// [lo, hi) (the cooperative parse's leftovers).
-template <bool LIST, class Off>
+template <class Off>
 __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ text, uint64_t len,
                                                        const Off* __restrict__ starts,
                                                        const uint64_t* __restrict__ range,   // [lo, hi)
                                                        uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
-                                                       uint32_t* __restrict__ fb, unsigned long long* fbn,
-                                                       const uint32_t* __restrict__ in, const unsigned long long* inn)
+                                                       uint32_t* __restrict__ fb, unsigned long long* fbn)
 {
     __shared__ uint8_t cls[256];
     __shared__ uint32_t rbl[256];
@@ -1138,14 +983,13 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
         rbl[threadIdx.x] = rb_entry(threadIdx.x);
     }
     __syncthreads();
-    const uint64_t lo = range[0], hi = LIST ? *inn : range[1];
+    const uint64_t lo = range[0], hi = range[1];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t k = (LIST ? 0 : lo) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t s_next = k < hi ? starts[LIST ? lo + in[k] : k] : 0;
-    for (; k < hi; k += stride) {
-        const uint64_t i = LIST ? lo + in[k] : k;
+    uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t s_next = i < hi ? starts[i] : 0;
+    for (; i < hi; i += stride) {
         const uint64_t s0 = s_next;
-        if (k + stride < hi) s_next = starts[LIST ? lo + in[k + stride] : k + stride];   // the next line's offset in flight
+        if (i + stride < hi) s_next = starts[i + stride];   // the next line's offset in flight
         uint64_t c = 0, h[2] = {0, 0};
         if (parse_line_fast(text, len, s0, cls, stage + threadIdx.x * HDR_BYTES, &c, h, rbl)) {
             counts[i] = c;
@@ -1160,8 +1004,7 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
 // lanes per line (parse_line_fast<true>): 16 lines a wave, each quad reading
 // 64 consecutive bytes of its line a step, instead of 64 lanes walking 64
 // lines 16 bytes at a time (whose in-flight lines are a cache working set
-// the 200x lines overflow, line_walk_grid).  SID_PARSE_QUAD=0: the per-lane
-// kernel on the reduced grid (A/B).
+// the 200x lines overflow, line_walk_grid).
 template <class Off>
 __global__ __launch_bounds__(TB) void sid_parse_quad_kernel(const char* __restrict__ text, uint64_t len,
                                                             const Off* __restrict__ starts,
@@ -1191,231 +1034,6 @@ __global__ __launch_bounds__(TB) void sid_parse_quad_kernel(const char* __restri
             } else {
                 fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
             }
-        }
-    }
-}
-
-// ------------------------------------------------------ cooperative parse --
-// The engine's parse (sid_chunk_parse): the same fast path as parse_line_fast,
-// laid out for the block instead of the lane.  A block takes 256 consecutive
-// lines:
-//   H  one lane per line, from the index's token-end mask (ix_low) alone:
-//      token starts 0-4 and the end of token 4 by bit tricks on 64-bit words
-//      (no byte of the header is classified); ref, position and the chrom's
-//      first 8 bytes by three 8-B reads; the line's 16-B windows of token 4
-//   C  the block's windows of token 4 dealt to its lanes in order (window w ->
-//      its line by a binary search of the window prefix in LDS): every lane
-//      counts one 16-B window at a time, so lines of any length keep every
-//      lane busy, and consecutive lanes read consecutive bytes; the counts
-//      meet in the line's LDS accumulator (one 64-bit atomic add a window)
-//   W  one lane per line: the '.'/',' counts to the ref's base, the counts and
-//      the header pair written (as parse_line_fast writes them)
-// A line with a token-end byte other than ' '/'\t' before its token 4 (or one
-// other than those and '\n' ending it), whose token 4 starts 64 or more bytes
-// into it, or that the fast path would leave (indel, '^' run, a ref whose
-// class is not a base) is listed for the per-line passes.
-constexpr int PC_LEN_MAX = 4096;   // token 4 bytes a line may have here (12-bit fields of the accumulator)
-
-// 8 text bytes at any offset: two aligned 8-B reads and a funnel shift
-__device__ __forceinline__ uint64_t text_u64(const char* __restrict__ text, uint64_t off)
-{
-    const uint64_t* p = (const uint64_t*)(text + (off & ~(uint64_t)7));
-    const uint32_t r = (uint32_t)(off & 7);
-    const uint64_t lo = p[0];
-    return r ? (lo >> (8 * r)) | (p[1] << (64 - 8 * r)) : lo;
-}
-// token-end bits of the 64 bytes from byte b (relative to the mask's base)
-__device__ __forceinline__ uint64_t low_bits(const uint64_t* __restrict__ low64, uint64_t b)
-{
-    const uint64_t w = b >> 6;
-    const uint32_t r = (uint32_t)(b & 63);
-    const uint64_t lo = low64[w];
-    return r ? (lo >> r) | (low64[w + 1] << (64 - r)) : lo;
-}
-
-// the 16-B window counts of token 4: valid = the window's bytes inside the
-// token, carry = bit 7 when its byte 0 follows a '^' (is skipped); returns A,
-// C, G, T and '.'/',' in 12-bit fields; *bad: an indel or a '^' run
-__device__ __forceinline__ unsigned long long window_counts(uint4 v, uint32_t valid, uint32_t& carry, bool& bad)
-{
-    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-    uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t x = ws[k];
-        const uint32_t vm = (__umul24((valid >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) << 7;
-        const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
-        const uint32_t skip = ((caret << 8) | carry) & vm;
-        bad = bad || (caret & skip) != 0;
-        carry = caret >> 24;
-        const uint32_t cm = vm & ~skip;
-        bad = bad || (eq_bytes(x | 0x06060606u, 0x2F2F2F2Fu) & cm) != 0;   // '+' '-' (')' '/')
-        const uint32_t f = x | 0x20202020u;
-        nA += __popc(eq_bytes(f, 0x61616161u) & cm);
-        nC += __popc(eq_bytes(f, 0x63636363u) & cm);
-        nG += __popc(eq_bytes(f, 0x67676767u) & cm);
-        nT += __popc(eq_bytes(f, 0x74747474u) & cm);
-        nM += __popc(eq_bytes(x | 0x02020202u, 0x2E2E2E2Eu) & cm);
-    }
-    return (unsigned long long)nA | ((unsigned long long)nC << 12) | ((unsigned long long)nG << 24) |
-           ((unsigned long long)nT << 36) | ((unsigned long long)nM << 48);
-}
-
-__global__ __launch_bounds__(TB) void sid_parse_coop_kernel(const char* __restrict__ text, uint64_t len,
-                                                            uint64_t tbase, const uint64_t* __restrict__ low64,
-                                                            const sid_off_t* __restrict__ starts,
-                                                            const uint64_t* __restrict__ range,
-                                                            uint64_t* __restrict__ counts,
-                                                            uint64_t* __restrict__ hdr, uint32_t* __restrict__ fb,
-                                                            unsigned long long* fbn)
-{
-    __shared__ uint8_t cls[256];
-    __shared__ uint32_t wpre[TB + 1];            // windows of the lines before each line
-    __shared__ uint64_t q4[TB];                  // first byte of each line's token 4
-    __shared__ uint32_t n4[TB];                  // its length
-    __shared__ unsigned long long acc[TB];       // A, C, G, T, '.'/',' in 12-bit fields
-    __shared__ uint32_t lbad[TB];
-    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
-    const uint64_t lo = range[0], hi = range[1];
-    const uint64_t i = lo + (uint64_t)blockIdx.x * TB + threadIdx.x;
-    const int tid = threadIdx.x;
-    __syncthreads();
-    // ---- H
-    bool ok = false;
-    uint32_t nw = 0, kd = 0;
-    uint64_t h0 = 0, h1 = 0, q = 0, e4 = 0;
-    if (i < hi) {
-        const uint64_t s0 = starts[i];
-        const uint64_t s1 = i + 1 < hi ? starts[i + 1] : len;   // the next line's start (bytes past it are not this line's)
-        const uint32_t span = (uint32_t)min(s1 - s0, (uint64_t)64);
-        uint64_t S = low_bits(low64, s0 - tbase);
-        if (span < 64) S |= ~0ull << span;
-        const uint64_t N = ~S;
-        uint64_t T = N & ~(N << 1);   // token starts
-        const int t0 = ctz64(T);
-        T &= T - 1;
-        const int t1 = ctz64(T);
-        T &= T - 1;
-        const int t2 = ctz64(T);
-        T &= T - 1;
-        T &= T - 1;
-        const int t4 = ctz64(T);
-        ok = t4 < 64 && ((S >> ((t2 + 1) & 63)) & 1);   // five tokens in the first 64 bytes, token 2 one byte
-        if (ok) {
-            // the token-end bytes before token 4 must be ' ' or '\t' (parsePileupLine
-            // splits on those two only; a NUL or other control byte: the per-line passes)
-            for (uint64_t m = S & ((1ull << t4) - 1); ok && m; m &= m - 1) {
-                const uint32_t b = (uint8_t)text[s0 + (uint64_t)ctz64(m)];
-                ok = b == ' ' || b == '\t';
-            }
-        }
-        if (ok) {
-            q = s0 + (uint64_t)t4;
-            // end of token 4: the first token-end byte after it (the line's '\n' at the latest)
-            uint64_t m = t4 < 63 ? S >> (t4 + 1) : 0;
-            if (m) {
-                e4 = q + 1 + (uint64_t)ctz64(m);
-            } else {
-                uint64_t b = s0 + 64;
-                for (;;) {
-                    if (b >= s1) {
-                        e4 = s1;
-                        break;
-                    }
-                    if (b - q >= (uint64_t)PC_LEN_MAX) {   // too long for here: the per-line passes take it
-                        e4 = b;
-                        break;
-                    }
-                    const uint64_t wm = low_bits(low64, b - tbase);
-                    if (wm) {
-                        e4 = min(s1, b + (uint64_t)ctz64(wm));
-                        break;
-                    }
-                    b += 64;
-                }
-            }
-            ok = e4 - q < (uint64_t)PC_LEN_MAX;
-            if (ok && e4 < len) {   // the byte that ends token 4: a separator or the line's end
-                const uint32_t b = (uint8_t)text[e4];
-                ok = b == ' ' || b == '\t' || b == '\n';
-            }
-        }
-        if (ok) {
-            const int l0 = ctz64(S >> t0);
-            const int lp = ctz64(S >> t1);
-            const uint32_t ref = (uint32_t)(uint8_t)text[s0 + t2];
-            const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
-            const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
-            kd = cls[up];
-            const uint32_t kc = cls[lw];
-            ok = kd < K_CARET && kc < K_CARET && kd == kc;
-            // the position as in parse_line_fast
-            const uint32_t L8 = min((uint32_t)lp, 8u);
-            const uint64_t p8 = text_u64(text, s0 + t1);
-            const uint32_t plo = (uint32_t)p8, phi = (uint32_t)(p8 >> 32);
-            const uint64_t nd = (uint64_t)not_digit(plo) | ((uint64_t)not_digit(phi) << 32);
-            const uint64_t inl = L8 >= 8 ? ~0ull : ((1ull << (8 * L8)) - 1);
-            const uint32_t d9 = (uint32_t)(uint8_t)text[s0 + t1 + 8] - '0';
-            const bool pos_ok = lp >= 1 && lp <= 9 && (nd & inl) == 0 && (lp < 9 || d9 < 10u);
-            const uint64_t dv = ((uint64_t)(phi - 0x30303030u) << 32) | (plo - 0x30303030u);
-            const uint64_t dz = L8 == 0 ? 0 : dv << ((8 * (8 - L8)) & 63);
-            const uint32_t z0 = (uint32_t)dz, z1 = (uint32_t)(dz >> 32);
-            const uint32_t hh = __umul24(__builtin_amdgcn_udot4(z0, 0x0000010Au, 0u, false), 100u) +
-                                __builtin_amdgcn_udot4(z0, 0x010A0000u, 0u, false);
-            const uint32_t ll = __umul24(__builtin_amdgcn_udot4(z1, 0x0000010Au, 0u, false), 100u) +
-                                __builtin_amdgcn_udot4(z1, 0x010A0000u, 0u, false);
-            uint32_t pos = __umul24(hh, 10000u) + ll;
-            if (lp == 9) pos = pos * 10u + d9;
-            h0 = pos_ok ? (1ull << 63) | ((uint64_t)t0 << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
-            h1 = text_u64(text, s0 + t0) & (l0 >= 8 ? ~0ull : ((1ull << (8 * l0)) - 1));
-            nw = ok ? (uint32_t)(((e4 - 1) >> 4) - (q >> 4) + 1) : 0u;
-        }
-    }
-    uint32_t tot;
-    const uint32_t pre = block_exscan(nw, &tot);
-    wpre[tid] = pre;
-    if (tid == TB - 1) wpre[TB] = tot;
-    q4[tid] = q;
-    n4[tid] = (uint32_t)(e4 - q);
-    acc[tid] = 0;
-    lbad[tid] = 0;
-    __syncthreads();
-    // ---- C: window w on lane w mod 256 (a wave's loads cover 1 KiB of
-    // consecutive windows; 64-B runs per lane measured 40% slower)
-    for (uint32_t w = tid; w < tot; w += TB) {
-        uint32_t L = 0;
-#pragma unroll
-        for (uint32_t st = TB / 2; st > 0; st >>= 1)
-            if (wpre[L + st] <= w) L += st;
-        const uint64_t qa = q4[L], qe = qa + n4[L];
-        const uint32_t j = w - wpre[L];
-        const uint64_t a = (qa & ~(uint64_t)15) + 16ull * j;
-        const uint4 v = *(const uint4*)(text + a);
-        const uint32_t lead = j == 0 ? (uint32_t)(qa & 15) : 0u;
-        const uint32_t room = (uint32_t)min(qe - a, (uint64_t)16);
-        const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
-        // bit 7: byte 0 is skipped (a '^' ends the window before; a '^' run fails the line wherever it lies)
-        uint32_t carry = (j > 0 && text[a - 1] == '^') ? 0x80u : 0u;
-        bool bad = false;
-        atomicAdd(&acc[L], window_counts(v, valid, carry, bad));
-        if (bad) lbad[L] = 1;
-    }
-    __syncthreads();
-    // ---- W
-    if (i < hi) {
-        if (ok && !lbad[tid]) {
-            const unsigned long long a = acc[tid];
-            uint32_t nA = (uint32_t)a & 0xFFFu, nC = (uint32_t)(a >> 12) & 0xFFFu;
-            uint32_t nG = (uint32_t)(a >> 24) & 0xFFFu, nT = (uint32_t)(a >> 36) & 0xFFFu;
-            const uint32_t nM = (uint32_t)(a >> 48) & 0xFFFu;
-            nA += kd == K_A ? nM : 0;
-            nC += kd == K_C ? nM : 0;
-            nG += kd == K_G ? nM : 0;
-            nT += kd == K_T ? nM : 0;
-            counts[i] = (uint64_t)nA | ((uint64_t)nC << 16) | ((uint64_t)nG << 32) | ((uint64_t)nT << 48);
-            *(ulonglong2*)(hdr + 2 * i) = make_ulonglong2(h0, h1);
-        } else {
-            fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
         }
     }
 }
@@ -1470,36 +1088,25 @@ static unsigned line_walk_grid(uint64_t n, uint64_t len, unsigned cap)
     return (unsigned)std::min<uint64_t>(cap, (uint64_t)std::max(1L, bpc) * (uint64_t)ncu);
 }
 
-// lines over 256 B on average are parsed by a quad of lanes each
-// (sid_parse_quad_kernel); SID_PARSE_QUAD=0: one lane per line on the
-// reduced grid (A/B)
-static bool parse_quad()
-{
-    static const bool on = !std::getenv("SID_PARSE_QUAD") || std::atoi(std::getenv("SID_PARSE_QUAD")) != 0;
-    return on;
-}
-
 // the two passes over sites [range[0], range[1]) (the range lives on the device)
 template <class Off>
 static void launch_parse(const char* text, uint64_t len, const Off* starts, const uint64_t* range, uint64_t n,
                          uint64_t* counts, uint64_t* hdr, uint32_t* fb, unsigned long long* fbn,
                          unsigned long long* err, int qmode, hipStream_t st)
 {
-    static const char* env = std::getenv("SID_PARSE_GRID");
-    static const uint64_t PG = env ? (uint64_t)std::max(1, std::atoi(env)) : 16384;   // blocks of the grid-stride parse
+    constexpr uint64_t PG = 16384;   // blocks of the grid-stride parse
     const unsigned pg = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + TB - 1) / TB, 1), PG);
     if (qmode) {   // (the byte-wise walks of -m quality measured slower on the smaller grid: 925 vs 626 us at 200x)
         sid_parse_serial_kernel<<<pg, TB, 0, st>>>(text, len, starts, range, counts, hdr, nullptr, nullptr, err, 1);
         return;
     }
     (void)hipMemsetAsync(fbn, 0, sizeof *fbn, st);
-    if (parse_quad() && n && len > 256 * n) {   // long lines: a quad of lanes per line, the full grid
+    if (n && len > 256 * n) {   // long lines (over 256 B on average): a quad of lanes per line, the full grid
         const unsigned pq = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + TB / 4 - 1) / (TB / 4), 1), PG);
         sid_parse_quad_kernel<Off><<<pq, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn);
     } else {
-        const unsigned pgf = env ? pg : line_walk_grid(n, len, pg);
-        sid_parse_kernel<false, Off><<<pgf, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, nullptr,
-                                                         nullptr);
+        sid_parse_kernel<Off><<<line_walk_grid(n, len, pg), TB, 0, st>>>(text, len, starts, range, counts, hdr, fb,
+                                                                         fbn);
     }
     sid_parse_serial_kernel<<<256, TB, 0, st>>>(text, len, starts, range, counts, hdr, fb, fbn, err, 0);
 }
@@ -1706,9 +1313,7 @@ __global__ __launch_bounds__(TB) void sid_fmt_write_kernel(const char* __restric
 constexpr int FTB = 512;                  // threads (= sites) per formatter block
 constexpr int FMT_LDS2 = 32 * 1024;       // its record buffer: 4 blocks (32 waves) per CU
 constexpr int LPB = 8;                    // formatter blocks per workgroup of the -m local length kernel
-#ifndef SID_PUT_WAVES
-#define SID_PUT_WAVES 8                   // the -m local writer's min waves per SIMD (its LDS allows 8)
-#endif
+constexpr int SID_PUT_WAVES = 8;          // the -m local writer's min waves per SIMD (its LDS allows 8)
 
 // sum of one u32 per thread over an NT-thread block (every thread gets it)
 template <int NT>
@@ -1880,9 +1485,6 @@ struct LocalLen {
 // site, whose record comes from its code and confidences.  The writer then
 // reads 4 B a site instead of the 8 B counts, and skips getMajorAlleleIndices.
 constexpr uint32_t SID_CLS_MISS = 0xFFFFFFFFu;
-#ifndef SID_CLS_NT
-#define SID_CLS_NT 0   // 1: the class words stored non-temporal, as the counts were (A/B)
-#endif
 static_assert(SID_TAB_N + SID_TAB2_N <= (1u << 20), "class entries fit the word's 20 bits");
 __device__ __forceinline__ uint32_t local_word(uint32_t k, uint32_t f, uint32_t s)
 {
@@ -1899,11 +1501,7 @@ __device__ __forceinline__ int local_site_len(const Head& h, uint64_t c, uint64_
     const uint32_t k = local_entry(nf, ns, cov - nf - ns);
     const uint32_t L = k < SID_TAB_N ? L1[k] : k != UINT32_MAX ? LL.len2[k - SID_TAB_N] : 0xFFu;
     const bool miss = L == 0xFFu;
-#if SID_CLS_NT
-    ST_MID(LL.cls + i, miss ? SID_CLS_MISS : local_word(k, f, s));
-#else
     LL.cls[i] = miss ? SID_CLS_MISS : local_word(k, f, s);   // (read back by the writer soon: through the caches)
-#endif
     if (miss) {
         LL.miss[atomicAdd(LL.nmiss, 1ull)] = (uint32_t)i;   // its bytes: the fix-up's
         return 0;
@@ -1926,10 +1524,8 @@ __device__ __noinline__ int local_site_len_text(const char* text, uint64_t len, 
 // block's byte count.  Lines the fast path leaves get theirs after the
 // general routine (sid_local_len_list_kernel).  The tail-length table is read
 // through the caches (an LDS copy would cost the parse a block per CU).
-#ifndef SID_PARSE_LEN_WAVES
-#define SID_PARSE_LEN_WAVES 8
-#endif
-__global__ __launch_bounds__(TB, SID_PARSE_LEN_WAVES) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
+// (7 waves a SIMD, 71 VGPRs instead of 64, measured slower: DESIGN.md §9)
+__global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
                                                            const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ range,
                                                            uint64_t* __restrict__ counts,
@@ -3001,9 +2597,8 @@ extern "C" int sid_dtext_format(sid_ctx* ctx, const sid_dtext* T, size_t begin, 
     // and the allocation holds up the device work: 1 Mi-site pieces cost
     // 33-41 ms before the first write at 50M sites, 256 Ki-site pieces 14-16
     // ms with the same D2H rate; 64 Ki-site pieces D2H slower
-    // (round-1 measurement; SID_FMT_PIECE_BLOCKS overrides)
-    size_t PB = 1024;
-    if (const char* e = std::getenv("SID_FMT_PIECE_BLOCKS")) PB = std::max(1, std::atoi(e));
+    // (round-1 measurement)
+    constexpr size_t PB = 1024;
     const size_t nb = (n + TB - 1) / TB;
     uint32_t* d_bsum = nullptr;
     uint64_t* d_boff = nullptr;
@@ -3256,16 +2851,6 @@ static uint64_t chunk_tiles(uint64_t c0, uint64_t c1)
     return std::max<uint64_t>((c1 - t0 + TILE - 1) / TILE, 1);
 }
 
-// the cooperative parse (sid_parse_coop_kernel) instead of the per-line one:
-// SID_PARSE_COOP=1.  Off by default: the token-end mask it needs costs the
-// index more than the parse saves (C2 index 0.92 -> 1.55 ms,
-// parse 1.84 -> 1.95 ms per step; the C5 200x shard's parse 10.6 -> 9.1 ms)
-static bool parse_coop()
-{
-    static const bool on = std::getenv("SID_PARSE_COOP") && std::atoi(std::getenv("SID_PARSE_COOP")) != 0;
-    return on;
-}
-
 int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
 {
     // grow-only; hipFree waits for the device, so buffers still in use by
@@ -3278,18 +2863,13 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         if (W->tcnt) (void)hipFree(W->tcnt);
         if (W->toff) (void)hipFree(W->toff);
         if (W->masks) (void)hipFree(W->masks);
-        if (W->lowm) (void)hipFree(W->lowm);
         W->tcnt = nullptr;
         W->toff = nullptr;
         W->masks = nullptr;
-        W->lowm = nullptr;
         W->tile_cap = 0;
         WCHECK(hipMalloc(&W->tcnt, ((t * 4 + 7) & ~(size_t)7) + scan_ws_bytes(t)));
         WCHECK(hipMalloc(&W->toff, t * 8));
         WCHECK(hipMalloc(&W->masks, t * TB * sizeof(uint16_t)));   // a u16 per lane per 4 KiB tile
-        if (parse_coop()) {
-            WCHECK(hipMalloc(&W->lowm, t * TB * sizeof(uint16_t) + 64));   // (+ the word a 64-bit read may touch past the end)
-        }
         W->tile_cap = t;
     }
     if (sites > W->site_cap) {
@@ -3328,19 +2908,14 @@ void sid_chunk_release(sid_chunk_ws* W)
 {
     for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
                     (void*)W->bsum, (void*)W->boff, (void*)W->tcnt, (void*)W->toff, (void*)W->state,
-                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb, (void*)W->lowm, (void*)W->cls})
+                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb, (void*)W->cls})
         if (p) (void)hipFree(p);
     *W = sid_chunk_ws{};
 }
 
-// blocks of the strided index kernels (SID_IX_GRID; count kernel, index stage
-// per 50M sites: 512 blocks 1.89, 1024 1.25, 2048 0.99, 4096 0.97 ms)
-static unsigned ix_grid()
-{
-    static const unsigned g = std::getenv("SID_IX_GRID") ? (unsigned)std::max(1, std::atoi(std::getenv("SID_IX_GRID")))
-                                                         : 4096u;
-    return g;
-}
+// blocks of the strided index kernels (count kernel, index stage per 50M
+// sites: 512 blocks 1.89, 1024 1.25, 2048 0.99, 4096 0.97 ms)
+constexpr unsigned IX_GRID = 4096;
 
 // line starts of [c0, c1): masks and per-tile counts, scan; state[0] = sites
 // (the caller reads it back), state[1..2] = [0, sites), state[4] = no error yet
@@ -3349,27 +2924,19 @@ int sid_chunk_index(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     const uint64_t t0 = c0 & ~(uint64_t)15;
     const uint64_t ntiles = c1 > c0 ? (c1 - t0 + IX_TILE - 1) / IX_TILE : 0;
     if (ntiles * IX_SUB > W->tile_cap) return SID_EINVAL;
-    if (c1 > UINT32_MAX) return SID_ERANGE;   // line offsets are 32-bit (sid_off_t)
+    if (c1 > UINT32_MAX) return SID_ELINE;   // line offsets are 32-bit (sid_off_t): a line ran the chunk past 4 GiB
     if (ntiles == 0) {
         WCHECK(hipMemsetAsync(W->state, 0, 4 * sizeof(uint64_t), st));
         WCHECK(hipMemsetAsync(W->state + 4, 0xFF, sizeof(uint64_t), st));
         return SID_OK;
     }
-    const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, ix_grid());
-    const bool coop = parse_coop();
-    if (coop)
-        sid_index_count_kernel<true><<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state,
-                                                          W->lowm);
-    else
-        sid_index_count_kernel<false><<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state,
-                                                           nullptr);
+    const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, IX_GRID);
+    sid_index_count_kernel<<<grid, TB, 0, st>>>(base, t0, c0, c1, ntiles, W->masks, W->tcnt, W->state);
     launch_scan(W->tcnt, ntiles, W->toff, W->state, W->state + 1,
                 (uint64_t*)((char*)W->tcnt + ((ntiles * 4 + 7) & ~(size_t)7)), st);
     WCHECK(hipGetLastError());
     return SID_OK;
 }
-
-constexpr unsigned PC_LIST_GRID = 1024;   // blocks of the per-line pass over the cooperative parse's leftovers
 
 // line offsets from the index's masks + the two-pass parse of the n sites;
 // state[4] = min(offset * 8 + kind) over the malformed lines (all ones: none)
@@ -3382,19 +2949,16 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
     if (n == 0) return SID_OK;
     const uint64_t t0 = c0 & ~(uint64_t)15;
     const uint64_t ntiles = (c1 - t0 + IX_TILE - 1) / IX_TILE;
-    // (not for long lines: at 200x the parse runs on a small grid (line_walk_grid),
-    // where the fused kernel's register cap costs more than the length kernel:
-    // C5 parse + lengths 145 vs 141 ms)
     // (not for long lines: at 200x the fused kernel's extra registers and work
     // cost the parse more than the length kernel costs (C5: the per-lane parse
     // on the reduced grid, parse + lengths 145 vs 141 ms; the quad parse with
     // the lengths fused, 71.4 + 1.8 vs 65.9 + 5.4 ms per step)
-    const bool lens = lctx && !qmode && !parse_coop() && n < (1ull << 32) && (c1 - c0) <= 256 * n;
+    const bool lens = lctx && !qmode && n < (1ull << 32) && (c1 - c0) <= 256 * n;
     const uint64_t nb = (n + FTB - 1) / FTB;
     unsigned long long* fbn = (unsigned long long*)(W->state + 6);
     // (with lens the emit kernel also zeroes the formatter's block sums and
     // flags and the fallback counts: three memset launches fewer)
-    sid_index_emit_kernel<<<(unsigned)std::min<uint64_t>(ntiles, ix_grid()), TB, 0, st>>>(
+    sid_index_emit_kernel<<<(unsigned)std::min<uint64_t>(ntiles, IX_GRID), TB, 0, st>>>(
         W->masks, t0, ntiles, W->toff, W->starts, lens ? W->bsum : nullptr, lens ? nb : 0, lens ? W->lb : nullptr,
         lens ? fbn : nullptr);
     if (lens) {
@@ -3411,20 +2975,9 @@ int sid_chunk_parse(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
         sid_local_len_list_kernel<<<64, TB, 0, st>>>(base, c1, W->starts, W->hdr, W->counts, late, fbn + 1, LL);
         W->lens_ready = true;
         W->cls_ready = true;
-    } else if (qmode || !parse_coop()) {
+    } else {
         launch_parse(base, c1, W->starts, W->state + 1, n, W->counts, W->hdr, W->fb,
                      (unsigned long long*)(W->state + 6), (unsigned long long*)(W->state + 4), qmode, st);
-    } else {
-        // the cooperative parse; its leftovers to the per-line fast path, that one's to the general routine
-        unsigned long long* fbn = (unsigned long long*)(W->state + 6);
-        uint32_t* fb2 = W->fb + W->site_cap;
-        WCHECK(hipMemsetAsync(fbn, 0, 2 * sizeof *fbn, st));
-        sid_parse_coop_kernel<<<(unsigned)((n + TB - 1) / TB), TB, 0, st>>>(
-            base, c1, t0, (const uint64_t*)W->lowm, W->starts, W->state + 1, W->counts, W->hdr, W->fb, fbn);
-        sid_parse_kernel<true, sid_off_t><<<PC_LIST_GRID, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr,
-                                                            fb2, fbn + 1, W->fb, fbn);
-        sid_parse_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->starts, W->state + 1, W->counts, W->hdr, fb2,
-                                                    fbn + 1, (unsigned long long*)(W->state + 4), 0);
     }
     WCHECK(hipGetLastError());
     return SID_OK;
@@ -3485,7 +3038,7 @@ int sid_chunk_fmt_put(sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n
 
 bool sid_chunk_local_ok(const sid_ctx* ctx)
 {
-    return ctx->opts.method == SID_METHOD_LOCAL && !ctx->K.general && !ctx->ws.direct && ctx->ws.str1;
+    return ctx->opts.method == SID_METHOD_LOCAL && !ctx->K.general && ctx->ws.str1;
 }
 
 // the string tables hold -m local's record tails, conf_type "p_value" included

@@ -120,3 +120,24 @@ def test_shared_gpu_rehearsal_runs_the_node_cli():
     assert cli["devices"] == 2 and cli["sites"] == 600_000
     assert cli["cli_stats"]["sites"] == 600_000
     assert cli["sites_per_s_wall"] > 0
+    # the whole node's CPU path beside it: the oracle over the same file, one
+    # shard process per CPU the job may use
+    import bench
+    cpu = d["cpu_baseline"]
+    assert cpu["cores"] == bench.cpu_share(os.sched_getaffinity(0))[0]
+    assert cpu["value"] > 0 and cpu["kind"] == "port"
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_strong_config_value_leg():
+    """C5 (bench.py bench_strong) at a small total: the rank's eighth as
+    pinned host text through the value leg's engine, device_path beside it."""
+    r = run_bench(["--config", "C5", "--sites", "1600000", "--steps", "2", "--warmup", "1", "--device-steps", "2",
+                   "--no-extras"], 500)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    d = json.loads([ln for ln in r.stdout.decode().splitlines() if ln.startswith('{"metric"')][0])
+    assert d["config"]["sites_per_gpu"] == 200_000 and d["config"]["sites_all_ranks"] == 200_000
+    assert d["scaling"] == "weak" and d["value"] > 0
+    assert d["pcie"]["text_bytes"] == d["config"]["text_bytes_rank0"] and d["pcie"]["csv_bytes"] > 0
+    assert d["device_path"]["sites_per_s"] > 0 and d["roofline"]["achieved"] > 0

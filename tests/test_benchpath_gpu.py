@@ -224,3 +224,43 @@ def test_c4_device_path_equals_oracle(sid, bench_mod, c4, hold):
     else:
         assert st.chunks_held == st.chunks
     assert_same(out, ref, f"C4 device path (2 GiB chunks, hold {hold})")
+
+
+# ---- C4 / C5 value leg (bench.py bench_strong -> pcie_leg): the shard's text
+# in pinned host memory, the engine pcie_engine builds (128 MiB host chunks,
+# records copied into the pinned host arena during the ingest), the records
+# read back from the arena.
+
+def pcie_records(bench_mod, sid, cfg, text, ln, n):
+    host = text[:ln].cpu().pin_memory()
+    eng = bench_mod.pcie_engine(cfg, 0, n, ln)
+    eng.source_host_ptr(host.data_ptr(), ln, keep=host)
+    st = eng.ingest()
+    eng.estimate()
+    _, st2 = eng.emit()
+    got = eng.records_bytes(st.chunks)
+    eng.close()
+    assert st.sites == n and st.chunks_held == st.chunks
+    assert st2.bytes_out == len(got)
+    return st, sid.HEADER + got
+
+
+@pytest.mark.timeout(900)
+def test_c5_pcie_path_equals_oracle(sid, bench_mod, c5):
+    """15M sites of 200x text (6.3 GB, ~50 host chunks of 128 MiB: the quad
+    parse over long lines cut by the host chunking) through the value leg's
+    engine, byte for byte against the 16-shard oracle CLI."""
+    cfg, text, ln, n, ref = c5
+    st, got = pcie_records(bench_mod, sid, cfg, text, ln, n)
+    assert st.chunks >= 10
+    assert_same(got, ref, "C5 PCIe path (pinned host text, 128 MiB chunks, host arena)")
+
+
+@pytest.mark.timeout(900)
+def test_c4_pcie_path_equals_oracle(sid, bench_mod, c4):
+    """The C4 slice across chr1/chr2 (60M sites, 4.9 GB) through the value
+    leg's engine."""
+    cfg, text, ln, n, ref = c4
+    st, got = pcie_records(bench_mod, sid, cfg, text, ln, n)
+    assert st.chunks >= 10
+    assert_same(got, ref, "C4 PCIe path (pinned host text, 128 MiB chunks, host arena)")

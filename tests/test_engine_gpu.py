@@ -486,3 +486,75 @@ def test_device_sink_formats_past_the_hold_budget_once(sid, source):
     prof = eng.profile_read()
     assert prof["chunks"] == 2 * st.chunks   # one index + parse per chunk and run
     eng.close()
+
+
+@pytest.fixture(scope="module")
+def pageable_30mb(sid, oracle, tmp_path_factory):
+    """~30 MB of 30x text as a file, and the oracle's CSV of it."""
+    d = tmp_path_factory.mktemp("reg")
+    text = sid.synth_text(51, 370_000, 30.0, sites_per_chrom=150_000)
+    p = d / "reg.plp"
+    p.write_bytes(text)
+    ref = oracle.run_cli([str(p)])
+    assert ref.returncode == 0
+    return text, str(p), ref.stdout
+
+
+@pytest.mark.parametrize("register", ["1", "0"])
+@pytest.mark.parametrize("devices", ["1", "2"])
+@pytest.mark.parametrize("chunk", [3 << 20, (8 << 20) - 12345])
+def test_registered_uploads_cli(sid, pageable_30mb, register, devices, chunk):
+    """The CLI over a regular file uploads each chunk from its page-aligned
+    body registered for DMA, its partial first and last pages through the
+    runtime's pageable path (run.cpp UploadReg), chunks dealt over the
+    devices; SID_UPLOAD_REGISTER=0 is the pageable path for everything.  Both
+    write the oracle's CSV, and --stats says which path ran."""
+    text, path, ref = pageable_30mb
+    a = run(sid.CLI_PATH, ["--stats", "--chunk-bytes", str(chunk), "--devices", devices, path],
+            env=dict(os.environ, SID_UPLOAD_REGISTER=register))
+    assert a.returncode == 0, a.stderr[-400:]
+    assert a.stdout == ref
+    st = json.loads(a.stderr.splitlines()[-1])
+    assert st["chunks"] >= 4
+    if register == "1":
+        # every chunk whose page-aligned body is at least 1 MiB (all but
+        # perhaps a short last one)
+        assert st["chunks_registered"] >= st["chunks"] - 1
+        assert st["register_s"] > 0
+    else:
+        assert st["chunks_registered"] == 0
+    assert st["h2d_bytes"] == len(text) and st["h2d_s"] > 0
+
+
+def test_registered_uploads_engine_bytes(sid, pageable_30mb):
+    """The same through the engine from host bytes the caller did not pin
+    (not page-aligned: chunk 0 has a pageable head too)."""
+    text, _, ref = pageable_30mb
+    for devices in (1, 2):
+        eng = sid.Engine(chunk_bytes=(5 << 20) + 7, devices=devices)
+        eng.source_text(text)
+        out, st = eng.run()
+        eng.close()
+        assert out == ref
+        assert st.chunks >= 5 and st.chunks_registered >= st.chunks - 1
+        assert st.h2d_bytes == len(text)
+
+
+def test_line_past_the_chunk_limit_is_refused(sid):
+    """Line offsets on the device are 32-bit: a line that carries a chunk past
+    4 GiB is refused with SID_ELINE (its own message), not mis-parsed."""
+    import torch
+    n = (4 << 30) + (2 << 20)
+    buf = torch.full((n + 512,), ord("A"), dtype=torch.uint8, device="cuda")
+    buf[n - 1] = ord("\n")
+    buf[n:] = 0
+    torch.cuda.synchronize()
+    eng = sid.Engine(chunk_bytes=64 << 20)
+    eng.source_device_text(buf.data_ptr(), n, keep=buf)
+    with pytest.raises(sid.SidError) as ei:
+        eng.ingest()
+    assert ei.value.status == 13
+    assert b"too long" in sid.lib().sid_strerror(13)
+    eng.close()
+    del buf
+    torch.cuda.empty_cache()

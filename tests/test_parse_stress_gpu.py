@@ -1,11 +1,9 @@
 """The engine's parse passes against the oracle CLI (the reference's
-pileup.cpp / call.cpp / sid.cpp restated), byte for byte: the per-line parse
-(the default) and the cooperative one (SID_PARSE_COOP=1, textpath.hip
-sid_parse_coop_kernel: token structure from the index's token-end mask,
-read-bases windows dealt to a block's lanes) with the per-line passes it
-hands lines to.
+pileup.cpp / call.cpp / sid.cpp restated), byte for byte: the fast paths (the
+tile parse, the per-line and quad parses) and the general routine they hand
+lines to.
 
-The texts aim at the cooperative kernel's cases (pileup.cpp:13-153):
+The texts aim at the fast paths' edge cases (pileup.cpp:13-153):
 '^' + mapping quality at every offset of a 16-B window ('^' at a window's last
 byte skips the next window's first), '^' runs, '$', indels, CRLF line ends and
 NUL or other control bytes after token 4 (their tile goes to the per-line
@@ -24,9 +22,8 @@ from test_parser import blank, fuzz_lines
 pytestmark = pytest.mark.gpu
 
 
-def cli(sid, args, coop):
-    env = dict(os.environ, SID_PARSE_COOP=str(coop))
-    return subprocess.run([sid.CLI_PATH] + list(args), capture_output=True, timeout=600, env=env)
+def cli(sid, args):
+    return subprocess.run([sid.CLI_PATH] + list(args), capture_output=True, timeout=600)
 
 
 def first_diff(a, b):
@@ -40,21 +37,19 @@ def first_diff(a, b):
 
 
 def same_as_oracle(sid, oracle, path, flags, extra):
-    """The CLI with the per-line parse (the default) and with the cooperative
-    parse (SID_PARSE_COOP=1) against the oracle CLI."""
+    """The CLI against the oracle CLI: stdout, stderr and exit code."""
     b = oracle.run_cli(flags + [str(path)])
-    for coop in (0, 1):
-        a = cli(sid, extra + flags + [str(path)], coop)
-        assert a.returncode == b.returncode, (coop, a.stderr[-300:], b.stderr[-300:])
-        same_out = a.stdout == b.stdout
-        assert same_out, (coop, extra, flags, first_diff(a.stdout, b.stdout))
-        same_err = a.stderr == b.stderr
-        assert same_err, (coop, a.stderr[-400:], b.stderr[-400:])
+    a = cli(sid, extra + flags + [str(path)])
+    assert a.returncode == b.returncode, (a.stderr[-300:], b.stderr[-300:])
+    same_out = a.stdout == b.stdout
+    assert same_out, (extra, flags, first_diff(a.stdout, b.stdout))
+    same_err = a.stderr == b.stderr
+    assert same_err, (a.stderr[-400:], b.stderr[-400:])
     return b
 
 
 def mutate(rng, line):
-    """One synthetic 30x line with one of the cooperative parse's cases."""
+    """One synthetic 30x line with one of the fast paths' edge cases."""
     chrom, pos, ref, depth, bases, qual = line.split(b"\t")[:6]
     r = int(rng.integers(0, 14))
     if r == 0:      # '^' + a mapping-quality byte at random places, sometimes '^^' (a '^' run)

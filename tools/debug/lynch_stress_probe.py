@@ -11,7 +11,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
 import sid_amd as sid  # noqa: E402
 import sid_amd.gpu as G  # noqa: E402
 import oracle as O  # noqa: E402
-from test_parse_coop_gpu import stress_text  # noqa: E402
+from test_parse_stress_gpu import stress_text  # noqa: E402
 
 text = stress_text(sid, 41, 20000, 30.0)
 counts = sid.parse_text(text).counts.copy()

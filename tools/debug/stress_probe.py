@@ -1,4 +1,4 @@
-"""Run the cooperative-parse stress texts (tests/test_parse_coop_gpu.py)
+"""Run the cooperative-parse stress texts (tests/test_parse_stress_gpu.py)
 through the CLIs of two builds and the oracle CLI, each call under a time
 limit, printing one line per call (which case is slow or differs)."""
 import os
@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
 import sid_amd as sid  # noqa: E402
 import oracle as O  # noqa: E402
-from test_parse_coop_gpu import stress_text  # noqa: E402
+from test_parse_stress_gpu import stress_text  # noqa: E402
 
 out = os.path.join(ROOT, "gpurun_out")
 os.makedirs(out, exist_ok=True)
