@@ -201,29 +201,24 @@ def parse_quad(text_per_site):
     return text_per_site > 256
 
 
-def parse_len(fused, text_per_site=81.0):
-    """-m local: the records' lengths computed by the parse (run.cpp,
-    sid_parse_len_kernel), for lines of up to 256 bytes (textpath.hip
-    sid_chunk_parse)."""
+def tile_parse(fused, text_per_site=81.0):
+    """-m local over lines of up to 256 B on average: the engine's tile parse
+    (run.cpp, textpath.hip sid_chunk_tile_local) -- the line index fused into
+    the parse (the text read once), the record lengths, the fix-up and the
+    writer's offsets in the parse stage; no index stage."""
     return fused == "local" and text_per_site <= 256
 
 
 def stage_bytes(stage, text_per_site, csv_per_site, fused):
     """Algorithmic HBM bytes per site of each engine stage.
     fused: a fmt_kind, the call / lookup fused into the formatter (it reads
-    the 8 B counts instead of the call kernel's 17 B code + confs); with
-    parse_len the length stage has only the fix-up and the block-sum scan
-    left (4 B per 512 sites, read and written)."""
+    the 8 B counts instead of the call kernel's 17 B code + confs)."""
     site_in = 8 if fused else 17
-    pl = parse_len(fused, text_per_site)
-    if stage == "fmt_len" and pl:
-        return 2 * 4 / 512 + 8 / 512
-    if pl and stage in ("parse", "fmt_write"):
-        # the fused parse writes each site's 4 B class word instead of its 8 B
-        # counts (textpath.hip local_word), which the writer reads instead;
-        # line offsets 4 B (sid_off_t), written by the emit, read by the parse
-        return {"parse": text_per_site + text_per_site / 8 + 4 + 4 + 4 + 16,
-                "fmt_write": 4 + 16 + csv_per_site}[stage]
+    if tile_parse(fused, text_per_site) and stage in ("parse", "fmt_write"):
+        # the tile parse reads the text once and writes each site's 4 B class
+        # word and 16 B header pair (textpath.hip sid_tile_parse_kernel); the
+        # writer reads those and writes the records
+        return {"parse": text_per_site + 4 + 16, "fmt_write": 4 + 16 + csv_per_site}[stage]
     return {
         "index": text_per_site + text_per_site / 8,    # text read once, line-start masks written
         # text read; line-start masks (1/8 of the text) read back, 4 B line
@@ -242,17 +237,16 @@ def stage_bytes(stage, text_per_site, csv_per_site, fused):
 
 
 def stage_kernels(stage, fused, text_per_site=81.0):
-    pl = parse_len(fused, text_per_site)
+    tp = tile_parse(fused, text_per_site)
     return {
         "index": ["sid_index_count_kernel", "sid_scan_*"],
-        "parse": ["sid_index_emit_kernel"] + (
-            ["sid_parse_len_kernel", "sid_parse_serial_kernel", "sid_local_len_list_kernel"] if pl
-            else [("sid_parse_quad_kernel" if parse_quad(text_per_site) else "sid_parse_kernel"),
-                  "sid_parse_serial_kernel"]),
+        "parse": (["sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_tile_len_list_kernel",
+                   "sid_local_fixlen_kernel", "sid_scan_*"] if tp else
+                  ["sid_index_emit_kernel", ("sid_parse_quad_kernel" if parse_quad(text_per_site) else
+                                             "sid_parse_kernel"), "sid_parse_serial_kernel"]),
         "call": ["sid_lookup_rec_kernel"],
         "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel"],
-        "fmt_len": {"local": (["sid_local_fixlen_kernel"] if pl else
-                              ["sid_local_len_kernel", "sid_local_fixlen_kernel"]),
+        "fmt_len": {"local": ["sid_local_len_kernel", "sid_local_fixlen_kernel"],
                     "lynch": ["sid_lynch_len_kernel"]}.get(fused, ["sid_fmt_blen_kernel"]) + ["sid_scan_*"],
         "fmt_write": {"local": ["sid_local_put_kernel"], "lynch": ["sid_lynch_put_kernel"]}.get(
             fused, ["sid_fmt_put_kernel"]),
@@ -913,43 +907,52 @@ def bench_cli_node(R, cfg, holder, ln, n):
     res, cpu = None, None
     if R.rank == 0:
         try:
-            env = dict(os.environ)
-            runs = []
             # the CLI runs unbound (it places its own threads per GPU): this
             # thread's mask widened for the fork, which the child inherits, and
             # restored after (no preexec_fn: this process runs other threads)
             mask = os.sched_getaffinity(0)
-            for _ in range(4):
-                with open(os.devnull, "wb") as dn:
-                    os.sched_setaffinity(0, R.cpus0)
+            args = [cli, "--stats", "--devices", str(R.world)] + method_flags(cfg) + [path]
+
+            def median_of(env):
+                runs = []
+                for _ in range(4):
+                    with open(os.devnull, "wb") as dn:
+                        os.sched_setaffinity(0, R.cpus0)
+                        try:
+                            t0 = time.perf_counter()
+                            r = subprocess.run(args, stdout=dn, stderr=subprocess.PIPE, env=env)
+                            dt = time.perf_counter() - t0
+                        finally:
+                            os.sched_setaffinity(0, mask)
+                    if r.returncode != 0:
+                        return {"error": r.returncode, "stderr": r.stderr.decode()[-400:]}, None
                     try:
-                        t0 = time.perf_counter()
-                        r = subprocess.run([cli, "--stats", "--devices", str(R.world)] +
-                                           ([] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) +
-                                            ["-m", cfg["method"]]) + [path],
-                                           stdout=dn, stderr=subprocess.PIPE, env=env)
-                        dt = time.perf_counter() - t0
-                    finally:
-                        os.sched_setaffinity(0, mask)
-                if r.returncode != 0:
-                    res = {"error": r.returncode, "stderr": r.stderr.decode()[-400:]}
-                    break
-                try:
-                    stt = json.loads(r.stderr.decode().strip().splitlines()[-1])
-                except Exception:
-                    stt = {}
-                runs.append((dt, stt))
-            if res is None:
+                        stt = json.loads(r.stderr.decode().strip().splitlines()[-1])
+                    except Exception:
+                        stt = {}
+                    runs.append((dt, stt))
                 dt, stt = sorted(runs[1:], key=lambda x: x[0])[len(runs[1:]) // 2]
+                return {"wall_s": dt, "wall_s_runs": [x[0] for x in runs], "cli_stats": stt}, dt
+            # the uploads from registered pages (the default) and through the
+            # runtime's pageable path (SID_UPLOAD_REGISTER=0), one after the other
+            reg, dt = median_of(dict(os.environ, SID_UPLOAD_REGISTER="1"))
+            if dt is None:
+                res = reg
+            else:
+                pageable, dt0 = median_of(dict(os.environ, SID_UPLOAD_REGISTER="0"))
                 sites = n * R.world
+                stt = reg["cli_stats"]
                 res = {"devices": R.world, "sites": sites, "text_bytes": total, "wall_s": dt,
                        "wall_s_is": "median of 3 runs after one warm-up", "sites_per_s_wall": sites / dt,
-                       "sites_per_s_cli_clock": stt.get("sites_per_s"), "wall_s_runs": [x[0] for x in runs],
-                       "cli_stats": stt, "file_write_s_rank0": write_s,
+                       "sites_per_s_cli_clock": stt.get("sites_per_s"), "wall_s_runs": reg["wall_s_runs"],
+                       "cli_stats": stt, "placement": stt.get("placement"), "file_write_s_rank0": write_s,
+                       "upload_pageable": dict(pageable, sites_per_s_wall=sites / dt0 if dt0 else None),
                        "note": f"build/sid --devices {R.world} FILE > /dev/null on one file holding every "
                                "rank's shard (the whole node's drop-in: one process, every GPU); wall = "
-                               "process start + HIP init + mapping + H2D + kernels + D2H + write"}
-                if cfg["method"] == "local":
+                               "process start + HIP init + mapping + H2D + kernels + D2H + write; the uploads "
+                               "from registered pages (the default), and in upload_pageable through the "
+                               "runtime's pageable path (SID_UPLOAD_REGISTER=0)"}
+                if cfg["method"] == "local" and dt is not None:
                     # the whole node's CPU path beside it: the oracle over the same file, one
                     # line-aligned shard process per CPU the job may use
                     P, share = cpu_share(R.cpus0)

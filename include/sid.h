@@ -344,6 +344,20 @@ int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg, sid_engin
 int sid_engine_destroy(sid_engine* e);
 int sid_engine_devices(const sid_engine* e);
 sid_ctx* sid_engine_context(sid_engine* e, int i);
+/* Host placement of pipeline i (a multi-GPU node: each GPU's uploader,
+ * compute and drain threads run on the CPUs local to its PCI device, and its
+ * pinned host buffers are allocated from them, so their pages sit on the
+ * GPU's NUMA node and its DMA does not cross sockets). */
+typedef struct {
+    int device;             /* HIP device                                          */
+    int gpu_numa_node;      /* NUMA node of the GPU's PCI device (-1: unknown)     */
+    int cpus;               /* CPUs its threads are bound to (0: not bound)        */
+    int first_cpu;          /* the lowest of them (-1: not bound)                  */
+    int arena_numa_node;    /* NUMA node of the host arena's first page (-1: none) */
+    int ring_numa_node;     /* ... of the emit ring's first page (-1: none)        */
+    char pci[16];           /* PCI bus id, e.g. "0000:05:00.0"                     */
+} sid_placement;
+int sid_engine_placement(const sid_engine* e, int i, sid_placement* out);
 /* Sources.  The engine keeps the pointer / descriptor until the next source. */
 int sid_engine_source_text(sid_engine* e, const char* text, uint64_t len);          /* host memory */
 int sid_engine_source_file(sid_engine* e, int fd, uint64_t offset, uint64_t len);   /* regular file */

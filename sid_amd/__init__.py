@@ -74,6 +74,12 @@ class RunStats(C.Structure):
                 ("register_s", C.c_double), ("h2d_s", C.c_double), ("h2d_bytes", C.c_uint64)]
 
 
+class Placement(C.Structure):
+    """sid_placement (include/sid.h): a pipeline's host placement."""
+    _fields_ = [("device", C.c_int), ("gpu_numa_node", C.c_int), ("cpus", C.c_int), ("first_cpu", C.c_int),
+                ("arena_numa_node", C.c_int), ("ring_numa_node", C.c_int), ("pci", C.c_char * 16)]
+
+
 class EngineProf(C.Structure):
     _fields_ = [("chunks", C.c_uint64), ("index_ms", C.c_double), ("parse_ms", C.c_double), ("call_ms", C.c_double),
                 ("hist_ms", C.c_double), ("fmt_len_ms", C.c_double), ("fmt_write_ms", C.c_double)]
@@ -133,6 +139,7 @@ SIGNATURES = [
     ("sid_engine_destroy", _I, [_P]),
     ("sid_engine_devices", _I, [_P]),
     ("sid_engine_context", _P, [_P, _I]),
+    ("sid_engine_placement", _I, [_P, _I, C.POINTER(Placement)]),
     ("sid_engine_source_text", _I, [_P, _P, _U64]),
     ("sid_engine_source_file", _I, [_P, _I, _U64, _U64]),
     ("sid_engine_source_device_text", _I, [_P, _P, _U64]),
@@ -472,6 +479,14 @@ class Engine:
 
     def context(self, i=0):
         return lib().sid_engine_context(self.h, i)
+
+    def placement(self, i=0) -> dict:
+        """Pipeline i's host placement: its GPU's NUMA node, the CPUs its
+        threads are bound to, the NUMA nodes of its pinned host buffers."""
+        p = Placement()
+        check(lib().sid_engine_placement(self.h, i, C.byref(p)), "sid_engine_placement")
+        return {"device": p.device, "pci": p.pci.decode(), "gpu_numa_node": p.gpu_numa_node, "cpus": p.cpus,
+                "first_cpu": p.first_cpu, "arena_numa_node": p.arena_numa_node, "ring_numa_node": p.ring_numa_node}
 
     def source_text(self, text: bytes):
         self._keep = C.create_string_buffer(text, len(text)) if text else None

@@ -413,6 +413,19 @@ int main(int argc, char** argv)
         if (rc == SID_EIO) std::exit(EXIT_FAILURE);
         CHECK(rc, "emit");
         const double t3 = now();
+        std::string place;   // per pipeline: its GPU, the CPUs its threads ran on, its pinned buffers' NUMA nodes
+        if (opt.stats)
+            for (int i = 0; i < sid_engine_devices(eng); ++i) {
+                sid_placement pl;
+                if (sid_engine_placement(eng, i, &pl) != SID_OK) continue;
+                char b[256];
+                std::snprintf(b, sizeof b,
+                              "%s{\"device\": %d, \"pci\": \"%s\", \"gpu_numa_node\": %d, \"cpus\": %d, "
+                              "\"first_cpu\": %d, \"arena_numa_node\": %d, \"ring_numa_node\": %d}",
+                              place.empty() ? "" : ", ", pl.device, pl.pci, pl.gpu_numa_node, pl.cpus, pl.first_cpu,
+                              pl.arena_numa_node, pl.ring_numa_node);
+                place += b;
+            }
         if (opt.stats)
             std::fprintf(stderr,
                          "{\"sites\": %llu, \"devices\": %d, \"threads\": %d, \"path\": \"stream\", "
@@ -420,14 +433,15 @@ int main(int argc, char** argv)
                          "\"sites_per_s\": %.1f, \"chunks\": %llu, \"chunks_held\": %llu, "
                          "\"chunks_retained\": %llu, \"chunks_reloaded\": %llu, \"bytes_in\": %llu, "
                          "\"bytes_out\": %llu, \"ingest_s\": %.6f, \"chunks_registered\": %llu, "
-                         "\"register_s\": %.6f, \"h2d_s\": %.6f, \"h2d_bytes\": %llu, "
+                         "\"register_s\": %.6f, \"h2d_s\": %.6f, \"h2d_bytes\": %llu, \"placement\": [%s], "
                          "\"main_entry_unix\": %.6f, \"main_exit_unix\": %.6f}\n",
                          (unsigned long long)st.sites, D, T, tc - t0, t1 - t0, t2 - t1, t3 - t2, t3 - t0,
                          st.sites / std::max(1e-9, t3 - t0), (unsigned long long)st.chunks,
                          (unsigned long long)st.chunks_held, (unsigned long long)st.chunks_retained,
                          (unsigned long long)st.chunks_reloaded, (unsigned long long)st.bytes_in,
                          (unsigned long long)st.bytes_out, st.ingest_s, (unsigned long long)st.chunks_registered,
-                         st.register_s, st.h2d_s, (unsigned long long)st.h2d_bytes, t_entry, unix_now());
+                         st.register_s, st.h2d_s, (unsigned long long)st.h2d_bytes, place.c_str(), t_entry,
+                         unix_now());
         // device memory, pinned staging and the mapping go with the process
         finish(0);
     }

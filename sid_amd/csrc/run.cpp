@@ -26,8 +26,11 @@
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -246,6 +249,11 @@ struct Slot {
 
 struct Dev {
     int index = 0, device = 0;
+    // host placement (sid_engine_placement): the CPUs local to the GPU's PCI
+    // device within the process's own, and its NUMA node
+    cpu_set_t cpus;
+    int ncpus = 0, first_cpu = -1, numa_node = -1;
+    char pci[16] = {0};
     sid_ctx* ctx = nullptr;
     hipStream_t s_up = nullptr, s_comp = nullptr, s_d2h = nullptr;
     std::vector<Slot> slots;
@@ -322,6 +330,14 @@ struct Dev {
         hh_off += (bytes + 255) & ~(uint64_t)255;
         return p;
     }
+    // the tile parse (sid_chunk_tile_local): its slots per tile for the next
+    // chunk (log2: the most lines a tile of the last chunk had, a sixteenth
+    // on top), its shape (a quad of lanes per line for lines over 256 B on
+    // average), and whether it takes the lines at all (at most
+    // 2^SID_TILE_CAP_MAX a tile)
+    uint32_t tile_log2 = 8;
+    bool tile_quad = false;
+    bool tile_ok = true;
     uint64_t hold_budget = 0, retain_budget = 0;
     std::atomic<uint64_t> hold_used{0}, retain_used{0};
     std::atomic<bool> hold_full{false};
@@ -399,6 +415,97 @@ struct Dev {
         ev_cache.push_back(ev);
     }
 };
+
+// The CPUs of a sysfs cpulist ("0-15,128-143") within `allowed`
+int parse_cpulist(const char* txt, const cpu_set_t& allowed, cpu_set_t* out, int* first)
+{
+    CPU_ZERO(out);
+    int n = 0;
+    *first = -1;
+    const char* p = txt;
+    while (*p) {
+        char* q = nullptr;
+        const long lo = std::strtol(p, &q, 10);
+        if (q == p) break;
+        long hi = lo;
+        p = q;
+        if (*p == '-') {
+            hi = std::strtol(p + 1, &q, 10);
+            p = q;
+        }
+        for (long c = lo; c <= hi && c < CPU_SETSIZE; ++c)
+            if (c >= 0 && CPU_ISSET(c, &allowed) && !CPU_ISSET(c, out)) {
+                CPU_SET(c, out);
+                if (*first < 0 || c < *first) *first = (int)c;
+                ++n;
+            }
+        while (*p == ',' || *p == '\n' || *p == ' ') ++p;
+    }
+    return n;
+}
+
+// d's GPU: its PCI bus id, NUMA node and local CPUs (sysfs), kept for
+// binding when they are a proper subset of the process's CPUs
+void find_placement(Dev& d)
+{
+    CPU_ZERO(&d.cpus);
+    if (hipDeviceGetPCIBusId(d.pci, sizeof d.pci, d.device) != hipSuccess) {
+        (void)hipGetLastError();
+        d.pci[0] = 0;
+        return;
+    }
+    for (char* c = d.pci; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+    char path[128], buf[4096];
+    std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", d.pci);
+    if (FILE* f = std::fopen(path, "r")) {
+        if (std::fscanf(f, "%d", &d.numa_node) != 1) d.numa_node = -1;
+        std::fclose(f);
+    }
+    std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/local_cpulist", d.pci);
+    FILE* f = std::fopen(path, "r");
+    if (!f) return;
+    const size_t m = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[m] = 0;
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+    cpu_set_t mine;
+    int first = -1;
+    const int n = parse_cpulist(buf, allowed, &mine, &first);
+    if (n == 0 || n == CPU_COUNT(&allowed)) return;   // nothing to choose
+    d.cpus = mine;
+    d.ncpus = n;
+    d.first_cpu = first;
+}
+
+// the calling thread onto d's CPUs (no-op when not bound)
+void bind_thread(const Dev& d)
+{
+    if (d.ncpus > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof d.cpus, &d.cpus);
+}
+
+// NUMA node of the page holding p (-1: unknown)
+int page_node(const void* p)
+{
+    if (!p) return -1;
+    int node = -1;
+    // get_mempolicy(&node, NULL, 0, p, MPOL_F_NODE | MPOL_F_ADDR)
+    if (syscall(SYS_get_mempolicy, &node, nullptr, 0ul, p, 1ul | 2ul) != 0) return -1;
+    return node;
+}
+
+// f() on a thread bound to d's CPUs (pinned host buffers then come from the
+// GPU's NUMA node: the pages are allocated by the thread that pins them)
+template <class F>
+void on_node(const Dev& d, F f)
+{
+    if (d.ncpus == 0) return f();
+    std::thread t([&] {
+        bind_thread(d);
+        f();
+    });
+    t.join();
+}
 
 }  // namespace
 
@@ -625,8 +732,11 @@ extern "C" int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg
     // second thread while sid_create builds the class tables)
     auto make = [&](int i) {
         Dev* d = e->devs[i].get();
+        find_placement(*d);
+        bind_thread(*d);   // (this GPU's start-up thread: its host allocations local to it)
         hipError_t x = hipSuccess;
         std::thread qs([&] {
+            bind_thread(*d);
             x = hipSetDevice(d->device);
             if (x == hipSuccess) x = hipStreamCreateWithFlags(&d->s_up, hipStreamNonBlocking);
             if (x == hipSuccess) x = hipStreamCreateWithFlags(&d->s_comp, hipStreamNonBlocking);
@@ -646,10 +756,9 @@ extern "C" int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg
     auto per_gpu = [&](int g) {
         for (int i = g * lanes; i < std::min(D, (g + 1) * lanes); ++i) make(i);
     };
-    {
+    {   // (each on a thread of its own: make() binds its thread to the GPU's CPUs)
         std::vector<std::thread> th;
-        for (int g = 1; g < G; ++g) th.emplace_back(per_gpu, g);
-        per_gpu(0);
+        for (int g = 0; g < G; ++g) th.emplace_back(per_gpu, g);
         for (auto& t : th) t.join();
     }
     (void)hipSetDevice(e->devs[0]->device);
@@ -727,6 +836,22 @@ extern "C" sid_ctx* sid_engine_context(sid_engine* e, int i)
 {
     if (!e || i < 0 || i >= (int)e->devs.size()) return nullptr;
     return e->devs[i]->ctx;
+}
+
+extern "C" int sid_engine_placement(const sid_engine* e, int i, sid_placement* out)
+{
+    if (!e || !out || i < 0 || i >= (int)e->devs.size()) return SID_EINVAL;
+    const Dev& d = *e->devs[i];
+    std::memset(out, 0, sizeof *out);
+    out->device = d.device;
+    out->gpu_numa_node = d.numa_node;
+    out->cpus = d.ncpus;
+    out->first_cpu = d.first_cpu;
+    out->arena_numa_node = page_node(d.hh);
+    out->ring_numa_node = d.pinned.empty() ? -1 : page_node(d.pinned[0]);
+    std::memcpy(out->pci, d.pci, sizeof out->pci);
+    out->pci[sizeof out->pci - 1] = 0;
+    return SID_OK;
 }
 
 static void assign_devices(sid_engine* e)
@@ -1018,6 +1143,7 @@ struct UploadReg {
 // the uploader of device d: the chunks of `list` into device buffers, in order
 void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass)
 {
+    bind_thread(d);
     if (hipSetDevice(d.device) != hipSuccess) return (void)fail(e, SID_EHIP);
     UploadReg reg(e, pass);
     // the chunk this uploader copies after j from the host (UINT64_MAX: none)
@@ -1213,6 +1339,7 @@ int call_sites(sid_engine* e, Dev& d, const Loaded& L, uint64_t n)
 // the compute thread of device d, for one pass
 void compute(sid_engine* e, Dev& d, int pass)
 {
+    bind_thread(d);
     if (hipSetDevice(d.device) != hipSuccess) return (void)fail(e, SID_EHIP);
     sid_chunk_ws& W = d.ws;
     uint64_t* hs = d.h_small;
@@ -1271,6 +1398,96 @@ void compute(sid_engine* e, Dev& d, int pass)
         W.cls_ready = false;    // (... and the class words)
         const uint64_t tbytes = L.c1 - (L.c0 & ~(uint64_t)15);
         if (x == hipSuccess && !pre_indexed) rc = sid_chunk_reserve(&W, tbytes, 0);
+        const bool lynch_hist = pass == 1 && e->lynch;
+        const bool format = pass == 2 || (needs_format_pass1(e) && (!d.hold_full.load() || sink_all_pass1(e)));
+        // -m local / quality (and pass 2 of the Lynch paths): call, then the
+        // one-pass formatter into a buffer of the records' upper bound -- the
+        // device's hold arena in pass 1 (committed to the exact bytes after),
+        // else a pooled scratch buffer
+        char* out = nullptr;
+        uint64_t cap = 0;   // 0: arena memory (never returned to the pool)
+        bool via_host = false;   // pass 1: records go on to the host arena (a pooled device buffer meanwhile)
+        bool sunk = false;       // pass 1, device sink: a scratch buffer, dropped
+        hipEvent_t pe = nullptr;
+        uint64_t n = 0;
+        // -m local formatting in this pass, lines of up to 256 B on average (as
+        // the device's last chunk had): the tile parse -- the text read once,
+        // no host round trip before the writer (sid_chunk_tile_local).  A tile
+        // with more lines than its slots sends the chunk again through the
+        // two-pass path below (its records dropped), the next chunks with
+        // more slots
+        bool tiled = false;
+        if (x == hipSuccess && rc == SID_OK && format && !lynch_hist && !qmode && d.tile_ok &&
+            e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx) && !(pass == 2 && r.pre)) {
+            const uint32_t lg = d.tile_log2;
+            const bool quad = d.tile_quad;
+            rc = sid_chunk_reserve(&W, tbytes, sid_chunk_tile_slots(L.c0, L.c1, lg, quad));
+            if (rc != SID_OK) return (void)fail(e, rc);
+            const uint64_t bound = sid_chunk_tile_bound(L.c0, L.c1, lg, quad);
+            // the records' buffer, taken as the two-pass path below takes it
+            // (near the hold budget that path decides, with its exact bound)
+            if (pass == 1 && d.hh && !d.hh_full) {
+                out = d.pool.get(bound, &cap, d.s_comp);
+                via_host = out != nullptr;
+                if (!out) cap = 0;
+            }
+            if (via_host) {
+            } else if (pass == 1 && sink_all_pass1(e)) {
+                out = d.pool.get(bound, &cap, d.s_comp);
+                sunk = out != nullptr;
+                if (!out) cap = 0;
+            } else if (pass == 1 && d.hold_used.load() + bound > d.hold_budget) {
+            } else if (pass == 1) {
+                out = d.arena_reserve(bound, d.hold_budget - d.hold_used.load());
+            } else {
+                out = d.pool.get(bound, &cap, d.s_comp);
+                if (!out) cap = 0;
+            }
+            if (out) {
+                pe = d.prof_begin(P);
+                rc = sid_chunk_tile_local(d.ctx, &W, L.base, L.c0, L.c1, lg, quad, e->conf_type, d.s_comp);
+                d.prof_end(1, pe);
+                if (rc == SID_OK) {
+                    pe = d.prof_begin(P);
+                    rc = sid_chunk_local_put(d.ctx, &W, L.base, L.c1, 0, e->conf_type, out, d.s_comp);
+                    d.prof_end(5, pe);
+                }
+                W.tile_log2 = 0;   // (the workspace's dense layout again for the two-pass path)
+                if (rc != SID_OK) return (void)fail(e, rc);
+                // bytes, range flag, sites, parse error key, the most lines in a tile
+                x = hipMemcpyAsync(hs + 8, W.lb + 1, 5 * 8, hipMemcpyDeviceToHost, d.s_comp);
+                if (x == hipSuccess) x = sync();
+                if (x != hipSuccess) return (void)hipfail(e, x);
+                const uint64_t maxl = hs[12];
+                auto log2_up = [](uint64_t v) {
+                    uint32_t k = 0;
+                    while ((1ull << k) < v) ++k;
+                    return k;
+                };
+                if (maxl <= (1ull << lg)) {
+                    tiled = true;
+                    n = hs[10];
+                    r.parsed = n;
+                    hs[4] = hs[11];
+                    // the next chunk's shape and slots (a new shape: from this
+                    // chunk's lines per byte, a quarter on top)
+                    const bool q2 = L.c1 - L.c0 > 256 * n;
+                    const uint64_t want = q2 == quad ? maxl + maxl / 16 + 1
+                                                     : (uint64_t)((double)n * (q2 ? 24576 : 16384) /
+                                                                  (double)std::max<uint64_t>(1, L.c1 - L.c0) * 1.25) + 1;
+                    d.tile_quad = q2;
+                    d.tile_log2 = std::min(SID_TILE_CAP_MAX, std::max(SID_TILE_CAP_MIN, log2_up(want)));
+                } else {
+                    if (cap) d.pool.put(out, cap, d.s_comp);
+                    out = nullptr;
+                    cap = 0;
+                    via_host = sunk = false;
+                    d.tile_log2 = std::min(SID_TILE_CAP_MAX, log2_up(maxl));
+                    d.tile_ok = maxl <= (1ull << SID_TILE_CAP_MAX);
+                }
+            }
+        }
+        if (!tiled) {
         // pass 2 of a Lynch path: the parse kept since pass 1 stands in for the
         // workspace's line offsets, counts and header pairs (restored below)
         struct View {
@@ -1283,8 +1500,6 @@ void compute(sid_engine* e, Dev& d, int pass)
                 if (on) W.starts = starts, W.counts = counts, W.hdr = hdr;
             }
         } view{W, W.starts, W.counts, W.hdr};
-        hipEvent_t pe = nullptr;
-        uint64_t n = 0;
         // the kept parse's layout: starts (4 B), counts (8 B), header pairs
         // (16 B), each at a 16-B aligned offset (the lookup reads counts as
         // 16-B site pairs)
@@ -1340,8 +1555,6 @@ void compute(sid_engine* e, Dev& d, int pass)
             d.prof_end(1, pe);
             if (rc != SID_OK) return (void)fail(e, rc);
         }
-        const bool lynch_hist = pass == 1 && e->lynch;
-        const bool format = pass == 2 || (needs_format_pass1(e) && (!d.hold_full.load() || sink_all_pass1(e)));
         if (lynch_hist) {
             x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
             if (x != hipSuccess) return (void)hipfail(e, x);
@@ -1352,14 +1565,6 @@ void compute(sid_engine* e, Dev& d, int pass)
             if (rc != SID_OK) return (void)fail(e, rc);
             if (x != hipSuccess) return (void)hipfail(e, x);
         }
-        // -m local / quality (and pass 2 of the Lynch paths): call, then the
-        // one-pass formatter into a buffer of the records' upper bound -- the
-        // device's hold arena in pass 1 (committed to the exact bytes after),
-        // else a pooled scratch buffer
-        char* out = nullptr;
-        uint64_t cap = 0;   // 0: arena memory (never returned to the pool)
-        bool via_host = false;   // pass 1: records go on to the host arena (a pooled device buffer meanwhile)
-        bool sunk = false;       // pass 1, device sink: a scratch buffer, dropped
         // -m local: the call fused into the formatter (sid_chunk_local_*)
         const bool fused = e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx);
         // likelihood_ratio / bayes pass 2: the class lookup fused into the
@@ -1433,6 +1638,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                 hs[4] = hs[11];
             }
         }
+        }   // (the two-pass path)
         if (!lynch_hist && !out) {
             x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
             if (x == hipSuccess) x = sync();
@@ -1544,6 +1750,7 @@ void compute(sid_engine* e, Dev& d, int pass)
 // the drain of device d: CSV buffers through the pinned ring to the writer
 void drain(sid_engine* e, Dev& d)
 {
+    bind_thread(d);
     if (hipSetDevice(d.device) != hipSuccess) return (void)fail(e, SID_EHIP);
     OutItem it;
     while (d.drain_q.pop(it)) {
@@ -1691,7 +1898,9 @@ static int setup_budgets(sid_engine* e)
         const uint64_t hb = e->cfg.device_sink == 1 ? 0 : e->cfg.host_hold_bytes;
         if (hb && d.hh_cap < hb) {
             d.hh_free();
-            if (!d.hh_alloc(hb)) return SID_ENOMEM;
+            bool ok = false;
+            on_node(d, [&] { ok = hipSetDevice(d.device) == hipSuccess && d.hh_alloc(hb); });
+            if (!ok) return SID_ENOMEM;
         }
     }
     return SID_OK;
@@ -1718,7 +1927,15 @@ static int setup_generator(sid_engine* e)
 // pinning slows the ingest beside it and the exit tail grows with it)
 constexpr int EMIT_RING_N = 4;
 constexpr uint64_t EMIT_RING_BYTES = 16ull << 20;
+static int alloc_ring_here(Dev& d);
+// (on a thread bound to the GPU's CPUs: the ring's pages from its NUMA node)
 static int alloc_ring(Dev& d)
+{
+    int rc = SID_OK;
+    on_node(d, [&] { rc = alloc_ring_here(d); });
+    return rc;
+}
+static int alloc_ring_here(Dev& d)
 {
     if (hipSetDevice(d.device) != hipSuccess) return SID_EHIP;
     const uint64_t bytes = EMIT_RING_BYTES;

@@ -749,18 +749,20 @@ __device__ __forceinline__ uint32_t rb_window(const uint4 v, uint32_t valid, int
 
 // The read-bases count by the table: the first window (the token's start
 // inside it) masked, then whole windows while they lie inside the text.
-// first: the first window's 16 bytes, in the header's LDS stage (no second
-// global load of bytes the header already read).  (The next windows from the
-// stage too, where the 48 staged bytes hold them, measured slower: the loads
-// hit the caches already)
-__device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, uint64_t len, uint64_t q, uint32_t kd,
-                                               const uint32_t* lut, const uint4* first, uint64_t* out)
+// first: the first window's 16 bytes, in LDS with the header (no second load
+// of bytes the header already read).  ld(a): the 16-B window at text offset a
+// (global memory, or the tile parse's LDS copy).  (The next windows from the
+// per-line parse's stage too, where its 48 staged bytes hold them, measured
+// slower: the loads hit the caches already)
+template <class Ld>
+__device__ __forceinline__ bool read_bases_lut(Ld ld, uint64_t len, uint64_t q, uint32_t kd, const uint32_t* lut,
+                                               const uint4* first, uint64_t* out)
 {
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
     uint64_t a = q & ~(uint64_t)15;
     uint32_t carry = 0;   // bit 7: byte 0 of the next word is skipped
     bool done = false, bad = false;
-    uint4 vn = *(const uint4*)(text + a + 16);   // the next window in flight while the first is counted
+    uint4 vn = ld(a + 16);   // the next window in flight while the first is counted
     uint32_t acc = 0;
     auto masked = [&](const uint4& v, uint32_t lead) {
         const int room = len > a ? (int)min(len - a, (uint64_t)16) : 0;
@@ -779,7 +781,7 @@ __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, ui
     a += 16;
     while (!done) {
         const uint4 v = vn;
-        vn = *(const uint4*)(text + a + 16);
+        vn = ld(a + 16);
         add(a + 16 <= len ? rb_window<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u));
         a += 16;
     }
@@ -801,8 +803,9 @@ __device__ __forceinline__ bool read_bases_lut(const char* __restrict__ text, ui
 // skipped is a '^' run, which fails in that lane); the token ends in the
 // quad's first window holding its end, and the windows after it are dropped.
 // Every lane of the quad returns the same result.
-__device__ __forceinline__ bool read_bases_quad(const char* __restrict__ text, uint64_t len, uint64_t q, uint32_t kd,
-                                                const uint32_t* lut, const uint4* first, uint64_t* out)
+template <class Ld>
+__device__ __forceinline__ bool read_bases_quad(Ld ld, uint64_t len, uint64_t q, uint32_t kd, const uint32_t* lut,
+                                                const uint4* first, uint64_t* out)
 {
     const uint32_t j = threadIdx.x & 3u;
     const uint64_t a0 = q & ~(uint64_t)15;
@@ -812,7 +815,7 @@ __device__ __forceinline__ bool read_bases_quad(const char* __restrict__ text, u
     for (uint32_t it = 0;; ++it) {   // uniform across the quad
         const uint32_t k = 4u * it + j;
         const uint64_t a = a0 + 16ull * k;
-        const uint4 v = k == 0 ? *first : *(const uint4*)(text + a);   // (past the line's end: the readable padding)
+        const uint4 v = k == 0 ? *first : ld(a);   // (past the line's end: the readable padding)
         const int room = len > a ? (int)min(len - a, (uint64_t)16) : 0;
         const uint32_t lead = k == 0 ? (uint32_t)(q & 15) : 0u;
         const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
@@ -858,38 +861,20 @@ __device__ __forceinline__ bool read_bases_quad(const char* __restrict__ text, u
     return true;
 }
 
-// The fast path of one line (pileup.cpp:13-46 + :70-153 for the lines that
-// need none of the general routine's cases), branch-free over SWAR byte masks:
-//   header   the 48 bytes from the line's 16-B window: separator (' ', '\t')
-//            and low-byte (< 0x21) masks -> token starts 0-4 by bit tricks;
-//            tokens 0-3 must be free of '\n', NUL and other control bytes;
-//            ref and the position digits read from the lane's LDS copy
-//   token 4  16 bytes per step, per 4-byte word:
-//            A/C/G/T either case     -> their counters (w | 0x20 folds the case)
-//            '.' / ','               -> one "matches ref" counter, added to the
-//                                       ref's class at the end
-//            '^'                     -> the next byte is skipped; a '^' that is
-//                                       itself skipped (a '^' run) fails
-//            '+'/'-' (and ')'/'/')   -> fail (indel: the general routine)
-//            first byte < 0x21       -> end of the token, which must be ' ',
-//                                       '\t', '\n' or NUL, else fail
-// Returns false when the line needs the general routine.
-// QUAD: the read bases counted by the line's quad of lanes (read_bases_quad;
-// every lane of the quad parses the same line, so its header is the same in
-// all four)
-template <bool QUAD = false>
-__device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, uint64_t len, uint64_t s0,
-                                                const uint8_t* cls, char* stage, uint64_t* out, uint64_t* hdr,
-                                                const uint32_t* rbl)
+// The fast path's header (pileup.cpp:13-46), branch-free over SWAR byte
+// masks: the 48 bytes from the line's 16-B window (v0..v2, also at `stage`
+// in LDS for byte reads) -> low-byte (< 0x21) mask -> token starts 1-4 by bit
+// tricks; token 0 at the line start, exactly one ' '/'\t' before each of
+// tokens 1-4 and a one-byte token 2 (else the general routine, which has
+// strtok_r's semantics); ref and the position digits from the LDS copy.
+// sh: the line's offset in v0; avail: the chunk's bytes from the line start.
+// hdr: the formatter's header pair; returns the offset of token 4 from the
+// line start (< 48), or -1 for the general routine; *kd: the class '.'/','
+// stand for.
+__device__ __forceinline__ int parse_header(const uint4 v0, const uint4 v1, const uint4 v2, const char* stage,
+                                            uint32_t sh, uint64_t avail, const uint8_t* cls, uint64_t* hdr,
+                                            uint32_t* kdp)
 {
-    const uint64_t a0 = s0 & ~(uint64_t)15;
-    const uint32_t sh = (uint32_t)(s0 & 15);
-    const uint4 v0 = *(const uint4*)(text + a0);
-    const uint4 v1 = *(const uint4*)(text + a0 + 16);
-    const uint4 v2 = *(const uint4*)(text + a0 + 32);
-    *(uint4*)(stage) = v0;
-    *(uint4*)(stage + 16) = v1;
-    *(uint4*)(stage + 32) = v2;
     // low bytes (< 0x21: the separators, '\n', NUL, every other control byte)
     // of the 48 staged bytes as a 48-bit mask: 3 instructions a word
     const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
@@ -900,7 +885,6 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
                           (compress8(lowb[4], lowb[5]) << 16) | (compress8(lowb[6], lowb[7]) << 24);
     const uint32_t l_hi = compress8(lowb[8], lowb[9]) | (compress8(lowb[10], lowb[11]) << 8);
     // bit j = byte s0 + j, for the bytes inside the text and the 48 staged
-    const uint64_t avail = len > s0 ? len - s0 : 0;
     const uint32_t nb = (uint32_t)min((uint64_t)(HDR_BYTES - sh), avail);
     const uint64_t valid = (1ull << nb) - 1;   // (nb <= 48)
     const uint64_t L = ((((uint64_t)l_hi << 32) | l_lo) >> sh) & valid;
@@ -913,18 +897,15 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     const int t3 = ctz64(T);
     T &= T - 1;
     const int t4 = ctz64(T);
-    // The fast path's lines (the rest take the general routine, which has
-    // strtok_r's semantics): token 0 at the line start, and exactly one
-    // separator byte before each of tokens 1-4 -- the low bytes before token
-    // 4 are then the four gaps, which must be ' ' or '\t' (a '\n', NUL or
-    // other control byte there ends or splits a token differently) -- and a
-    // one-byte token 2 (the reference base)
+    // the low bytes before token 4 are then the four gaps, which must be ' '
+    // or '\t' (a '\n', NUL or other control byte there ends or splits a
+    // token differently)
     bool ok = (N & 1) && t4 < (int)nb && t3 == t2 + 2;
     ok = ok && __popcll(L & ((1ull << t4) - 1)) == 4;
-    if (!ok) return false;
+    if (!ok) return -1;
     const uint32_t gaps = (uint32_t)(uint8_t)stage[sh + t1 - 1] | ((uint32_t)(uint8_t)stage[sh + t2 - 1] << 8) |
                           ((uint32_t)(uint8_t)stage[sh + t2 + 1] << 16) | ((uint32_t)(uint8_t)stage[sh + t4 - 1] << 24);
-    if ((eq_bytes(gaps, 0x20202020u) | eq_bytes(gaps, 0x09090909u)) != 0x80808080u) return false;
+    if ((eq_bytes(gaps, 0x20202020u) | eq_bytes(gaps, 0x09090909u)) != 0x80808080u) return -1;
     const int t0 = 0;
     const int l0 = t1 - 1;
     const int lp = t2 - 1 - t1;
@@ -959,10 +940,47 @@ __device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, u
     const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
     const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
     const uint32_t kd = cls[up], kc = cls[lw];
-    if (kd >= K_CARET || kc >= K_CARET || kd != kc) return false;
-    if (QUAD)
-        return read_bases_quad(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out);
-    return read_bases_lut(text, len, s0 + (uint64_t)t4, kd, rbl, (const uint4*)(stage + ((sh + t4) & 0x30)), out);
+    if (kd >= K_CARET || kc >= K_CARET || kd != kc) return -1;
+    *kdp = kd;
+    return t4;
+}
+
+// The fast path of one line (pileup.cpp:13-46 + :70-153 for the lines that
+// need none of the general routine's cases): the header (parse_header), then
+// the read bases (token 4) 16 bytes per step, per 4-byte word:
+//   A/C/G/T either case     -> their counters
+//   '.' / ','               -> one "matches ref" counter, added to the ref's
+//                              class at the end
+//   '^'                     -> the next byte is skipped; a '^' that is itself
+//                              skipped (a '^' run) fails
+//   '+'/'-'                 -> fail (indel: the general routine)
+//   first byte < 0x21       -> end of the token, which must be ' ', '\t',
+//                              '\n' or NUL, else fail
+// Returns false when the line needs the general routine.  The 48 header bytes
+// are staged in the lane's LDS slot for byte reads.
+// QUAD: the read bases counted by the line's quad of lanes (read_bases_quad;
+// every lane of the quad parses the same line, so its header is the same in
+// all four)
+template <bool QUAD = false>
+__device__ __forceinline__ bool parse_line_fast(const char* __restrict__ text, uint64_t len, uint64_t s0,
+                                                const uint8_t* cls, char* stage, uint64_t* out, uint64_t* hdr,
+                                                const uint32_t* rbl)
+{
+    const uint64_t a0 = s0 & ~(uint64_t)15;
+    const uint32_t sh = (uint32_t)(s0 & 15);
+    const uint4 v0 = *(const uint4*)(text + a0);
+    const uint4 v1 = *(const uint4*)(text + a0 + 16);
+    const uint4 v2 = *(const uint4*)(text + a0 + 32);
+    *(uint4*)(stage) = v0;
+    *(uint4*)(stage + 16) = v1;
+    *(uint4*)(stage + 32) = v2;
+    uint32_t kd = 0;
+    const int t4 = parse_header(v0, v1, v2, stage, sh, len > s0 ? len - s0 : 0, cls, hdr, &kd);
+    if (t4 < 0) return false;
+    auto ld = [text](uint64_t a) { return *(const uint4*)(text + a); };
+    const uint4* first = (const uint4*)(stage + ((sh + t4) & 0x30));
+    if (QUAD) return read_bases_quad(ld, len, s0 + (uint64_t)t4, kd, rbl, first, out);
+    return read_bases_lut(ld, len, s0 + (uint64_t)t4, kd, rbl, first, out);
 }
 
 // Pass 1: the fast path over every line; a line it cannot take is appended to
@@ -1591,6 +1609,239 @@ __global__ __launch_bounds__(TB) void sid_local_len_list_kernel(const char* __re
     }
 }
 
+// ------------------------------------------------------------ tile parse --
+// The engine's -m local path for lines of up to 256 B on average (30x): the
+// line index fused into the parse, so the text is fetched from HBM once and
+// no host round trip separates index and parse (pileup.cpp:13-153 +
+// call.cpp:213-289 up to the record lengths).  One 256-thread block per tile
+// of TP_TILE bytes, copied to LDS with a halo of TP_HALO bytes after it (a
+// line that starts in the tile is read from LDS to its end in nearly every
+// case; one that runs past the halo reads the rest from HBM):
+//   load    the tile's 16-B windows, lanes contiguous, non-temporal (each
+//           byte is read once), into LDS
+//   index   line starts per window (the index kernel's masks), one block scan
+//           in file order -> the offsets of the tile's lines in LDS
+//   parse   one lane per line: the fast path (parse_header + read_bases_lut)
+//           from LDS; the call's class entry and record length
+//           (local_site_len), summed per wave into the writer block's bytes
+//   write   per line its slot g = tile * cap + j (j: the line's rank in the
+//           tile): class word and header pair; per tile its site count
+// Outputs are laid out per tile, cap slots each (slots past a tile's count
+// are never written or read), so no prefix over the tiles is needed before
+// the parse.  A tile with more lines than cap leaves the rest unparsed and
+// reports its count (lb[5]): the host runs the chunk again with a larger cap
+// (the chunk's records are dropped), or through the two-pass path.
+// The header pair's second word holds the chrom's first 8 bytes when the
+// pair is valid and the chrom at most 8 bytes long, else the line's offset
+// (slot_head): the writer never needs a line offset array.
+// Two shapes: 16 KiB tiles with a lane per line (30x: ~200 lines of ~81 B
+// per tile), and 24 KiB tiles with a quad of lanes per line (200x: ~58 lines
+// of ~426 B, 232 lanes; read_bases_quad, each quad reading 64 consecutive
+// bytes a step).
+constexpr uint32_t TP_ROWS = 4;                 // (the lane-per-line shape)
+constexpr uint32_t TP_ROWS_QUAD = 6;
+constexpr uint32_t TP_HALO = 1024;
+constexpr uint32_t TP_CAP_MAX = 1024;           // slots per tile at most (lines of 16 B on average)
+__host__ __device__ constexpr uint32_t tp_tile(bool quad) { return (quad ? TP_ROWS_QUAD : TP_ROWS) * TILE; }
+
+struct TileOut {
+    uint32_t cap_log2;          // slots per tile = 1 << cap_log2 (64 .. TP_CAP_MAX)
+    uint32_t* tcnt;             // per tile: its sites (at most the cap)
+    uint64_t* hdr;              // per slot: the header pair
+    uint64_t* counts;           // per slot: counts of the fix-up's and the general routine's sites
+    uint32_t* fb;               // the general routine's lines: slots,
+    uint32_t* fbo;              // ... and line offsets
+    unsigned long long* lb;     // [3] sites, [5] max lines in a tile, [6] fallback count (zeroed before)
+    uint64_t* state;            // [4] the chunk's parse error key: none yet
+};
+
+// a slot's chrom and position from its header pair (the tile parse's layout)
+__device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
+{
+    if (hw.x >> 63) {
+        Head h;
+        h.clen = (uint32_t)(hw.x >> 32) & 0xFFFu;
+        h.pos = (int32_t)(uint32_t)hw.x;
+        h.c8 = h.clen <= 8 ? hw.y : 0;
+        h.cb = h.clen <= 8 ? 0 : (uint64_t)(uint32_t)hw.y + ((hw.x >> 44) & 0x7FFFFull);
+        return h;
+    }
+    const uint64_t s0 = (uint32_t)hw.y;
+    return site_head_hw(R, &s0, make_ulonglong2(0, 0));
+}
+
+template <bool QUAD>
+__global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restrict__ text, uint64_t tile_base,
+                                                            uint64_t c0, uint64_t c1, TileOut O, LocalLen LL)
+{
+    constexpr uint32_t ROWS = QUAD ? TP_ROWS_QUAD : TP_ROWS, TP_TILE = ROWS * TILE;
+    constexpr uint32_t LPR = QUAD ? TB / 4 : TB;   // lines per round of the block
+    static_assert(TB == 256 && ROWS <= 8, "a lane's windows: two u64s of 16-bit line-start counts");
+    static_assert(FTB % 64 == 0, "a wave's slots lie in one writer block");
+    __shared__ __attribute__((aligned(16))) char tl[TP_TILE + TP_HALO + 64];
+    __shared__ uint16_t ls[TP_CAP_MAX];
+    __shared__ uint8_t cls[256];
+    __shared__ uint32_t rbl[256];
+    const uint32_t tid = threadIdx.x;
+    cls[tid] = (uint8_t)base_class(tid);
+    rbl[tid] = rb_entry(tid);
+    if (blockIdx.x == 0 && tid == 0) O.state[4] = ~0ull;   // no parse error yet
+    const uint64_t t = blockIdx.x;
+    const uint64_t g0 = tile_base + t * TP_TILE;           // the tile's first byte (16-B aligned)
+    // ---- load (windows at or past the chunk's end read as zeros)
+    uint4 v[ROWS];
+#pragma unroll
+    for (uint32_t k = 0; k < ROWS; ++k) {
+        const uint64_t at = g0 + k * TILE + tid * 16;
+        v[k] = at < c1 ? ld_nt(text + at) : make_uint4(0, 0, 0, 0);
+        *(uint4*)(tl + k * TILE + tid * 16) = v[k];
+    }
+    if (tid < TP_HALO / 16) {
+        const uint64_t at = g0 + TP_TILE + tid * 16;
+        *(uint4*)(tl + TP_TILE + tid * 16) = at < c1 ? *(const uint4*)(text + at) : make_uint4(0, 0, 0, 0);
+    }
+    if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
+    // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
+    const uint32_t prev0 = (g0 > c0 && g0 - 1 < c1) ? (text[g0 - 1] == '\n') : 1u;
+    __syncthreads();
+    // ---- line starts (bit j: byte j of the window starts a non-empty line in [c0, c1))
+    uint32_t m[ROWS];
+    uint64_t packed[2] = {0, 0};
+#pragma unroll
+    for (uint32_t k = 0; k < ROWS; ++k) {
+        const uint64_t at = g0 + k * TILE + tid * 16;
+        const uint4 w = v[k];
+        const uint32_t nl = compress8(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au)) |
+                            (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
+        const uint32_t prev = (k == 0 && tid == 0) ? prev0 : (uint32_t)(tl[max(k * TILE + tid * 16, 1u) - 1] == '\n');
+        uint32_t mk = ((nl << 1) | prev) & ~nl & 0xFFFFu;
+        if (at + 16 > c0 && at <= c0) {   // c0 in this window: it starts a line (unless a '\n'), nothing before it does
+            const uint32_t j = (uint32_t)(c0 - at);
+            mk = (mk | ((1u << j) & ~nl)) & ~((1u << j) - 1u);
+        }
+        if (at + 16 > c1) mk &= c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
+        if (at + 16 <= c0) mk = 0;
+        m[k] = mk;
+        packed[k / 4] |= (uint64_t)__popc(mk) << (16 * (k % 4));
+    }
+    // (a row of 4 KiB has at most 2048 line starts: 16-bit fields, four rows a word)
+    uint64_t tot[2] = {0, 0}, pre[2] = {0, 0};
+    pre[0] = block_exscan64(packed[0], &tot[0]);
+    if (ROWS > 4) pre[1] = block_exscan64(packed[1], &tot[1]);
+    const uint32_t cap = 1u << O.cap_log2;
+    uint32_t nlines = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < ROWS; ++k) {
+        uint32_t q = nlines + (uint32_t)((pre[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
+        for (uint32_t mk = m[k]; mk; mk &= mk - 1, ++q)
+            if (q < cap) ls[q] = (uint16_t)(k * TILE + tid * 16 + (uint32_t)(__ffs(mk) - 1));
+        nlines += (uint32_t)((tot[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
+    }
+    const uint32_t cnt = min(nlines, cap);
+    if (tid == 0) {
+        O.tcnt[t] = cnt;
+        if (cnt) atomicAdd(O.lb + 3, (unsigned long long)cnt);
+        atomicMax(O.lb + 5, (unsigned long long)nlines);
+    }
+    __syncthreads();
+    // ---- parse, one lane (a quad of lanes) per line, from LDS
+    auto ld = [&](uint64_t a) -> uint4 {
+        const uint64_t r = a - g0;
+        return r + 16 <= TP_TILE + TP_HALO ? *(const uint4*)(tl + r) : *(const uint4*)(text + a);
+    };
+    const uint64_t g_tile = t << O.cap_log2;
+    for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
+        const uint32_t j = j0 + (QUAD ? tid >> 2 : tid);
+        const bool lead = !QUAD || (tid & 3u) == 0;   // the lane that writes the line's outputs
+        int l = 0;
+        if (j < cnt) {
+            const uint32_t r0 = ls[j];
+            const uint64_t s0 = g0 + r0;
+            const uint64_t g = g_tile + j;
+            const char* stage = tl + (r0 & ~15u);
+            const uint32_t sh = r0 & 15u;
+            const uint4 v0 = *(const uint4*)stage, v1 = *(const uint4*)(stage + 16), v2 = *(const uint4*)(stage + 32);
+            uint64_t c = 0, h[2] = {0, 0};
+            uint32_t kd = 0;
+            const int t4 = parse_header(v0, v1, v2, stage, sh, c1 - s0, cls, h, &kd);
+            bool ok = t4 >= 0;
+            if (ok) {
+                const uint4* first = (const uint4*)(stage + ((sh + (uint32_t)t4) & 0x30u));
+                ok = QUAD ? read_bases_quad(ld, c1, s0 + (uint64_t)t4, kd, rbl, first, &c)
+                          : read_bases_lut(ld, c1, s0 + (uint64_t)t4, kd, rbl, first, &c);
+            }
+            if (!lead) {
+            } else if (ok) {
+                const bool hv = (h[0] >> 63) != 0;
+                const uint32_t clen = (uint32_t)(h[0] >> 32) & 0xFFFu;
+                if (!hv || clen > 8) h[1] = (uint32_t)s0;   // the writer reads the chrom, or tokenises, from the line
+                ST_MID(O.hdr + 2 * g, h[0]);
+                ST_MID(O.hdr + 2 * g + 1, h[1]);
+                if (hv) {
+                    Head hd;
+                    hd.clen = clen;
+                    hd.pos = (int32_t)(uint32_t)h[0];
+                    l = local_site_len(hd, c, g, LL.len1, LL);
+                } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
+                    l = local_site_len_text(text, c1, s0, c, g, LL);
+                }
+                if (l == 0) O.counts[g] = c;   // a fix-up site: the fix-up reads its counts
+            } else {
+                const unsigned long long k = atomicAdd(O.lb + 6, 1ull);
+                O.fb[k] = (uint32_t)g;
+                O.fbo[k] = (uint32_t)s0;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) l += __shfl_xor(l, off, 64);
+        if ((tid & 63u) == 0 && l)   // (the wave's lines: 64, or 16 with quads, in one writer block)
+            atomicAdd(LL.bsum + ((g_tile + j0 + (QUAD ? tid >> 2 : tid)) / FTB), (uint32_t)l);
+    }
+}
+
+// the general routine over the tile parse's leftovers (slot, line offset):
+// counts and a header pair with no chrom (the formatter tokenises the line),
+// the slot listed for its record length
+__global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restrict__ text, uint64_t len,
+                                                             const uint32_t* __restrict__ fb,
+                                                             const uint32_t* __restrict__ fbo,
+                                                             const unsigned long long* lb,
+                                                             uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
+                                                             unsigned long long* __restrict__ err,
+                                                             uint32_t* __restrict__ late, unsigned long long* nlate)
+{
+    __shared__ uint8_t cls[256];
+    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    __syncthreads();
+    const uint64_t m = lb[6];
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t g = fb[k];
+        const uint64_t s0 = fbo[k];
+        uint64_t c = 0;
+        parse_line_serial(text, len, s0, cls, &c, err, 0);
+        counts[g] = c;
+        hdr[2 * g] = 0;
+        hdr[2 * g + 1] = s0;
+        late[atomicAdd(nlate, 1ull)] = g;
+    }
+}
+
+// the record lengths of the general routine's slots
+__global__ __launch_bounds__(TB) void sid_tile_len_list_kernel(const char* __restrict__ text, uint64_t len,
+                                                               const uint64_t* __restrict__ hdr,
+                                                               const uint64_t* __restrict__ counts,
+                                                               const uint32_t* __restrict__ list,
+                                                               const unsigned long long* nlist, LocalLen LL)
+{
+    const uint64_t m = *nlist;
+    for (uint64_t j = (uint64_t)blockIdx.x * TB + threadIdx.x; j < m; j += (uint64_t)gridDim.x * TB) {
+        const uint32_t g = list[j];
+        Reader R{text, len};
+        const int l = local_site_len(slot_head(R, *(const ulonglong2*)(hdr + 2 * g)), counts[g], g, LL.len1, LL);
+        if (l) atomicAdd(LL.bsum + g / FTB, (uint32_t)l);
+    }
+}
+
 __global__ __launch_bounds__(FTB) void sid_local_len_kernel(const char* __restrict__ text, uint64_t len,
                                                            const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ hdr, uint64_t n,
@@ -1629,6 +1880,8 @@ __global__ __launch_bounds__(FTB) void sid_local_len_kernel(const char* __restri
     }
 }
 
+// SLOT: the tile parse's layout (site = slot, chrom and position by slot_head)
+template <bool SLOT>
 __global__ __launch_bounds__(TB) void sid_local_fixlen_kernel(const char* __restrict__ text, uint64_t len,
                                                              const sid_off_t* __restrict__ starts,
                                                              const uint64_t* __restrict__ hdr,
@@ -1649,8 +1902,9 @@ __global__ __launch_bounds__(TB) void sid_local_fixlen_kernel(const char* __rest
         hom[i] = h;
         het[i] = t;
         Reader R{text, len};
-        int l = record_len(site_head(R, starts + i, hdr + 2 * i), (uint8_t)c, sid_g6_prep(h), sid_g6_prep(t),
-                           ct.len);
+        const Head hd = SLOT ? slot_head(R, *(const ulonglong2*)(hdr + 2 * (uint64_t)i))
+                             : site_head(R, starts + i, hdr + 2 * i);
+        int l = record_len(hd, (uint8_t)c, sid_g6_prep(h), sid_g6_prep(t), ct.len);
         if (l < 0) {
             atomicExch(lb + 2, 1ull);
             l = 0;
@@ -1830,11 +2084,14 @@ __device__ __noinline__ void miss_put(const char* text, uint64_t len, Head h, ui
 }
 
 // CLS: the sites' class words from the fused parse (W->cls) stand in for
-// their counts (the entry and the bases come with the word)
+// their counts (the entry and the bases come with the word).  tcnt (the tile
+// parse's layout): n slots, slot i a site when i mod 2^cap_log2 is below its
+// tile's count, chrom and position by slot_head
 template <bool CLS>
 __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const char* __restrict__ text, uint64_t len,
                                                            const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ hdr, uint64_t n,
+                                                           const uint32_t* __restrict__ tcnt, uint32_t cap_log2,
                                                            const uint64_t* __restrict__ counts,
                                                            const uint32_t* __restrict__ cwords,
                                                            const char* __restrict__ str1,
@@ -1856,7 +2113,8 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     uint4 ea = make_uint4(0, 0, 0, 0), eb = ea;
     bool tab = false;
     uint8_t c = 0;
-    if (i < n) {
+    const bool site = i < n && (!tcnt || (uint32_t)(i & ((1u << cap_log2) - 1u)) < tcnt[i >> cap_log2]);
+    if (site) {
         uint32_t k;
         if (CLS) {
             const uint32_t w = cwords[i];
@@ -1873,7 +2131,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         // the Lynch writer, which looks the class up first, it pays)
         {
             Reader R{text, len};
-            h = site_head(R, starts + i, hdr + 2 * i);
+            h = tcnt ? slot_head(R, *(const ulonglong2*)(hdr + 2 * i)) : site_head(R, starts + i, hdr + 2 * i);
         }
         if (k != UINT32_MAX) {
             const uint4* e = (const uint4*)(k < SID_TAB_N ? str1 + (size_t)k * SID_STR_BYTES
@@ -3064,7 +3322,7 @@ int sid_chunk_local_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
         if (!W->lens_ready)   // (else the parse computed them: sid_parse_len_kernel)
             sid_local_len_kernel<<<grid, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, ctx->ws.len1,
                                                        ctx->ws.len2, W->bsum, miss, W->lb);
-        sid_local_fixlen_kernel<<<64, TB, 0, st>>>(base, c1, W->starts, W->hdr, W->counts, miss, W->lb, ctx->K,
+        sid_local_fixlen_kernel<false><<<64, TB, 0, st>>>(base, c1, W->starts, W->hdr, W->counts, miss, W->lb, ctx->K,
                                                    ctx->d_lnt, ct, W->code, W->hom, W->het, W->bsum, W->lb);
     }
     W->lens_ready = false;
@@ -3078,18 +3336,88 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
     CType ct;
     if (local_ctype(ctx, conf_type, &ct)) return SID_EINVAL;
     const uint64_t nb = (n + FTB - 1) / FTB;
+    if (W->tile_log2) {   // the tile parse's slots
+        const uint64_t nbs = (W->slots + FTB - 1) / FTB;
+        if (nbs == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
+                                 ? SID_OK : SID_EHIP;
+        sid_local_put_kernel<true><<<(unsigned)nbs, FTB, 0, st>>>(base, c1, nullptr, W->hdr, W->slots, W->tcnt,
+                                                                 W->tile_log2, W->counts, W->cls, ctx->ws.str1,
+                                                                 ctx->ws.str2, W->code, W->hom, W->het, ct, W->boff,
+                                                                 W->state, W->lb, out);
+        WCHECK(hipGetLastError());
+        return SID_OK;
+    }
     if (nb == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
                             ? SID_OK : SID_EHIP;
     if (W->cls_ready)
-        sid_local_put_kernel<true><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, W->cls,
+        sid_local_put_kernel<true><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0,
+                                                                W->counts, W->cls,
                                                                 ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
                                                                 ct, W->boff, W->state, W->lb, out);
     else
-        sid_local_put_kernel<false><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, W->counts, nullptr,
+        sid_local_put_kernel<false><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0,
+                                                                 W->counts, nullptr,
                                                                  ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
                                                                  ct, W->boff, W->state, W->lb, out);
     WCHECK(hipGetLastError());
     return SID_OK;
+}
+
+static uint64_t tile_count(uint64_t c0, uint64_t c1, bool quad)
+{
+    const uint64_t t0 = c0 & ~(uint64_t)15;
+    return c1 > c0 ? (c1 - t0 + tp_tile(quad) - 1) / tp_tile(quad) : 0;
+}
+
+uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap_log2, bool quad)
+{
+    return tile_count(c0, c1, quad) << cap_log2;
+}
+
+// a record is its chrom plus at most 64 bytes, and the chroms are bytes of
+// their lines (sid_chunk_fmt_bound), with at most every slot a site
+uint64_t sid_chunk_tile_bound(uint64_t c0, uint64_t c1, uint32_t cap_log2, bool quad)
+{
+    return sid_chunk_fmt_bound(sid_chunk_tile_slots(c0, c1, cap_log2, quad), c1 - c0);
+}
+
+int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
+                         uint32_t cap_log2, bool quad, const char* conf_type, hipStream_t st)
+{
+    CType ct;
+    if (local_ctype(ctx, conf_type, &ct)) return SID_EINVAL;
+    if (cap_log2 < SID_TILE_CAP_MIN || cap_log2 > SID_TILE_CAP_MAX) return SID_EINVAL;
+    if (c1 > UINT32_MAX) return SID_ELINE;   // line offsets are 32-bit: a line ran the chunk past 4 GiB
+    const uint64_t ntp = tile_count(c0, c1, quad);
+    const uint64_t slots = ntp << cap_log2;
+    if (slots > W->site_cap || ntp > W->tile_cap || slots >= (1ull << 32)) return SID_EINVAL;
+    W->lens_ready = false;
+    W->cls_ready = false;
+    W->tile_log2 = cap_log2;
+    W->slots = slots;
+    const uint64_t nb = (slots + FTB - 1) / FTB;
+    WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));   // [0] fix-up sites [1] bytes [2] range [3] sites [5] max lines [6] [7]
+    if (nb) WCHECK(hipMemsetAsync(W->bsum, 0, nb * 4, st));
+    if (ntp == 0) {
+        WCHECK(hipMemsetAsync(W->state + 4, 0xFF, sizeof(uint64_t), st));
+        return fmt_scan(W, nb, st);
+    }
+    uint32_t* late = W->fb + W->site_cap;
+    uint32_t* miss = W->fb + 2 * W->site_cap;
+    const LocalLen LL{ctx->ws.len1, ctx->ws.len2, W->bsum, miss, W->lb, W->cls};
+    const TileOut O{cap_log2, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
+    if (quad)
+        sid_tile_parse_kernel<true><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
+    else
+        sid_tile_parse_kernel<false><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
+    sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->counts, W->hdr,
+                                               (unsigned long long*)(W->state + 4), late, W->lb + 7);
+    sid_tile_len_list_kernel<<<64, TB, 0, st>>>(base, c1, W->hdr, W->counts, late, W->lb + 7, LL);
+    sid_local_fixlen_kernel<true><<<64, TB, 0, st>>>(base, c1, nullptr, W->hdr, W->counts, miss, W->lb, ctx->K,
+                                                     ctx->d_lnt, ct, W->code, W->hom, W->het, W->bsum, W->lb);
+    WCHECK(hipGetLastError());
+    W->cls_ready = true;
+    return fmt_scan(W, nb, st);
 }
 
 int sid_chunk_lynch_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st)

@@ -120,6 +120,15 @@ def test_shared_gpu_rehearsal_runs_the_node_cli():
     assert cli["devices"] == 2 and cli["sites"] == 600_000
     assert cli["cli_stats"]["sites"] == 600_000
     assert cli["sites_per_s_wall"] > 0
+    # per device: its GPU's PCI id and NUMA node, the CPUs its threads were
+    # bound to (none when the GPU's local CPUs are all this job has), and the
+    # NUMA node of its pinned host pages (run.cpp find_placement / on_node)
+    pl = cli["placement"]
+    assert len(pl) == 2 and all(p["pci"] and p["device"] == 0 for p in pl)
+    assert all(p["cpus"] == 0 or p["first_cpu"] >= 0 for p in pl)
+    # the same run through the runtime's pageable path (SID_UPLOAD_REGISTER=0)
+    assert cli["upload_pageable"]["cli_stats"]["chunks_registered"] == 0
+    assert cli["cli_stats"]["chunks_registered"] > 0
     # the whole node's CPU path beside it: the oracle over the same file, one
     # shard process per CPU the job may use
     import bench

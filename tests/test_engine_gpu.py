@@ -558,3 +558,33 @@ def test_line_past_the_chunk_limit_is_refused(sid):
     eng.close()
     del buf
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("extra", [[], ["--chunk-bytes", "100000", "--devices", "2"], ["--chunk-bytes", "33333"],
+                                   ["--host-hold", "1000000000", "--chunk-bytes", "250000"]],
+                         ids=["one-chunk", "100k-2dev", "33k", "host-arena"])
+def test_tile_parse_slot_caps(sid, oracle, tmp_path, extra):
+    """-m local's tile parse (textpath.hip sid_tile_parse_kernel) lays its
+    sites out in slots per 16 KiB tile, as many as the device's last chunk
+    needed (run.cpp tile_log2): runs of depth-0 lines (~20 B, ~800 lines a
+    tile: past the 256 slots 30x text takes, so a chunk runs again through
+    the two-pass path and the next ones get more slots), runs of 10-B lines
+    (more lines than the most slots a tile has: the two-pass path), lines of
+    3-5 KiB (past the tile's LDS halo: read from HBM), and 30x text between
+    them.  Every run's CSV is the oracle's."""
+    normal = sid.synth_text(61, 20_000, 30.0, sites_per_chrom=10 ** 6)
+    zero = b"".join(b"chr2\t%d\tA\t0\t*\t*\n" % i for i in range(1, 20_000))
+    tiny = b"".join(b"c\t%d\tA\t0\t*\n" % (i % 10) for i in range(1, 20_000))
+    rng = np.random.default_rng(61)
+    alphabet = np.frombuffer(b"ACGTacgt.,$", np.uint8)
+    longl = b"".join(b"chr3\t%d\tG\t900\t%s\t*\n" % (i, rng.choice(alphabet, 3000 + 7 * i).tobytes())
+                     for i in range(1, 300))
+    text = normal + zero + normal + tiny + normal + longl + normal
+    p = tmp_path / "caps.plp"
+    p.write_bytes(text)
+    b = oracle.run_cli([str(p)])
+    a = run(sid.CLI_PATH, extra + [str(p)])
+    assert b.returncode == 0
+    assert a.returncode == 0, a.stderr[-400:]
+    assert a.stdout == b.stdout
+    assert a.stderr == b.stderr
