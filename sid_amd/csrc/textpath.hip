@@ -1646,12 +1646,13 @@ __host__ __device__ constexpr uint32_t tp_tile(bool quad) { return (quad ? TP_RO
 
 struct TileOut {
     uint32_t cap_log2;          // slots per tile = 1 << cap_log2 (64 .. TP_CAP_MAX)
-    uint32_t* tcnt;             // per tile: its sites (at most the cap)
+    uint32_t* tcnt;             // per tile: its lines (above the cap: overflow; the writer takes the first cap)
     uint64_t* hdr;              // per slot: the header pair
     uint64_t* counts;           // per slot: counts of the fix-up's and the general routine's sites
     uint32_t* fb;               // the general routine's lines: slots,
     uint32_t* fbo;              // ... and line offsets
-    unsigned long long* lb;     // [3] sites, [5] max lines in a tile, [6] fallback count (zeroed before)
+    unsigned long long* lb;     // [6] fallback count (zeroed before); [3] sites and [5] the most lines in a
+                                //   tile from tcnt (sid_tile_serial_kernel)
     uint64_t* state;            // [4] the chunk's parse error key: none yet
 };
 
@@ -1738,11 +1739,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         nlines += (uint32_t)((tot[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
     }
     const uint32_t cnt = min(nlines, cap);
-    if (tid == 0) {
-        O.tcnt[t] = cnt;
-        if (cnt) atomicAdd(O.lb + 3, (unsigned long long)cnt);
-        atomicMax(O.lb + 5, (unsigned long long)nlines);
-    }
+    if (tid == 0) O.tcnt[t] = nlines;   // (no atomics on one address from every block: summed by the next kernel)
     __syncthreads();
     // ---- parse, one lane (a quad of lanes) per line, from LDS
     auto ld = [&](uint64_t a) -> uint4 {
@@ -1801,18 +1798,41 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
 
 // the general routine over the tile parse's leftovers (slot, line offset):
 // counts and a header pair with no chrom (the formatter tokenises the line),
-// the slot listed for its record length
+// the slot listed for its record length; and the tiles' line counts summed
+// (lb[3]: sites, the counts capped at the slots) and maxed (lb[5])
 __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restrict__ text, uint64_t len,
                                                              const uint32_t* __restrict__ fb,
                                                              const uint32_t* __restrict__ fbo,
-                                                             const unsigned long long* lb,
+                                                             unsigned long long* lb, const uint32_t* __restrict__ tcnt,
+                                                             uint64_t ntiles, uint32_t cap,
                                                              uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
                                                              unsigned long long* __restrict__ err,
                                                              uint32_t* __restrict__ late, unsigned long long* nlate)
 {
     __shared__ uint8_t cls[256];
+    __shared__ uint32_t red[2][TB / 64];
     if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
-    __syncthreads();
+    {
+        uint32_t sum = 0, mx = 0;
+        for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles;
+             t += (uint64_t)gridDim.x * blockDim.x) {
+            const uint32_t c = tcnt[t];
+            sum += min(c, cap);
+            mx = max(mx, c);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            sum += __shfl_xor(sum, off, 64);
+            mx = max(mx, (uint32_t)__shfl_xor(mx, off, 64));
+        }
+        if ((threadIdx.x & 63u) == 0) red[0][threadIdx.x >> 6] = sum, red[1][threadIdx.x >> 6] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < TB / 64; ++w) sum += red[0][w], mx = max(mx, red[1][w]);
+            if (sum) atomicAdd(lb + 3, (unsigned long long)sum);
+            if (mx) atomicMax(lb + 5, (unsigned long long)mx);
+        }
+    }
     const uint64_t m = lb[6];
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t g = fb[k];
@@ -3410,8 +3430,9 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
         sid_tile_parse_kernel<true><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
     else
         sid_tile_parse_kernel<false><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
-    sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->counts, W->hdr,
-                                               (unsigned long long*)(W->state + 4), late, W->lb + 7);
+    sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, 1u << cap_log2,
+                                               W->counts, W->hdr, (unsigned long long*)(W->state + 4), late,
+                                               W->lb + 7);
     sid_tile_len_list_kernel<<<64, TB, 0, st>>>(base, c1, W->hdr, W->counts, late, W->lb + 7, LL);
     sid_local_fixlen_kernel<true><<<64, TB, 0, st>>>(base, c1, nullptr, W->hdr, W->counts, miss, W->lb, ctx->K,
                                                      ctx->d_lnt, ct, W->code, W->hom, W->het, W->bsum, W->lb);
