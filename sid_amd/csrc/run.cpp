@@ -331,11 +331,11 @@ struct Dev {
         return p;
     }
     // the tile parse (sid_chunk_tile_local): its slots per tile for the next
-    // chunk (log2: the most lines a tile of the last chunk had, a sixteenth
-    // on top), its shape (a quad of lanes per line for lines over 256 B on
-    // average), and whether it takes the lines at all (at most
-    // 2^SID_TILE_CAP_MAX a tile)
-    uint32_t tile_log2 = 8;
+    // chunk (the most lines a tile of the last chunk had, a sixteenth on top,
+    // rounded up to 64), its shape (a quad of lanes per line for lines over
+    // 256 B on average), and whether it takes the lines at all (at most
+    // SID_TILE_CAP_MAX a tile)
+    uint32_t tile_cap = 320;
     bool tile_quad = false;
     bool tile_ok = true;
     uint64_t hold_budget = 0, retain_budget = 0;
@@ -1419,7 +1419,7 @@ void compute(sid_engine* e, Dev& d, int pass)
         bool tiled = false;
         if (x == hipSuccess && rc == SID_OK && format && !lynch_hist && !qmode && d.tile_ok &&
             e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx) && !(pass == 2 && r.pre)) {
-            const uint32_t lg = d.tile_log2;
+            const uint32_t lg = d.tile_cap;
             const bool quad = d.tile_quad;
             rc = sid_chunk_reserve(&W, tbytes, sid_chunk_tile_slots(L.c0, L.c1, lg, quad));
             if (rc != SID_OK) return (void)fail(e, rc);
@@ -1452,19 +1452,18 @@ void compute(sid_engine* e, Dev& d, int pass)
                     rc = sid_chunk_local_put(d.ctx, &W, L.base, L.c1, 0, e->conf_type, out, d.s_comp);
                     d.prof_end(5, pe);
                 }
-                W.tile_log2 = 0;   // (the workspace's dense layout again for the two-pass path)
+                W.slot_cap = 0;   // (the workspace's dense layout again for the two-pass path)
                 if (rc != SID_OK) return (void)fail(e, rc);
                 // bytes, range flag, sites, parse error key, the most lines in a tile
                 x = hipMemcpyAsync(hs + 8, W.lb + 1, 5 * 8, hipMemcpyDeviceToHost, d.s_comp);
                 if (x == hipSuccess) x = sync();
                 if (x != hipSuccess) return (void)hipfail(e, x);
                 const uint64_t maxl = hs[12];
-                auto log2_up = [](uint64_t v) {
-                    uint32_t k = 0;
-                    while ((1ull << k) < v) ++k;
-                    return k;
+                auto cap_for = [](uint64_t lines) {
+                    return (uint32_t)std::min<uint64_t>(SID_TILE_CAP_MAX,
+                                                        std::max<uint64_t>(SID_TILE_CAP_MIN, (lines + 63) & ~63ull));
                 };
-                if (maxl <= (1ull << lg)) {
+                if (maxl <= lg) {
                     tiled = true;
                     n = hs[10];
                     r.parsed = n;
@@ -1473,17 +1472,17 @@ void compute(sid_engine* e, Dev& d, int pass)
                     // chunk's lines per byte, a quarter on top)
                     const bool q2 = L.c1 - L.c0 > 256 * n;
                     const uint64_t want = q2 == quad ? maxl + maxl / 16 + 1
-                                                     : (uint64_t)((double)n * (q2 ? 24576 : 16384) /
+                                                     : (uint64_t)((double)n * (q2 ? 24576 : 20480) /
                                                                   (double)std::max<uint64_t>(1, L.c1 - L.c0) * 1.25) + 1;
                     d.tile_quad = q2;
-                    d.tile_log2 = std::min(SID_TILE_CAP_MAX, std::max(SID_TILE_CAP_MIN, log2_up(want)));
+                    d.tile_cap = cap_for(want);
                 } else {
                     if (cap) d.pool.put(out, cap, d.s_comp);
                     out = nullptr;
                     cap = 0;
                     via_host = sunk = false;
-                    d.tile_log2 = std::min(SID_TILE_CAP_MAX, log2_up(maxl));
-                    d.tile_ok = maxl <= (1ull << SID_TILE_CAP_MAX);
+                    d.tile_cap = cap_for(maxl + maxl / 16 + 1);
+                    d.tile_ok = maxl <= SID_TILE_CAP_MAX;
                 }
             }
         }

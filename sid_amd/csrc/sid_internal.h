@@ -165,8 +165,8 @@ struct sid_chunk_ws {
     unsigned long long* lb = nullptr;   // formatter flags and totals (sid_chunk_fmt_len)
     uint64_t* state = nullptr;    // [0] sites [1..2] parse range [3] CSV bytes [4] first error key [5] range flag
                                   // [6] [7] fallback lines
-    uint32_t tile_log2 = 0;       // 0: sites in file order (index + parse); else the tile parse's layout: slots
-    uint64_t slots = 0;           // of 2^tile_log2 per tile, `slots` of them (sid_chunk_tile_local)
+    uint32_t slot_cap = 0;        // 0: sites in file order (index + parse); else the tile parse's layout: slots
+    uint64_t slots = 0;           // of slot_cap per tile, `slots` of them (sid_chunk_tile_local)
 };
 int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites);
 void sid_chunk_release(sid_chunk_ws* W);
@@ -193,20 +193,20 @@ int sid_chunk_local_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
 int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n,
                         const char* conf_type, char* out, hipStream_t st);
 // -m local (sid_chunk_local_ok) in one pass over the text: the tile parse of
-// [c0, c1) with 2^cap_log2 slots per tile (SID_TILE_CAP_MIN .. _MAX), the
+// [c0, c1) with cap slots per tile (a multiple of 64, SID_TILE_CAP_MIN .. _MAX), the
 // record lengths, the fix-up and the writer's offsets; sid_chunk_local_put
 // then writes the records into a buffer of sid_chunk_tile_bound.  No host
 // round trip inside.  Afterwards lb[1] bytes, lb[2] range flag, lb[3] sites,
 // lb[4] the parse error key (after the put), lb[5] the most lines in one tile:
 // above the cap the chunk's results are void (run it again with a larger cap,
 // or through sid_chunk_index + sid_chunk_parse).  quad: 24 KiB tiles and a
-// quad of lanes per line (lines over 256 B on average), else 16 KiB tiles and
+// quad of lanes per line (lines over 256 B on average), else 20 KiB tiles and
 // a lane per line.
-constexpr uint32_t SID_TILE_CAP_MIN = 6, SID_TILE_CAP_MAX = 10;   // log2 slots per tile
-uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap_log2, bool quad);
-uint64_t sid_chunk_tile_bound(uint64_t c0, uint64_t c1, uint32_t cap_log2, bool quad);
-int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
-                         uint32_t cap_log2, bool quad, const char* conf_type, hipStream_t st);
+constexpr uint32_t SID_TILE_CAP_MIN = 64, SID_TILE_CAP_MAX = 1024;   // slots per tile
+uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap, bool quad);
+uint64_t sid_chunk_tile_bound(uint64_t c0, uint64_t c1, uint32_t cap, bool quad);
+int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint32_t cap,
+                         bool quad, const char* conf_type, hipStream_t st);
 // likelihood_ratio / bayes fused with the class lookup (sid_lynch_fmt_view)
 int sid_chunk_lynch_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st);
 int sid_chunk_lynch_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, char* out,

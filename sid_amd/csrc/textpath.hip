@@ -754,18 +754,19 @@ __device__ __forceinline__ uint32_t rb_window(const uint4 v, uint32_t valid, int
 // (global memory, or the tile parse's LDS copy).  (The next windows from the
 // per-line parse's stage too, where its 48 staged bytes hold them, measured
 // slower: the loads hit the caches already)
-template <class Ld>
-__device__ __forceinline__ bool read_bases_lut(Ld ld, uint64_t len, uint64_t q, uint32_t kd, const uint32_t* lut,
+// (Off: the offsets' type -- 32-bit for the tile parse's offsets from its tile)
+template <class Ld, class Off = uint64_t>
+__device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t kd, const uint32_t* lut,
                                                const uint4* first, uint64_t* out)
 {
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
-    uint64_t a = q & ~(uint64_t)15;
+    Off a = q & ~(Off)15;
     uint32_t carry = 0;   // bit 7: byte 0 of the next word is skipped
     bool done = false, bad = false;
     uint4 vn = ld(a + 16);   // the next window in flight while the first is counted
     uint32_t acc = 0;
     auto masked = [&](const uint4& v, uint32_t lead) {
-        const int room = len > a ? (int)min(len - a, (uint64_t)16) : 0;
+        const int room = len > a ? (int)min(len - a, (Off)16) : 0;
         const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
         return rb_window<true>(v, valid, room, lut, done, carry, bad);
     };
@@ -803,20 +804,20 @@ __device__ __forceinline__ bool read_bases_lut(Ld ld, uint64_t len, uint64_t q, 
 // skipped is a '^' run, which fails in that lane); the token ends in the
 // quad's first window holding its end, and the windows after it are dropped.
 // Every lane of the quad returns the same result.
-template <class Ld>
-__device__ __forceinline__ bool read_bases_quad(Ld ld, uint64_t len, uint64_t q, uint32_t kd, const uint32_t* lut,
+template <class Ld, class Off = uint64_t>
+__device__ __forceinline__ bool read_bases_quad(Ld ld, Off len, Off q, uint32_t kd, const uint32_t* lut,
                                                 const uint4* first, uint64_t* out)
 {
     const uint32_t j = threadIdx.x & 3u;
-    const uint64_t a0 = q & ~(uint64_t)15;
+    const Off a0 = q & ~(Off)15;
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0, acc = 0;
     bool bad = false;
     uint32_t prev3 = 0;   // lane 3's last byte was a '^' (the previous step's window 4(it-1)+3)
     for (uint32_t it = 0;; ++it) {   // uniform across the quad
         const uint32_t k = 4u * it + j;
-        const uint64_t a = a0 + 16ull * k;
+        const Off a = a0 + (Off)16 * k;
         const uint4 v = k == 0 ? *first : ld(a);   // (past the line's end: the readable padding)
-        const int room = len > a ? (int)min(len - a, (uint64_t)16) : 0;
+        const int room = len > a ? (int)min(len - a, (Off)16) : 0;
         const uint32_t lead = k == 0 ? (uint32_t)(q & 15) : 0u;
         const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
         const uint32_t last_caret = (v.w >> 24) == 0x5Eu ? 1u : 0u;
@@ -1634,18 +1635,19 @@ __global__ __launch_bounds__(TB) void sid_local_len_list_kernel(const char* __re
 // The header pair's second word holds the chrom's first 8 bytes when the
 // pair is valid and the chrom at most 8 bytes long, else the line's offset
 // (slot_head): the writer never needs a line offset array.
-// Two shapes: 16 KiB tiles with a lane per line (30x: ~200 lines of ~81 B
-// per tile), and 24 KiB tiles with a quad of lanes per line (200x: ~58 lines
-// of ~426 B, 232 lanes; read_bases_quad, each quad reading 64 consecutive
-// bytes a step).
-constexpr uint32_t TP_ROWS = 4;                 // (the lane-per-line shape)
+// Two shapes: 20 KiB tiles with a lane per line (30x: ~253 lines of ~81 B
+// per tile: one round of the block's 256 lanes, a few lines of a second now
+// and then; 16 KiB tiles, ~202 lines, left a fifth of the lanes idle), and
+// 24 KiB tiles with a quad of lanes per line (200x: ~58 lines of ~426 B, 232
+// lanes; read_bases_quad, each quad reading 64 consecutive bytes a step).
+constexpr uint32_t TP_ROWS = 5;                 // (the lane-per-line shape: ~253 lines a tile, one round of 256 lanes)
 constexpr uint32_t TP_ROWS_QUAD = 6;
 constexpr uint32_t TP_HALO = 1024;
 constexpr uint32_t TP_CAP_MAX = 1024;           // slots per tile at most (lines of 16 B on average)
 __host__ __device__ constexpr uint32_t tp_tile(bool quad) { return (quad ? TP_ROWS_QUAD : TP_ROWS) * TILE; }
 
 struct TileOut {
-    uint32_t cap_log2;          // slots per tile = 1 << cap_log2 (64 .. TP_CAP_MAX)
+    uint32_t cap;               // slots per tile (a multiple of 64, 64 .. TP_CAP_MAX)
     uint32_t* tcnt;             // per tile: its lines (above the cap: overflow; the writer takes the first cap)
     uint64_t* hdr;              // per slot: the header pair
     uint64_t* counts;           // per slot: counts of the fix-up's and the general routine's sites
@@ -1689,12 +1691,15 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     if (blockIdx.x == 0 && tid == 0) O.state[4] = ~0ull;   // no parse error yet
     const uint64_t t = blockIdx.x;
     const uint64_t g0 = tile_base + t * TP_TILE;           // the tile's first byte (16-B aligned)
+    // a tile inside the chunk (all but its first and last): no window needs
+    // the chunk's bounds (block-uniform)
+    const bool inner = g0 > c0 && g0 + TP_TILE <= c1;
     // ---- load (windows at or past the chunk's end read as zeros)
     uint4 v[ROWS];
 #pragma unroll
     for (uint32_t k = 0; k < ROWS; ++k) {
         const uint64_t at = g0 + k * TILE + tid * 16;
-        v[k] = at < c1 ? ld_nt(text + at) : make_uint4(0, 0, 0, 0);
+        v[k] = (inner || at < c1) ? ld_nt(text + at) : make_uint4(0, 0, 0, 0);
         *(uint4*)(tl + k * TILE + tid * 16) = v[k];
     }
     if (tid < TP_HALO / 16) {
@@ -1716,12 +1721,14 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
                             (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
         const uint32_t prev = (k == 0 && tid == 0) ? prev0 : (uint32_t)(tl[max(k * TILE + tid * 16, 1u) - 1] == '\n');
         uint32_t mk = ((nl << 1) | prev) & ~nl & 0xFFFFu;
-        if (at + 16 > c0 && at <= c0) {   // c0 in this window: it starts a line (unless a '\n'), nothing before it does
-            const uint32_t j = (uint32_t)(c0 - at);
-            mk = (mk | ((1u << j) & ~nl)) & ~((1u << j) - 1u);
+        if (!inner) {
+            if (at + 16 > c0 && at <= c0) {   // c0 in this window: it starts a line (unless a '\n'), nothing before it does
+                const uint32_t j = (uint32_t)(c0 - at);
+                mk = (mk | ((1u << j) & ~nl)) & ~((1u << j) - 1u);
+            }
+            if (at + 16 > c1) mk &= c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
+            if (at + 16 <= c0) mk = 0;
         }
-        if (at + 16 > c1) mk &= c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
-        if (at + 16 <= c0) mk = 0;
         m[k] = mk;
         packed[k / 4] |= (uint64_t)__popc(mk) << (16 * (k % 4));
     }
@@ -1729,7 +1736,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     uint64_t tot[2] = {0, 0}, pre[2] = {0, 0};
     pre[0] = block_exscan64(packed[0], &tot[0]);
     if (ROWS > 4) pre[1] = block_exscan64(packed[1], &tot[1]);
-    const uint32_t cap = 1u << O.cap_log2;
+    const uint32_t cap = O.cap;
     uint32_t nlines = 0;
 #pragma unroll
     for (uint32_t k = 0; k < ROWS; ++k) {
@@ -1741,12 +1748,17 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     const uint32_t cnt = min(nlines, cap);
     if (tid == 0) O.tcnt[t] = nlines;   // (no atomics on one address from every block: summed by the next kernel)
     __syncthreads();
-    // ---- parse, one lane (a quad of lanes) per line, from LDS
-    auto ld = [&](uint64_t a) -> uint4 {
-        const uint64_t r = a - g0;
-        return r + 16 <= TP_TILE + TP_HALO ? *(const uint4*)(tl + r) : *(const uint4*)(text + a);
+    // ---- parse, one lane (a quad of lanes) per line, from LDS; offsets
+    // from the tile's first byte (32 bits: a chunk spans less than 4 GiB)
+    const char* gtile = text + g0;
+    // (the global load non-temporal: two loads of a kind would be merged into
+    // one generic-address (flat) load of a selected pointer, the LDS reads too)
+    auto ld = [&](uint32_t r) -> uint4 {
+        if (r <= TP_TILE + TP_HALO - 16) return *(const uint4*)(tl + r);
+        return ld_nt(gtile + r);   // (a line running past the halo)
     };
-    const uint64_t g_tile = t << O.cap_log2;
+    const uint32_t len_t = (uint32_t)(c1 - g0);   // the chunk's end
+    const uint64_t g_tile = t * (uint64_t)cap;
     for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
         const uint32_t j = j0 + (QUAD ? tid >> 2 : tid);
         const bool lead = !QUAD || (tid & 3u) == 0;   // the lane that writes the line's outputs
@@ -1760,12 +1772,12 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             const uint4 v0 = *(const uint4*)stage, v1 = *(const uint4*)(stage + 16), v2 = *(const uint4*)(stage + 32);
             uint64_t c = 0, h[2] = {0, 0};
             uint32_t kd = 0;
-            const int t4 = parse_header(v0, v1, v2, stage, sh, c1 - s0, cls, h, &kd);
+            const int t4 = parse_header(v0, v1, v2, stage, sh, len_t - r0, cls, h, &kd);
             bool ok = t4 >= 0;
             if (ok) {
                 const uint4* first = (const uint4*)(stage + ((sh + (uint32_t)t4) & 0x30u));
-                ok = QUAD ? read_bases_quad(ld, c1, s0 + (uint64_t)t4, kd, rbl, first, &c)
-                          : read_bases_lut(ld, c1, s0 + (uint64_t)t4, kd, rbl, first, &c);
+                ok = QUAD ? read_bases_quad<decltype(ld), uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c)
+                          : read_bases_lut<decltype(ld), uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c);
             }
             if (!lead) {
             } else if (ok) {
@@ -2111,7 +2123,8 @@ template <bool CLS>
 __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const char* __restrict__ text, uint64_t len,
                                                            const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ hdr, uint64_t n,
-                                                           const uint32_t* __restrict__ tcnt, uint32_t cap_log2,
+                                                           const uint32_t* __restrict__ tcnt, uint32_t cap,
+                                                           uint64_t cap_magic,
                                                            const uint64_t* __restrict__ counts,
                                                            const uint32_t* __restrict__ cwords,
                                                            const char* __restrict__ str1,
@@ -2133,7 +2146,11 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     uint4 ea = make_uint4(0, 0, 0, 0), eb = ea;
     bool tab = false;
     uint8_t c = 0;
-    const bool site = i < n && (!tcnt || (uint32_t)(i & ((1u << cap_log2) - 1u)) < tcnt[i >> cap_log2]);
+    bool site = i < n;
+    if (tcnt && site) {   // slot i = tile * cap + j: a site when j is below the tile's count
+        const uint64_t t = __umul64hi(i, cap_magic);   // i / cap (cap_magic = ceil(2^64 / cap), i < 2^32)
+        site = (uint32_t)(i - t * cap) < tcnt[t];
+    }
     if (site) {
         uint32_t k;
         if (CLS) {
@@ -3356,12 +3373,13 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
     CType ct;
     if (local_ctype(ctx, conf_type, &ct)) return SID_EINVAL;
     const uint64_t nb = (n + FTB - 1) / FTB;
-    if (W->tile_log2) {   // the tile parse's slots
+    if (W->slot_cap) {   // the tile parse's slots
         const uint64_t nbs = (W->slots + FTB - 1) / FTB;
         if (nbs == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
                                  ? SID_OK : SID_EHIP;
+        const uint64_t magic = ~0ull / W->slot_cap + 1;   // ceil(2^64 / cap) (cap: a multiple of 64, not a power of 2)
         sid_local_put_kernel<true><<<(unsigned)nbs, FTB, 0, st>>>(base, c1, nullptr, W->hdr, W->slots, W->tcnt,
-                                                                 W->tile_log2, W->counts, W->cls, ctx->ws.str1,
+                                                                 W->slot_cap, magic, W->counts, W->cls, ctx->ws.str1,
                                                                  ctx->ws.str2, W->code, W->hom, W->het, ct, W->boff,
                                                                  W->state, W->lb, out);
         WCHECK(hipGetLastError());
@@ -3370,12 +3388,12 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
     if (nb == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
                             ? SID_OK : SID_EHIP;
     if (W->cls_ready)
-        sid_local_put_kernel<true><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0,
+        sid_local_put_kernel<true><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0, 0,
                                                                 W->counts, W->cls,
                                                                 ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
                                                                 ct, W->boff, W->state, W->lb, out);
     else
-        sid_local_put_kernel<false><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0,
+        sid_local_put_kernel<false><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0, 0,
                                                                  W->counts, nullptr,
                                                                  ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
                                                                  ct, W->boff, W->state, W->lb, out);
@@ -3389,31 +3407,31 @@ static uint64_t tile_count(uint64_t c0, uint64_t c1, bool quad)
     return c1 > c0 ? (c1 - t0 + tp_tile(quad) - 1) / tp_tile(quad) : 0;
 }
 
-uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap_log2, bool quad)
+uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap, bool quad)
 {
-    return tile_count(c0, c1, quad) << cap_log2;
+    return tile_count(c0, c1, quad) * cap;
 }
 
 // a record is its chrom plus at most 64 bytes, and the chroms are bytes of
 // their lines (sid_chunk_fmt_bound), with at most every slot a site
-uint64_t sid_chunk_tile_bound(uint64_t c0, uint64_t c1, uint32_t cap_log2, bool quad)
+uint64_t sid_chunk_tile_bound(uint64_t c0, uint64_t c1, uint32_t cap, bool quad)
 {
-    return sid_chunk_fmt_bound(sid_chunk_tile_slots(c0, c1, cap_log2, quad), c1 - c0);
+    return sid_chunk_fmt_bound(sid_chunk_tile_slots(c0, c1, cap, quad), c1 - c0);
 }
 
-int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1,
-                         uint32_t cap_log2, bool quad, const char* conf_type, hipStream_t st)
+int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint32_t cap,
+                         bool quad, const char* conf_type, hipStream_t st)
 {
     CType ct;
     if (local_ctype(ctx, conf_type, &ct)) return SID_EINVAL;
-    if (cap_log2 < SID_TILE_CAP_MIN || cap_log2 > SID_TILE_CAP_MAX) return SID_EINVAL;
+    if (cap < SID_TILE_CAP_MIN || cap > SID_TILE_CAP_MAX || cap % 64) return SID_EINVAL;
     if (c1 > UINT32_MAX) return SID_ELINE;   // line offsets are 32-bit: a line ran the chunk past 4 GiB
     const uint64_t ntp = tile_count(c0, c1, quad);
-    const uint64_t slots = ntp << cap_log2;
+    const uint64_t slots = ntp * cap;
     if (slots > W->site_cap || ntp > W->tile_cap || slots >= (1ull << 32)) return SID_EINVAL;
     W->lens_ready = false;
     W->cls_ready = false;
-    W->tile_log2 = cap_log2;
+    W->slot_cap = cap;
     W->slots = slots;
     const uint64_t nb = (slots + FTB - 1) / FTB;
     WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));   // [0] fix-up sites [1] bytes [2] range [3] sites [5] max lines [6] [7]
@@ -3425,12 +3443,12 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
     uint32_t* late = W->fb + W->site_cap;
     uint32_t* miss = W->fb + 2 * W->site_cap;
     const LocalLen LL{ctx->ws.len1, ctx->ws.len2, W->bsum, miss, W->lb, W->cls};
-    const TileOut O{cap_log2, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
+    const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
     if (quad)
         sid_tile_parse_kernel<true><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
     else
         sid_tile_parse_kernel<false><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
-    sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, 1u << cap_log2,
+    sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap,
                                                W->counts, W->hdr, (unsigned long long*)(W->state + 4), late,
                                                W->lb + 7);
     sid_tile_len_list_kernel<<<64, TB, 0, st>>>(base, c1, W->hdr, W->counts, late, W->lb + 7, LL);
