@@ -331,11 +331,11 @@ struct Dev {
         return p;
     }
     // the tile parse (sid_chunk_tile_local): its slots per tile for the next
-    // chunk (the most lines a tile of the last chunk had, a sixteenth on top,
-    // rounded up to 64), its shape (a quad of lanes per line for lines over
+    // chunk (the most lines a tile of the last chunk had, a thirty-second on
+    // top, rounded up to 32), its shape (a quad of lanes per line for lines over
     // 256 B on average), and whether it takes the lines at all (at most
     // SID_TILE_CAP_MAX a tile)
-    uint32_t tile_cap = 320;
+    uint32_t tile_cap = 288;
     bool tile_quad = false;
     bool tile_ok = true;
     uint64_t hold_budget = 0, retain_budget = 0;
@@ -1461,7 +1461,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                 const uint64_t maxl = hs[12];
                 auto cap_for = [](uint64_t lines) {
                     return (uint32_t)std::min<uint64_t>(SID_TILE_CAP_MAX,
-                                                        std::max<uint64_t>(SID_TILE_CAP_MIN, (lines + 63) & ~63ull));
+                                                        std::max<uint64_t>(SID_TILE_CAP_MIN, (lines + 31) & ~31ull));
                 };
                 if (maxl <= lg) {
                     tiled = true;
@@ -1471,7 +1471,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                     // the next chunk's shape and slots (a new shape: from this
                     // chunk's lines per byte, a quarter on top)
                     const bool q2 = L.c1 - L.c0 > 256 * n;
-                    const uint64_t want = q2 == quad ? maxl + maxl / 16 + 1
+                    const uint64_t want = q2 == quad ? maxl + maxl / 32 + 2
                                                      : (uint64_t)((double)n * (q2 ? 24576 : 20480) /
                                                                   (double)std::max<uint64_t>(1, L.c1 - L.c0) * 1.25) + 1;
                     d.tile_quad = q2;
@@ -1481,7 +1481,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                     out = nullptr;
                     cap = 0;
                     via_host = sunk = false;
-                    d.tile_cap = cap_for(maxl + maxl / 16 + 1);
+                    d.tile_cap = cap_for(maxl + maxl / 32 + 2);
                     d.tile_ok = maxl <= SID_TILE_CAP_MAX;
                 }
             }

@@ -1647,7 +1647,7 @@ constexpr uint32_t TP_CAP_MAX = 1024;           // slots per tile at most (lines
 __host__ __device__ constexpr uint32_t tp_tile(bool quad) { return (quad ? TP_ROWS_QUAD : TP_ROWS) * TILE; }
 
 struct TileOut {
-    uint32_t cap;               // slots per tile (a multiple of 64, 64 .. TP_CAP_MAX)
+    uint32_t cap;               // slots per tile (a multiple of 32, SID_TILE_CAP_MIN .. _MAX)
     uint32_t* tcnt;             // per tile: its lines (above the cap: overflow; the writer takes the first cap)
     uint64_t* hdr;              // per slot: the header pair
     uint64_t* counts;           // per slot: counts of the fix-up's and the general routine's sites
@@ -1801,10 +1801,17 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
                 O.fbo[k] = (uint32_t)s0;
             }
         }
+        // the record bytes into the writer blocks' sums: the wave's slots (64,
+        // or 16 with quads, from a multiple of 16) lie in one block or two
+        const uint64_t gw = (g_tile + j0 + (QUAD ? (tid & ~63u) >> 2 : (tid & ~63u))) / FTB;
+        int lo = (g_tile + j) / FTB == gw ? l : 0, hi = l - lo;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) l += __shfl_xor(l, off, 64);
-        if ((tid & 63u) == 0 && l)   // (the wave's lines: 64, or 16 with quads, in one writer block)
-            atomicAdd(LL.bsum + ((g_tile + j0 + (QUAD ? tid >> 2 : tid)) / FTB), (uint32_t)l);
+        for (int off = 32; off > 0; off >>= 1) {
+            lo += __shfl_xor(lo, off, 64);
+            hi += __shfl_xor(hi, off, 64);
+        }
+        if ((tid & 63u) == 0 && lo) atomicAdd(LL.bsum + gw, (uint32_t)lo);
+        if ((tid & 63u) == 0 && hi) atomicAdd(LL.bsum + gw + 1, (uint32_t)hi);
     }
 }
 
@@ -3377,7 +3384,7 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
         const uint64_t nbs = (W->slots + FTB - 1) / FTB;
         if (nbs == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
                                  ? SID_OK : SID_EHIP;
-        const uint64_t magic = ~0ull / W->slot_cap + 1;   // ceil(2^64 / cap) (cap: a multiple of 64, not a power of 2)
+        const uint64_t magic = ~0ull / W->slot_cap + 1;   // ceil(2^64 / cap) (cap: a multiple of 32, not a power of 2)
         sid_local_put_kernel<true><<<(unsigned)nbs, FTB, 0, st>>>(base, c1, nullptr, W->hdr, W->slots, W->tcnt,
                                                                  W->slot_cap, magic, W->counts, W->cls, ctx->ws.str1,
                                                                  ctx->ws.str2, W->code, W->hom, W->het, ct, W->boff,
@@ -3424,7 +3431,7 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
 {
     CType ct;
     if (local_ctype(ctx, conf_type, &ct)) return SID_EINVAL;
-    if (cap < SID_TILE_CAP_MIN || cap > SID_TILE_CAP_MAX || cap % 64) return SID_EINVAL;
+    if (cap < SID_TILE_CAP_MIN || cap > SID_TILE_CAP_MAX || cap % 32) return SID_EINVAL;
     if (c1 > UINT32_MAX) return SID_ELINE;   // line offsets are 32-bit: a line ran the chunk past 4 GiB
     const uint64_t ntp = tile_count(c0, c1, quad);
     const uint64_t slots = ntp * cap;
