@@ -2154,14 +2154,20 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     bool tab = false;
     uint8_t c = 0;
     bool site = i < n;
+    // the slot's class word and header pair loaded beside its tile's count
+    // (a slot that holds no site: allocated, its words never used)
+    uint32_t w0 = 0;
+    ulonglong2 hw0 = make_ulonglong2(0, 0);
     if (tcnt && site) {   // slot i = tile * cap + j: a site when j is below the tile's count
+        if (CLS) w0 = cwords[i];
+        hw0 = *(const ulonglong2*)(hdr + 2 * i);
         const uint64_t t = __umul64hi(i, cap_magic);   // i / cap (cap_magic = ceil(2^64 / cap), i < 2^32)
         site = (uint32_t)(i - t * cap) < tcnt[t];
     }
     if (site) {
         uint32_t k;
         if (CLS) {
-            const uint32_t w = cwords[i];
+            const uint32_t w = tcnt ? w0 : cwords[i];
             k = w == SID_CLS_MISS ? UINT32_MAX : w & 0xFFFFFu;
             f = (w >> 28) & 3u;
             s = w >> 30;
@@ -2175,7 +2181,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         // the Lynch writer, which looks the class up first, it pays)
         {
             Reader R{text, len};
-            h = tcnt ? slot_head(R, *(const ulonglong2*)(hdr + 2 * i)) : site_head(R, starts + i, hdr + 2 * i);
+            h = tcnt ? slot_head(R, hw0) : site_head(R, starts + i, hdr + 2 * i);
         }
         if (k != UINT32_MAX) {
             const uint4* e = (const uint4*)(k < SID_TAB_N ? str1 + (size_t)k * SID_STR_BYTES
