@@ -754,6 +754,41 @@ __device__ __forceinline__ uint32_t rb_window(const uint4 v, uint32_t valid, int
 // (global memory, or the tile parse's LDS copy).  (The next windows from the
 // per-line parse's stage too, where its 48 staged bytes hold them, measured
 // slower: the loads hit the caches already)
+// rb_window over the window's 16-bit masks: the token-end and '^' bytes of
+// the four words compressed to 16 bits once, the window's logic (end, skip,
+// '^' runs, carry) on those, the bytes to count expanded back per word for
+// the table.  (A/B against the per-word form: SID_RB16.)
+#ifndef SID_RB16
+#define SID_RB16 0
+#endif
+template <bool MASKED>
+__device__ __forceinline__ uint32_t rb_window16(const uint4 v, uint32_t valid, int room, const uint32_t* lut,
+                                                bool& done, uint32_t& carry, bool& bad)
+{
+    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t L = compress8(low_bytes(ws[0]), low_bytes(ws[1])) |
+                       (compress8(low_bytes(ws[2]), low_bytes(ws[3])) << 8);
+    const uint32_t C = compress8(eq_bytes(ws[0], 0x5E5E5E5Eu), eq_bytes(ws[1], 0x5E5E5E5Eu)) |
+                       (compress8(eq_bytes(ws[2], 0x5E5E5E5Eu), eq_bytes(ws[3], 0x5E5E5E5Eu)) << 8);
+    uint32_t vm = done ? 0u : (MASKED ? valid : 0xFFFFu);
+    const uint32_t lo = L & vm;
+    const uint32_t first = lo & (0u - lo);      // the token's end, if in this window
+    vm &= first - 1u;                           // bytes before it (all if none)
+    done = done || first != 0 || (MASKED && room < 16);
+    const uint32_t caret = C & vm;
+    const uint32_t skip = ((caret << 1) | carry) & vm;
+    bad = bad || (caret & skip) != 0;           // '^' run
+    carry = (caret >> 15) & 1u;
+    const uint32_t cm = (vm | first) & ~skip;   // the bytes looked up
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t bm = (__umul24((cm >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) * 0xFFu;
+        acc += rb_word(lut, ws[k] & bm);
+    }
+    return acc;
+}
+
 // (Off: the offsets' type -- 32-bit for the tile parse's offsets from its tile)
 template <class Ld, class Off = uint64_t>
 __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t kd, const uint32_t* lut,
@@ -768,7 +803,11 @@ __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t k
     auto masked = [&](const uint4& v, uint32_t lead) {
         const int room = len > a ? (int)min(len - a, (Off)16) : 0;
         const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
+#if SID_RB16
+        return rb_window16<true>(v, valid, room, lut, done, carry, bad);
+#else
         return rb_window<true>(v, valid, room, lut, done, carry, bad);
+#endif
     };
     auto add = [&](uint32_t w) {
         nA += w & 31u;
@@ -783,7 +822,11 @@ __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t k
     while (!done) {
         const uint4 v = vn;
         vn = ld(a + 16);
+#if SID_RB16
+        add(a + 16 <= len ? rb_window16<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u));
+#else
         add(a + 16 <= len ? rb_window<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u));
+#endif
         a += 16;
     }
     if (bad || (acc >> RB_BAD_SHIFT) != 0) return false;
