@@ -1486,6 +1486,73 @@ void compute(sid_engine* e, Dev& d, int pass)
                 }
             }
         }
+        // The Lynch paths' first pass likewise: the tile parse into every
+        // site's counts and header pair, compacted into the buffer kept for
+        // pass 2 (the two-pass parse's layout), then the histogram.  Without
+        // room for that buffer (the retain budget), the two-pass path below
+        // (pass 2 then indexes and parses the text again).
+        if (!tiled && x == hipSuccess && rc == SID_OK && lynch_hist && !qmode && d.tile_ok) {
+            const uint32_t cp = d.tile_cap;
+            const bool quad = d.tile_quad;
+            rc = sid_chunk_reserve(&W, tbytes, sid_chunk_tile_slots(L.c0, L.c1, cp, quad));
+            if (rc != SID_OK) return (void)fail(e, rc);
+            pe = d.prof_begin(P);
+            rc = sid_chunk_tile_counts(&W, L.base, L.c0, L.c1, cp, quad, d.s_comp);
+            if (rc != SID_OK) return (void)fail(e, rc);
+            x = hipMemcpyAsync(hs, W.state, 8, hipMemcpyDeviceToHost, d.s_comp);   // sites
+            if (x == hipSuccess) x = hipMemcpyAsync(hs + 4, W.state + 4, 8, hipMemcpyDeviceToHost, d.s_comp);
+            if (x == hipSuccess) x = hipMemcpyAsync(hs + 12, W.lb + 5, 8, hipMemcpyDeviceToHost, d.s_comp);
+            if (x == hipSuccess) x = sync();
+            if (x != hipSuccess) return (void)hipfail(e, x);
+            const uint64_t maxl = hs[12], m = hs[0];
+            auto cap_for = [](uint64_t lines) {
+                return (uint32_t)std::min<uint64_t>(SID_TILE_CAP_MAX,
+                                                    std::max<uint64_t>(SID_TILE_CAP_MIN, (lines + 31) & ~31ull));
+            };
+            if (maxl > cp) {   // a tile with more lines than slots: the two-pass path
+                W.slot_cap = 0;
+                d.prof_end(1, pe);
+                d.tile_cap = cap_for(maxl + maxl / 32 + 2);
+                d.tile_ok = maxl <= SID_TILE_CAP_MAX;
+            } else {
+                const uint64_t m2 = (m + 1) & ~(uint64_t)1, m4 = (m + 3) & ~(uint64_t)3;
+                const uint64_t pre_bytes = 4 * m4 + 24 * m2;
+                uint64_t pc = 0;
+                char* pre = m && d.retain_used.load() + pre_bytes <= d.retain_budget
+                                ? d.pool.get(pre_bytes, &pc, d.s_comp) : nullptr;
+                if (m == 0 || pre) {
+                    uint64_t* counts = nullptr;
+                    if (pre) {
+                        r.pre = pre;
+                        r.pre_cap = pc;
+                        d.retain_used += pc;
+                        counts = (uint64_t*)(pre + 4 * m4);
+                        rc = sid_chunk_tile_compact(&W, (sid_off_t*)pre, counts, counts + m2, d.s_comp);
+                        if (rc != SID_OK) return (void)fail(e, rc);
+                    }
+                    W.slot_cap = 0;
+                    d.prof_end(1, pe);
+                    n = m;
+                    r.parsed = n;
+                    pe = d.prof_begin(P);
+                    rc = sid_profile_accumulate(d.ctx, (const uint16_t*)counts, n, d.s_comp);   // synchronises
+                    d.prof_end(3, pe);
+                    if (rc == SID_OK && n == 0) x = sync();
+                    if (rc != SID_OK) return (void)fail(e, rc);
+                    if (x != hipSuccess) return (void)hipfail(e, x);
+                    tiled = true;
+                    const bool q2 = L.c1 - L.c0 > 256 * n;
+                    const uint64_t want = q2 == quad ? maxl + maxl / 32 + 2
+                                                     : (uint64_t)((double)n * (q2 ? 24576 : 20480) /
+                                                                  (double)std::max<uint64_t>(1, L.c1 - L.c0) * 1.25) + 1;
+                    d.tile_quad = q2;
+                    d.tile_cap = cap_for(want);
+                } else {
+                    W.slot_cap = 0;   // no room to keep the parse: the two-pass path
+                    d.prof_end(1, pe);
+                }
+            }
+        }
         if (!tiled) {
         // pass 2 of a Lynch path: the parse kept since pass 1 stands in for the
         // workspace's line offsets, counts and header pairs (restored below)

@@ -167,6 +167,8 @@ struct sid_chunk_ws {
                                   // [6] [7] fallback lines
     uint32_t slot_cap = 0;        // 0: sites in file order (index + parse); else the tile parse's layout: slots
     uint64_t slots = 0;           // of slot_cap per tile, `slots` of them (sid_chunk_tile_local)
+    bool tile_quad = false;       // (sid_chunk_tile_counts: the shape and tiles, for the compaction)
+    uint64_t tile_ntp = 0;
 };
 int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites);
 void sid_chunk_release(sid_chunk_ws* W);
@@ -207,6 +209,16 @@ uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap, bool quad)
 uint64_t sid_chunk_tile_bound(uint64_t c0, uint64_t c1, uint32_t cap, bool quad);
 int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint32_t cap,
                          bool quad, const char* conf_type, hipStream_t st);
+// The Lynch paths' first pass in one pass over the text: the tile parse of
+// [c0, c1) into every site's counts and header pair (slots as above), the
+// general routine's lines, and the tiles' prefix; afterwards state[0] = the
+// chunk's sites, state[4] the parse error key, lb[5] the most lines in one
+// tile (above the cap: void, as sid_chunk_tile_local).  Then
+// sid_chunk_tile_compact writes the sites in file order into the caller's
+// arrays (line offsets, counts, header pairs: the two-pass parse's layout).
+int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint32_t cap, bool quad,
+                          hipStream_t st);
+int sid_chunk_tile_compact(sid_chunk_ws* W, sid_off_t* starts, uint64_t* counts, uint64_t* hdr, hipStream_t st);
 // likelihood_ratio / bayes fused with the class lookup (sid_lynch_fmt_view)
 int sid_chunk_lynch_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st);
 int sid_chunk_lynch_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, char* out,

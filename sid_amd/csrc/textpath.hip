@@ -1716,7 +1716,9 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
     return site_head_hw(R, &s0, make_ulonglong2(0, 0));
 }
 
-template <bool QUAD>
+// LOCAL: -m local's class words and record lengths (sid_chunk_tile_local);
+// else every site's counts (the Lynch paths' first pass, sid_chunk_tile_counts)
+template <bool QUAD, bool LOCAL>
 __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restrict__ text, uint64_t tile_base,
                                                             uint64_t c0, uint64_t c1, TileOut O, LocalLen LL)
 {
@@ -1829,7 +1831,9 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
                 if (!hv || clen > 8) h[1] = (uint32_t)s0;   // the writer reads the chrom, or tokenises, from the line
                 ST_MID(O.hdr + 2 * g, h[0]);
                 ST_MID(O.hdr + 2 * g + 1, h[1]);
-                if (hv) {
+                if (!LOCAL) {
+                    ST_MID(O.counts + g, c);
+                } else if (hv) {
                     Head hd;
                     hd.clen = clen;
                     hd.pos = (int32_t)(uint32_t)h[0];
@@ -1837,13 +1841,14 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
                 } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
                     l = local_site_len_text(text, c1, s0, c, g, LL);
                 }
-                if (l == 0) O.counts[g] = c;   // a fix-up site: the fix-up reads its counts
+                if (LOCAL && l == 0) O.counts[g] = c;   // a fix-up site: the fix-up reads its counts
             } else {
                 const unsigned long long k = atomicAdd(O.lb + 6, 1ull);
                 O.fb[k] = (uint32_t)g;
                 O.fbo[k] = (uint32_t)s0;
             }
         }
+        if (!LOCAL) continue;
         // the record bytes into the writer blocks' sums: the wave's slots (64,
         // or 16 with quads, from a multiple of 16) lie in one block or two
         const uint64_t gw = (g_tile + j0 + (QUAD ? (tid & ~63u) >> 2 : (tid & ~63u))) / FTB;
@@ -1904,7 +1909,34 @@ __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restr
         counts[g] = c;
         hdr[2 * g] = 0;
         hdr[2 * g + 1] = s0;
-        late[atomicAdd(nlate, 1ull)] = g;
+        if (late) late[atomicAdd(nlate, 1ull)] = g;
+    }
+}
+
+// The tile parse's sites into file order (the Lynch paths' kept parse,
+// run.cpp use_pre: line offsets, counts, header pairs): slot g = tile * cap +
+// j goes to toff[tile] + j (toff: the tiles' exclusive prefix of their
+// counts); the line offset where the header pair keeps it (a chrom over 8
+// bytes, no valid pair), else 0 (unread)
+__global__ __launch_bounds__(TB) void sid_tile_compact_kernel(const uint32_t* __restrict__ tcnt,
+                                                              const uint64_t* __restrict__ toff, uint64_t slots,
+                                                              uint32_t cap, uint64_t cap_magic,
+                                                              const uint64_t* __restrict__ counts,
+                                                              const uint64_t* __restrict__ hdr,
+                                                              sid_off_t* __restrict__ d_starts,
+                                                              uint64_t* __restrict__ d_counts,
+                                                              uint64_t* __restrict__ d_hdr)
+{
+    for (uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x; g < slots; g += (uint64_t)gridDim.x * TB) {
+        const uint64_t t = __umul64hi(g, cap_magic);   // g / cap
+        const uint32_t j = (uint32_t)(g - t * cap);
+        if (j >= tcnt[t]) continue;
+        const uint64_t i = toff[t] + j;
+        const ulonglong2 hw = *(const ulonglong2*)(hdr + 2 * g);
+        const bool keep = (hw.x >> 63) && ((hw.x >> 32) & 0xFFFu) <= 8;   // the pair holds the chrom's bytes
+        d_counts[i] = counts[g];
+        *(ulonglong2*)(d_hdr + 2 * i) = hw;
+        d_starts[i] = keep ? 0u : (sid_off_t)hw.y;
     }
 }
 
@@ -3501,9 +3533,9 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
     const LocalLen LL{ctx->ws.len1, ctx->ws.len2, W->bsum, miss, W->lb, W->cls};
     const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
     if (quad)
-        sid_tile_parse_kernel<true><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
+        sid_tile_parse_kernel<true, true><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
     else
-        sid_tile_parse_kernel<false><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
+        sid_tile_parse_kernel<false, true><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
     sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap,
                                                W->counts, W->hdr, (unsigned long long*)(W->state + 4), late,
                                                W->lb + 7);
@@ -3513,6 +3545,53 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
     WCHECK(hipGetLastError());
     W->cls_ready = true;
     return fmt_scan(W, nb, st);
+}
+
+int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint32_t cap, bool quad,
+                          hipStream_t st)
+{
+    if (cap < SID_TILE_CAP_MIN || cap > SID_TILE_CAP_MAX || cap % 32) return SID_EINVAL;
+    if (c1 > UINT32_MAX) return SID_ELINE;   // line offsets are 32-bit: a line ran the chunk past 4 GiB
+    const uint64_t ntp = tile_count(c0, c1, quad);
+    const uint64_t slots = ntp * cap;
+    if (slots > W->site_cap || ntp > W->tile_cap || slots >= (1ull << 32)) return SID_EINVAL;
+    W->lens_ready = false;
+    W->cls_ready = false;
+    W->slot_cap = cap;
+    W->slots = slots;
+    W->tile_quad = quad;
+    W->tile_ntp = ntp;
+    WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));
+    WCHECK(hipMemsetAsync(W->state, 0, 8, st));   // the scan's running base: the chunk's sites
+    if (ntp == 0) {
+        WCHECK(hipMemsetAsync(W->state + 4, 0xFF, sizeof(uint64_t), st));
+        return SID_OK;
+    }
+    const LocalLen LL{};
+    const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
+    if (quad)
+        sid_tile_parse_kernel<true, false><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
+    else
+        sid_tile_parse_kernel<false, false><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
+    sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap, W->counts,
+                                               W->hdr, (unsigned long long*)(W->state + 4), nullptr, nullptr);
+    // the tiles' first sites in file order (state[0]: the chunk's sites; over the cap: void)
+    launch_scan(W->tcnt, ntp, W->toff, W->state, nullptr,
+                (uint64_t*)((char*)W->tcnt + ((ntp * 4 + 7) & ~(size_t)7)), st);
+    WCHECK(hipGetLastError());
+    return SID_OK;
+}
+
+int sid_chunk_tile_compact(sid_chunk_ws* W, sid_off_t* starts, uint64_t* counts, uint64_t* hdr, hipStream_t st)
+{
+    if (!W->slot_cap) return SID_ESTATE;
+    const uint64_t magic = ~0ull / W->slot_cap + 1;
+    const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((W->slots + TB - 1) / TB, 1), 8192);
+    sid_tile_compact_kernel<<<grid, TB, 0, st>>>(W->tcnt, W->toff, W->slots, W->slot_cap, magic, W->counts, W->hdr,
+                                                 starts, counts, hdr);
+    W->slot_cap = 0;   // the dense layout again
+    WCHECK(hipGetLastError());
+    return SID_OK;
 }
 
 int sid_chunk_lynch_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n, hipStream_t st)
