@@ -202,11 +202,12 @@ def parse_quad(text_per_site):
 
 
 def tile_parse(fused, text_per_site=81.0):
-    """-m local over lines of up to 256 B on average: the engine's tile parse
-    (run.cpp, textpath.hip sid_chunk_tile_local) -- the line index fused into
-    the parse (the text read once), the record lengths, the fix-up and the
-    writer's offsets in the parse stage; no index stage."""
-    return fused == "local" and text_per_site <= 256
+    """-m local: the engine's tile parse (run.cpp, textpath.hip
+    sid_chunk_tile_local; a lane per line at 30x, a quad of lanes per line at
+    200x) -- the line index fused into the parse (the text read once), the
+    record lengths, the fix-up and the writer's offsets in the parse stage; no
+    index stage."""
+    return fused == "local"
 
 
 def stage_bytes(stage, text_per_site, csv_per_site, fused):
@@ -608,6 +609,12 @@ def bench_strong(R, a, cfg):
     text, ln = generate_resident(torch, sid_amd, R.dev, R.gpu, cfg, first, n)
     gen_ms = (time.perf_counter() - t0) * 1e3
     lynch = cfg["method"] != "local" or cfg["R"]
+    if a.device_only:
+        a.chunk_mib = a.chunk_mib or STRONG_RESIDENT_CHUNK_MIB
+        dp = device_path(R, a, cfg, text, ln, lynch)
+        return {"metric": METRIC, "value": dp["sites_per_s"], "unit": "sites/s", "n_gpus": R.n_gpus,
+                "steps": dp["steps"], "ms_per_step": dp["ms_per_step"], "roofline": dp.pop("roofline"),
+                "device_path": dp, "note": "--device-only (profiling): value is the device path's"}, []
     host = torch.empty(ln, dtype=torch.uint8, pin_memory=True)   # on the GPU's NUMA node (numa_bind)
     host.copy_(text[:ln])
     torch.cuda.synchronize(R.dev)

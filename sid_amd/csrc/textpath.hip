@@ -715,52 +715,16 @@ __device__ __forceinline__ uint32_t rb_word(const uint32_t* lut, uint32_t x)
     return lut[x & 0xFFu] + lut[(x >> 8) & 0xFFu] + lut[(x >> 16) & 0xFFu] + lut[x >> 24];
 }
 
-// One 16-B window of token 4: per word, the bytes before the token's end
-// (the first byte < 0x21; `done` from then on), the '^' skip (carried into
-// the next word), the counted bytes kept and the others zeroed, then four
-// table lookups; the token's end byte is looked up too (its entry flags a
-// control byte).  MASKED: only the bytes `valid` (the window's bytes at or
-// after the token's start and before the text's end, room = bytes before
-// the end) count; else the whole window lies inside the text.
-template <bool MASKED>
-__device__ __forceinline__ uint32_t rb_window(const uint4 v, uint32_t valid, int room, const uint32_t* lut, bool& done,
-                                              uint32_t& carry, bool& bad)
-{
-    const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-    uint32_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t x = ws[k];
-        uint32_t vm = MASKED ? (__umul24((valid >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) << 7 : 0x80808080u;
-        vm = done ? 0u : vm;
-        const uint32_t lo = low_bytes(x) & vm;
-        const uint32_t first = lo & (0u - lo);               // the token's end, if in this word
-        vm &= first - 1u;                                    // bytes before it (all if none)
-        done = done || first != 0 || (MASKED && room - 4 * k < 4);
-        const uint32_t caret = eq_bytes(x, 0x5E5E5E5Eu) & vm;
-        const uint32_t skip = ((caret << 8) | carry) & vm;
-        bad = bad || (caret & skip) != 0;                    // '^' run
-        carry = caret >> 24;
-        const uint32_t cm = (vm | first) & ~skip;            // bit 7 of the bytes looked up
-        acc += rb_word(lut, x & (cm | (cm - (cm >> 7))));    // (0xFF for each of them)
-    }
-    return acc;
-}
-
-// The read-bases count by the table: the first window (the token's start
-// inside it) masked, then whole windows while they lie inside the text.
-// first: the first window's 16 bytes, in LDS with the header (no second load
-// of bytes the header already read).  ld(a): the 16-B window at text offset a
-// (global memory, or the tile parse's LDS copy).  (The next windows from the
-// per-line parse's stage too, where its 48 staged bytes hold them, measured
-// slower: the loads hit the caches already)
-// rb_window over the window's 16-bit masks: the token-end and '^' bytes of
-// the four words compressed to 16 bits once, the window's logic (end, skip,
-// '^' runs, carry) on those, the bytes to count expanded back per word for
-// the table.  (A/B against the per-word form: SID_RB16.)
-#ifndef SID_RB16
-#define SID_RB16 0
-#endif
+// One 16-B window of token 4 over its 16-bit masks: the token-end (the
+// first byte < 0x21; `done` from then on) and '^' bytes of the four words
+// compressed to 16 bits once; the '^' skip (carried into the next window), a
+// '^' run (bad), the bytes before the end kept and the skipped ones dropped;
+// then the kept bytes expanded back per word for four table lookups each (the
+// token's end byte is looked up too: its entry flags a control byte).
+// MASKED: only the bytes `valid` (the window's bytes at or after the token's
+// start and before the text's end, room = bytes before the end) count; else
+// the whole window lies inside the text.  (A per-word form of the same logic
+// measured 1-2 % slower at 30x, 4 % at 200x.)
 template <bool MASKED>
 __device__ __forceinline__ uint32_t rb_window16(const uint4 v, uint32_t valid, int room, const uint32_t* lut,
                                                 bool& done, uint32_t& carry, bool& bad)
@@ -789,25 +753,28 @@ __device__ __forceinline__ uint32_t rb_window16(const uint4 v, uint32_t valid, i
     return acc;
 }
 
-// (Off: the offsets' type -- 32-bit for the tile parse's offsets from its tile)
+// The read-bases count by the table: the first window (the token's start
+// inside it) masked, then whole windows while they lie inside the text.
+// first: the first window's 16 bytes, in LDS with the header (no second load
+// of bytes the header already read).  ld(a): the 16-B window at text offset a
+// (global memory, or the tile parse's LDS copy).  (The next windows from the
+// per-line parse's stage too, where its 48 staged bytes hold them, measured
+// slower: the loads hit the caches already)  Off: the
+// offsets' type (32-bit for the tile parse's offsets from its tile).
 template <class Ld, class Off = uint64_t>
 __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t kd, const uint32_t* lut,
                                                const uint4* first, uint64_t* out)
 {
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
     Off a = q & ~(Off)15;
-    uint32_t carry = 0;   // bit 7: byte 0 of the next word is skipped
+    uint32_t carry = 0;   // 1: byte 0 of the next window is skipped
     bool done = false, bad = false;
     uint4 vn = ld(a + 16);   // the next window in flight while the first is counted
     uint32_t acc = 0;
     auto masked = [&](const uint4& v, uint32_t lead) {
         const int room = len > a ? (int)min(len - a, (Off)16) : 0;
         const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
-#if SID_RB16
         return rb_window16<true>(v, valid, room, lut, done, carry, bad);
-#else
-        return rb_window<true>(v, valid, room, lut, done, carry, bad);
-#endif
     };
     auto add = [&](uint32_t w) {
         nA += w & 31u;
@@ -822,11 +789,7 @@ __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t k
     while (!done) {
         const uint4 v = vn;
         vn = ld(a + 16);
-#if SID_RB16
         add(a + 16 <= len ? rb_window16<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u));
-#else
-        add(a + 16 <= len ? rb_window<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u));
-#endif
         a += 16;
     }
     if (bad || (acc >> RB_BAD_SHIFT) != 0) return false;
@@ -868,8 +831,8 @@ __device__ __forceinline__ bool read_bases_quad(Ld ld, Off len, Off q, uint32_t 
         const uint32_t cin = k == 0 ? 0u : (j ? from_left : prev3);
         prev3 = (uint32_t)__shfl((int)last_caret, 3, 4);
         bool done = false, wbad = false;
-        uint32_t carry = cin << 7;
-        const uint32_t w = rb_window<true>(v, valid, room, lut, done, carry, wbad);
+        uint32_t carry = cin;
+        const uint32_t w = rb_window16<true>(v, valid, room, lut, done, carry, wbad);
         // the quad's first window that ends the token (or the text)
         const uint64_t bal = __ballot(done);
         const uint32_t qb = (uint32_t)(bal >> (threadIdx.x & 60u)) & 15u;
@@ -1586,8 +1549,8 @@ __device__ __noinline__ int local_site_len_text(const char* text, uint64_t len, 
 // block's byte count.  Lines the fast path leaves get theirs after the
 // general routine (sid_local_len_list_kernel).  The tail-length table is read
 // through the caches (an LDS copy would cost the parse a block per CU).
-// (7 waves a SIMD, 71 VGPRs instead of 64, measured slower: DESIGN.md §9)
-__global__ __launch_bounds__(TB, 8) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
+// (the two-pass fallback's parse since the tile parse: 7 waves a SIMD)
+__global__ __launch_bounds__(TB) void sid_parse_len_kernel(const char* __restrict__ text, uint64_t len,
                                                            const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ range,
                                                            uint64_t* __restrict__ counts,
@@ -1717,14 +1680,33 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
 }
 
 // LOCAL: -m local's class words and record lengths (sid_chunk_tile_local);
-// else every site's counts (the Lynch paths' first pass, sid_chunk_tile_counts)
+// else every site's counts (the Lynch paths' first pass, sid_chunk_tile_counts).
+// One block per tile.  While a block parses its tile, one load per 128-B
+// line of tile blockIdx.x + pf_dist is in flight (pf_dist: the blocks
+// resident on the device, a multiple of the 8 XCDs; that tile's block then
+// runs about when this one ends, on the same XCD, and its loads hit L2).
+#ifndef SID_TP_PF
+#define SID_TP_PF 1
+#endif
+#ifdef SID_TP_STAMP
+// (diagnostic builds: per-phase wall-clock sums of the tile parse's blocks)
+constexpr uint32_t TP_STAMP_N = 1u << 20;
+__device__ uint32_t tp_stamp[TP_STAMP_N][4];
+#define TP_STAMP_AT(v) const uint64_t v = tid == 0 ? wall_clock64() : 0
+#else
+#define TP_STAMP_AT(v)
+#endif
 template <bool QUAD, bool LOCAL>
 __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restrict__ text, uint64_t tile_base,
-                                                            uint64_t c0, uint64_t c1, TileOut O, LocalLen LL)
+                                                            uint64_t c0, uint64_t c1, uint64_t ntiles,
+                                                            uint32_t pf_dist, TileOut O, LocalLen LL)
 {
     constexpr uint32_t ROWS = QUAD ? TP_ROWS_QUAD : TP_ROWS, TP_TILE = ROWS * TILE;
     constexpr uint32_t LPR = QUAD ? TB / 4 : TB;   // lines per round of the block
-    static_assert(TB == 256 && ROWS <= 8, "a lane's windows: two u64s of 16-bit line-start counts");
+    // a row (4 KiB) has at most 2048 line starts: 12-bit fields, five rows
+    // in one u64 (one block scan); six rows: 16-bit fields, two scans
+    constexpr uint32_t FB = ROWS <= 5 ? 12 : 16, FPW = ROWS <= 5 ? 5 : 4, NW = (ROWS + FPW - 1) / FPW;
+    static_assert(TB == 256 && ROWS <= 8, "a lane's windows: two u64s of line-start counts");
     static_assert(FTB % 64 == 0, "a wave's slots lie in one writer block");
     __shared__ __attribute__((aligned(16))) char tl[TP_TILE + TP_HALO + 64];
     __shared__ uint16_t ls[TP_CAP_MAX];
@@ -1734,132 +1716,160 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     cls[tid] = (uint8_t)base_class(tid);
     rbl[tid] = rb_entry(tid);
     if (blockIdx.x == 0 && tid == 0) O.state[4] = ~0ull;   // no parse error yet
-    const uint64_t t = blockIdx.x;
-    const uint64_t g0 = tile_base + t * TP_TILE;           // the tile's first byte (16-B aligned)
-    // a tile inside the chunk (all but its first and last): no window needs
-    // the chunk's bounds (block-uniform)
-    const bool inner = g0 > c0 && g0 + TP_TILE <= c1;
-    // ---- load (windows at or past the chunk's end read as zeros)
-    uint4 v[ROWS];
-#pragma unroll
-    for (uint32_t k = 0; k < ROWS; ++k) {
-        const uint64_t at = g0 + k * TILE + tid * 16;
-        v[k] = (inner || at < c1) ? ld_nt(text + at) : make_uint4(0, 0, 0, 0);
-        *(uint4*)(tl + k * TILE + tid * 16) = v[k];
-    }
-    if (tid < TP_HALO / 16) {
-        const uint64_t at = g0 + TP_TILE + tid * 16;
-        *(uint4*)(tl + TP_TILE + tid * 16) = at < c1 ? *(const uint4*)(text + at) : make_uint4(0, 0, 0, 0);
-    }
-    if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
-    // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
-    const uint32_t prev0 = (g0 > c0 && g0 - 1 < c1) ? (text[g0 - 1] == '\n') : 1u;
-    __syncthreads();
-    // ---- line starts (bit j: byte j of the window starts a non-empty line in [c0, c1))
-    uint32_t m[ROWS];
-    uint64_t packed[2] = {0, 0};
-#pragma unroll
-    for (uint32_t k = 0; k < ROWS; ++k) {
-        const uint64_t at = g0 + k * TILE + tid * 16;
-        const uint4 w = v[k];
-        const uint32_t nl = compress8(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au)) |
-                            (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
-        const uint32_t prev = (k == 0 && tid == 0) ? prev0 : (uint32_t)(tl[max(k * TILE + tid * 16, 1u) - 1] == '\n');
-        uint32_t mk = ((nl << 1) | prev) & ~nl & 0xFFFFu;
-        if (!inner) {
-            if (at + 16 > c0 && at <= c0) {   // c0 in this window: it starts a line (unless a '\n'), nothing before it does
-                const uint32_t j = (uint32_t)(c0 - at);
-                mk = (mk | ((1u << j) & ~nl)) & ~((1u << j) - 1u);
-            }
-            if (at + 16 > c1) mk &= c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
-            if (at + 16 <= c0) mk = 0;
-        }
-        m[k] = mk;
-        packed[k / 4] |= (uint64_t)__popc(mk) << (16 * (k % 4));
-    }
-    // (a row of 4 KiB has at most 2048 line starts: 16-bit fields, four rows a word)
-    uint64_t tot[2] = {0, 0}, pre[2] = {0, 0};
-    pre[0] = block_exscan64(packed[0], &tot[0]);
-    if (ROWS > 4) pre[1] = block_exscan64(packed[1], &tot[1]);
     const uint32_t cap = O.cap;
-    uint32_t nlines = 0;
+    {
+        const uint64_t t = blockIdx.x;
+        TP_STAMP_AT(st0);
+        const uint64_t g0 = tile_base + t * TP_TILE;           // the tile's first byte (16-B aligned)
+        // a tile inside the chunk (all but its first and last): no window needs
+        // the chunk's bounds (block-uniform)
+        const bool inner = g0 > c0 && g0 + TP_TILE <= c1;
+        // ---- load (windows at or past the chunk's end read as zeros)
+        uint4 v[ROWS];
 #pragma unroll
-    for (uint32_t k = 0; k < ROWS; ++k) {
-        uint32_t q = nlines + (uint32_t)((pre[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
-        for (uint32_t mk = m[k]; mk; mk &= mk - 1, ++q)
-            if (q < cap) ls[q] = (uint16_t)(k * TILE + tid * 16 + (uint32_t)(__ffs(mk) - 1));
-        nlines += (uint32_t)((tot[k / 4] >> (16 * (k % 4))) & 0xFFFFu);
-    }
-    const uint32_t cnt = min(nlines, cap);
-    if (tid == 0) O.tcnt[t] = nlines;   // (no atomics on one address from every block: summed by the next kernel)
-    __syncthreads();
-    // ---- parse, one lane (a quad of lanes) per line, from LDS; offsets
-    // from the tile's first byte (32 bits: a chunk spans less than 4 GiB)
-    const char* gtile = text + g0;
-    // (the global load non-temporal: two loads of a kind would be merged into
-    // one generic-address (flat) load of a selected pointer, the LDS reads too)
-    auto ld = [&](uint32_t r) -> uint4 {
-        if (r <= TP_TILE + TP_HALO - 16) return *(const uint4*)(tl + r);
-        return ld_nt(gtile + r);   // (a line running past the halo)
-    };
-    const uint32_t len_t = (uint32_t)(c1 - g0);   // the chunk's end
-    const uint64_t g_tile = t * (uint64_t)cap;
-    for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
-        const uint32_t j = j0 + (QUAD ? tid >> 2 : tid);
-        const bool lead = !QUAD || (tid & 3u) == 0;   // the lane that writes the line's outputs
-        int l = 0;
-        if (j < cnt) {
-            const uint32_t r0 = ls[j];
-            const uint64_t s0 = g0 + r0;
-            const uint64_t g = g_tile + j;
-            const char* stage = tl + (r0 & ~15u);
-            const uint32_t sh = r0 & 15u;
-            const uint4 v0 = *(const uint4*)stage, v1 = *(const uint4*)(stage + 16), v2 = *(const uint4*)(stage + 32);
-            uint64_t c = 0, h[2] = {0, 0};
-            uint32_t kd = 0;
-            const int t4 = parse_header(v0, v1, v2, stage, sh, len_t - r0, cls, h, &kd);
-            bool ok = t4 >= 0;
-            if (ok) {
-                const uint4* first = (const uint4*)(stage + ((sh + (uint32_t)t4) & 0x30u));
-                ok = QUAD ? read_bases_quad<decltype(ld), uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c)
-                          : read_bases_lut<decltype(ld), uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c);
-            }
-            if (!lead) {
-            } else if (ok) {
-                const bool hv = (h[0] >> 63) != 0;
-                const uint32_t clen = (uint32_t)(h[0] >> 32) & 0xFFFu;
-                if (!hv || clen > 8) h[1] = (uint32_t)s0;   // the writer reads the chrom, or tokenises, from the line
-                ST_MID(O.hdr + 2 * g, h[0]);
-                ST_MID(O.hdr + 2 * g + 1, h[1]);
-                if (!LOCAL) {
-                    ST_MID(O.counts + g, c);
-                } else if (hv) {
-                    Head hd;
-                    hd.clen = clen;
-                    hd.pos = (int32_t)(uint32_t)h[0];
-                    l = local_site_len(hd, c, g, LL.len1, LL);
-                } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
-                    l = local_site_len_text(text, c1, s0, c, g, LL);
+        for (uint32_t k = 0; k < ROWS; ++k) {
+            const uint64_t at = g0 + k * TILE + tid * 16;
+            v[k] = (inner || at < c1) ? ld_nt(text + at) : make_uint4(0, 0, 0, 0);
+            *(uint4*)(tl + k * TILE + tid * 16) = v[k];
+        }
+        if (tid < TP_HALO / 16) {
+            const uint64_t at = g0 + TP_TILE + tid * 16;
+            *(uint4*)(tl + TP_TILE + tid * 16) = at < c1 ? *(const uint4*)(text + at) : make_uint4(0, 0, 0, 0);
+        }
+        if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
+        // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
+        const uint32_t prev0 = tid ? 0u : (g0 > c0 && g0 - 1 < c1) ? (text[g0 - 1] == '\n') : 1u;
+        __syncthreads();
+        TP_STAMP_AT(st1);
+        // ---- line starts (bit j: byte j of the window starts a non-empty line in [c0, c1))
+        uint32_t m[ROWS];
+        uint64_t packed[NW];
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) packed[w] = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < ROWS; ++k) {
+            const uint64_t at = g0 + k * TILE + tid * 16;
+            const uint4 w = v[k];
+            const uint32_t nl = compress8(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au)) |
+                                (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
+            const uint32_t prev = (k == 0 && tid == 0) ? prev0 : (uint32_t)(tl[max(k * TILE + tid * 16, 1u) - 1] == '\n');
+            uint32_t mk = ((nl << 1) | prev) & ~nl & 0xFFFFu;
+            if (!inner) {
+                if (at + 16 > c0 && at <= c0) {   // c0 in this window: it starts a line (unless a '\n'), nothing before it does
+                    const uint32_t j = (uint32_t)(c0 - at);
+                    mk = (mk | ((1u << j) & ~nl)) & ~((1u << j) - 1u);
                 }
-                if (LOCAL && l == 0) O.counts[g] = c;   // a fix-up site: the fix-up reads its counts
-            } else {
-                const unsigned long long k = atomicAdd(O.lb + 6, 1ull);
-                O.fb[k] = (uint32_t)g;
-                O.fbo[k] = (uint32_t)s0;
+                if (at + 16 > c1) mk &= c1 > at ? (1u << (uint32_t)(c1 - at)) - 1u : 0u;
+                if (at + 16 <= c0) mk = 0;
             }
+            m[k] = mk;
+            packed[k / FPW] |= (uint64_t)__popc(mk) << (FB * (k % FPW));
         }
-        if (!LOCAL) continue;
-        // the record bytes into the writer blocks' sums: the wave's slots (64,
-        // or 16 with quads, from a multiple of 16) lie in one block or two
-        const uint64_t gw = (g_tile + j0 + (QUAD ? (tid & ~63u) >> 2 : (tid & ~63u))) / FTB;
-        int lo = (g_tile + j) / FTB == gw ? l : 0, hi = l - lo;
+        uint64_t tot[NW], pre[NW];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            lo += __shfl_xor(lo, off, 64);
-            hi += __shfl_xor(hi, off, 64);
+        for (uint32_t w = 0; w < NW; ++w) pre[w] = block_exscan64(packed[w], &tot[w]);
+        constexpr uint64_t FM = (1ull << FB) - 1;
+        uint32_t nlines = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < ROWS; ++k) {
+            uint32_t q = nlines + (uint32_t)((pre[k / FPW] >> (FB * (k % FPW))) & FM);
+            for (uint32_t mk = m[k]; mk; mk &= mk - 1, ++q)
+                if (q < cap) ls[q] = (uint16_t)(k * TILE + tid * 16 + (uint32_t)(__ffs(mk) - 1));
+            nlines += (uint32_t)((tot[k / FPW] >> (FB * (k % FPW))) & FM);
         }
-        if ((tid & 63u) == 0 && lo) atomicAdd(LL.bsum + gw, (uint32_t)lo);
-        if ((tid & 63u) == 0 && hi) atomicAdd(LL.bsum + gw + 1, (uint32_t)hi);
+        const uint32_t cnt = min(nlines, cap);
+        if (tid == 0) O.tcnt[t] = nlines;   // (no atomics on one address from every block: summed by the next kernel)
+        __syncthreads();
+        TP_STAMP_AT(st2);
+        // a later tile's lines into L2: one 4-B load per 128-B line (the
+        // value kept to the kernel's end, so the loads stay in flight)
+        uint32_t pf = 0;
+        {
+            const uint64_t u = t + pf_dist;
+            const uint32_t off = tid * 128u;
+            const uint64_t at = tile_base + u * TP_TILE + off;
+            if (SID_TP_PF && u < ntiles && off < TP_TILE + TP_HALO && at < c1) pf = *(const uint32_t*)(text + at);
+        }
+        // ---- parse, one lane (a quad of lanes) per line, from LDS; offsets
+        // from the tile's first byte (32 bits: a chunk spans less than 4 GiB)
+        const char* gtile = text + g0;
+        // (the global load non-temporal: two loads of a kind would be merged into
+        // one generic-address (flat) load of a selected pointer, the LDS reads too)
+        auto ld = [&](uint32_t r) -> uint4 {
+            if (r <= TP_TILE + TP_HALO - 16) return *(const uint4*)(tl + r);
+            return ld_nt(gtile + r);   // (a line running past the halo)
+        };
+        const uint32_t len_t = (uint32_t)(c1 - g0);   // the chunk's end
+        const uint64_t g_tile = t * (uint64_t)cap;
+        for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
+            const uint32_t j = j0 + (QUAD ? tid >> 2 : tid);
+            const bool lead = !QUAD || (tid & 3u) == 0;   // the lane that writes the line's outputs
+            int l = 0;
+            if (j < cnt) {
+                const uint32_t r0 = ls[j];
+                const uint64_t s0 = g0 + r0;
+                const uint64_t g = g_tile + j;
+                const char* stage = tl + (r0 & ~15u);
+                const uint32_t sh = r0 & 15u;
+                const uint4 v0 = *(const uint4*)stage, v1 = *(const uint4*)(stage + 16), v2 = *(const uint4*)(stage + 32);
+                uint64_t c = 0, h[2] = {0, 0};
+                uint32_t kd = 0;
+                const int t4 = parse_header(v0, v1, v2, stage, sh, len_t - r0, cls, h, &kd);
+                bool ok = t4 >= 0;
+                if (ok) {
+                    const uint4* first = (const uint4*)(stage + ((sh + (uint32_t)t4) & 0x30u));
+                    ok = QUAD ? read_bases_quad<decltype(ld), uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c)
+                              : read_bases_lut<decltype(ld), uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c);
+                }
+                if (!lead) {
+                } else if (ok) {
+                    const bool hv = (h[0] >> 63) != 0;
+                    const uint32_t clen = (uint32_t)(h[0] >> 32) & 0xFFFu;
+                    if (!hv || clen > 8) h[1] = (uint32_t)s0;   // the writer reads the chrom, or tokenises, from the line
+                    ST_MID(O.hdr + 2 * g, h[0]);
+                    ST_MID(O.hdr + 2 * g + 1, h[1]);
+                    if (!LOCAL) {
+                        ST_MID(O.counts + g, c);
+                    } else if (hv) {
+                        Head hd;
+                        hd.clen = clen;
+                        hd.pos = (int32_t)(uint32_t)h[0];
+                        l = local_site_len(hd, c, g, LL.len1, LL);
+                    } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
+                        l = local_site_len_text(text, c1, s0, c, g, LL);
+                    }
+                    if (LOCAL && l == 0) O.counts[g] = c;   // a fix-up site: the fix-up reads its counts
+                } else {
+                    const unsigned long long k = atomicAdd(O.lb + 6, 1ull);
+                    O.fb[k] = (uint32_t)g;
+                    O.fbo[k] = (uint32_t)s0;
+                }
+            }
+            if (!LOCAL) continue;
+            // the record bytes into the writer blocks' sums: the wave's slots (64,
+            // or 16 with quads, from a multiple of 16) lie in one block or two
+            const uint64_t gw = (g_tile + j0 + (QUAD ? (tid & ~63u) >> 2 : (tid & ~63u))) / FTB;
+            int lo = (g_tile + j) / FTB == gw ? l : 0, hi = l - lo;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                lo += __shfl_xor(lo, off, 64);
+                hi += __shfl_xor(hi, off, 64);
+            }
+            if ((tid & 63u) == 0 && lo) atomicAdd(LL.bsum + gw, (uint32_t)lo);
+            if ((tid & 63u) == 0 && hi) atomicAdd(LL.bsum + gw + 1, (uint32_t)hi);
+        }
+        // (the prefetch's value: kept live to here, never true)
+        if (pf == 0x5A5A5A5Au && c1 == 0) O.state[5] = pf;
+#ifdef SID_TP_STAMP
+        __syncthreads();
+        if (tid == 0 && t < TP_STAMP_N) {
+            const uint64_t st3 = wall_clock64();
+            tp_stamp[t][0] = (uint32_t)(st1 - st0);
+            tp_stamp[t][1] = (uint32_t)(st2 - st1);
+            tp_stamp[t][2] = (uint32_t)(st3 - st2);
+            tp_stamp[t][3] = (uint32_t)(st0 >> 4);   // start (160 ns units)
+        }
+#endif
     }
 }
 
@@ -3495,6 +3505,55 @@ static uint64_t tile_count(uint64_t c0, uint64_t c1, bool quad)
     return c1 > c0 ? (c1 - t0 + tp_tile(quad) - 1) / tp_tile(quad) : 0;
 }
 
+// The tile parse's prefetch distance: the blocks resident on the device at
+// once (occupancy x CUs), a multiple of the 8 XCDs
+template <bool QUAD, bool LOCAL>
+static uint32_t tile_pf_dist()
+{
+    static const uint32_t resident = [] {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sid_tile_parse_kernel<QUAD, LOCAL>, TB, 0) !=
+                hipSuccess)
+            return 1536u;
+        return (uint32_t)std::max(8, (cus * std::max(per, 1)) & ~7);
+    }();
+    return resident;
+}
+
+template <bool LOCAL>
+static void launch_tile_parse(bool quad, const char* base, uint64_t c0, uint64_t c1, uint64_t ntp, const TileOut& O,
+                              const LocalLen& LL, hipStream_t st)
+{
+    const uint64_t tb = c0 & ~(uint64_t)15;
+    if (quad)
+        sid_tile_parse_kernel<true, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp,
+                                                                         tile_pf_dist<true, LOCAL>(), O, LL);
+    else
+        sid_tile_parse_kernel<false, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp,
+                                                                          tile_pf_dist<false, LOCAL>(), O, LL);
+#ifdef SID_TP_STAMP
+    {
+        const uint64_t m = std::min<uint64_t>(ntp, TP_STAMP_N);
+        std::vector<uint32_t> v(m * 4);
+        if (hipStreamSynchronize(st) == hipSuccess &&
+            hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(tp_stamp), m * 16) == hipSuccess && m) {
+            double a[3] = {0, 0, 0};
+            uint32_t lo = UINT32_MAX, hi = 0;
+            for (uint64_t k = 0; k < m; ++k) {
+                for (int j = 0; j < 3; ++j) a[j] += v[4 * k + j];
+                lo = std::min(lo, v[4 * k + 3]);
+                hi = std::max(hi, v[4 * k + 3]);
+            }
+            fprintf(stderr, "tp_stamp quad=%d tiles=%llu us/block: load %.2f index %.2f parse %.2f; starts span %.1f us\n",
+                    (int)quad, (unsigned long long)m, a[0] / 100.0 / m, a[1] / 100.0 / m, a[2] / 100.0 / m,
+                    (hi - lo) * 0.16);
+        }
+    }
+#endif
+}
+
 uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap, bool quad)
 {
     return tile_count(c0, c1, quad) * cap;
@@ -3532,10 +3591,7 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
     uint32_t* miss = W->fb + 2 * W->site_cap;
     const LocalLen LL{ctx->ws.len1, ctx->ws.len2, W->bsum, miss, W->lb, W->cls};
     const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
-    if (quad)
-        sid_tile_parse_kernel<true, true><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
-    else
-        sid_tile_parse_kernel<false, true><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
+    launch_tile_parse<true>(quad, base, c0, c1, ntp, O, LL, st);
     sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap,
                                                W->counts, W->hdr, (unsigned long long*)(W->state + 4), late,
                                                W->lb + 7);
@@ -3569,10 +3625,7 @@ int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64
     }
     const LocalLen LL{};
     const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
-    if (quad)
-        sid_tile_parse_kernel<true, false><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
-    else
-        sid_tile_parse_kernel<false, false><<<(unsigned)ntp, TB, 0, st>>>(base, c0 & ~(uint64_t)15, c0, c1, O, LL);
+    launch_tile_parse<false>(quad, base, c0, c1, ntp, O, LL, st);
     sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap, W->counts,
                                                W->hdr, (unsigned long long*)(W->state + 4), nullptr, nullptr);
     // the tiles' first sites in file order (state[0]: the chunk's sites; over the cap: void)

@@ -3,7 +3,7 @@
 # counters in passes of their own, never with the trace domains):
 #   trace   --kernel-trace --stats over the bench as the driver runs it
 #   dtrace  the same over the device path only (--device-only)
-#   insts / fetch / write / stall   --pmc passes over the device path
+#   insts / fetch / write / stall / lds   --pmc passes over the device path
 # then tools/pmc_summary.py -> gpurun_out/prof_<TAG>/summary.json and, with
 # STAGES=1, tools/pmc_stages.py -> profiles/pmc_<stage>_<TAG>.json
 # usage: PASSES="trace dtrace insts fetch write" tools/gpu/profile.sh TAG [--config C2]
@@ -28,6 +28,7 @@ for pass in ${PASSES:-trace dtrace insts fetch write}; do
     insts) pmc insts SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
     fetch) pmc fetch FETCH_SIZE ;;
     write) pmc write WRITE_SIZE ;;
+    lds) pmc lds SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_WAVES ;;
     stall) pmc stall SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS ;;
     esac
     echo "$pass ok"
