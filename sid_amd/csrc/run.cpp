@@ -1472,7 +1472,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                     // chunk's lines per byte, a quarter on top)
                     const bool q2 = L.c1 - L.c0 > 256 * n;
                     const uint64_t want = q2 == quad ? maxl + maxl / 32 + 2
-                                                     : (uint64_t)((double)n * (q2 ? 24576 : 20480) /
+                                                     : (uint64_t)((double)n * sid_tile_unit(q2) /
                                                                   (double)std::max<uint64_t>(1, L.c1 - L.c0) * 1.25) + 1;
                     d.tile_quad = q2;
                     d.tile_cap = cap_for(want);
@@ -1543,7 +1543,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                     tiled = true;
                     const bool q2 = L.c1 - L.c0 > 256 * n;
                     const uint64_t want = q2 == quad ? maxl + maxl / 32 + 2
-                                                     : (uint64_t)((double)n * (q2 ? 24576 : 20480) /
+                                                     : (uint64_t)((double)n * sid_tile_unit(q2) /
                                                                   (double)std::max<uint64_t>(1, L.c1 - L.c0) * 1.25) + 1;
                     d.tile_quad = q2;
                     d.tile_cap = cap_for(want);

@@ -206,6 +206,7 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
 // a lane per line.
 constexpr uint32_t SID_TILE_CAP_MIN = 64, SID_TILE_CAP_MAX = 1024;   // slots per tile
 uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap, bool quad);
+uint32_t sid_tile_unit(bool quad);   // text bytes per tile (the slot layout's unit)
 uint64_t sid_chunk_tile_bound(uint64_t c0, uint64_t c1, uint32_t cap, bool quad);
 int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint32_t cap,
                          bool quad, const char* conf_type, hipStream_t st);

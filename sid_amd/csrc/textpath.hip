@@ -103,6 +103,20 @@ __device__ __forceinline__ uint64_t block_exscan64(uint64_t v, uint64_t* total)
     return base + x - v;
 }
 
+// inclusive scan of one u32 per lane over the wave, by DPP (no LDS):
+// row_shr 1/2/4/8 within each row of 16 lanes, then row_bcast 15 / 31 carry
+// the rows' sums up
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+
 // this thread's SCAN_PER inputs (16-B loads when the run is whole)
 __device__ __forceinline__ void scan_load(const uint32_t* __restrict__ in, uint64_t m, uint64_t b0, uint32_t* v)
 {
@@ -1650,6 +1664,7 @@ constexpr uint32_t TP_ROWS = 5;                 // (the lane-per-line shape: ~25
 constexpr uint32_t TP_ROWS_QUAD = 6;
 constexpr uint32_t TP_HALO = 1024;
 constexpr uint32_t TP_CAP_MAX = 1024;           // slots per tile at most (lines of 16 B on average)
+static_assert(TP_CAP_MAX == SID_TILE_CAP_MAX, "the host's cap bound");
 __host__ __device__ constexpr uint32_t tp_tile(bool quad) { return (quad ? TP_ROWS_QUAD : TP_ROWS) * TILE; }
 
 struct TileOut {
@@ -1679,6 +1694,57 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
     return site_head_hw(R, &s0, make_ulonglong2(0, 0));
 }
 
+// One line of a tile (or segment) from its LDS copy (tl: the copy of the
+// text from global offset g0 on, ld: a 16-B window at an offset from g0, from
+// LDS or past its end from HBM): the fast path (parse_header, then
+// read_bases_quad / _lut), then the line's outputs into slot g by the lead
+// lane (header pair; -m local's class word and record length, returned; the
+// Lynch paths' counts), or its slot and offset listed for the general routine
+template <bool QUAD, bool LOCAL, class Ld>
+__device__ __forceinline__ int tile_line(const char* __restrict__ text, const char* tl, Ld ld, uint64_t g0, uint32_t r0,
+                                         uint64_t g, uint32_t len_t, uint64_t c1, bool lead, const uint8_t* cls,
+                                         const uint32_t* rbl, const TileOut& O, const LocalLen& LL)
+{
+    int l = 0;
+    const uint64_t s0 = g0 + r0;
+    const char* stage = tl + (r0 & ~15u);
+    const uint32_t sh = r0 & 15u;
+    const uint4 v0 = *(const uint4*)stage, v1 = *(const uint4*)(stage + 16), v2 = *(const uint4*)(stage + 32);
+    uint64_t c = 0, h[2] = {0, 0};
+    uint32_t kd = 0;
+    const int t4 = parse_header(v0, v1, v2, stage, sh, len_t - r0, cls, h, &kd);
+    bool ok = t4 >= 0;
+    if (ok) {
+        const uint4* first = (const uint4*)(stage + ((sh + (uint32_t)t4) & 0x30u));
+        ok = QUAD ? read_bases_quad<Ld, uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c)
+                  : read_bases_lut<Ld, uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c);
+    }
+    if (!lead) {
+    } else if (ok) {
+        const bool hv = (h[0] >> 63) != 0;
+        const uint32_t clen = (uint32_t)(h[0] >> 32) & 0xFFFu;
+        if (!hv || clen > 8) h[1] = (uint32_t)s0;   // the writer reads the chrom, or tokenises, from the line
+        ST_MID(O.hdr + 2 * g, h[0]);
+        ST_MID(O.hdr + 2 * g + 1, h[1]);
+        if (!LOCAL) {
+            ST_MID(O.counts + g, c);
+        } else if (hv) {
+            Head hd;
+            hd.clen = clen;
+            hd.pos = (int32_t)(uint32_t)h[0];
+            l = local_site_len(hd, c, g, LL.len1, LL);
+        } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
+            l = local_site_len_text(text, c1, s0, c, g, LL);
+        }
+        if (LOCAL && l == 0) O.counts[g] = c;   // a fix-up site: the fix-up reads its counts
+    } else {
+        const unsigned long long k = atomicAdd(O.lb + 6, 1ull);
+        O.fb[k] = (uint32_t)g;
+        O.fbo[k] = (uint32_t)s0;
+    }
+    return l;
+}
+
 // LOCAL: -m local's class words and record lengths (sid_chunk_tile_local);
 // else every site's counts (the Lynch paths' first pass, sid_chunk_tile_counts).
 // One block per tile.  While a block parses its tile, one load per 128-B
@@ -1687,6 +1753,9 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
 // runs about when this one ends, on the same XCD, and its loads hit L2).
 #ifndef SID_TP_PF
 #define SID_TP_PF 1
+#endif
+#ifndef SID_TP_PF_EARLY
+#define SID_TP_PF_EARLY 0
 #endif
 #ifdef SID_TP_STAMP
 // (diagnostic builds: per-phase wall-clock sums of the tile parse's blocks)
@@ -1703,15 +1772,16 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
 {
     constexpr uint32_t ROWS = QUAD ? TP_ROWS_QUAD : TP_ROWS, TP_TILE = ROWS * TILE;
     constexpr uint32_t LPR = QUAD ? TB / 4 : TB;   // lines per round of the block
-    // a row (4 KiB) has at most 2048 line starts: 12-bit fields, five rows
-    // in one u64 (one block scan); six rows: 16-bit fields, two scans
-    constexpr uint32_t FB = ROWS <= 5 ? 12 : 16, FPW = ROWS <= 5 ? 5 : 4, NW = (ROWS + FPW - 1) / FPW;
-    static_assert(TB == 256 && ROWS <= 8, "a lane's windows: two u64s of line-start counts");
+    // a window has at most 8 line starts, a wave's row at most 512: 10-bit
+    // fields, three rows a word
+    constexpr uint32_t NW = (ROWS + 2) / 3;
+    static_assert(TB == 256 && ROWS <= 9, "a lane's windows: three u32s of line-start counts");
     static_assert(FTB % 64 == 0, "a wave's slots lie in one writer block");
     __shared__ __attribute__((aligned(16))) char tl[TP_TILE + TP_HALO + 64];
     __shared__ uint16_t ls[TP_CAP_MAX];
     __shared__ uint8_t cls[256];
     __shared__ uint32_t rbl[256];
+    __shared__ uint32_t wtot[TB / 64][NW];
     const uint32_t tid = threadIdx.x;
     cls[tid] = (uint8_t)base_class(tid);
     rbl[tid] = rb_entry(tid);
@@ -1720,6 +1790,19 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     {
         const uint64_t t = blockIdx.x;
         TP_STAMP_AT(st0);
+        // a later tile's lines into L2: one 4-B load per 128-B line (the
+        // value kept to the kernel's end, so the loads stay in flight)
+        uint32_t pf = 0;
+#define PREFETCH_LATER_TILE()                                                                                        \
+        do {                                                                                                         \
+            const uint64_t u = t + pf_dist;                                                                          \
+            const uint32_t off = tid * 128u;                                                                         \
+            const uint64_t at = tile_base + u * TP_TILE + off;                                                       \
+            if (SID_TP_PF && u < ntiles && off < TP_TILE + TP_HALO && at < c1) pf = *(const uint32_t*)(text + at); \
+        } while (0)
+#if SID_TP_PF_EARLY
+        PREFETCH_LATER_TILE();
+#endif
         const uint64_t g0 = tile_base + t * TP_TILE;           // the tile's first byte (16-B aligned)
         // a tile inside the chunk (all but its first and last): no window needs
         // the chunk's bounds (block-uniform)
@@ -1743,16 +1826,20 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         TP_STAMP_AT(st1);
         // ---- line starts (bit j: byte j of the window starts a non-empty line in [c0, c1))
         uint32_t m[ROWS];
-        uint64_t packed[NW];
+        uint32_t packed[NW];
 #pragma unroll
         for (uint32_t w = 0; w < NW; ++w) packed[w] = 0;
+        // the byte before each window (one LDS round trip for all rows)
+        uint32_t pb[ROWS];
+#pragma unroll
+        for (uint32_t k = 0; k < ROWS; ++k) pb[k] = (uint8_t)tl[max(k * TILE + tid * 16, 1u) - 1];
 #pragma unroll
         for (uint32_t k = 0; k < ROWS; ++k) {
             const uint64_t at = g0 + k * TILE + tid * 16;
             const uint4 w = v[k];
             const uint32_t nl = compress8(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au)) |
                                 (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
-            const uint32_t prev = (k == 0 && tid == 0) ? prev0 : (uint32_t)(tl[max(k * TILE + tid * 16, 1u) - 1] == '\n');
+            const uint32_t prev = (k == 0 && tid == 0) ? prev0 : (uint32_t)(pb[k] == '\n');
             uint32_t mk = ((nl << 1) | prev) & ~nl & 0xFFFFu;
             if (!inner) {
                 if (at + 16 > c0 && at <= c0) {   // c0 in this window: it starts a line (unless a '\n'), nothing before it does
@@ -1763,33 +1850,53 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
                 if (at + 16 <= c0) mk = 0;
             }
             m[k] = mk;
-            packed[k / FPW] |= (uint64_t)__popc(mk) << (FB * (k % FPW));
+            packed[k / 3] |= (uint32_t)__popc(mk) << (10 * (k % 3));
         }
-        uint64_t tot[NW], pre[NW];
+        // their ranks in file order: a scan over the wave's lanes (DPP, no
+        // LDS round trip), the waves before this one from LDS
+        uint32_t incl[NW];
 #pragma unroll
-        for (uint32_t w = 0; w < NW; ++w) pre[w] = block_exscan64(packed[w], &tot[w]);
-        constexpr uint64_t FM = (1ull << FB) - 1;
+        for (uint32_t w = 0; w < NW; ++w) incl[w] = wave_scan_incl(packed[w]);
+        const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+        if ((tid & 63u) == 63u) {
+#pragma unroll
+            for (uint32_t w = 0; w < NW; ++w) wtot[wid][w] = incl[w];
+        }
+        __syncthreads();
+        // the waves' sums, wave-uniform (scalar): a word's fields 0 and 2,
+        // and field 1, summed apart (up to 2048 a row: 12 bits, room to grow)
+        uint32_t bA[NW], bB[NW], tA[NW], tB[NW];
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) {
+            bA[w] = bB[w] = tA[w] = tB[w] = 0;
+#pragma unroll
+            for (uint32_t w2 = 0; w2 < TB / 64; ++w2) {
+                const uint32_t x = __builtin_amdgcn_readfirstlane(wtot[w2][w]);
+                const uint32_t xa = x & 0x3FF003FFu, xb = x & 0x000FFC00u;
+                tA[w] += xa;
+                tB[w] += xb;
+                bA[w] += w2 < wid ? xa : 0u;
+                bB[w] += w2 < wid ? xb : 0u;
+            }
+        }
         uint32_t nlines = 0;
 #pragma unroll
         for (uint32_t k = 0; k < ROWS; ++k) {
-            uint32_t q = nlines + (uint32_t)((pre[k / FPW] >> (FB * (k % FPW))) & FM);
+            const uint32_t sh = 10 * (k % 3), w = k / 3;
+            const uint32_t before = (((k % 3) == 1 ? bB[w] : bA[w]) >> sh) & 4095u;
+            const uint32_t total = (((k % 3) == 1 ? tB[w] : tA[w]) >> sh) & 4095u;
+            uint32_t q = nlines + before + (((incl[w] - packed[w]) >> sh) & 1023u);
             for (uint32_t mk = m[k]; mk; mk &= mk - 1, ++q)
                 if (q < cap) ls[q] = (uint16_t)(k * TILE + tid * 16 + (uint32_t)(__ffs(mk) - 1));
-            nlines += (uint32_t)((tot[k / FPW] >> (FB * (k % FPW))) & FM);
+            nlines += total;
         }
         const uint32_t cnt = min(nlines, cap);
         if (tid == 0) O.tcnt[t] = nlines;   // (no atomics on one address from every block: summed by the next kernel)
         __syncthreads();
         TP_STAMP_AT(st2);
-        // a later tile's lines into L2: one 4-B load per 128-B line (the
-        // value kept to the kernel's end, so the loads stay in flight)
-        uint32_t pf = 0;
-        {
-            const uint64_t u = t + pf_dist;
-            const uint32_t off = tid * 128u;
-            const uint64_t at = tile_base + u * TP_TILE + off;
-            if (SID_TP_PF && u < ntiles && off < TP_TILE + TP_HALO && at < c1) pf = *(const uint32_t*)(text + at);
-        }
+#if !SID_TP_PF_EARLY
+        PREFETCH_LATER_TILE();
+#endif
         // ---- parse, one lane (a quad of lanes) per line, from LDS; offsets
         // from the tile's first byte (32 bits: a chunk spans less than 4 GiB)
         const char* gtile = text + g0;
@@ -1805,46 +1912,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             const uint32_t j = j0 + (QUAD ? tid >> 2 : tid);
             const bool lead = !QUAD || (tid & 3u) == 0;   // the lane that writes the line's outputs
             int l = 0;
-            if (j < cnt) {
-                const uint32_t r0 = ls[j];
-                const uint64_t s0 = g0 + r0;
-                const uint64_t g = g_tile + j;
-                const char* stage = tl + (r0 & ~15u);
-                const uint32_t sh = r0 & 15u;
-                const uint4 v0 = *(const uint4*)stage, v1 = *(const uint4*)(stage + 16), v2 = *(const uint4*)(stage + 32);
-                uint64_t c = 0, h[2] = {0, 0};
-                uint32_t kd = 0;
-                const int t4 = parse_header(v0, v1, v2, stage, sh, len_t - r0, cls, h, &kd);
-                bool ok = t4 >= 0;
-                if (ok) {
-                    const uint4* first = (const uint4*)(stage + ((sh + (uint32_t)t4) & 0x30u));
-                    ok = QUAD ? read_bases_quad<decltype(ld), uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c)
-                              : read_bases_lut<decltype(ld), uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c);
-                }
-                if (!lead) {
-                } else if (ok) {
-                    const bool hv = (h[0] >> 63) != 0;
-                    const uint32_t clen = (uint32_t)(h[0] >> 32) & 0xFFFu;
-                    if (!hv || clen > 8) h[1] = (uint32_t)s0;   // the writer reads the chrom, or tokenises, from the line
-                    ST_MID(O.hdr + 2 * g, h[0]);
-                    ST_MID(O.hdr + 2 * g + 1, h[1]);
-                    if (!LOCAL) {
-                        ST_MID(O.counts + g, c);
-                    } else if (hv) {
-                        Head hd;
-                        hd.clen = clen;
-                        hd.pos = (int32_t)(uint32_t)h[0];
-                        l = local_site_len(hd, c, g, LL.len1, LL);
-                    } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
-                        l = local_site_len_text(text, c1, s0, c, g, LL);
-                    }
-                    if (LOCAL && l == 0) O.counts[g] = c;   // a fix-up site: the fix-up reads its counts
-                } else {
-                    const unsigned long long k = atomicAdd(O.lb + 6, 1ull);
-                    O.fb[k] = (uint32_t)g;
-                    O.fbo[k] = (uint32_t)s0;
-                }
-            }
+            if (j < cnt) l = tile_line<QUAD, LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, lead, cls, rbl, O, LL);
             if (!LOCAL) continue;
             // the record bytes into the writer blocks' sums: the wave's slots (64,
             // or 16 with quads, from a multiple of 16) lie in one block or two
@@ -3507,19 +3575,15 @@ static uint64_t tile_count(uint64_t c0, uint64_t c1, bool quad)
 
 // The tile parse's prefetch distance: the blocks resident on the device at
 // once (occupancy x CUs), a multiple of the 8 XCDs
-template <bool QUAD, bool LOCAL>
-static uint32_t tile_pf_dist()
+template <class K>
+static uint32_t resident_blocks(K kernel)
 {
-    static const uint32_t resident = [] {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sid_tile_parse_kernel<QUAD, LOCAL>, TB, 0) !=
-                hipSuccess)
-            return 1536u;
-        return (uint32_t)std::max(8, (cus * std::max(per, 1)) & ~7);
-    }();
-    return resident;
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, TB, 0) != hipSuccess)
+        return 1536u;
+    return (uint32_t)std::max(8, (cus * std::max(per, 1)) & ~7);
 }
 
 template <bool LOCAL>
@@ -3527,12 +3591,13 @@ static void launch_tile_parse(bool quad, const char* base, uint64_t c0, uint64_t
                               const LocalLen& LL, hipStream_t st)
 {
     const uint64_t tb = c0 & ~(uint64_t)15;
-    if (quad)
-        sid_tile_parse_kernel<true, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp,
-                                                                         tile_pf_dist<true, LOCAL>(), O, LL);
-    else
-        sid_tile_parse_kernel<false, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp,
-                                                                          tile_pf_dist<false, LOCAL>(), O, LL);
+    if (quad) {
+        static const uint32_t pf = resident_blocks(sid_tile_parse_kernel<true, LOCAL>);
+        sid_tile_parse_kernel<true, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp, pf, O, LL);
+    } else {
+        static const uint32_t pf = resident_blocks(sid_tile_parse_kernel<false, LOCAL>);
+        sid_tile_parse_kernel<false, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp, pf, O, LL);
+    }
 #ifdef SID_TP_STAMP
     {
         const uint64_t m = std::min<uint64_t>(ntp, TP_STAMP_N);
@@ -3546,13 +3611,16 @@ static void launch_tile_parse(bool quad, const char* base, uint64_t c0, uint64_t
                 lo = std::min(lo, v[4 * k + 3]);
                 hi = std::max(hi, v[4 * k + 3]);
             }
-            fprintf(stderr, "tp_stamp quad=%d tiles=%llu us/block: load %.2f index %.2f parse %.2f; starts span %.1f us\n",
+            fprintf(stderr, "tp_stamp quad=%d blocks=%llu us/block: load %.2f index %.2f parse %.2f; starts span %.1f us\n",
                     (int)quad, (unsigned long long)m, a[0] / 100.0 / m, a[1] / 100.0 / m, a[2] / 100.0 / m,
                     (hi - lo) * 0.16);
         }
     }
 #endif
 }
+
+// the unit of the tile parse's slot layout (bytes of text a tile)
+uint32_t sid_tile_unit(bool quad) { return tp_tile(quad); }
 
 uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap, bool quad)
 {
