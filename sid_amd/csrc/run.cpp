@@ -331,13 +331,42 @@ struct Dev {
         return p;
     }
     // the tile parse (sid_chunk_tile_local): its slots per tile for the next
-    // chunk (the most lines a tile of the last chunk had, a thirty-second on
-    // top, rounded up to 32), its shape (a quad of lanes per line for lines over
-    // 256 B on average), and whether it takes the lines at all (at most
-    // SID_TILE_CAP_MAX a tile)
+    // chunk (tile_next / tile_over), its shape (a quad of lanes per line for
+    // lines over 256 B on average), and whether it takes the lines at all (at
+    // most SID_TILE_CAP_MAX a tile)
     uint32_t tile_cap = 288;
     bool tile_quad = false;
     bool tile_ok = true;
+    // slots per tile for at most `lines` lines a tile: multiples of 16, up to
+    // the shape's list (a quad tile of lines too short for its list: the lane
+    // shape instead)
+    void tile_set(uint64_t lines, bool quad)
+    {
+        if (quad && lines > SID_TILE_CAP_MAX_QUAD) {
+            quad = false;
+            lines = lines * sid_tile_unit(false) / sid_tile_unit(true) + 1;
+        }
+        tile_quad = quad;
+        tile_cap = (uint32_t)std::min<uint64_t>(quad ? SID_TILE_CAP_MAX_QUAD : SID_TILE_CAP_MAX,
+                                                std::max<uint64_t>(SID_TILE_CAP_MIN, (lines + 15) & ~15ull));
+    }
+    // after a tiled chunk of n sites over `bytes` of text whose tiles had at
+    // most maxl lines: the next chunk's shape (a quad of lanes per line over
+    // 256 B a line) and slots (the same shape: maxl, a thirty-second and 2 on
+    // top; a new shape: from this chunk's lines per byte, a quarter on top)
+    void tile_next(uint64_t maxl, uint64_t n, uint64_t bytes, bool quad)
+    {
+        const bool q2 = bytes > 256 * n;
+        tile_set(q2 == quad ? maxl + maxl / 32 + 2
+                            : (uint64_t)((double)n * sid_tile_unit(q2) / (double)std::max<uint64_t>(1, bytes) * 1.25) + 1,
+                 q2);
+    }
+    // a tile had more lines than slots (the chunk goes the two-pass way)
+    void tile_over(uint64_t maxl, bool quad)
+    {
+        tile_set(maxl + maxl / 32 + 2, quad);
+        tile_ok = maxl <= SID_TILE_CAP_MAX;
+    }
     uint64_t hold_budget = 0, retain_budget = 0;
     std::atomic<uint64_t> hold_used{0}, retain_used{0};
     std::atomic<bool> hold_full{false};
@@ -1459,10 +1488,6 @@ void compute(sid_engine* e, Dev& d, int pass)
                 if (x == hipSuccess) x = sync();
                 if (x != hipSuccess) return (void)hipfail(e, x);
                 const uint64_t maxl = hs[12];
-                auto cap_for = [](uint64_t lines) {
-                    return (uint32_t)std::min<uint64_t>(SID_TILE_CAP_MAX,
-                                                        std::max<uint64_t>(SID_TILE_CAP_MIN, (lines + 31) & ~31ull));
-                };
                 if (maxl <= lg) {
                     tiled = true;
                     n = hs[10];
@@ -1470,19 +1495,13 @@ void compute(sid_engine* e, Dev& d, int pass)
                     hs[4] = hs[11];
                     // the next chunk's shape and slots (a new shape: from this
                     // chunk's lines per byte, a quarter on top)
-                    const bool q2 = L.c1 - L.c0 > 256 * n;
-                    const uint64_t want = q2 == quad ? maxl + maxl / 32 + 2
-                                                     : (uint64_t)((double)n * sid_tile_unit(q2) /
-                                                                  (double)std::max<uint64_t>(1, L.c1 - L.c0) * 1.25) + 1;
-                    d.tile_quad = q2;
-                    d.tile_cap = cap_for(want);
+                    d.tile_next(maxl, n, L.c1 - L.c0, quad);
                 } else {
                     if (cap) d.pool.put(out, cap, d.s_comp);
                     out = nullptr;
                     cap = 0;
                     via_host = sunk = false;
-                    d.tile_cap = cap_for(maxl + maxl / 32 + 2);
-                    d.tile_ok = maxl <= SID_TILE_CAP_MAX;
+                    d.tile_over(maxl, quad);
                 }
             }
         }
@@ -1505,15 +1524,10 @@ void compute(sid_engine* e, Dev& d, int pass)
             if (x == hipSuccess) x = sync();
             if (x != hipSuccess) return (void)hipfail(e, x);
             const uint64_t maxl = hs[12], m = hs[0];
-            auto cap_for = [](uint64_t lines) {
-                return (uint32_t)std::min<uint64_t>(SID_TILE_CAP_MAX,
-                                                    std::max<uint64_t>(SID_TILE_CAP_MIN, (lines + 31) & ~31ull));
-            };
             if (maxl > cp) {   // a tile with more lines than slots: the two-pass path
                 W.slot_cap = 0;
                 d.prof_end(1, pe);
-                d.tile_cap = cap_for(maxl + maxl / 32 + 2);
-                d.tile_ok = maxl <= SID_TILE_CAP_MAX;
+                d.tile_over(maxl, quad);
             } else {
                 const uint64_t m2 = (m + 1) & ~(uint64_t)1, m4 = (m + 3) & ~(uint64_t)3;
                 const uint64_t pre_bytes = 4 * m4 + 24 * m2;
@@ -1541,12 +1555,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                     if (rc != SID_OK) return (void)fail(e, rc);
                     if (x != hipSuccess) return (void)hipfail(e, x);
                     tiled = true;
-                    const bool q2 = L.c1 - L.c0 > 256 * n;
-                    const uint64_t want = q2 == quad ? maxl + maxl / 32 + 2
-                                                     : (uint64_t)((double)n * sid_tile_unit(q2) /
-                                                                  (double)std::max<uint64_t>(1, L.c1 - L.c0) * 1.25) + 1;
-                    d.tile_quad = q2;
-                    d.tile_cap = cap_for(want);
+                    d.tile_next(maxl, n, L.c1 - L.c0, quad);
                 } else {
                     W.slot_cap = 0;   // no room to keep the parse: the two-pass path
                     d.prof_end(1, pe);

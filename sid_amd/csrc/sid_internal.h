@@ -204,7 +204,8 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
 // or through sid_chunk_index + sid_chunk_parse).  quad: 24 KiB tiles and a
 // quad of lanes per line (lines over 256 B on average), else 20 KiB tiles and
 // a lane per line.
-constexpr uint32_t SID_TILE_CAP_MIN = 64, SID_TILE_CAP_MAX = 1024;   // slots per tile
+constexpr uint32_t SID_TILE_CAP_MIN = 64, SID_TILE_CAP_MAX = 1024;   // slots per tile (multiples of 16)
+constexpr uint32_t SID_TILE_CAP_MAX_QUAD = 256;                       // ... of the quad shape
 uint64_t sid_chunk_tile_slots(uint64_t c0, uint64_t c1, uint32_t cap, bool quad);
 uint32_t sid_tile_unit(bool quad);   // text bytes per tile (the slot layout's unit)
 uint64_t sid_chunk_tile_bound(uint64_t c0, uint64_t c1, uint32_t cap, bool quad);

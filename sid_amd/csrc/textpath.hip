@@ -1635,7 +1635,7 @@ __global__ __launch_bounds__(TB) void sid_local_len_list_kernel(const char* __re
 // line index fused into the parse, so the text is fetched from HBM once and
 // no host round trip separates index and parse (pileup.cpp:13-153 +
 // call.cpp:213-289 up to the record lengths).  One 256-thread block per tile
-// of TP_TILE bytes, copied to LDS with a halo of TP_HALO bytes after it (a
+// of TP_TILE bytes, copied to LDS with a halo (tp_halo) after it (a
 // line that starts in the tile is read from LDS to its end in nearly every
 // case; one that runs past the halo reads the rest from HBM):
 //   load    the tile's 16-B windows, lanes contiguous, non-temporal (each
@@ -1662,9 +1662,12 @@ __global__ __launch_bounds__(TB) void sid_local_len_list_kernel(const char* __re
 // lanes; read_bases_quad, each quad reading 64 consecutive bytes a step).
 constexpr uint32_t TP_ROWS = 5;                 // (the lane-per-line shape: ~253 lines a tile, one round of 256 lanes)
 constexpr uint32_t TP_ROWS_QUAD = 6;
-constexpr uint32_t TP_HALO = 1024;
-constexpr uint32_t TP_CAP_MAX = 1024;           // slots per tile at most (lines of 16 B on average)
-static_assert(TP_CAP_MAX == SID_TILE_CAP_MAX, "the host's cap bound");
+// the halo and the line list per shape: the quad shape's tiles hold few
+// lines (the host picks it for lines over 256 B on average), so 256 slots.
+// (A 512-B halo, LDS for six blocks a CU instead of five, measured slower:
+// 12.93 vs 12.78 ms per C5 step.)
+__host__ __device__ constexpr uint32_t tp_halo(bool) { return 1024; }
+__host__ __device__ constexpr uint32_t tp_cap_max(bool quad) { return quad ? SID_TILE_CAP_MAX_QUAD : SID_TILE_CAP_MAX; }
 __host__ __device__ constexpr uint32_t tp_tile(bool quad) { return (quad ? TP_ROWS_QUAD : TP_ROWS) * TILE; }
 
 struct TileOut {
@@ -1777,8 +1780,9 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     constexpr uint32_t NW = (ROWS + 2) / 3;
     static_assert(TB == 256 && ROWS <= 9, "a lane's windows: three u32s of line-start counts");
     static_assert(FTB % 64 == 0, "a wave's slots lie in one writer block");
+    constexpr uint32_t TP_HALO = tp_halo(QUAD);
     __shared__ __attribute__((aligned(16))) char tl[TP_TILE + TP_HALO + 64];
-    __shared__ uint16_t ls[TP_CAP_MAX];
+    __shared__ uint16_t ls[tp_cap_max(QUAD)];
     __shared__ uint8_t cls[256];
     __shared__ uint32_t rbl[256];
     __shared__ uint32_t wtot[TB / 64][NW];
@@ -3639,7 +3643,7 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
 {
     CType ct;
     if (local_ctype(ctx, conf_type, &ct)) return SID_EINVAL;
-    if (cap < SID_TILE_CAP_MIN || cap > SID_TILE_CAP_MAX || cap % 32) return SID_EINVAL;
+    if (cap < SID_TILE_CAP_MIN || cap > tp_cap_max(quad) || cap % 16) return SID_EINVAL;
     if (c1 > UINT32_MAX) return SID_ELINE;   // line offsets are 32-bit: a line ran the chunk past 4 GiB
     const uint64_t ntp = tile_count(c0, c1, quad);
     const uint64_t slots = ntp * cap;
@@ -3674,7 +3678,7 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
 int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64_t c1, uint32_t cap, bool quad,
                           hipStream_t st)
 {
-    if (cap < SID_TILE_CAP_MIN || cap > SID_TILE_CAP_MAX || cap % 32) return SID_EINVAL;
+    if (cap < SID_TILE_CAP_MIN || cap > tp_cap_max(quad) || cap % 16) return SID_EINVAL;
     if (c1 > UINT32_MAX) return SID_ELINE;   // line offsets are 32-bit: a line ran the chunk past 4 GiB
     const uint64_t ntp = tile_count(c0, c1, quad);
     const uint64_t slots = ntp * cap;

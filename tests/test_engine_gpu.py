@@ -49,6 +49,33 @@ def test_chunked_cli_matches_oracle(sid, oracle, inputs, name, flags, extra):
     assert a.stderr == b.stderr
 
 
+@pytest.mark.parametrize("extra", [["--chunk-bytes", "300000"], ["--chunk-bytes", "1000000", "--devices", "2"]],
+                         ids=["300k", "1m-2dev"])
+def test_tile_parse_quad_shape(sid, oracle, tmp_path, extra):
+    """The quad shape (lines over 256 B on average: a quad of lanes per line,
+    24 KiB tiles, at most 256 slots a tile) and its way out
+    (run.cpp Dev::tile_set): 200x text, then depth-0 lines (~1200 a tile:
+    past the quad list, so the next chunks take the lane shape), 200x text
+    again (back to quads), 30x text, and 200x lines with reads over the halo.
+    Every run's CSV is the oracle's."""
+    deep = sid.synth_text(62, 6_000, 200.0, sites_per_chrom=10 ** 6)
+    normal = sid.synth_text(63, 6_000, 30.0, sites_per_chrom=10 ** 6)
+    zero = b"".join(b"chr2\t%d\tA\t0\t*\t*\n" % i for i in range(1, 30_000))
+    rng = np.random.default_rng(62)
+    alphabet = np.frombuffer(b"ACGTacgt.,$", np.uint8)
+    longl = b"".join(b"chr3\t%d\tG\t600\t%s\t%s\n" % (i, rng.choice(alphabet, 600 + 3 * i).tobytes(),
+                                                        b"I" * (600 + 3 * i)) for i in range(1, 400))
+    text = deep + zero + deep + normal + longl + deep
+    p = tmp_path / "quad.plp"
+    p.write_bytes(text)
+    b = oracle.run_cli([str(p)])
+    a = run(sid.CLI_PATH, extra + [str(p)])
+    assert b.returncode == 0
+    assert a.returncode == 0, a.stderr[-400:]
+    assert a.stdout == b.stdout
+    assert a.stderr == b.stderr
+
+
 @pytest.mark.parametrize("extra", [["--hold-bytes", "1"], ["--hold-bytes", "1", "--retain-bytes", "1"],
                                    ["--hold-bytes", "200000", "--retain-bytes", "150000"]],
                          ids=["all-in-pass-2-kept", "all-reloaded", "mixed"])
@@ -565,10 +592,10 @@ def test_line_past_the_chunk_limit_is_refused(sid):
                          ids=["one-chunk", "100k-2dev", "33k", "host-arena"])
 def test_tile_parse_slot_caps(sid, oracle, tmp_path, extra):
     """-m local's tile parse (textpath.hip sid_tile_parse_kernel) lays its
-    sites out in slots per 16 KiB tile, as many as the device's last chunk
-    needed (run.cpp tile_log2): runs of depth-0 lines (~20 B, ~800 lines a
-    tile: past the 256 slots 30x text takes, so a chunk runs again through
-    the two-pass path and the next ones get more slots), runs of 10-B lines
+    sites out in slots per 20 KiB tile, as many as the device's last chunk
+    needed (run.cpp Dev::tile_next / tile_over): runs of depth-0 lines (~20
+    B, ~1000 lines a tile: past the 288 slots 30x text takes, so a chunk runs
+    again through the two-pass path and the next ones get more slots), runs of 10-B lines
     (more lines than the most slots a tile has: the two-pass path), lines of
     3-5 KiB (past the tile's LDS halo: read from HBM), and 30x text between
     them.  Every run's CSV is the oracle's."""
