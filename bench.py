@@ -215,6 +215,12 @@ def stage_bytes(stage, text_per_site, csv_per_site, fused):
     fused: a fmt_kind, the call / lookup fused into the formatter (it reads
     the 8 B counts instead of the call kernel's 17 B code + confs)."""
     site_in = 8 if fused else 17
+    if fused == "lynch" and stage == "parse":
+        # the Lynch paths' first pass: the tile parse writes every site's
+        # counts (8) and header pair (16) per slot, compacted into the buffer
+        # kept for pass 2 (those read, line offsets (4), counts and pairs
+        # written: textpath.hip sid_tile_compact_kernel)
+        return text_per_site + 24 + 24 + 28
     if tile_parse(fused, text_per_site) and stage in ("parse", "fmt_write"):
         # the tile parse reads the text once and writes each site's 4 B class
         # word and 16 B header pair (textpath.hip sid_tile_parse_kernel); the
@@ -243,6 +249,8 @@ def stage_kernels(stage, fused, text_per_site=81.0):
         "index": ["sid_index_count_kernel", "sid_scan_*"],
         "parse": (["sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_tile_len_list_kernel",
                    "sid_local_fixlen_kernel", "sid_scan_*"] if tp else
+                  ["sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_tile_compact_kernel", "sid_scan_*"]
+                  if fused == "lynch" else
                   ["sid_index_emit_kernel", ("sid_parse_quad_kernel" if parse_quad(text_per_site) else
                                              "sid_parse_kernel"), "sid_parse_serial_kernel"]),
         "call": ["sid_lookup_rec_kernel"],
@@ -536,7 +544,8 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
                 "source": "device_path: HIP event pairs around each engine stage on the compute stream"}
     return {"sites_per_s": sites_all * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
             "stages_ms": stages, "stage_roofline": roofs, "roofline": roofline,
-            "chunks_per_step": chunks,
+            "chunks_per_step": chunks, "chunks_tiled_last_step": st.chunks_tiled,
+            "tile_overflows_last_step": st.tile_overflows,
             "path": {"bytes_per_site": tps + cps, "text_per_site": tps, "csv_per_site": cps,
                      "GBps": (text_bytes + st2.bytes_out) / (elapsed / steps) / 1e9 if text_bytes else None,
                      "note": "text in + CSV out per step (the path's minimum HBM traffic) / ms_per_step"},
@@ -581,7 +590,8 @@ def pcie_stats(a, ln, st, st2, elapsed, lynch):
     pcie = {"text_bytes": ln, "csv_bytes": st2.bytes_out,
             "GBps_h2d": ln / (elapsed / a.steps) / 1e9, "GBps_d2h": st2.bytes_out / (elapsed / a.steps) / 1e9,
             "chunks": st.chunks, "chunks_held_in_host_arena": st.chunks_held, "ingest_s": st.ingest_s,
-            "emit_s": st2.emit_s, "h2d_s_last_step": st.h2d_s,
+            "emit_s": st2.emit_s, "h2d_s_last_step": st.h2d_s, "chunks_tiled_last_step": st.chunks_tiled,
+            "tile_overflows_last_step": st.tile_overflows,
             "h2d_GBps_last_step": st.h2d_bytes / st.h2d_s / 1e9 if st.h2d_s else None}
     pcie["ceiling"] = pcie_ceiling(ln, st2.bytes_out, lynch, elapsed / a.steps)
     return pcie
@@ -685,7 +695,7 @@ def generate_resident(torch, sid_amd, dev, gpu, cfg, first, n):
 
 
 VALU_ISSUE_PER_S = 256 * 4 / 2 * 2.4e9   # wave64 VALU instructions/s: 1024 SIMDs, one per 2 cycles, 2.4 GHz
-PMC_ROUND = os.environ.get("SID_PMC_ROUND", "r04")
+PMC_ROUND = os.environ.get("SID_PMC_ROUND", "r05")
 
 
 def pcie_ceiling(text_bytes, csv_bytes, lynch, step_s):

@@ -338,6 +338,10 @@ typedef struct {
                                     events on the upload streams), summed over
                                     the devices                                    */
     uint64_t h2d_bytes;          /* bytes those copies moved                       */
+    uint64_t chunks_tiled;       /* parsed by the tile parse (text read once)       */
+    uint64_t tile_overflows;     /* chunks with a tile of more lines than its slots
+                                    (parsed again by the two-pass path; the next
+                                    chunks get more slots)                         */
 } sid_run_stats;
 void sid_engine_cfg_default(sid_engine_cfg* cfg);
 int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg, sid_engine** out);

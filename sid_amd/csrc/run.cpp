@@ -375,6 +375,7 @@ struct Dev {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> h2d_pending;
     std::vector<hipEvent_t> h2d_free;
     uint64_t h2d_bytes = 0;
+    uint64_t tiled = 0, tile_overflows = 0;   // this run's chunks (the device's compute thread)
     hipEvent_t h2d_event()
     {
         hipEvent_t ev = nullptr;
@@ -1490,6 +1491,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                 const uint64_t maxl = hs[12];
                 if (maxl <= lg) {
                     tiled = true;
+                    ++d.tiled;
                     n = hs[10];
                     r.parsed = n;
                     hs[4] = hs[11];
@@ -1501,6 +1503,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                     out = nullptr;
                     cap = 0;
                     via_host = sunk = false;
+                    ++d.tile_overflows;
                     d.tile_over(maxl, quad);
                 }
             }
@@ -1527,6 +1530,7 @@ void compute(sid_engine* e, Dev& d, int pass)
             if (maxl > cp) {   // a tile with more lines than slots: the two-pass path
                 W.slot_cap = 0;
                 d.prof_end(1, pe);
+                ++d.tile_overflows;
                 d.tile_over(maxl, quad);
             } else {
                 const uint64_t m2 = (m + 1) & ~(uint64_t)1, m4 = (m + 3) & ~(uint64_t)3;
@@ -1555,6 +1559,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                     if (rc != SID_OK) return (void)fail(e, rc);
                     if (x != hipSuccess) return (void)hipfail(e, x);
                     tiled = true;
+                    ++d.tiled;
                     d.tile_next(maxl, n, L.c1 - L.c0, quad);
                 } else {
                     W.slot_cap = 0;   // no room to keep the parse: the two-pass path
@@ -1940,6 +1945,7 @@ static void reset_run(sid_engine* e)
         d.hh_full = false;
         (void)d.h2d_collect();   // (a failed run's copies: its devices were synchronised)
         d.h2d_bytes = 0;
+        d.tiled = d.tile_overflows = 0;
     }
     e->hist_merged = false;
 }
@@ -2063,7 +2069,7 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         return e->rc.load();
     }
     double h2d_s = 0;
-    uint64_t h2d_bytes = 0;
+    uint64_t h2d_bytes = 0, tiled = 0, tile_over = 0;
     for (auto& dp : e->devs) {
         (void)hipSetDevice(dp->device);
         if (hipStreamSynchronize(dp->s_comp) != hipSuccess || hipStreamSynchronize(dp->s_up) != hipSuccess ||
@@ -2072,6 +2078,9 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         h2d_s += dp->h2d_collect();
         h2d_bytes += dp->h2d_bytes;
         dp->h2d_bytes = 0;
+        tiled += dp->tiled;
+        tile_over += dp->tile_overflows;
+        dp->tiled = dp->tile_overflows = 0;
     }
     uint64_t sites = 0, bytes = 0, held = 0, kept = 0;
     for (auto& r : e->recs) {
@@ -2094,6 +2103,8 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         st->register_s = e->t_register.load() * 1e-9;
         st->h2d_s = h2d_s;
         st->h2d_bytes = h2d_bytes;
+        st->chunks_tiled = tiled;
+        st->tile_overflows = tile_over;
     }
     timing_report(e, "ingest", wall() - t0);
     const uint64_t fe = e->first_err.load();

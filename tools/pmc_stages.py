@@ -36,7 +36,15 @@ def main():
     pm = json.load(open(tmp))
     b = json.load(open(bench))
     sites = b["roofline"]["sites_per_launch"]
+    tile = "sid_tile_parse_kernel" in pm
     for stage, ks in STAGES.items():
+        if tile and stage == "parse":
+            # the tile parse's stage (the two-pass kernels only ran for chunks
+            # whose tiles overflowed their slots: not the stage's steady state)
+            ks = ["sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_tile_len_list_kernel",
+                  "sid_tile_compact_kernel"]
+        if tile and stage == "index":
+            continue
         tot, parts = 0.0, {}
         for k in ks:
             r = pm.get(k)
