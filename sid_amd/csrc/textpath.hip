@@ -1934,6 +1934,10 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     }
 }
 
+// (64 blocks: the tiles' sum and maximum are one atomic per block on one
+// address each, which serialise; 256 blocks took 20 us a launch)
+constexpr unsigned TILE_SERIAL_GRID = 64;
+
 // the general routine over the tile parse's leftovers (slot, line offset):
 // counts and a header pair with no chrom (the formatter tokenises the line),
 // the slot listed for its record length; and the tiles' line counts summed
@@ -3653,7 +3657,7 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
     const LocalLen LL{ctx->ws.len1, ctx->ws.len2, W->bsum, miss, W->lb, W->cls};
     const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
     launch_tile_parse<true>(quad, base, c0, c1, ntp, O, LL, st);
-    sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap,
+    sid_tile_serial_kernel<<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap,
                                                W->counts, W->hdr, (unsigned long long*)(W->state + 4), late,
                                                W->lb + 7);
     sid_tile_len_list_kernel<<<64, TB, 0, st>>>(base, c1, W->hdr, W->counts, late, W->lb + 7, LL);
@@ -3687,7 +3691,7 @@ int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64
     const LocalLen LL{};
     const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
     launch_tile_parse<false>(quad, base, c0, c1, ntp, O, LL, st);
-    sid_tile_serial_kernel<<<256, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap, W->counts,
+    sid_tile_serial_kernel<<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap, W->counts,
                                                W->hdr, (unsigned long long*)(W->state + 4), nullptr, nullptr);
     // the tiles' first sites in file order (state[0]: the chunk's sites; over the cap: void)
     launch_scan(W->tcnt, ntp, W->toff, W->state, nullptr,
