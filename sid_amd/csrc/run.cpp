@@ -1385,6 +1385,10 @@ void compute(sid_engine* e, Dev& d, int pass)
     // that reads the formatter's byte count); indexed: its site count is in hs[0]
     Loaded nextL;
     bool have_next = false, next_indexed = false;
+    // ... or its tile parse behind this chunk's writer (tiled: with next_lg
+    // slots a tile, the next_quad shape)
+    bool next_tiled = false, next_quad = false;
+    uint32_t next_lg = 0;
     auto take = [&](Loaded& out) {
         if (have_next) {
             out = nextL;
@@ -1397,6 +1401,8 @@ void compute(sid_engine* e, Dev& d, int pass)
     while (take(L)) {
         const bool pre_indexed = next_indexed;
         next_indexed = false;
+        bool pre_tiled = next_tiled;
+        next_tiled = false;
         if (e->rc.load() != SID_OK) break;
         ChunkRec& r = e->recs[L.j];
         auto release_slot = [&]() {
@@ -1416,18 +1422,21 @@ void compute(sid_engine* e, Dev& d, int pass)
             continue;
         }
         if (pass == 1 && L.j > e->first_err.load()) {
+            if (pre_tiled) W.slot_cap = 0;
             release_slot();
             continue;
         }
         int rc = SID_OK;
         hipError_t x = hipSuccess;
-        if (L.ev && !pre_indexed) x = hipStreamWaitEvent(d.s_comp, L.ev, 0);
+        if (L.ev && !pre_indexed && !pre_tiled) x = hipStreamWaitEvent(d.s_comp, L.ev, 0);
         const bool P = e->prof;
         if (P && pass == 1) d.prof_chunks++;   // chunks, not passes: a Lynch run formats each chunk again in pass 2
-        W.lens_ready = false;   // (set by this chunk's parse when it computes the -m local record lengths)
-        W.cls_ready = false;    // (... and the class words)
+        if (!pre_tiled) {
+            W.lens_ready = false;   // (set by this chunk's parse when it computes the -m local record lengths)
+            W.cls_ready = false;    // (... and the class words)
+        }
         const uint64_t tbytes = L.c1 - (L.c0 & ~(uint64_t)15);
-        if (x == hipSuccess && !pre_indexed) rc = sid_chunk_reserve(&W, tbytes, 0);
+        if (x == hipSuccess && !pre_indexed && !pre_tiled) rc = sid_chunk_reserve(&W, tbytes, 0);
         const bool lynch_hist = pass == 1 && e->lynch;
         const bool format = pass == 2 || (needs_format_pass1(e) && (!d.hold_full.load() || sink_all_pass1(e)));
         // -m local / quality (and pass 2 of the Lynch paths): call, then the
@@ -1446,12 +1455,20 @@ void compute(sid_engine* e, Dev& d, int pass)
         // with more lines than its slots sends the chunk again through the
         // two-pass path below (its records dropped), the next chunks with
         // more slots
+        // (pre_tiled: this chunk's tile parse already ran behind the previous
+        // chunk's writer, with the slots and shape of that time)
         bool tiled = false;
-        if (x == hipSuccess && rc == SID_OK && format && !lynch_hist && !qmode && d.tile_ok &&
-            e->opts.method == SID_METHOD_LOCAL && sid_chunk_local_ok(d.ctx) && !(pass == 2 && r.pre)) {
-            const uint32_t lg = d.tile_cap;
-            const bool quad = d.tile_quad;
-            rc = sid_chunk_reserve(&W, tbytes, sid_chunk_tile_slots(L.c0, L.c1, lg, quad));
+        const bool tile_path = x == hipSuccess && rc == SID_OK && format && !lynch_hist && !qmode &&
+                               (d.tile_ok || pre_tiled) && e->opts.method == SID_METHOD_LOCAL &&
+                               sid_chunk_local_ok(d.ctx) && !(pass == 2 && r.pre);
+        if (pre_tiled && !tile_path) {
+            W.slot_cap = 0;   // (its slots unused: the dense layout again)
+            pre_tiled = false;
+        }
+        if (tile_path) {
+            const uint32_t lg = pre_tiled ? next_lg : d.tile_cap;
+            const bool quad = pre_tiled ? next_quad : d.tile_quad;
+            if (!pre_tiled) rc = sid_chunk_reserve(&W, tbytes, sid_chunk_tile_slots(L.c0, L.c1, lg, quad));
             if (rc != SID_OK) return (void)fail(e, rc);
             const uint64_t bound = sid_chunk_tile_bound(L.c0, L.c1, lg, quad);
             // the records' buffer, taken as the two-pass path below takes it
@@ -1473,10 +1490,16 @@ void compute(sid_engine* e, Dev& d, int pass)
                 out = d.pool.get(bound, &cap, d.s_comp);
                 if (!out) cap = 0;
             }
+            if (!out && pre_tiled) {
+                W.slot_cap = 0;
+                pre_tiled = false;
+            }
             if (out) {
-                pe = d.prof_begin(P);
-                rc = sid_chunk_tile_local(d.ctx, &W, L.base, L.c0, L.c1, lg, quad, e->conf_type, d.s_comp);
-                d.prof_end(1, pe);
+                if (!pre_tiled) {
+                    pe = d.prof_begin(P);
+                    rc = sid_chunk_tile_local(d.ctx, &W, L.base, L.c0, L.c1, lg, quad, e->conf_type, d.s_comp);
+                    d.prof_end(1, pe);
+                }
                 if (rc == SID_OK) {
                     pe = d.prof_begin(P);
                     rc = sid_chunk_local_put(d.ctx, &W, L.base, L.c1, 0, e->conf_type, out, d.s_comp);
@@ -1486,6 +1509,34 @@ void compute(sid_engine* e, Dev& d, int pass)
                 if (rc != SID_OK) return (void)fail(e, rc);
                 // bytes, range flag, sites, parse error key, the most lines in a tile
                 x = hipMemcpyAsync(hs + 8, W.lb + 1, 5 * 8, hipMemcpyDeviceToHost, d.s_comp);
+                // the next chunk's tile parse behind this writer (stream order:
+                // it rewrites the slots and W.lb after the writer and the copy
+                // have read them), so the GPU does not idle over the host round
+                // trip; with this chunk's slots and shape (a change takes effect
+                // a chunk later), dropped if this chunk overflows
+                if (x == hipSuccess && d.loaded.try_pop(nextL)) {
+                    have_next = true;
+                    const ChunkRec& r2 = e->recs[nextL.j];
+                    if (nextL.kind == 0 && !(pass == 2 && r2.pre) && !(pass == 1 && nextL.j > e->first_err.load())) {
+                        const uint32_t lg2 = d.tile_cap;
+                        const bool q2 = d.tile_quad;
+                        if (nextL.ev) x = hipStreamWaitEvent(d.s_comp, nextL.ev, 0);
+                        int rc2 = SID_OK;
+                        // growth frees buffers: hipFree waits for the queued work first
+                        if (x == hipSuccess)
+                            rc2 = sid_chunk_reserve(&W, nextL.c1 - (nextL.c0 & ~(uint64_t)15),
+                                                    sid_chunk_tile_slots(nextL.c0, nextL.c1, lg2, q2));
+                        hipEvent_t pe2 = d.prof_begin(P);
+                        if (rc2 == SID_OK && x == hipSuccess)
+                            rc2 = sid_chunk_tile_local(d.ctx, &W, nextL.base, nextL.c0, nextL.c1, lg2, q2,
+                                                       e->conf_type, d.s_comp);
+                        d.prof_end(1, pe2);
+                        if (rc2 != SID_OK) return (void)fail(e, rc2);
+                        next_tiled = x == hipSuccess;
+                        next_lg = lg2;
+                        next_quad = q2;
+                    }
+                }
                 if (x == hipSuccess) x = sync();
                 if (x != hipSuccess) return (void)hipfail(e, x);
                 const uint64_t maxl = hs[12];
@@ -1505,6 +1556,10 @@ void compute(sid_engine* e, Dev& d, int pass)
                     via_host = sunk = false;
                     ++d.tile_overflows;
                     d.tile_over(maxl, quad);
+                    // this chunk goes the two-pass way through the workspace:
+                    // the next chunk's tile parse is dropped (it runs again)
+                    W.slot_cap = 0;
+                    next_tiled = false;
                 }
             }
         }
@@ -1824,6 +1879,7 @@ void compute(sid_engine* e, Dev& d, int pass)
         it.ev = ev;
         if (!d.drain_q.push(it)) break;
     }
+    W.slot_cap = 0;   // (a tile parse run ahead for a chunk this pass then skipped)
     if (pass == 2) d.drain_q.close();
 }
 
@@ -1946,6 +2002,7 @@ static void reset_run(sid_engine* e)
         (void)d.h2d_collect();   // (a failed run's copies: its devices were synchronised)
         d.h2d_bytes = 0;
         d.tiled = d.tile_overflows = 0;
+        d.ws.slot_cap = 0;   // (a failed run may leave the slot layout set)
     }
     e->hist_merged = false;
 }

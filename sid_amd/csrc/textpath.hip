@@ -1755,12 +1755,16 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
 // resident on the device, a multiple of the 8 XCDs; that tile's block then
 // runs about when this one ends, on the same XCD, and its loads hit L2).
 #ifdef SID_TP_STAMP
-// (diagnostic builds: per-phase wall-clock sums of the tile parse's blocks)
+// (diagnostic builds: per-phase wall-clock stamps of the tile parse's and the
+// -m local writer's blocks, thread 0 of each)
 constexpr uint32_t TP_STAMP_N = 1u << 20;
 __device__ uint32_t tp_stamp[TP_STAMP_N][4];
+__device__ uint32_t put_stamp[TP_STAMP_N][4];
 #define TP_STAMP_AT(v) const uint64_t v = tid == 0 ? wall_clock64() : 0
+#define PUT_STAMP_AT(v) const uint64_t v = threadIdx.x == 0 ? wall_clock64() : 0
 #else
 #define TP_STAMP_AT(v)
+#define PUT_STAMP_AT(v)
 #endif
 template <bool QUAD, bool LOCAL>
 __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restrict__ text, uint64_t tile_base,
@@ -1807,9 +1811,22 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
         // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
         const uint32_t prev0 = tid ? 0u : (g0 > c0 && g0 - 1 < c1) ? (text[g0 - 1] == '\n') : 1u;
+        // ---- line starts (bit j: byte j of the window starts a non-empty
+        // line in [c0, c1)): the windows' own part from the registers while
+        // the block's other loads land (newline bits 16-31, the starts after
+        // a newline inside the window 0-15), the byte before each window after
+        // the barrier
+        uint32_t nm[ROWS];
+#pragma unroll
+        for (uint32_t k = 0; k < ROWS; ++k) {
+            const uint4 w = v[k];
+            const uint32_t nl = compress8(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au)) |
+                                (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
+            nm[k] = (nl << 16) | ((nl << 1) & ~nl & 0xFFFFu);
+            asm volatile("" : "+v"(nm[k]));   // (computed here, not sunk past the barrier)
+        }
         __syncthreads();
         TP_STAMP_AT(st1);
-        // ---- line starts (bit j: byte j of the window starts a non-empty line in [c0, c1))
         uint32_t m[ROWS];
         uint32_t packed[NW];
 #pragma unroll
@@ -1821,11 +1838,9 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
 #pragma unroll
         for (uint32_t k = 0; k < ROWS; ++k) {
             const uint64_t at = g0 + k * TILE + tid * 16;
-            const uint4 w = v[k];
-            const uint32_t nl = compress8(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au)) |
-                                (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
+            const uint32_t nl = nm[k] >> 16;
             const uint32_t prev = (k == 0 && tid == 0) ? prev0 : (uint32_t)(pb[k] == '\n');
-            uint32_t mk = ((nl << 1) | prev) & ~nl & 0xFFFFu;
+            uint32_t mk = (nm[k] & 0xFFFFu) | (prev & ~nl & 1u);
             if (!inner) {
                 if (at + 16 > c0 && at <= c0) {   // c0 in this window: it starts a line (unless a '\n'), nothing before it does
                     const uint32_t j = (uint32_t)(c0 - at);
@@ -2293,6 +2308,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
                                                            unsigned long long* lb, char* __restrict__ out)
 {
     constexpr int NQ = (FMT_LDS2 + 64) / 16;   // records, slack
+    PUT_STAMP_AT(ps0);
     __shared__ uint4 buf4[NQ];
     for (int k = threadIdx.x; k < NQ; k += FTB) buf4[k] = make_uint4(0, 0, 0, 0);
     unsigned long long* const B = (unsigned long long*)buf4;
@@ -2349,9 +2365,11 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
             l = miss_len(h, c, hom[i], het[i], ct);
         }
     }
+    PUT_STAMP_AT(ps1);
     if (blockIdx.x == 0 && threadIdx.x == 0) lb[4] = state[4];
     uint32_t tot;
     const uint32_t my = block_exscan<FTB>((uint32_t)l, &tot);   // (its barriers also order the zeroing)
+    PUT_STAMP_AT(ps2);
     char* const dst = out + boff[blockIdx.x];
     if (tot > FMT_LDS2) {   // long records (long chromosome names): straight to global, byte by byte
         if (l && tab) record_put_tail(text, len, h, c, ea, eb, dst + my);
@@ -2383,7 +2401,17 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         miss_or(text, len, h, c, hom[i], het[i], ct, B, my);
     }
     __syncthreads();
+    PUT_STAMP_AT(ps3);
     block_store<true>((const char*)buf4, tot, dst);
+#ifdef SID_TP_STAMP
+    if (CLS && tcnt && threadIdx.x == 0 && blockIdx.x < TP_STAMP_N) {
+        const uint64_t ps4 = wall_clock64();
+        put_stamp[blockIdx.x][0] = (uint32_t)(ps1 - ps0);
+        put_stamp[blockIdx.x][1] = (uint32_t)(ps2 - ps1);
+        put_stamp[blockIdx.x][2] = (uint32_t)(ps3 - ps2);
+        put_stamp[blockIdx.x][3] = (uint32_t)(ps4 - ps3);
+    }
+#endif
 }
 
 // ---- likelihood_ratio / bayes, fused with the class lookup: a site's
@@ -3546,6 +3574,20 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
                                                                  ctx->ws.str2, W->code, W->hom, W->het, ct, W->boff,
                                                                  W->state, W->lb, out);
         WCHECK(hipGetLastError());
+#ifdef SID_TP_STAMP
+        {
+            const uint64_t m = std::min<uint64_t>(nbs, TP_STAMP_N);
+            std::vector<uint32_t> v(m * 4);
+            if (hipStreamSynchronize(st) == hipSuccess &&
+                hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(put_stamp), m * 16) == hipSuccess && m) {
+                double a[4] = {0, 0, 0, 0};
+                for (uint64_t k = 0; k < m; ++k)
+                    for (int j = 0; j < 4; ++j) a[j] += v[4 * k + j];
+                fprintf(stderr, "put_stamp blocks=%llu us/block: loads+len %.2f scan %.2f lds %.2f store %.2f\n",
+                        (unsigned long long)m, a[0] / 100.0 / m, a[1] / 100.0 / m, a[2] / 100.0 / m, a[3] / 100.0 / m);
+            }
+        }
+#endif
         return SID_OK;
     }
     if (nb == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
