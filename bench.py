@@ -490,9 +490,11 @@ def device_engine(cfg, gpu, chunk_mib, device_sink=1, **kw):
 
 
 def device_path(R, a, cfg, text, ln, lynch, gen=None):
-    """The same sid run over text resident in HBM, records left in HBM, with
-    HIP event pairs around every engine stage on the compute stream: the
-    kernels' own rate and the roofline of the dominant stage."""
+    """The same sid run over text resident in HBM, records left in HBM: the
+    kernels' own rate (the timed steps as the product runs them), then the
+    same steps again with HIP event pairs around every engine stage on the
+    compute stream (timing events: each pair costs the stream a few us) for
+    the stage split and the roofline of the dominant stage."""
     steps = a.device_steps or max(a.steps, 10)
     eng = device_engine(cfg, R.gpu, a.chunk_mib)
     if gen is None:
@@ -503,13 +505,18 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
     eng.profile(False)
 
     def step():
+        return R.run_step(eng, lynch)
+
+    def pstep():
         eng.profile(True)
         return R.run_step(eng, lynch)
     for _ in range(2):
         R.run_step(eng, lynch)
-    eng.profile_read()
     elapsed, (st, st2, _) = R.timed(step, steps, 0)
+    eng.profile_read()
+    elapsed_prof, _ = R.timed(pstep, steps, 0)
     prof = eng.profile_read()
+    elapsed_prof = R.max_over_ranks([elapsed_prof])[0]
     eng.profile(False)
     eng.close()
     stages = {k[:-3]: v / steps for k, v in prof.items() if k.endswith("_ms")}
@@ -543,7 +550,10 @@ def device_path(R, a, cfg, text, ln, lynch, gen=None):
                 "valu": valu_issue(dom, per_launch_sites, d["launch_ms"], stage_kernels(dom, fused, tps), a.config),
                 "source": "device_path: HIP event pairs around each engine stage on the compute stream"}
     return {"sites_per_s": sites_all * steps / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
-            "stages_ms": stages, "stage_roofline": roofs, "roofline": roofline,
+            "ms_per_step_profiled": elapsed_prof / steps * 1e3,
+            "stages_ms": stages, "stages_note": "HIP event pairs around every stage, in a second run of the same "
+                                                "steps (ms_per_step_profiled)",
+            "stage_roofline": roofs, "roofline": roofline,
             "chunks_per_step": chunks, "chunks_tiled_last_step": st.chunks_tiled,
             "tile_overflows_last_step": st.tile_overflows,
             "path": {"bytes_per_site": tps + cps, "text_per_site": tps, "csv_per_site": cps,
