@@ -1514,7 +1514,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                 // have read them), so the GPU does not idle over the host round
                 // trip; with this chunk's slots and shape (a change takes effect
                 // a chunk later), dropped if this chunk overflows
-                if (x == hipSuccess && d.loaded.try_pop(nextL)) {
+                if (x == hipSuccess && !have_next && d.loaded.try_pop(nextL)) {
                     have_next = true;
                     const ChunkRec& r2 = e->recs[nextL.j];
                     if (nextL.kind == 0 && !(pass == 2 && r2.pre) && !(pass == 1 && nextL.j > e->first_err.load())) {
@@ -1750,7 +1750,9 @@ void compute(sid_engine* e, Dev& d, int pass)
                 x = hipMemcpyAsync(hs + 8, W.lb + 1, 32, hipMemcpyDeviceToHost, d.s_comp);   // bytes, flags, error
                 // the next chunk's line index behind the formatter (stream
                 // order: it rewrites W.state only after the formatter has read it)
-                if (x == hipSuccess && d.loaded.try_pop(nextL)) {
+                // (not when the tile path already took the next chunk: this
+                // chunk overflowed its slots and came here)
+                if (x == hipSuccess && !have_next && d.loaded.try_pop(nextL)) {
                     have_next = true;
                     const ChunkRec& r2 = e->recs[nextL.j];
                     if (nextL.kind == 0 && !(pass == 2 && r2.pre) && !(pass == 1 && nextL.j > e->first_err.load())) {
