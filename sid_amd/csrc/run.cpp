@@ -2100,9 +2100,11 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
     const double t0 = wall();
     reset_run(e);
     int rc = setup_budgets(e);
+    const double t_budget = wall();
     if (rc == SID_OK) rc = setup_generator(e);
     if (rc != SID_OK) return rc;
     start_queues(e);
+    const double t_setup = wall();
     const int D = (int)e->devs.size();
     if (e->lynch)
         for (auto& dp : e->devs)
@@ -2121,12 +2123,17 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         th.emplace_back([e] {
             for (auto& dp : e->devs) (void)alloc_ring(*dp);
         });
+    const double t_spawn = wall();
     for (auto& t : th) t.join();
+    const double t_join = wall();
     if (e->rc.load() != SID_OK) {
         close_all(e);
         for (auto& dp : e->devs) (void)hipSetDevice(dp->device), (void)hipDeviceSynchronize();
         return e->rc.load();
     }
+    if (std::getenv("SID_ENGINE_TIMING"))
+        std::fprintf(stderr, "{\"ingest_setup_s\": %.6f, \"budgets_s\": %.6f, \"spawn_s\": %.6f, \"join_s\": %.6f}\n",
+                     t_setup - t0, t_budget - t0, t_spawn - t_setup, t_join - t_spawn);
     double h2d_s = 0;
     uint64_t h2d_bytes = 0, tiled = 0, tile_over = 0;
     for (auto& dp : e->devs) {
