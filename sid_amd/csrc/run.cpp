@@ -340,6 +340,7 @@ struct Dev {
     // slots per tile for at most `lines` lines a tile: multiples of 16, up to
     // the shape's list (a quad tile of lines too short for its list: the lane
     // shape instead)
+    uint64_t tile_hi = 0;   // the lines a tile should have room for (a decaying maximum over chunks)
     void tile_set(uint64_t lines, bool quad)
     {
         if (quad && lines > SID_TILE_CAP_MAX_QUAD) {
@@ -347,19 +348,24 @@ struct Dev {
             lines = lines * sid_tile_unit(false) / sid_tile_unit(true) + 1;
         }
         tile_quad = quad;
+        tile_hi = lines;
         tile_cap = (uint32_t)std::min<uint64_t>(quad ? SID_TILE_CAP_MAX_QUAD : SID_TILE_CAP_MAX,
                                                 std::max<uint64_t>(SID_TILE_CAP_MIN, (lines + 15) & ~15ull));
     }
     // after a tiled chunk of n sites over `bytes` of text whose tiles had at
     // most maxl lines: the next chunk's shape (a quad of lanes per line over
     // 256 B a line) and slots (the same shape: maxl, a thirty-second and 2 on
-    // top; a new shape: from this chunk's lines per byte, a quarter on top)
+    // top, or the room recent chunks needed, less a sixty-fourth a chunk --
+    // chunks whose fullest tiles alternate would otherwise overflow every
+    // other chunk; a new shape: from this chunk's lines per byte, a quarter on
+    // top)
     void tile_next(uint64_t maxl, uint64_t n, uint64_t bytes, bool quad)
     {
         const bool q2 = bytes > 256 * n;
-        tile_set(q2 == quad ? maxl + maxl / 32 + 2
-                            : (uint64_t)((double)n * sid_tile_unit(q2) / (double)std::max<uint64_t>(1, bytes) * 1.25) + 1,
-                 q2);
+        if (q2 == quad)
+            tile_set(std::max<uint64_t>(maxl + maxl / 32 + 2, tile_hi - tile_hi / 64), q2);
+        else
+            tile_set((uint64_t)((double)n * sid_tile_unit(q2) / (double)std::max<uint64_t>(1, bytes) * 1.25) + 1, q2);
     }
     // a tile had more lines than slots (the chunk goes the two-pass way)
     void tile_over(uint64_t maxl, bool quad)

@@ -1811,22 +1811,12 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
         // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
         const uint32_t prev0 = tid ? 0u : (g0 > c0 && g0 - 1 < c1) ? (text[g0 - 1] == '\n') : 1u;
-        // ---- line starts (bit j: byte j of the window starts a non-empty
-        // line in [c0, c1)): the windows' own part from the registers while
-        // the block's other loads land (newline bits 16-31, the starts after
-        // a newline inside the window 0-15), the byte before each window after
-        // the barrier
-        uint32_t nm[ROWS];
-#pragma unroll
-        for (uint32_t k = 0; k < ROWS; ++k) {
-            const uint4 w = v[k];
-            const uint32_t nl = compress8(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au)) |
-                                (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
-            nm[k] = (nl << 16) | ((nl << 1) & ~nl & 0xFFFFu);
-            asm volatile("" : "+v"(nm[k]));   // (computed here, not sunk past the barrier)
-        }
         __syncthreads();
         TP_STAMP_AT(st1);
+        // ---- line starts (bit j: byte j of the window starts a non-empty line in [c0, c1))
+        // (the windows' newline masks computed before the barrier, while the
+        // block's other loads land, measured 1 % slower: parse 1.912 vs 1.889
+        // ms per C2 step)
         uint32_t m[ROWS];
         uint32_t packed[NW];
 #pragma unroll
@@ -1838,9 +1828,11 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
 #pragma unroll
         for (uint32_t k = 0; k < ROWS; ++k) {
             const uint64_t at = g0 + k * TILE + tid * 16;
-            const uint32_t nl = nm[k] >> 16;
+            const uint4 w = v[k];
+            const uint32_t nl = compress8(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au)) |
+                                (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
             const uint32_t prev = (k == 0 && tid == 0) ? prev0 : (uint32_t)(pb[k] == '\n');
-            uint32_t mk = (nm[k] & 0xFFFFu) | (prev & ~nl & 1u);
+            uint32_t mk = ((nl << 1) | prev) & ~nl & 0xFFFFu;
             if (!inner) {
                 if (at + 16 > c0 && at <= c0) {   // c0 in this window: it starts a line (unless a '\n'), nothing before it does
                     const uint32_t j = (uint32_t)(c0 - at);
