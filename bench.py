@@ -472,11 +472,11 @@ def bench_weak(R, a, cfg):
     return out, []
 
 
-# C4 / C5 with the rank's shard resident in HBM: 2 GiB chunks, the engine's
-# default for resident text (C4 on one GPU: 1.50e10 sites/s against 1.41e10
-# with 1 GiB chunks, profiles/bench_c4_r04.json; the device sink formats into
-# a pooled buffer, so the records need no hold arena beside the text)
-STRONG_RESIDENT_CHUNK_MIB = 2048
+# C4 / C5 with the rank's shard resident in HBM: 4000 MiB chunks, the
+# engine's default for resident text (C5 per shard: 13.74 vs 14.16 ms with
+# 2 GiB chunks, profiles/ab_engine_r05.log; the device sink formats into a
+# pooled buffer, so the records need no hold arena beside the text)
+STRONG_RESIDENT_CHUNK_MIB = 4000
 
 
 def device_engine(cfg, gpu, chunk_mib, device_sink=1, **kw):

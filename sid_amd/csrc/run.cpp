@@ -623,7 +623,7 @@ int hipfail(sid_engine* e, hipError_t x)
 // larger ones (every chunk costs a few fixed launches and two host round
 // trips; the workspace is a few hundred MB per GiB of text)
 const uint64_t CHUNK_HOST = 128ull << 20;
-const uint64_t CHUNK_DEVICE = 2ull << 30;   // C2: 1 GiB 5.78-5.84, 2 GiB 5.51-5.59, 4.2 GB 5.59-5.61 ms per 50M sites
+const uint64_t CHUNK_DEVICE = 4000ull << 20;   // C2 2.95-2.97 vs 2.97-2.99 ms with 2 GiB, C5 13.7 vs 14.2 ms (round 5)
 const uint64_t CHUNK_SYNTH = 512ull << 20;
 
 uint64_t chunk_bytes(const sid_engine* e)

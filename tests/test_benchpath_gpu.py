@@ -5,7 +5,7 @@ C2 (BASELINE.json configs[1]): seed 2, 50M sites, -m local.  C3 (configs[2]):
 seed 3, 50M sites, -R -m likelihood_ratio.  For each, the text is made by the
 device generator exactly as bench.py makes it, then run through
   - the device path (bench.py `device_path`): text resident in HBM, the
-    engine's defaults for it (2 GiB chunks, the HBM hold arena; C3: the
+    engine's defaults for it (4000 MiB chunks, the HBM hold arena; C3: the
     pass-1 parse kept for pass 2), the records copied back and written;
   - the PCIe path (bench.py `value`): the text in pinned host memory,
     128 MiB chunks, records copied into the engine's pinned host arena
@@ -87,8 +87,8 @@ def test_c2_device_path_equals_oracle(sid, c2):
     eng.source_device_text(text.data_ptr(), ln, keep=text)
     out, st = eng.run()
     eng.close()
-    assert st.sites == N and st.chunks == 2 and st.chunks_held == 2
-    assert_same(out, ref, "C2 device path (text in HBM, 2 GiB chunks, hold arena)")
+    assert st.sites == N and st.chunks == 1 and st.chunks_held == 1   # (4.07 GB: one 4000 MiB chunk)
+    assert_same(out, ref, "C2 device path (text in HBM, the default chunks, hold arena)")
 
 
 @pytest.mark.timeout(900)
@@ -150,7 +150,7 @@ def test_c3_pcie_path_equals_oracle(sid, c3):
 
 # ---- C4 / C5 (configs[3], configs[4]): the strong-scaling device path ----
 # bench.py bench_strong: the rank's shard generated into HBM by
-# generate_resident, then device_path's engine (device_engine) with 2 GiB
+# generate_resident, then device_path's engine (device_engine) with 4000 MiB
 # chunks (STRONG_RESIDENT_CHUNK_MIB).  Here the same engine with device_sink
 # 0, so the records come back, at sizes that span several chunks.
 
@@ -168,9 +168,8 @@ def resident_shard(bench_mod, sid, cfg, first, n):
 @pytest.fixture(scope="module")
 def c5(sid, gpu, oracle, bench_mod, tmp_path_factory):
     """15M sites of C5 (seed 5, 200x, 125M-site chromosomes): ~6.3 GB of text,
-    6 chunks of 1 GiB or 3 of 2 GiB; lines of ~420 B, so the parse runs on the
-    line-length-sized grid with the separate -m local length kernel
-    (textpath.hip sid_chunk_parse: lines over 256 B)."""
+    6 chunks of 1 GiB, 3 of 2 GiB or 2 of 4000 MiB; lines of ~420 B, so the
+    tile parse takes its quad shape after the first chunk."""
     cfg = bench_mod.CONFIGS["C5"]
     n = 15_000_000
     text, ln = resident_shard(bench_mod, sid, cfg, 0, n)
@@ -180,18 +179,18 @@ def c5(sid, gpu, oracle, bench_mod, tmp_path_factory):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("chunk_mib", [2048, 1024], ids=["bench-2GiB", "1GiB"])
+@pytest.mark.parametrize("chunk_mib", [4000, 2048, 1024], ids=["bench-4000MiB", "2GiB", "1GiB"])
 def test_c5_device_path_equals_oracle(sid, bench_mod, c5, chunk_mib):
     cfg, text, ln, n, ref = c5
-    if chunk_mib == 2048:
-        assert bench_mod.STRONG_RESIDENT_CHUNK_MIB == 2048   # the chunking bench_strong uses
+    if chunk_mib == 4000:
+        assert bench_mod.STRONG_RESIDENT_CHUNK_MIB == 4000   # the chunking bench_strong uses
     eng = bench_mod.device_engine(cfg, 0, chunk_mib, device_sink=0)
     eng.source_device_text(text.data_ptr(), ln, keep=text)
     out, st = eng.run()
     eng.close()
     assert st.sites == n
-    assert st.chunks >= max(3, ln // (chunk_mib << 20))
-    assert_same(out, ref, f"C5 device path ({chunk_mib or 2048} MiB chunks)")
+    assert st.chunks >= max(2, ln // (chunk_mib << 20))
+    assert_same(out, ref, f"C5 device path ({chunk_mib} MiB chunks)")
 
 
 @pytest.fixture(scope="module")
@@ -214,7 +213,7 @@ def test_c4_device_path_equals_oracle(sid, bench_mod, c4, hold):
     against a hold budget of 40% of the HBM the text leaves), the chunks past
     the budget are formatted in pass 2 from the resident text."""
     cfg, text, ln, n, ref = c4
-    eng = bench_mod.device_engine(cfg, 0, bench_mod.STRONG_RESIDENT_CHUNK_MIB, device_sink=0, hold_bytes=hold)
+    eng = bench_mod.device_engine(cfg, 0, 2048, device_sink=0, hold_bytes=hold)   # (three chunks: some held, some not)
     eng.source_device_text(text.data_ptr(), ln, keep=text)
     out, st = eng.run()
     eng.close()
