@@ -3532,22 +3532,9 @@ __global__ __launch_bounds__(SCAN_ONE_TB) void sid_scan_one_kernel(const uint32_
         tot += t;
     }
     uint64_t acc = before + (x - sum);
-    // (16-B loads again, independent of the running sum, so they pipeline;
-    // element by element the loads waited on each other's adds)
-#pragma unroll 4
-    for (uint64_t i = lo; i < hi; i += 4) {
-        if (i + 4 <= hi) {
-            const uint4 q = *(const uint4*)(in + i);
-            ulonglong2* o = (ulonglong2*)(out + i);   // (out: 16-B aligned, i a multiple of 4)
-            o[0] = make_ulonglong2(acc, acc + q.x);
-            o[1] = make_ulonglong2(acc + q.x + q.y, acc + q.x + q.y + q.z);
-            acc += (uint64_t)q.x + q.y + q.z + q.w;
-        } else {
-            for (uint64_t k = i; k < hi; ++k) {
-                out[k] = acc;
-                acc += in[k];
-            }
-        }
+    for (uint64_t i = lo; i < hi; ++i) {
+        out[i] = acc;
+        acc += in[i];
     }
     __syncthreads();   // every thread has read *base
     if (threadIdx.x == 0) *base = tot;
