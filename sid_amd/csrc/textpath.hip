@@ -1979,7 +1979,8 @@ __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restr
                                                              unsigned long long* lb, const uint32_t* __restrict__ tcnt,
                                                              uint64_t ntiles, uint32_t cap,
                                                              uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
-                                                             unsigned long long* __restrict__ err, LocalLen LL)
+                                                             unsigned long long* __restrict__ err,
+                                                             uint32_t* __restrict__ late, unsigned long long* nlate)
 {
     __shared__ uint8_t cls[256];
     __shared__ uint32_t red[2][TB / 64];
@@ -2014,11 +2015,7 @@ __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restr
         counts[g] = c;
         hdr[2 * g] = 0;
         hdr[2 * g + 1] = s0;
-        if (LL.bsum) {   // -m local: the record length (the formatter's tokeniser for the chrom and position)
-            Reader R{text, len};
-            const int l = local_site_len(slot_head(R, make_ulonglong2(0, s0)), c, g, LL.len1, LL);
-            if (l) atomicAdd(LL.bsum + g / FTB, (uint32_t)l);
-        }
+        if (late) late[atomicAdd(nlate, 1ull)] = g;
     }
 }
 
@@ -2046,6 +2043,22 @@ __global__ __launch_bounds__(TB) void sid_tile_compact_kernel(const uint32_t* __
         d_counts[i] = counts[g];
         *(ulonglong2*)(d_hdr + 2 * i) = hw;
         d_starts[i] = keep ? 0u : (sid_off_t)hw.y;
+    }
+}
+
+// the record lengths of the general routine's slots
+__global__ __launch_bounds__(TB) void sid_tile_len_list_kernel(const char* __restrict__ text, uint64_t len,
+                                                               const uint64_t* __restrict__ hdr,
+                                                               const uint64_t* __restrict__ counts,
+                                                               const uint32_t* __restrict__ list,
+                                                               const unsigned long long* nlist, LocalLen LL)
+{
+    const uint64_t m = *nlist;
+    for (uint64_t j = (uint64_t)blockIdx.x * TB + threadIdx.x; j < m; j += (uint64_t)gridDim.x * TB) {
+        const uint32_t g = list[j];
+        Reader R{text, len};
+        const int l = local_site_len(slot_head(R, *(const ulonglong2*)(hdr + 2 * g)), counts[g], g, LL.len1, LL);
+        if (l) atomicAdd(LL.bsum + g / FTB, (uint32_t)l);
     }
 }
 
@@ -3491,62 +3504,10 @@ uint64_t sid_chunk_fmt_bound(uint64_t n, uint64_t text_bytes) { return 64 * n + 
 
 // the formatter's steps 1-2 (record bytes per block, their offsets); lb[1]
 // = the chunk's bytes afterwards
-// The formatter's block sums -> offsets in one launch when they are few
-// (up to SCAN_ONE_MAX: a 4000 MiB chunk of 30x text has ~111K writer
-// blocks): one block, each thread a run of a multiple of 4 sums (16-B loads),
-// the runs' totals scanned over the block; out = *base + the
-// exclusive prefix, *base += the total.  (The three-kernel scan took 14 us a
-// chunk in three launches.)
-constexpr uint32_t SCAN_ONE_TB = 1024;
-constexpr uint64_t SCAN_ONE_MAX = SCAN_ONE_TB * 128ull;
-__global__ __launch_bounds__(SCAN_ONE_TB) void sid_scan_one_kernel(const uint32_t* __restrict__ in, uint64_t m,
-                                                                  uint64_t* __restrict__ out, uint64_t* base)
-{
-    __shared__ uint64_t wsum[SCAN_ONE_TB / 64];
-    const uint64_t per = ((m + SCAN_ONE_TB - 1) / SCAN_ONE_TB + 3) & ~3ull;
-    const uint64_t lo = threadIdx.x * per, hi = min(lo + per, m);
-    uint64_t sum = 0;   // (64-bit: a chunk's records may pass 4 GB, long chromosome names)
-    for (uint64_t i = lo; i < hi; i += 4) {
-        if (i + 4 <= hi) {
-            const uint4 q = *(const uint4*)(in + i);   // (lo: a multiple of 4; in: 16-B aligned)
-            sum += (uint64_t)q.x + q.y + q.z + q.w;
-        } else {
-            for (uint64_t k = i; k < hi; ++k) sum += in[k];
-        }
-    }
-    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-    uint64_t x = sum;
-#pragma unroll
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint64_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    if (lane == 63u) wsum[wid] = x;
-    __syncthreads();
-    const uint64_t b = *base;
-    uint64_t before = b, tot = b;
-#pragma unroll
-    for (uint32_t w = 0; w < SCAN_ONE_TB / 64; ++w) {
-        const uint64_t t = wsum[w];
-        before += w < wid ? t : 0ull;
-        tot += t;
-    }
-    uint64_t acc = before + (x - sum);
-    for (uint64_t i = lo; i < hi; ++i) {
-        out[i] = acc;
-        acc += in[i];
-    }
-    __syncthreads();   // every thread has read *base
-    if (threadIdx.x == 0) *base = tot;
-}
-
 static int fmt_scan(sid_chunk_ws* W, uint64_t nb, hipStream_t st)
 {
-    if (nb <= SCAN_ONE_MAX)
-        sid_scan_one_kernel<<<1, SCAN_ONE_TB, 0, st>>>(W->bsum, nb, W->boff, (uint64_t*)(W->lb + 1));
-    else
-        launch_scan(W->bsum, nb, W->boff, (uint64_t*)(W->lb + 1), nullptr,
-                    (uint64_t*)((char*)W->bsum + ((nb * 4 + 7) & ~(size_t)7)), st);
+    launch_scan(W->bsum, nb, W->boff, (uint64_t*)(W->lb + 1), nullptr,
+                (uint64_t*)((char*)W->bsum + ((nb * 4 + 7) & ~(size_t)7)), st);
     WCHECK(hipGetLastError());
     return SID_OK;
 }
@@ -3751,13 +3712,15 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
         WCHECK(hipMemsetAsync(W->state + 4, 0xFF, sizeof(uint64_t), st));
         return fmt_scan(W, nb, st);
     }
+    uint32_t* late = W->fb + W->site_cap;
     uint32_t* miss = W->fb + 2 * W->site_cap;
     const LocalLen LL{ctx->ws.len1, ctx->ws.len2, W->bsum, miss, W->lb, W->cls};
     const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
     launch_tile_parse<true>(quad, base, c0, c1, ntp, O, LL, st);
     sid_tile_serial_kernel<<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap,
-                                                            W->counts, W->hdr, (unsigned long long*)(W->state + 4),
-                                                            LL);
+                                               W->counts, W->hdr, (unsigned long long*)(W->state + 4), late,
+                                               W->lb + 7);
+    sid_tile_len_list_kernel<<<64, TB, 0, st>>>(base, c1, W->hdr, W->counts, late, W->lb + 7, LL);
     sid_local_fixlen_kernel<true><<<64, TB, 0, st>>>(base, c1, nullptr, W->hdr, W->counts, miss, W->lb, ctx->K,
                                                      ctx->d_lnt, ct, W->code, W->hom, W->het, W->bsum, W->lb);
     WCHECK(hipGetLastError());
@@ -3789,7 +3752,7 @@ int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64
     const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
     launch_tile_parse<false>(quad, base, c0, c1, ntp, O, LL, st);
     sid_tile_serial_kernel<<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap, W->counts,
-                                                            W->hdr, (unsigned long long*)(W->state + 4), LocalLen{});
+                                               W->hdr, (unsigned long long*)(W->state + 4), nullptr, nullptr);
     // the tiles' first sites in file order (state[0]: the chunk's sites; over the cap: void)
     launch_scan(W->tcnt, ntp, W->toff, W->state, nullptr,
                 (uint64_t*)((char*)W->tcnt + ((ntp * 4 + 7) & ~(size_t)7)), st);
