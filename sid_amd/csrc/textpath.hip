@@ -1790,11 +1790,7 @@ __device__ uint32_t put_stamp[TP_STAMP_N][4];
 #define TP_STAMP_AT(v)
 #define PUT_STAMP_AT(v)
 #endif
-// PERSIST: the device's resident blocks walk the tiles (tile blockIdx.x,
-// + gridDim.x, ...), each holding its next tile's 16-B windows in registers,
-// loaded while it parses the current one from LDS (no block waits for its
-// tile's loads after the first); else one block per tile, the L2 prefetch.
-template <bool QUAD, bool LOCAL, bool PERSIST = false>
+template <bool QUAD, bool LOCAL>
 __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restrict__ text, uint64_t tile_base,
                                                             uint64_t c0, uint64_t c1, uint64_t ntiles,
                                                             uint32_t pf_dist, TileOut O, LocalLen LL)
@@ -1817,37 +1813,28 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     rbl[tid] = rb_entry(tid);
     if (blockIdx.x == 0 && tid == 0) O.state[4] = ~0ull;   // no parse error yet
     const uint32_t cap = O.cap;
-    // a tile's windows (at or past the chunk's end: zeros), its halo window
-    // (tid < TP_HALO / 16) and whether the byte before it is a '\n' (tid 0;
-    // 1 when there is none: the tile starts the chunk)
-    uint4 v[ROWS], vh = make_uint4(0, 0, 0, 0);
-    uint32_t prev0 = 0;
-    auto fetch = [&](uint64_t u) {
-        const uint64_t g0 = tile_base + u * TP_TILE;
-        const bool inner = g0 > c0 && g0 + TP_TILE <= c1;
-#pragma unroll
-        for (uint32_t k = 0; k < ROWS; ++k) {
-            const uint64_t at = g0 + k * TILE + tid * 16;
-            v[k] = (inner || at < c1) ? ld_nt(text + at) : make_uint4(0, 0, 0, 0);
-        }
-        if (tid < TP_HALO / 16) {
-            const uint64_t at = g0 + TP_TILE + tid * 16;
-            vh = at < c1 ? ld_nt(text + at) : make_uint4(0, 0, 0, 0);
-        }
-        prev0 = tid ? 0u : (g0 > c0 && g0 - 1 < c1) ? (text[g0 - 1] == '\n') : 1u;
-    };
-    // one tile (t: block-uniform); the loop below, or one call
-    auto body = [&](const uint64_t t) {
+    {
+        const uint64_t t = blockIdx.x;
         TP_STAMP_AT(st0);
         const uint64_t g0 = tile_base + t * TP_TILE;           // the tile's first byte (16-B aligned)
         // a tile inside the chunk (all but its first and last): no window needs
         // the chunk's bounds (block-uniform)
         const bool inner = g0 > c0 && g0 + TP_TILE <= c1;
-        // ---- the tile into LDS
+        // ---- load (windows at or past the chunk's end read as zeros)
+        uint4 v[ROWS];
 #pragma unroll
-        for (uint32_t k = 0; k < ROWS; ++k) *(uint4*)(tl + k * TILE + tid * 16) = v[k];
-        if (tid < TP_HALO / 16) *(uint4*)(tl + TP_TILE + tid * 16) = vh;
+        for (uint32_t k = 0; k < ROWS; ++k) {
+            const uint64_t at = g0 + k * TILE + tid * 16;
+            v[k] = (inner || at < c1) ? ld_nt(text + at) : make_uint4(0, 0, 0, 0);
+            *(uint4*)(tl + k * TILE + tid * 16) = v[k];
+        }
+        if (tid < TP_HALO / 16) {
+            const uint64_t at = g0 + TP_TILE + tid * 16;
+            *(uint4*)(tl + TP_TILE + tid * 16) = at < c1 ? *(const uint4*)(text + at) : make_uint4(0, 0, 0, 0);
+        }
         if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
+        // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
+        const uint32_t prev0 = tid ? 0u : (g0 > c0 && g0 - 1 < c1) ? (text[g0 - 1] == '\n') : 1u;
         __syncthreads();
         TP_STAMP_AT(st1);
         // ---- line starts (bit j: byte j of the window starts a non-empty line in [c0, c1))
@@ -1923,15 +1910,12 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         if (tid == 0) O.tcnt[t] = nlines;   // (no atomics on one address from every block: summed by the next kernel)
         __syncthreads();
         TP_STAMP_AT(st2);
-        // PERSIST: the block's next tile into registers while this one parses;
-        // else a later tile's lines into L2: one 4-B load per 128-B line (the
+        // a later tile's lines into L2: one 4-B load per 128-B line (the
         // value kept to the kernel's end, so the loads stay in flight).
         // (Issued at the block's start instead, before its own loads: C2
         // parse 2.02-2.04 vs 1.95-1.96 ms per step.)
         uint32_t pf = 0;
-        if (PERSIST) {
-            if (t + gridDim.x < ntiles) fetch(t + gridDim.x);
-        } else {
+        {
             const uint64_t u = t + pf_dist;
             const uint32_t off = tid * 128u;
             const uint64_t at = tile_base + u * TP_TILE + off;
@@ -1967,8 +1951,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             if ((tid & 63u) == 0 && hi) atomicAdd(LL.bsum + gw + 1, (uint32_t)hi);
         }
         // (the prefetch's value: kept live to here, never true)
-        if (!PERSIST && pf == 0x5A5A5A5Au && c1 == 0) O.state[5] = pf;
-        if (PERSIST) __syncthreads();   // this tile's LDS read before the next one's stores
+        if (pf == 0x5A5A5A5Au && c1 == 0) O.state[5] = pf;
 #ifdef SID_TP_STAMP
         __syncthreads();
         if (tid == 0 && t < TP_STAMP_N) {
@@ -1979,13 +1962,6 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             tp_stamp[t][3] = (uint32_t)(st0 >> 4);   // start (160 ns units)
         }
 #endif
-    };
-    if (blockIdx.x >= ntiles) return;
-    fetch(blockIdx.x);
-    if (PERSIST) {
-        for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) body(t);
-    } else {
-        body(blockIdx.x);
     }
 }
 
@@ -3654,12 +3630,8 @@ static uint64_t tile_count(uint64_t c0, uint64_t c1, bool quad)
     return c1 > c0 ? (c1 - t0 + tp_tile(quad) - 1) / tp_tile(quad) : 0;
 }
 
-// The tile parse's prefetch distance, or its persistent grid: the blocks
-// resident on the device at once (occupancy x CUs), a multiple of the 8 XCDs
-// (SID_TP_PERSIST: 1 the quad shape persistent, 2 both shapes)
-#ifndef SID_TP_PERSIST
-#define SID_TP_PERSIST 2
-#endif
+// The tile parse's prefetch distance: the blocks resident on the device at
+// once (occupancy x CUs), a multiple of the 8 XCDs
 template <class K>
 static uint32_t resident_blocks(K kernel)
 {
@@ -3676,17 +3648,9 @@ static void launch_tile_parse(bool quad, const char* base, uint64_t c0, uint64_t
                               const LocalLen& LL, hipStream_t st)
 {
     const uint64_t tb = c0 & ~(uint64_t)15;
-    if (quad && SID_TP_PERSIST >= 1) {
-        static const uint32_t res = resident_blocks(sid_tile_parse_kernel<true, LOCAL, true>);
-        sid_tile_parse_kernel<true, LOCAL, true><<<(unsigned)std::min<uint64_t>(ntp, res), TB, 0, st>>>(
-            base, tb, c0, c1, ntp, 0, O, LL);
-    } else if (quad) {
+    if (quad) {
         static const uint32_t pf = resident_blocks(sid_tile_parse_kernel<true, LOCAL>);
         sid_tile_parse_kernel<true, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp, pf, O, LL);
-    } else if (SID_TP_PERSIST >= 2) {
-        static const uint32_t res = resident_blocks(sid_tile_parse_kernel<false, LOCAL, true>);
-        sid_tile_parse_kernel<false, LOCAL, true><<<(unsigned)std::min<uint64_t>(ntp, res), TB, 0, st>>>(
-            base, tb, c0, c1, ntp, 0, O, LL);
     } else {
         static const uint32_t pf = resident_blocks(sid_tile_parse_kernel<false, LOCAL>);
         sid_tile_parse_kernel<false, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp, pf, O, LL);
