@@ -1803,6 +1803,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     static_assert(TB == 256 && ROWS <= 9, "a lane's windows: three u32s of line-start counts");
     static_assert(FTB % 64 == 0, "a wave's slots lie in one writer block");
     constexpr uint32_t TP_HALO = tp_halo(QUAD);
+    static_assert(TP_HALO % 1024 == 0 && TP_HALO / 16 <= TB, "the halo loaded by whole waves, a window a lane");
     __shared__ __attribute__((aligned(16))) char tl[TP_TILE + TP_HALO + 64];
     __shared__ uint16_t ls[tp_cap_max(QUAD)];
     __shared__ uint8_t cls[256];
@@ -1820,21 +1821,33 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         // a tile inside the chunk (all but its first and last): no window needs
         // the chunk's bounds (block-uniform)
         const bool inner = g0 > c0 && g0 + TP_TILE <= c1;
-        // ---- load (windows at or past the chunk's end read as zeros)
+        // ---- load (windows at or past the chunk's end read as zeros).  Every
+        // load issued before the first is used, with no branch between them: a
+        // window past the chunk's end loads the tile's first window instead
+        // (g0 < c1, readable as every window before c1 is) and is zeroed.
+        // (Loads under a branch each, stored to LDS as they came, compiled to
+        // one round trip per row: a wait for each before the next was issued.)
+        const uint64_t hat = g0 + TP_TILE + tid * 16;
+        const bool hok = hat < c1;
+        uint4 hv = make_uint4(0, 0, 0, 0);
+        if (tid < TP_HALO / 16) hv = *(const uint4*)(text + (hok ? hat : g0));   // (whole waves)
+        // the byte before the tile (one address for the block)
+        const bool pok = g0 > c0 && g0 - 1 < c1;
+        const uint32_t pbyte = (uint8_t)text[pok ? g0 - 1 : g0];
         uint4 v[ROWS];
 #pragma unroll
         for (uint32_t k = 0; k < ROWS; ++k) {
             const uint64_t at = g0 + k * TILE + tid * 16;
-            v[k] = (inner || at < c1) ? ld_nt(text + at) : make_uint4(0, 0, 0, 0);
-            *(uint4*)(tl + k * TILE + tid * 16) = v[k];
+            const bool ok = inner || at < c1;
+            const uint4 x = ld_nt(text + (ok ? at : g0));
+            v[k] = ok ? x : make_uint4(0, 0, 0, 0);
         }
-        if (tid < TP_HALO / 16) {
-            const uint64_t at = g0 + TP_TILE + tid * 16;
-            *(uint4*)(tl + TP_TILE + tid * 16) = at < c1 ? *(const uint4*)(text + at) : make_uint4(0, 0, 0, 0);
-        }
+#pragma unroll
+        for (uint32_t k = 0; k < ROWS; ++k) *(uint4*)(tl + k * TILE + tid * 16) = v[k];
+        if (tid < TP_HALO / 16) *(uint4*)(tl + TP_TILE + tid * 16) = hok ? hv : make_uint4(0, 0, 0, 0);
         if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
         // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
-        const uint32_t prev0 = tid ? 0u : (g0 > c0 && g0 - 1 < c1) ? (text[g0 - 1] == '\n') : 1u;
+        const uint32_t prev0 = tid ? 0u : pok ? (pbyte == '\n') : 1u;
         __syncthreads();
         TP_STAMP_AT(st1);
         // ---- line starts (bit j: byte j of the window starts a non-empty line in [c0, c1))
