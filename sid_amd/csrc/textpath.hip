@@ -116,6 +116,23 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
     return x;
 }
+// the wave's sum, wave-uniform (a scalar)
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(x), 63);
+}
+// a lane's value from a lane of its quad by DPP quad_perm (no LDS round trip
+// as __shfl's ds_bpermute takes; the quad's four lanes active together):
+// QP = the source lane for lanes 0-3, two bits each
+template <uint32_t QP>
+__device__ __forceinline__ uint32_t quad_get(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, (int)QP, 0xF, 0xF, false);
+}
+constexpr uint32_t QP_LEFT = 0x93;    // lane j <- j-1 mod 4 (3, 0, 1, 2)
+constexpr uint32_t QP_LANE3 = 0xFF;   // every lane <- 3
+constexpr uint32_t QP_XOR1 = 0xB1;    // (1, 0, 3, 2)
+constexpr uint32_t QP_XOR2 = 0x4E;    // (2, 3, 0, 1)
 
 // exclusive scan of one u32 per thread over an NT-thread block, once per
 // kernel (its LDS slots are not reused): the waves by DPP (wave_scan_incl),
@@ -865,9 +882,9 @@ __device__ __forceinline__ bool read_bases_quad(Ld ld, Off len, Off q, uint32_t 
         const uint32_t lead = k == 0 ? (uint32_t)(q & 15) : 0u;
         const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
         const uint32_t last_caret = (v.w >> 24) == 0x5Eu ? 1u : 0u;
-        const uint32_t from_left = (uint32_t)__shfl((int)last_caret, (int)((j + 3u) & 3u), 4);
+        const uint32_t from_left = quad_get<QP_LEFT>(last_caret);
         const uint32_t cin = k == 0 ? 0u : (j ? from_left : prev3);
-        prev3 = (uint32_t)__shfl((int)last_caret, 3, 4);
+        prev3 = quad_get<QP_LANE3>(last_caret);
         bool done = false, wbad = false;
         uint32_t carry = cin;
         const uint32_t w = rb_window16<true>(v, valid, room, lut, done, carry, wbad);
@@ -886,16 +903,23 @@ __device__ __forceinline__ bool read_bases_quad(Ld ld, Off len, Off q, uint32_t 
         }
         if (qb) break;
     }
-#pragma unroll
-    for (int m = 1; m < 4; m <<= 1) {
-        nA += (uint32_t)__shfl_xor((int)nA, m, 4);
-        nC += (uint32_t)__shfl_xor((int)nC, m, 4);
-        nG += (uint32_t)__shfl_xor((int)nG, m, 4);
-        nT += (uint32_t)__shfl_xor((int)nT, m, 4);
-        nM += (uint32_t)__shfl_xor((int)nM, m, 4);
-        acc |= (uint32_t)__shfl_xor((int)acc, m, 4);
-        bad = __shfl_xor((int)bad, m, 4) != 0 || bad;
-    }
+    auto quad_sum = [](uint32_t& x) {
+        x += quad_get<QP_XOR1>(x);
+        x += quad_get<QP_XOR2>(x);
+    };
+    auto quad_or = [](uint32_t& x) {
+        x |= quad_get<QP_XOR1>(x);
+        x |= quad_get<QP_XOR2>(x);
+    };
+    quad_sum(nA);
+    quad_sum(nC);
+    quad_sum(nG);
+    quad_sum(nT);
+    quad_sum(nM);
+    uint32_t bf = acc | (bad ? 1u << 31 : 0u);   // (bit 31 of the entries' sum never set: bits 0-30)
+    quad_or(bf);
+    acc = bf & 0x7FFFFFFFu;
+    bad = (bf >> 31) != 0;
     if (bad || (acc >> RB_BAD_SHIFT) != 0) return false;
     nA += kd == K_A ? nM : 0;
     nC += kd == K_C ? nM : 0;
@@ -1556,13 +1580,20 @@ __device__ __forceinline__ uint32_t local_word(uint32_t k, uint32_t f, uint32_t 
 
 // The site's record length (0: a fix-up site, listed in LL.miss; a record
 // is never empty) and its class word into LL.cls[i]
+// (L1W: a window of the first table's tail lengths in LDS, entries
+// [L1W_LO, L1W_LO + L1W_N): the entries of the profiles the shape's coverage
+// gives most, read without a global load's latency at the end of the line)
+template <uint32_t L1W_LO = 0, uint32_t L1W_N = 0>
 __device__ __forceinline__ int local_site_len(const Head& h, uint64_t c, uint64_t i, const uint8_t* L1,
-                                              const LocalLen& LL)
+                                              const LocalLen& LL, const uint8_t* l1w = nullptr)
 {
     uint32_t f, s, nf, ns, cov;
     sid_major(c, f, s, nf, ns, cov);
     const uint32_t k = local_entry(nf, ns, cov - nf - ns);
-    const uint32_t L = k < SID_TAB_N ? L1[k] : k != UINT32_MAX ? LL.len2[k - SID_TAB_N] : 0xFFu;
+    const uint32_t L = L1W_N && k - L1W_LO < L1W_N ? l1w[k - L1W_LO]
+                     : k < SID_TAB_N               ? L1[k]
+                     : k != UINT32_MAX             ? LL.len2[k - SID_TAB_N]
+                                                   : 0xFFu;
     const bool miss = L == 0xFFu;
     LL.cls[i] = miss ? SID_CLS_MISS : local_word(k, f, s);   // (read back by the writer soon: through the caches)
     if (miss) {
@@ -1631,9 +1662,8 @@ __global__ __launch_bounds__(TB) void sid_parse_len_kernel(const char* __restric
                 fb[atomicAdd(fbn, 1ull)] = (uint32_t)(i - lo);
             }
         }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) l += __shfl_xor(l, off, 64);
-        if ((threadIdx.x & 63u) == 0 && l) atomicAdd(LL.bsum + (wb - lo) / FTB, (uint32_t)l);
+        const uint32_t sl = wave_sum((uint32_t)l);
+        if ((threadIdx.x & 63u) == 0 && sl) atomicAdd(LL.bsum + (wb - lo) / FTB, sl);
     }
 }
 
@@ -1727,10 +1757,18 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
 // read_bases_quad / _lut), then the line's outputs into slot g by the lead
 // lane (header pair; -m local's class word and record length, returned; the
 // Lynch paths' counts), or its slot and offset listed for the general routine
+// the LDS window of the tail lengths: the quad shape's, profiles of ~200x
+// (major count 128-255; C5 parse 11.41 -> 11.28 ms per step).  None for the
+// lane shape: a 2 KiB window of the ~30x profiles (major count below 64)
+// measured slower there (C2 parse 1.79 -> 1.92 ms: LDS for five blocks a CU
+// instead of six)
+__host__ __device__ constexpr uint32_t l1w_lo(bool quad) { return quad ? 128u * SID_TAB_NS * SID_TAB_NR : 0u; }
+__host__ __device__ constexpr uint32_t l1w_n(bool quad) { return quad ? 128u * SID_TAB_NS * SID_TAB_NR : 0u; }
 template <bool QUAD, bool LOCAL, class Ld>
 __device__ __forceinline__ int tile_line(const char* __restrict__ text, const char* tl, Ld ld, uint64_t g0, uint32_t r0,
                                          uint64_t g, uint32_t len_t, uint64_t c1, bool lead, const uint8_t* cls,
-                                         const uint32_t* rbl, const TileOut& O, const LocalLen& LL)
+                                         const uint32_t* rbl, const TileOut& O, const LocalLen& LL,
+                                         const uint8_t* l1w)
 {
     int l = 0;
     const uint64_t s0 = g0 + r0;
@@ -1759,7 +1797,7 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
             Head hd;
             hd.clen = clen;
             hd.pos = (int32_t)(uint32_t)h[0];
-            l = local_site_len(hd, c, g, LL.len1, LL);
+            l = local_site_len<l1w_lo(QUAD), l1w_n(QUAD)>(hd, c, g, LL.len1, LL, l1w);
         } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
             l = local_site_len_text(text, c1, s0, c, g, LL);
         }
@@ -1809,6 +1847,9 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     __shared__ uint8_t cls[256];
     __shared__ uint32_t rbl[256];
     __shared__ uint32_t wtot[TB / 64][NW];
+    constexpr uint32_t L1W_N = LOCAL ? l1w_n(QUAD) : 0u;
+    static_assert(L1W_N == 0 || L1W_N == 16 * TB, "the window: 16 bytes a lane");
+    __shared__ __attribute__((aligned(16))) uint8_t l1w[L1W_N ? L1W_N : 16];
     const uint32_t tid = threadIdx.x;
     cls[tid] = (uint8_t)base_class(tid);
     rbl[tid] = rb_entry(tid);
@@ -1834,6 +1875,9 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         // the byte before the tile (one address for the block)
         const bool pok = g0 > c0 && g0 - 1 < c1;
         const uint32_t pbyte = (uint8_t)text[pok ? g0 - 1 : g0];
+        // the tail lengths' window (L2-resident: every block reads it)
+        uint4 wv = make_uint4(0, 0, 0, 0);
+        if constexpr (L1W_N != 0) wv = *(const uint4*)(LL.len1 + l1w_lo(QUAD) + tid * 16);
         uint4 v[ROWS];
 #pragma unroll
         for (uint32_t k = 0; k < ROWS; ++k) {
@@ -1846,6 +1890,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         for (uint32_t k = 0; k < ROWS; ++k) *(uint4*)(tl + k * TILE + tid * 16) = v[k];
         if (tid < TP_HALO / 16) *(uint4*)(tl + TP_TILE + tid * 16) = hok ? hv : make_uint4(0, 0, 0, 0);
         if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
+        if constexpr (L1W_N != 0) *(uint4*)(l1w + tid * 16) = wv;
         // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
         const uint32_t prev0 = tid ? 0u : pok ? (pbyte == '\n') : 1u;
         __syncthreads();
@@ -1949,19 +1994,16 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             const uint32_t j = j0 + (QUAD ? tid >> 2 : tid);
             const bool lead = !QUAD || (tid & 3u) == 0;   // the lane that writes the line's outputs
             int l = 0;
-            if (j < cnt) l = tile_line<QUAD, LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, lead, cls, rbl, O, LL);
+            if (j < cnt)
+                l = tile_line<QUAD, LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, lead, cls, rbl, O, LL, l1w);
             if (!LOCAL) continue;
             // the record bytes into the writer blocks' sums: the wave's slots (64,
             // or 16 with quads, from a multiple of 16) lie in one block or two
             const uint64_t gw = (g_tile + j0 + (QUAD ? (tid & ~63u) >> 2 : (tid & ~63u))) / FTB;
-            int lo = (g_tile + j) / FTB == gw ? l : 0, hi = l - lo;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                lo += __shfl_xor(lo, off, 64);
-                hi += __shfl_xor(hi, off, 64);
-            }
-            if ((tid & 63u) == 0 && lo) atomicAdd(LL.bsum + gw, (uint32_t)lo);
-            if ((tid & 63u) == 0 && hi) atomicAdd(LL.bsum + gw + 1, (uint32_t)hi);
+            const uint32_t lo = (g_tile + j) / FTB == gw ? (uint32_t)l : 0u;
+            const uint32_t slo = wave_sum(lo), shi = wave_sum((uint32_t)l - lo);
+            if ((tid & 63u) == 0 && slo) atomicAdd(LL.bsum + gw, slo);
+            if ((tid & 63u) == 0 && shi) atomicAdd(LL.bsum + gw + 1, shi);
         }
         // (the prefetch's value: kept live to here, never true)
         if (pf == 0x5A5A5A5Au && c1 == 0) O.state[5] = pf;
