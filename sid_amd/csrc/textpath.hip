@@ -1719,7 +1719,10 @@ constexpr uint32_t TP_ROWS_QUAD = 6;
 // the halo and the line list per shape: the quad shape's tiles hold few
 // lines (the host picks it for lines over 256 B on average), so 256 slots.
 // (A 512-B halo, LDS for six blocks a CU instead of five, measured slower:
-// 12.93 vs 12.78 ms per C5 step.)
+// 12.93 vs 12.78 ms per C5 step; again with the loads issued together and
+// no tail-length window, 11.46 vs 11.28 ms; with the window, still five
+// blocks, 11.24 vs 11.28 ms: noise.  The LDS limit is byte-exact:
+// tools/debug/lds_occ_probe.hip, 27306 B six blocks, 27307 B five.)
 __host__ __device__ constexpr uint32_t tp_halo(bool) { return 1024; }
 __host__ __device__ constexpr uint32_t tp_cap_max(bool quad) { return quad ? SID_TILE_CAP_MAX_QUAD : SID_TILE_CAP_MAX; }
 __host__ __device__ constexpr uint32_t tp_tile(bool quad) { return (quad ? TP_ROWS_QUAD : TP_ROWS) * TILE; }
