@@ -50,6 +50,49 @@ constexpr int TILE = TB * 16;           // bytes per line-index tile
 constexpr int SCAN_TB = 1024;
 
 // ------------------------------------------------------------ block scan --
+// inclusive scans over the wave by DPP (no LDS round trip): row_shr 1/2/4/8
+// within each row of 16 lanes, then row_bcast 15 / 31 carry the rows' sums
+// up.  The 64-bit form moves both halves and adds with the carry.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+// the wave's maximum of unsigned values, wave-uniform (0 fills the lanes a
+// shift leaves empty: the identity)
+__device__ __forceinline__ uint32_t wave_max(uint32_t x)
+{
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+template <int CTRL, int ROWS, bool BOUND>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, ROWS, 0xF, BOUND);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, ROWS, 0xF, BOUND);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_scan_incl64(uint64_t x)
+{
+    x += dpp64<0x111, 0xF, true>(x);
+    x += dpp64<0x112, 0xF, true>(x);
+    x += dpp64<0x114, 0xF, true>(x);
+    x += dpp64<0x118, 0xF, true>(x);
+    x += dpp64<0x142, 0xA, false>(x);
+    x += dpp64<0x143, 0xC, false>(x);
+    return x;
+}
+
 // exclusive scan of one u32 per thread over a 256-thread block; returns the
 // prefix, *total = block sum
 template <int NT = TB>
@@ -57,11 +100,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* total)
 {
     __shared__ uint32_t wsum[NT / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t x = v;
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
+    const uint32_t x = wave_scan_incl(v);
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
     uint32_t base = 0, tot = 0;
@@ -86,11 +125,7 @@ __device__ __forceinline__ uint64_t block_exscan64(uint64_t v, uint64_t* total)
 {
     __shared__ uint64_t wsum[TB / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint64_t x = v;
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint64_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
+    const uint64_t x = wave_scan_incl64(v);
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
     uint64_t base = 0, tot = 0;
@@ -103,19 +138,6 @@ __device__ __forceinline__ uint64_t block_exscan64(uint64_t v, uint64_t* total)
     return base + x - v;
 }
 
-// inclusive scan of one u32 per lane over the wave, by DPP (no LDS):
-// row_shr 1/2/4/8 within each row of 16 lanes, then row_bcast 15 / 31 carry
-// the rows' sums up
-__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
-{
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
-    return x;
-}
 // the wave's sum, wave-uniform (a scalar)
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x)
 {
@@ -200,11 +222,7 @@ __global__ __launch_bounds__(SCAN_TB) void sid_scan_top_kernel(uint64_t* __restr
     uint64_t s = 0;
     for (uint64_t i = lo; i < hi; ++i) s += bsum[i];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint64_t x = s;
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint64_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
+    const uint64_t x = wave_scan_incl64(s);
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
     const uint64_t b = *base;
@@ -2044,18 +2062,34 @@ __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restr
     __shared__ uint32_t red[2][TB / 64];
     if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
     {
+        // four tiles a 16-B load, four loads in flight a lane (one pass over
+        // ~200k tiles at this grid; a load a tile, each waited for before the
+        // next, took ~12 us a chunk)
         uint32_t sum = 0, mx = 0;
-        for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles;
-             t += (uint64_t)gridDim.x * blockDim.x) {
-            const uint32_t c = tcnt[t];
+        auto add = [&](uint32_t c) {
             sum += min(c, cap);
             mx = max(mx, c);
-        }
+        };
+        const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x, nq = ntiles / 4;
+        const uint4* tq = (const uint4*)tcnt;   // (hipMalloc'd: 16-B aligned)
+        for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += 4 * nthr) {
+            uint4 c4[4];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            sum += __shfl_xor(sum, off, 64);
-            mx = max(mx, (uint32_t)__shfl_xor(mx, off, 64));
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t qu = q + u * nthr;
+                c4[u] = qu < nq ? tq[qu] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                add(c4[u].x);
+                add(c4[u].y);
+                add(c4[u].z);
+                add(c4[u].w);
+            }
         }
+        if (blockIdx.x == 0 && threadIdx.x < ntiles - 4 * nq) add(tcnt[4 * nq + threadIdx.x]);
+        sum = wave_sum(sum);
+        mx = wave_max(mx);
         if ((threadIdx.x & 63u) == 0) red[0][threadIdx.x >> 6] = sum, red[1][threadIdx.x >> 6] = mx;
         __syncthreads();
         if (threadIdx.x == 0) {
