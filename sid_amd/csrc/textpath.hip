@@ -1598,27 +1598,31 @@ __device__ __forceinline__ uint32_t local_word(uint32_t k, uint32_t f, uint32_t 
 
 // The site's record length (0: a fix-up site, listed in LL.miss; a record
 // is never empty) and its class word into LL.cls[i]
-// (L1W: a window of the first table's tail lengths in LDS, entries
-// [L1W_LO, L1W_LO + L1W_N): the entries of the profiles the shape's coverage
-// gives most, read without a global load's latency at the end of the line)
-template <uint32_t L1W_LO = 0, uint32_t L1W_N = 0>
-__device__ __forceinline__ int local_site_len(const Head& h, uint64_t c, uint64_t i, const uint8_t* L1,
-                                              const LocalLen& LL, const uint8_t* l1w = nullptr)
+// local_site_tail: the tail's length of the record (its bytes after "chrom,
+// pos,label,"; local_rec_len), -1 for a fix-up site.  (The tail lengths of
+// the ~200x profiles copied into LDS by every quad-shape block, 4 KiB, took
+// C5's parse 11.41 -> 11.28 ms per step, but cost more than it saved beside
+// quad_head: 11.19 with it, 11.03 without; for the lane shape, 2 KiB of the
+// ~30x profiles: C2 parse 1.79 -> 1.92 ms.)
+__device__ __forceinline__ int local_site_tail(uint64_t c, uint64_t i, const uint8_t* L1, const LocalLen& LL)
 {
     uint32_t f, s, nf, ns, cov;
     sid_major(c, f, s, nf, ns, cov);
     const uint32_t k = local_entry(nf, ns, cov - nf - ns);
-    const uint32_t L = L1W_N && k - L1W_LO < L1W_N ? l1w[k - L1W_LO]
-                     : k < SID_TAB_N               ? L1[k]
-                     : k != UINT32_MAX             ? LL.len2[k - SID_TAB_N]
-                                                   : 0xFFu;
+    const uint32_t L = k < SID_TAB_N ? L1[k] : k != UINT32_MAX ? LL.len2[k - SID_TAB_N] : 0xFFu;
     const bool miss = L == 0xFFu;
     LL.cls[i] = miss ? SID_CLS_MISS : local_word(k, f, s);   // (read back by the writer soon: through the caches)
     if (miss) {
         LL.miss[atomicAdd(LL.nmiss, 1ull)] = (uint32_t)i;   // its bytes: the fix-up's
-        return 0;
+        return -1;
     }
-    return local_rec_len(h, L);
+    return (int)L;
+}
+__device__ __forceinline__ int local_site_len(const Head& h, uint64_t c, uint64_t i, const uint8_t* L1,
+                                              const LocalLen& LL)
+{
+    const int L = local_site_tail(c, i, L1, LL);
+    return L < 0 ? 0 : local_rec_len(h, (uint32_t)L);
 }
 
 // (out of line: its tokeniser would set the parse's register count)
@@ -1772,24 +1776,17 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
     return site_head_hw(R, &s0, make_ulonglong2(0, 0));
 }
 
-// One line of a tile (or segment) from its LDS copy (tl: the copy of the
-// text from global offset g0 on, ld: a 16-B window at an offset from g0, from
-// LDS or past its end from HBM): the fast path (parse_header, then
-// read_bases_quad / _lut), then the line's outputs into slot g by the lead
-// lane (header pair; -m local's class word and record length, returned; the
-// Lynch paths' counts), or its slot and offset listed for the general routine
-// the LDS window of the tail lengths: the quad shape's, profiles of ~200x
-// (major count 128-255; C5 parse 11.41 -> 11.28 ms per step).  None for the
-// lane shape: a 2 KiB window of the ~30x profiles (major count below 64)
-// measured slower there (C2 parse 1.79 -> 1.92 ms: LDS for five blocks a CU
-// instead of six)
-__host__ __device__ constexpr uint32_t l1w_lo(bool quad) { return quad ? 128u * SID_TAB_NS * SID_TAB_NR : 0u; }
-__host__ __device__ constexpr uint32_t l1w_n(bool quad) { return quad ? 128u * SID_TAB_NS * SID_TAB_NR : 0u; }
-template <bool QUAD, bool LOCAL, class Ld>
+// One line of a lane-shape tile from its LDS copy (tl: the copy of the text
+// from global offset g0 on, ld: a 16-B window at an offset from g0, from LDS
+// or past its end from HBM): the fast path (parse_header, then
+// read_bases_lut), then the line's outputs into slot g (header pair; -m
+// local's class word and record length, returned; the Lynch paths' counts),
+// or its slot and offset listed for the general routine.  (The quad shape:
+// quad_head, then quad_line.)
+template <bool LOCAL, class Ld>
 __device__ __forceinline__ int tile_line(const char* __restrict__ text, const char* tl, Ld ld, uint64_t g0, uint32_t r0,
                                          uint64_t g, uint32_t len_t, uint64_t c1, bool lead, const uint8_t* cls,
-                                         const uint32_t* rbl, const TileOut& O, const LocalLen& LL,
-                                         const uint8_t* l1w)
+                                         const uint32_t* rbl, const TileOut& O, const LocalLen& LL)
 {
     int l = 0;
     const uint64_t s0 = g0 + r0;
@@ -1802,8 +1799,7 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
     bool ok = t4 >= 0;
     if (ok) {
         const uint4* first = (const uint4*)(stage + ((sh + (uint32_t)t4) & 0x30u));
-        ok = QUAD ? read_bases_quad<Ld, uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c)
-                  : read_bases_lut<Ld, uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c);
+        ok = read_bases_lut<Ld, uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c);
     }
     if (!lead) {
     } else if (ok) {
@@ -1818,7 +1814,7 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
             Head hd;
             hd.clen = clen;
             hd.pos = (int32_t)(uint32_t)h[0];
-            l = local_site_len<l1w_lo(QUAD), l1w_n(QUAD)>(hd, c, g, LL.len1, LL, l1w);
+            l = local_site_len(hd, c, g, LL.len1, LL);
         } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
             l = local_site_len_text(text, c1, s0, c, g, LL);
         }
@@ -1828,6 +1824,79 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
         O.fb[k] = (uint32_t)g;
         O.fbo[k] = (uint32_t)s0;
     }
+    return l;
+}
+
+// The quad shape in two steps.  A line's header is the same work in each of
+// its quad's four lanes, so it is parsed a lane per line first (the tile's
+// ~58 lines of 200x: one wave instead of four), its outputs stored, and what
+// the quad needs passed on in LDS: bit 0 the header parsed, bits 1-6 the
+// offset of token 4, 7-9 the class '.'/',' stand for, 10 the header pair
+// valid, 11-23 the record's length but its tail ("chrom,pos,label,":
+// local_rec_len with no tail).  A line whose header takes the general
+// routine is listed for it here.
+template <bool LOCAL>
+__device__ __forceinline__ uint32_t quad_head(const char* tl, uint64_t g0, uint32_t r0, uint64_t g, uint32_t len_t,
+                                              const uint8_t* cls, const TileOut& O)
+{
+    const uint64_t s0 = g0 + r0;
+    const char* stage = tl + (r0 & ~15u);
+    const uint32_t sh = r0 & 15u;
+    const uint4 v0 = *(const uint4*)stage, v1 = *(const uint4*)(stage + 16), v2 = *(const uint4*)(stage + 32);
+    uint64_t h[2] = {0, 0};
+    uint32_t kd = 0;
+    const int t4 = parse_header(v0, v1, v2, stage, sh, len_t - r0, cls, h, &kd);
+    if (t4 < 0) {
+        const unsigned long long k = atomicAdd(O.lb + 6, 1ull);
+        O.fb[k] = (uint32_t)g;
+        O.fbo[k] = (uint32_t)s0;
+        return 0;
+    }
+    const bool hv = (h[0] >> 63) != 0;
+    const uint32_t clen = (uint32_t)(h[0] >> 32) & 0xFFFu;
+    if (!hv || clen > 8) h[1] = (uint32_t)s0;   // the writer reads the chrom, or tokenises, from the line
+    // (stored before the read bases are counted: a line the general routine
+    // then takes gets both words again from sid_tile_serial_kernel)
+    ST_MID(O.hdr + 2 * g, h[0]);
+    ST_MID(O.hdr + 2 * g + 1, h[1]);
+    Head hd;
+    hd.clen = clen;
+    hd.pos = (int32_t)(uint32_t)h[0];
+    const uint32_t base = hv ? (uint32_t)local_rec_len(hd, 0) : 0u;   // (< 2^13: the chrom below 4096 B)
+    return 1u | ((uint32_t)t4 << 1) | (kd << 7) | ((uint32_t)hv << 10) | (base << 11);
+}
+
+// the quad's part of a line (its header from quad_head): the read bases by
+// the quad, then the lead lane's outputs as tile_line's
+template <bool LOCAL, class Ld>
+__device__ __forceinline__ int quad_line(const char* __restrict__ text, const char* tl, Ld ld, uint64_t g0, uint32_t r0,
+                                         uint32_t mt, uint64_t g, uint32_t len_t, uint64_t c1, bool lead,
+                                         const uint32_t* rbl, const TileOut& O, const LocalLen& LL)
+{
+    if (!(mt & 1u)) return 0;   // (the whole quad: the general routine's line)
+    const uint32_t q = r0 + (uint32_t)((mt >> 1) & 63u), kd = (uint32_t)(mt >> 7) & 7u;
+    uint64_t c = 0;
+    const bool ok = read_bases_quad<Ld, uint32_t>(ld, len_t, q, kd, rbl, (const uint4*)(tl + (q & ~15u)), &c);
+    if (!lead) return 0;
+    const uint64_t s0 = g0 + r0;
+    if (!ok) {
+        const unsigned long long k = atomicAdd(O.lb + 6, 1ull);
+        O.fb[k] = (uint32_t)g;
+        O.fbo[k] = (uint32_t)s0;
+        return 0;
+    }
+    if (!LOCAL) {
+        ST_MID(O.counts + g, c);
+        return 0;
+    }
+    int l;
+    if ((mt >> 10) & 1u) {
+        const int L = local_site_tail(c, g, LL.len1, LL);
+        l = L < 0 ? 0 : (int)(mt >> 11) + L;
+    } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
+        l = local_site_len_text(text, c1, s0, c, g, LL);
+    }
+    if (l == 0) O.counts[g] = c;   // a fix-up site: the fix-up reads its counts
     return l;
 }
 
@@ -1868,9 +1937,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     __shared__ uint8_t cls[256];
     __shared__ uint32_t rbl[256];
     __shared__ uint32_t wtot[TB / 64][NW];
-    constexpr uint32_t L1W_N = LOCAL ? l1w_n(QUAD) : 0u;
-    static_assert(L1W_N == 0 || L1W_N == 16 * TB, "the window: 16 bytes a lane");
-    __shared__ __attribute__((aligned(16))) uint8_t l1w[L1W_N ? L1W_N : 16];
+    __shared__ uint32_t qmeta[QUAD ? tp_cap_max(true) : 1];   // the quad shape's headers (quad_head)
     const uint32_t tid = threadIdx.x;
     cls[tid] = (uint8_t)base_class(tid);
     rbl[tid] = rb_entry(tid);
@@ -1896,9 +1963,6 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         // the byte before the tile (one address for the block)
         const bool pok = g0 > c0 && g0 - 1 < c1;
         const uint32_t pbyte = (uint8_t)text[pok ? g0 - 1 : g0];
-        // the tail lengths' window (L2-resident: every block reads it)
-        uint4 wv = make_uint4(0, 0, 0, 0);
-        if constexpr (L1W_N != 0) wv = *(const uint4*)(LL.len1 + l1w_lo(QUAD) + tid * 16);
         uint4 v[ROWS];
 #pragma unroll
         for (uint32_t k = 0; k < ROWS; ++k) {
@@ -1911,7 +1975,6 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         for (uint32_t k = 0; k < ROWS; ++k) *(uint4*)(tl + k * TILE + tid * 16) = v[k];
         if (tid < TP_HALO / 16) *(uint4*)(tl + TP_TILE + tid * 16) = hok ? hv : make_uint4(0, 0, 0, 0);
         if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
-        if constexpr (L1W_N != 0) *(uint4*)(l1w + tid * 16) = wv;
         // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
         const uint32_t prev0 = tid ? 0u : pok ? (pbyte == '\n') : 1u;
         __syncthreads();
@@ -2011,12 +2074,21 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         };
         const uint32_t len_t = (uint32_t)(c1 - g0);   // the chunk's end
         const uint64_t g_tile = t * (uint64_t)cap;
+        if constexpr (QUAD) {   // the headers, a lane per line (cnt <= cap <= TB)
+            static_assert(tp_cap_max(true) <= TB, "a lane per line of the quad shape's tile");
+            if (tid < cnt) qmeta[tid] = quad_head<LOCAL>(tl, g0, ls[tid], g_tile + tid, len_t, cls, O);
+            __syncthreads();
+        }
         for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
             const uint32_t j = j0 + (QUAD ? tid >> 2 : tid);
             const bool lead = !QUAD || (tid & 3u) == 0;   // the lane that writes the line's outputs
             int l = 0;
-            if (j < cnt)
-                l = tile_line<QUAD, LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, lead, cls, rbl, O, LL, l1w);
+            if (j < cnt) {
+                if constexpr (QUAD)
+                    l = quad_line<LOCAL>(text, tl, ld, g0, ls[j], qmeta[j], g_tile + j, len_t, c1, lead, rbl, O, LL);
+                else
+                    l = tile_line<LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, lead, cls, rbl, O, LL);
+            }
             if (!LOCAL) continue;
             // the record bytes into the writer blocks' sums: the wave's slots (64,
             // or 16 with quads, from a multiple of 16) lie in one block or two
