@@ -1866,33 +1866,44 @@ __device__ __forceinline__ uint32_t quad_head(const char* tl, uint64_t g0, uint3
     return 1u | ((uint32_t)t4 << 1) | (kd << 7) | ((uint32_t)hv << 10) | (base << 11);
 }
 
-// the quad's part of a line (its header from quad_head): the read bases by
-// the quad, then the lead lane's outputs as tile_line's
+// the quad's part of a line (its header from quad_head): the read bases
+// counted by the quad; the lead lane lists the line for the general routine
+// when they need it, else stores its counts (the Lynch paths'), or, for
+// -m local, keeps them in LDS for quad_tail (bit 31 of the line's word: counted)
 template <bool LOCAL, class Ld>
-__device__ __forceinline__ int quad_line(const char* __restrict__ text, const char* tl, Ld ld, uint64_t g0, uint32_t r0,
-                                         uint32_t mt, uint64_t g, uint32_t len_t, uint64_t c1, bool lead,
-                                         const uint32_t* rbl, const TileOut& O, const LocalLen& LL)
+__device__ __forceinline__ void quad_bases(const char* tl, Ld ld, uint64_t g0, uint32_t r0, uint32_t* meta,
+                                           uint64_t* cnt_l, uint64_t g, uint32_t len_t, bool lead,
+                                           const uint32_t* rbl, const TileOut& O)
 {
-    if (!(mt & 1u)) return 0;   // (the whole quad: the general routine's line)
-    const uint32_t q = r0 + (uint32_t)((mt >> 1) & 63u), kd = (uint32_t)(mt >> 7) & 7u;
+    const uint32_t mt = *meta;
+    if (!(mt & 1u)) return;   // (the whole quad: the general routine's line)
+    const uint32_t q = r0 + ((mt >> 1) & 63u), kd = (mt >> 7) & 7u;
     uint64_t c = 0;
     const bool ok = read_bases_quad<Ld, uint32_t>(ld, len_t, q, kd, rbl, (const uint4*)(tl + (q & ~15u)), &c);
-    if (!lead) return 0;
-    const uint64_t s0 = g0 + r0;
+    if (!lead) return;
     if (!ok) {
         const unsigned long long k = atomicAdd(O.lb + 6, 1ull);
         O.fb[k] = (uint32_t)g;
-        O.fbo[k] = (uint32_t)s0;
-        return 0;
-    }
-    if (!LOCAL) {
+        O.fbo[k] = (uint32_t)(g0 + r0);
+    } else if (!LOCAL) {
         ST_MID(O.counts + g, c);
-        return 0;
+    } else {
+        *cnt_l = c;
+        *meta = mt | (1u << 31);
     }
+}
+
+// -m local's call of a counted quad-shape line, a lane per line as the
+// header: the class word, the record's length (returned; 0 for a fix-up site
+// or a line not counted here)
+__device__ __forceinline__ int quad_tail(const char* __restrict__ text, uint64_t s0, uint32_t mt, uint64_t c, uint64_t g,
+                                         uint64_t c1, const TileOut& O, const LocalLen& LL)
+{
+    if (!(mt >> 31)) return 0;
     int l;
     if ((mt >> 10) & 1u) {
         const int L = local_site_tail(c, g, LL.len1, LL);
-        l = L < 0 ? 0 : (int)(mt >> 11) + L;
+        l = L < 0 ? 0 : (int)((mt >> 11) & 0x1FFFu) + L;
     } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
         l = local_site_len_text(text, c1, s0, c, g, LL);
     }
@@ -1938,6 +1949,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     __shared__ uint32_t rbl[256];
     __shared__ uint32_t wtot[TB / 64][NW];
     __shared__ uint32_t qmeta[QUAD ? tp_cap_max(true) : 1];   // the quad shape's headers (quad_head)
+    __shared__ uint64_t qcnt[QUAD && LOCAL ? tp_cap_max(true) : 1];   // ... and counts (quad_bases)
     const uint32_t tid = threadIdx.x;
     cls[tid] = (uint8_t)base_class(tid);
     rbl[tid] = rb_entry(tid);
@@ -2074,29 +2086,39 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         };
         const uint32_t len_t = (uint32_t)(c1 - g0);   // the chunk's end
         const uint64_t g_tile = t * (uint64_t)cap;
-        if constexpr (QUAD) {   // the headers, a lane per line (cnt <= cap <= TB)
-            static_assert(tp_cap_max(true) <= TB, "a lane per line of the quad shape's tile");
-            if (tid < cnt) qmeta[tid] = quad_head<LOCAL>(tl, g0, ls[tid], g_tile + tid, len_t, cls, O);
-            __syncthreads();
-        }
-        for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
-            const uint32_t j = j0 + (QUAD ? tid >> 2 : tid);
-            const bool lead = !QUAD || (tid & 3u) == 0;   // the lane that writes the line's outputs
-            int l = 0;
-            if (j < cnt) {
-                if constexpr (QUAD)
-                    l = quad_line<LOCAL>(text, tl, ld, g0, ls[j], qmeta[j], g_tile + j, len_t, c1, lead, rbl, O, LL);
-                else
-                    l = tile_line<LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, lead, cls, rbl, O, LL);
-            }
-            if (!LOCAL) continue;
-            // the record bytes into the writer blocks' sums: the wave's slots (64,
-            // or 16 with quads, from a multiple of 16) lie in one block or two
-            const uint64_t gw = (g_tile + j0 + (QUAD ? (tid & ~63u) >> 2 : (tid & ~63u))) / FTB;
+        // the record bytes of a round's lines (slot g_tile + j0 + lane's line)
+        // into the writer blocks' sums: a wave's slots (64, or 16 with quads,
+        // from a multiple of 16) lie in one block or two
+        auto bsum_add = [&](uint32_t wslot0, uint32_t j, int l) {
+            const uint64_t gw = (g_tile + wslot0) / FTB;
             const uint32_t lo = (g_tile + j) / FTB == gw ? (uint32_t)l : 0u;
             const uint32_t slo = wave_sum(lo), shi = wave_sum((uint32_t)l - lo);
             if ((tid & 63u) == 0 && slo) atomicAdd(LL.bsum + gw, slo);
             if ((tid & 63u) == 0 && shi) atomicAdd(LL.bsum + gw + 1, shi);
+        };
+        if constexpr (QUAD) {
+            // the headers a lane per line, the read bases a quad per line,
+            // -m local's call a lane per line again (cnt <= cap <= TB)
+            static_assert(tp_cap_max(true) <= TB, "a lane per line of the quad shape's tile");
+            if (tid < cnt) qmeta[tid] = quad_head<LOCAL>(tl, g0, ls[tid], g_tile + tid, len_t, cls, O);
+            __syncthreads();
+            for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
+                const uint32_t j = j0 + (tid >> 2);
+                if (j < cnt) quad_bases<LOCAL>(tl, ld, g0, ls[j], qmeta + j, qcnt + j, g_tile + j, len_t, (tid & 3u) == 0, rbl, O);
+            }
+            if constexpr (LOCAL) {
+                __syncthreads();
+                int l = 0;
+                if (tid < cnt) l = quad_tail(text, g0 + ls[tid], qmeta[tid], qcnt[tid], g_tile + tid, c1, O, LL);
+                bsum_add(tid & ~63u, tid, l);
+            }
+        } else {
+            for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
+                const uint32_t j = j0 + tid;
+                int l = 0;
+                if (j < cnt) l = tile_line<LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, true, cls, rbl, O, LL);
+                if constexpr (LOCAL) bsum_add(j0 + (tid & ~63u), j, l);
+            }
         }
         // (the prefetch's value: kept live to here, never true)
         if (pf == 0x5A5A5A5Au && c1 == 0) O.state[5] = pf;
