@@ -1785,7 +1785,7 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
 // quad_head, then quad_line.)
 template <bool LOCAL, class Ld>
 __device__ __forceinline__ int tile_line(const char* __restrict__ text, const char* tl, Ld ld, uint64_t g0, uint32_t r0,
-                                         uint64_t g, uint32_t len_t, uint64_t c1, bool lead, const uint8_t* cls,
+                                         uint64_t g, uint32_t len_t, uint64_t c1, const uint8_t* cls,
                                          const uint32_t* rbl, const TileOut& O, const LocalLen& LL)
 {
     int l = 0;
@@ -1801,8 +1801,7 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
         const uint4* first = (const uint4*)(stage + ((sh + (uint32_t)t4) & 0x30u));
         ok = read_bases_lut<Ld, uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c);
     }
-    if (!lead) {
-    } else if (ok) {
+    if (ok) {
         const bool hv = (h[0] >> 63) != 0;
         const uint32_t clen = (uint32_t)(h[0] >> 32) & 0xFFFu;
         if (!hv || clen > 8) h[1] = (uint32_t)s0;   // the writer reads the chrom, or tokenises, from the line
@@ -2116,7 +2115,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
                 const uint32_t j = j0 + tid;
                 int l = 0;
-                if (j < cnt) l = tile_line<LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, true, cls, rbl, O, LL);
+                if (j < cnt) l = tile_line<LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, cls, rbl, O, LL);
                 if constexpr (LOCAL) bsum_add(j0 + (tid & ~63u), j, l);
             }
         }
