@@ -247,8 +247,7 @@ def stage_kernels(stage, fused, text_per_site=81.0):
     tp = tile_parse(fused, text_per_site)
     return {
         "index": ["sid_index_count_kernel", "sid_scan_*"],
-        "parse": (["sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_tile_len_list_kernel",
-                   "sid_local_fixlen_kernel", "sid_scan_*"] if tp else
+        "parse": (["sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_scan_*"] if tp else
                   ["sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_tile_compact_kernel", "sid_scan_*"]
                   if fused == "lynch" else
                   ["sid_index_emit_kernel", ("sid_parse_quad_kernel" if parse_quad(text_per_site) else

@@ -1604,6 +1604,7 @@ __device__ __forceinline__ uint32_t local_word(uint32_t k, uint32_t f, uint32_t 
 // C5's parse 11.41 -> 11.28 ms per step, but cost more than it saved beside
 // quad_head: 11.19 with it, 11.03 without; for the lane shape, 2 KiB of the
 // ~30x profiles: C2 parse 1.79 -> 1.92 ms.)
+template <bool LIST = true>   // LIST: a fix-up site listed in LL.miss (else the caller fixes it up)
 __device__ __forceinline__ int local_site_tail(uint64_t c, uint64_t i, const uint8_t* L1, const LocalLen& LL)
 {
     uint32_t f, s, nf, ns, cov;
@@ -1613,7 +1614,7 @@ __device__ __forceinline__ int local_site_tail(uint64_t c, uint64_t i, const uin
     const bool miss = L == 0xFFu;
     LL.cls[i] = miss ? SID_CLS_MISS : local_word(k, f, s);   // (read back by the writer soon: through the caches)
     if (miss) {
-        LL.miss[atomicAdd(LL.nmiss, 1ull)] = (uint32_t)i;   // its bytes: the fix-up's
+        if (LIST) LL.miss[atomicAdd(LL.nmiss, 1ull)] = (uint32_t)i;   // its bytes: the fix-up's
         return -1;
     }
     return (int)L;
@@ -2138,18 +2139,49 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
 // address each, which serialise; 256 blocks took 20 us a launch)
 constexpr unsigned TILE_SERIAL_GRID = 64;
 
+// -m local's fix-up (the sites no class table covers: local.hip's
+// fixup_site) and its record length into the writer block's bytes
+struct LocalFix {
+    LocalLen LL;
+    sid_local_k K;
+    const double* lnt;
+    CType ct;
+    uint8_t* code;
+    double* hom;
+    double* het;
+};
+__device__ __forceinline__ void fix_site(uint64_t i, const Head& hd, uint64_t c, const LocalFix& F,
+                                         unsigned long long* lb)
+{
+    double h, t;
+    const uint32_t code = fixup_site(c, nullptr, F.K, F.lnt, h, t);
+    F.code[i] = (uint8_t)code;
+    F.hom[i] = h;
+    F.het[i] = t;
+    int l = record_len(hd, (uint8_t)code, sid_g6_prep(h), sid_g6_prep(t), F.ct.len);
+    if (l < 0) {
+        atomicExch(lb + 2, 1ull);
+        l = 0;
+    }
+    atomicAdd(F.LL.bsum + i / FTB, (uint32_t)l);
+}
+
 // the general routine over the tile parse's leftovers (slot, line offset):
 // counts and a header pair with no chrom (the formatter tokenises the line),
 // the slot listed for its record length; and the tiles' line counts summed
-// (lb[3]: sites, the counts capped at the slots) and maxed (lb[5])
+// (lb[3]: sites, the counts capped at the slots) and maxed (lb[5]).
+// LOCAL (-m local, sid_chunk_tile_local): also each leftover line's call and
+// record length, a fix-up where no class table covers it, and the fix-ups
+// the tile parse listed (LL.miss) -- the work of two more launches a chunk
+// (a record-length kernel over the leftovers, then the fix-up kernel)
+template <bool LOCAL>
 __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restrict__ text, uint64_t len,
                                                              const uint32_t* __restrict__ fb,
                                                              const uint32_t* __restrict__ fbo,
                                                              unsigned long long* lb, const uint32_t* __restrict__ tcnt,
                                                              uint64_t ntiles, uint32_t cap,
                                                              uint64_t* __restrict__ counts, uint64_t* __restrict__ hdr,
-                                                             unsigned long long* __restrict__ err,
-                                                             uint32_t* __restrict__ late, unsigned long long* nlate)
+                                                             unsigned long long* __restrict__ err, LocalFix F)
 {
     __shared__ uint8_t cls[256];
     __shared__ uint32_t red[2][TB / 64];
@@ -2200,7 +2232,21 @@ __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restr
         counts[g] = c;
         hdr[2 * g] = 0;
         hdr[2 * g + 1] = s0;
-        if (late) late[atomicAdd(nlate, 1ull)] = g;
+        if constexpr (LOCAL) {
+            Reader R{text, len};
+            const Head hd = slot_head(R, make_ulonglong2(0, s0));
+            const int L = local_site_tail<false>(c, g, F.LL.len1, F.LL);
+            if (L >= 0) atomicAdd(F.LL.bsum + g / FTB, (uint32_t)local_rec_len(hd, (uint32_t)L));
+            else fix_site(g, hd, c, F, lb);
+        }
+    }
+    if constexpr (LOCAL) {   // the tile parse's fix-up sites
+        const uint64_t nm = *F.LL.nmiss;
+        for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nm; j += (uint64_t)gridDim.x * blockDim.x) {
+            const uint64_t i = F.LL.miss[j];
+            Reader R{text, len};
+            fix_site(i, slot_head(R, *(const ulonglong2*)(hdr + 2 * i)), counts[i], F, lb);
+        }
     }
 }
 
@@ -2228,22 +2274,6 @@ __global__ __launch_bounds__(TB) void sid_tile_compact_kernel(const uint32_t* __
         d_counts[i] = counts[g];
         *(ulonglong2*)(d_hdr + 2 * i) = hw;
         d_starts[i] = keep ? 0u : (sid_off_t)hw.y;
-    }
-}
-
-// the record lengths of the general routine's slots
-__global__ __launch_bounds__(TB) void sid_tile_len_list_kernel(const char* __restrict__ text, uint64_t len,
-                                                               const uint64_t* __restrict__ hdr,
-                                                               const uint64_t* __restrict__ counts,
-                                                               const uint32_t* __restrict__ list,
-                                                               const unsigned long long* nlist, LocalLen LL)
-{
-    const uint64_t m = *nlist;
-    for (uint64_t j = (uint64_t)blockIdx.x * TB + threadIdx.x; j < m; j += (uint64_t)gridDim.x * TB) {
-        const uint32_t g = list[j];
-        Reader R{text, len};
-        const int l = local_site_len(slot_head(R, *(const ulonglong2*)(hdr + 2 * g)), counts[g], g, LL.len1, LL);
-        if (l) atomicAdd(LL.bsum + g / FTB, (uint32_t)l);
     }
 }
 
@@ -3897,17 +3927,14 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
         WCHECK(hipMemsetAsync(W->state + 4, 0xFF, sizeof(uint64_t), st));
         return fmt_scan(W, nb, st);
     }
-    uint32_t* late = W->fb + W->site_cap;
     uint32_t* miss = W->fb + 2 * W->site_cap;
     const LocalLen LL{ctx->ws.len1, ctx->ws.len2, W->bsum, miss, W->lb, W->cls};
     const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
     launch_tile_parse<true>(quad, base, c0, c1, ntp, O, LL, st);
-    sid_tile_serial_kernel<<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap,
-                                               W->counts, W->hdr, (unsigned long long*)(W->state + 4), late,
-                                               W->lb + 7);
-    sid_tile_len_list_kernel<<<64, TB, 0, st>>>(base, c1, W->hdr, W->counts, late, W->lb + 7, LL);
-    sid_local_fixlen_kernel<true><<<64, TB, 0, st>>>(base, c1, nullptr, W->hdr, W->counts, miss, W->lb, ctx->K,
-                                                     ctx->d_lnt, ct, W->code, W->hom, W->het, W->bsum, W->lb);
+    const LocalFix F{LL, ctx->K, ctx->d_lnt, ct, W->code, W->hom, W->het};
+    sid_tile_serial_kernel<true><<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp,
+                                                     cap, W->counts, W->hdr,
+                                                     (unsigned long long*)(W->state + 4), F);
     WCHECK(hipGetLastError());
     W->cls_ready = true;
     return fmt_scan(W, nb, st);
@@ -3936,8 +3963,9 @@ int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64
     const LocalLen LL{};
     const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
     launch_tile_parse<false>(quad, base, c0, c1, ntp, O, LL, st);
-    sid_tile_serial_kernel<<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp, cap, W->counts,
-                                               W->hdr, (unsigned long long*)(W->state + 4), nullptr, nullptr);
+    sid_tile_serial_kernel<false><<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp,
+                                                      cap, W->counts, W->hdr,
+                                                      (unsigned long long*)(W->state + 4), LocalFix{});
     // the tiles' first sites in file order (state[0]: the chunk's sites; over the cap: void)
     launch_scan(W->tcnt, ntp, W->toff, W->state, nullptr,
                 (uint64_t*)((char*)W->tcnt + ((ntp * 4 + 7) & ~(size_t)7)), st);

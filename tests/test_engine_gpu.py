@@ -76,6 +76,44 @@ def test_tile_parse_quad_shape(sid, oracle, tmp_path, extra):
     assert a.stderr == b.stderr
 
 
+@pytest.mark.parametrize("extra", [["--chunk-bytes", "200000"], ["--chunk-bytes", "1000000", "--devices", "2"]],
+                         ids=["200k", "1m-2dev"])
+def test_tile_fixups_and_general_routine(sid, oracle, tmp_path, extra):
+    """Sites no class table covers (four alleles in numbers: the fix-up,
+    textpath.hip fix_site) in both tile shapes, from the fast path (the tile
+    parse lists them) and from the general routine (a '+'/'-' indel in the
+    read bases: sid_tile_serial_kernel fixes them up itself), mixed with
+    covered sites and lines of every other kind; the CSV is the oracle's."""
+    rng = np.random.default_rng(64)
+
+    def lines(chrom, n, depth, indel_every):
+        out = []
+        for i in range(1, n + 1):
+            k = rng.integers(0, 4, 4) * (depth // 8) + rng.integers(0, 3, 4)
+            bases = bytearray(b"A" * int(k[0]) + b"c" * int(k[1]) + b"G" * int(k[2]) + b"t" * int(k[3]) +
+                              b"." * int(rng.integers(0, depth // 2)))
+            rng.shuffle(bases)
+            if indel_every and i % indel_every == 0:
+                bases[len(bases) // 2:len(bases) // 2] = b"+2AC"
+            if i % 7 == 0:
+                bases[0:0] = b"^I"
+            b = bytes(bases) or b"*"
+            out.append(b"%s\t%d\tA\t%d\t%s\t%s\n" % (chrom, i, len(b), b, b"I" * len(b)))
+        return b"".join(out)
+
+    text = (lines(b"chr1", 3000, 40, 5) + sid.synth_text(65, 3000, 30.0, sites_per_chrom=10 ** 6) +
+            lines(b"chr2", 1500, 1200, 4) + sid.synth_text(66, 2000, 200.0, sites_per_chrom=10 ** 6) +
+            lines(b"chr3", 2000, 40, 0))
+    p = tmp_path / "fixups.plp"
+    p.write_bytes(text)
+    b = oracle.run_cli([str(p)])
+    a = run(sid.CLI_PATH, extra + [str(p)])
+    assert b.returncode == 0
+    assert a.returncode == 0, a.stderr[-400:]
+    assert a.stdout == b.stdout
+    assert a.stderr == b.stderr
+
+
 @pytest.mark.parametrize("extra", [["--hold-bytes", "1"], ["--hold-bytes", "1", "--retain-bytes", "1"],
                                    ["--hold-bytes", "200000", "--retain-bytes", "150000"]],
                          ids=["all-in-pass-2-kept", "all-reloaded", "mixed"])

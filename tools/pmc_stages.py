@@ -20,7 +20,7 @@ STAGES = {   # the scan kernels (shared by the index and the formatter, ~20 us) 
     "parse": ["sid_index_emit_kernel", "sid_parse_kernel", "sid_parse_len_kernel", "sid_parse_quad_kernel",
               "sid_parse_serial_kernel", "sid_local_len_list_kernel",
               # the tile parse (-m local, lines up to 256 B): index, parse, lengths and fix-up in one stage
-              "sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_tile_len_list_kernel"],
+              "sid_tile_parse_kernel", "sid_tile_serial_kernel"],
     "call": ["sid_lookup_rec_kernel"],
     "hist": ["sid_hist_dense_kernel", "sid_hist_reduce_kernel", "sid_hist_list_kernel"],
     "fmt_len": ["sid_local_len_kernel", "sid_local_fixlen_kernel", "sid_fmt_blen_kernel", "sid_lynch_len_kernel"],
@@ -41,8 +41,7 @@ def main():
         if tile and stage == "parse":
             # the tile parse's stage (the two-pass kernels only ran for chunks
             # whose tiles overflowed their slots: not the stage's steady state)
-            ks = ["sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_tile_len_list_kernel",
-                  "sid_tile_compact_kernel"]
+            ks = ["sid_tile_parse_kernel", "sid_tile_serial_kernel", "sid_tile_compact_kernel"]
         if tile and stage == "index":
             continue
         tot, parts = 0.0, {}
