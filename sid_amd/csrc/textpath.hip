@@ -2781,6 +2781,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_lynch_put_kernel(const
                                                                           const uint64_t* state, unsigned long long* lb,
                                                                           char* __restrict__ out)
 {
+    __builtin_amdgcn_s_setprio(3);   // (the loads and the class lookup: as sid_local_put_kernel)
     constexpr int NQ = (FMT_LDS2 + 64) / 16;   // records, slack
     __shared__ uint4 buf4[NQ];
     for (int k = threadIdx.x; k < NQ; k += FTB) buf4[k] = make_uint4(0, 0, 0, 0);
@@ -2804,6 +2805,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_lynch_put_kernel(const
             l = lynch_rec_len(h, e0.x & 0xFFu);
         }
     }
+    __builtin_amdgcn_s_setprio(0);
     if (blockIdx.x == 0 && threadIdx.x == 0) lb[4] = state[4];
     uint32_t tot;
     const uint32_t my = block_exscan_once<FTB>((uint32_t)l, &tot);   // (its barrier also orders the zeroing)
