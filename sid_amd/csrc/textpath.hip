@@ -2116,7 +2116,9 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             __syncthreads();
             for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
                 const uint32_t j = j0 + (tid >> 2);
-                if (j < cnt) quad_bases<LOCAL>(tl, ld, g0, ls[j], qmeta + j, qcnt + j, g_tile + j, len_t, (tid & 3u) == 0, rbl, O);
+                if (j < cnt)
+                    quad_bases<LOCAL>(tl, ld, g0, ls[j], qmeta + j, qcnt + (LOCAL ? j : 0), g_tile + j, len_t,
+                                      (tid & 3u) == 0, rbl, O);
             }
             if constexpr (LOCAL) {
                 __syncthreads();
