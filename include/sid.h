@@ -342,6 +342,9 @@ typedef struct {
     uint64_t tile_overflows;     /* chunks with a tile of more lines than its slots
                                     (parsed again by the two-pass path; the next
                                     chunks get more slots)                         */
+    uint64_t tile_overflows_queued; /* of those, overflows with the device's next
+                                    chunk already popped behind it (its run-ahead
+                                    tile parse dropped, the chunk kept)            */
 } sid_run_stats;
 void sid_engine_cfg_default(sid_engine_cfg* cfg);
 int sid_engine_create(const sid_opts* opts, const sid_engine_cfg* cfg, sid_engine** out);

@@ -132,11 +132,13 @@ int main(int argc, char** argv)
     /* test/bench harness, not a reference option: ORACLE_RANGE=OFF:LEN reads
        only the (line-aligned) bytes [OFF, OFF + LEN) of the file -- the CPU
        baseline's shard processes over one file (bench.py) */
-    unsigned long long limit = ~0ull;
+    unsigned long long limit = ~0ull, range_off = 0;
     if (getenv("ORACLE_RANGE")) {
         unsigned long long off = 0, n = 0;
-        if (sscanf(getenv("ORACLE_RANGE"), "%llu:%llu", &off, &n) == 2 && fseeko(in, (off_t)off, SEEK_SET) == 0)
+        if (sscanf(getenv("ORACLE_RANGE"), "%llu:%llu", &off, &n) == 2 && fseeko(in, (off_t)off, SEEK_SET) == 0) {
             limit = n;
+            range_off = off;
+        }
     }
     int method = -1;
     if (strcmp(o.method, "local") == 0) method = ORACLE_LOCAL;
@@ -149,12 +151,14 @@ int main(int argc, char** argv)
     double *h = NULL, *t = NULL;
     const char* conf_type = method == ORACLE_BAYES ? "probability" : "p_value";
     if (method == 3) {
-        /* readFile(in, true, true): the whole text, errors first */
+        /* readFile(in, true, true): the whole text (the range's bytes with
+           ORACLE_RANGE, as read_file below takes them), errors first */
         char* text = NULL;
         size_t len = 0, tcap = 0;
         char buf[1 << 16];
         size_t r;
-        while ((r = fread(buf, 1, sizeof buf, in)) > 0) {
+        while (len < limit &&
+               (r = fread(buf, 1, (size_t)(limit - len < sizeof buf ? limit - len : sizeof buf), in)) > 0) {
             if (len + r > tcap) {
                 tcap = 2 * (len + r);
                 text = (char*)realloc(text, tcap);
@@ -183,7 +187,7 @@ int main(int argc, char** argv)
         t = (double*)malloc((nq ? nq : 1) * sizeof(double));
         oracle_call_quality_text(text, len, o.estimate_prior, o.snp_prior, o.significance_level, code, h, t, nq,
                                  &nq, 0);
-        rewind(in);
+        if (fseeko(in, (off_t)range_off, SEEK_SET) != 0) abort();
         read_file(in, &s, limit);   /* chrom and pos; cannot fail after the quality parse */
         free(text);
     } else if (method >= 0) {

@@ -72,7 +72,8 @@ class RunStats(C.Structure):
                 ("err_offset", C.c_uint64), ("ingest_s", C.c_double), ("estimate_s", C.c_double),
                 ("emit_s", C.c_double), ("estimate", Estimate), ("chunks_registered", C.c_uint64),
                 ("register_s", C.c_double), ("h2d_s", C.c_double), ("h2d_bytes", C.c_uint64),
-                ("chunks_tiled", C.c_uint64), ("tile_overflows", C.c_uint64)]
+                ("chunks_tiled", C.c_uint64), ("tile_overflows", C.c_uint64),
+                ("tile_overflows_queued", C.c_uint64)]
 
 
 class Placement(C.Structure):

@@ -434,7 +434,7 @@ int main(int argc, char** argv)
                          "\"chunks_retained\": %llu, \"chunks_reloaded\": %llu, \"bytes_in\": %llu, "
                          "\"bytes_out\": %llu, \"ingest_s\": %.6f, \"chunks_registered\": %llu, "
                          "\"register_s\": %.6f, \"h2d_s\": %.6f, \"h2d_bytes\": %llu, \"chunks_tiled\": %llu, "
-                         "\"tile_overflows\": %llu, \"placement\": [%s], "
+                         "\"tile_overflows\": %llu, \"tile_overflows_queued\": %llu, \"placement\": [%s], "
                          "\"main_entry_unix\": %.6f, \"main_exit_unix\": %.6f}\n",
                          (unsigned long long)st.sites, D, T, tc - t0, t1 - t0, t2 - t1, t3 - t2, t3 - t0,
                          st.sites / std::max(1e-9, t3 - t0), (unsigned long long)st.chunks,
@@ -442,7 +442,8 @@ int main(int argc, char** argv)
                          (unsigned long long)st.chunks_reloaded, (unsigned long long)st.bytes_in,
                          (unsigned long long)st.bytes_out, st.ingest_s, (unsigned long long)st.chunks_registered,
                          st.register_s, st.h2d_s, (unsigned long long)st.h2d_bytes,
-                         (unsigned long long)st.chunks_tiled, (unsigned long long)st.tile_overflows, place.c_str(),
+                         (unsigned long long)st.chunks_tiled, (unsigned long long)st.tile_overflows,
+                         (unsigned long long)st.tile_overflows_queued, place.c_str(),
                          t_entry,
                          unix_now());
         // device memory, pinned staging and the mapping go with the process

@@ -367,11 +367,38 @@ struct Dev {
         else
             tile_set((uint64_t)((double)n * sid_tile_unit(q2) / (double)std::max<uint64_t>(1, bytes) * 1.25) + 1, q2);
     }
-    // a tile had more lines than slots (the chunk goes the two-pass way)
+    // a tile had more lines than slots (the chunk goes the two-pass way); the
+    // tile parse stays off while no shape has room for them: judged in the
+    // units of the shape tile_set chose (a quad tile's lines counted in lane
+    // tiles when it switched to the lane shape)
     void tile_over(uint64_t maxl, bool quad)
     {
         tile_set(maxl + maxl / 32 + 2, quad);
-        tile_ok = maxl <= SID_TILE_CAP_MAX;
+        const uint64_t need = quad && !tile_quad ? maxl * sid_tile_unit(false) / sid_tile_unit(true) + 1 : maxl;
+        tile_ok = need <= (tile_quad ? SID_TILE_CAP_MAX_QUAD : SID_TILE_CAP_MAX);
+    }
+    // the tile parse off (a run of tiny lines): after a two-pass chunk of n
+    // sites over `bytes` whose lines per byte leave a lane tile half its
+    // largest list, on again with that chunk's density (a quarter on top);
+    // a tile of tiny lines in it overflows and turns it off again
+    void tile_retry(uint64_t n, uint64_t bytes)
+    {
+        const uint64_t per = (uint64_t)((double)n * sid_tile_unit(false) / (double)std::max<uint64_t>(1, bytes) * 1.25) + 1;
+        if (tile_ok || 2 * per > SID_TILE_CAP_MAX) return;
+        tile_hi = 0;
+        tile_set(per, false);
+        tile_ok = true;
+    }
+    // a new run: a device the last run left with the tile parse off starts
+    // from the defaults (a run that kept it on keeps its shape and slots, the
+    // next run's likely fit)
+    void tile_reset()
+    {
+        if (tile_ok) return;
+        tile_cap = 288;
+        tile_quad = false;
+        tile_hi = 0;
+        tile_ok = true;
     }
     uint64_t hold_budget = 0, retain_budget = 0;
     std::atomic<uint64_t> hold_used{0}, retain_used{0};
@@ -381,7 +408,7 @@ struct Dev {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> h2d_pending;
     std::vector<hipEvent_t> h2d_free;
     uint64_t h2d_bytes = 0;
-    uint64_t tiled = 0, tile_overflows = 0;   // this run's chunks (the device's compute thread)
+    uint64_t tiled = 0, tile_overflows = 0, tile_over_queued = 0;   // this run's chunks (the device's compute thread)
     hipEvent_t h2d_event()
     {
         hipEvent_t ev = nullptr;
@@ -1464,7 +1491,8 @@ void compute(sid_engine* e, Dev& d, int pass)
         // (pre_tiled: this chunk's tile parse already ran behind the previous
         // chunk's writer, with the slots and shape of that time)
         bool tiled = false;
-        const bool tile_path = x == hipSuccess && rc == SID_OK && format && !lynch_hist && !qmode &&
+        const bool tile_was_off = !d.tile_ok;   // (this chunk then goes the two-pass way, and may turn it on)
+        const bool tile_path =x == hipSuccess && rc == SID_OK && format && !lynch_hist && !qmode &&
                                (d.tile_ok || pre_tiled) && e->opts.method == SID_METHOD_LOCAL &&
                                sid_chunk_local_ok(d.ctx) && !(pass == 2 && r.pre);
         if (pre_tiled && !tile_path) {
@@ -1561,6 +1589,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                     cap = 0;
                     via_host = sunk = false;
                     ++d.tile_overflows;
+                    d.tile_over_queued += have_next;
                     d.tile_over(maxl, quad);
                     // this chunk goes the two-pass way through the workspace:
                     // the next chunk's tile parse is dropped (it runs again)
@@ -1672,6 +1701,7 @@ void compute(sid_engine* e, Dev& d, int pass)
             rc = sid_chunk_reserve(&W, 0, n);
             if (rc != SID_OK) return (void)fail(e, rc);
             r.parsed = n;
+            if (tile_was_off && !qmode) d.tile_retry(n, L.c1 - L.c0);
             // Lynch paths: the parse goes straight into a buffer kept for
             // pass 2 (which then skips index and parse) while the retain
             // budget allows: 28 B a site, cheaper than indexing and parsing
@@ -2009,7 +2039,8 @@ static void reset_run(sid_engine* e)
         d.hh_full = false;
         (void)d.h2d_collect();   // (a failed run's copies: its devices were synchronised)
         d.h2d_bytes = 0;
-        d.tiled = d.tile_overflows = 0;
+        d.tiled = d.tile_overflows = d.tile_over_queued = 0;
+        d.tile_reset();
         d.ws.slot_cap = 0;   // (a failed run may leave the slot layout set)
     }
     e->hist_merged = false;
@@ -2141,7 +2172,7 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         std::fprintf(stderr, "{\"ingest_setup_s\": %.6f, \"budgets_s\": %.6f, \"spawn_s\": %.6f, \"join_s\": %.6f}\n",
                      t_setup - t0, t_budget - t0, t_spawn - t_setup, t_join - t_spawn);
     double h2d_s = 0;
-    uint64_t h2d_bytes = 0, tiled = 0, tile_over = 0;
+    uint64_t h2d_bytes = 0, tiled = 0, tile_over = 0, tile_oq = 0;
     for (auto& dp : e->devs) {
         (void)hipSetDevice(dp->device);
         if (hipStreamSynchronize(dp->s_comp) != hipSuccess || hipStreamSynchronize(dp->s_up) != hipSuccess ||
@@ -2152,7 +2183,8 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         dp->h2d_bytes = 0;
         tiled += dp->tiled;
         tile_over += dp->tile_overflows;
-        dp->tiled = dp->tile_overflows = 0;
+        tile_oq += dp->tile_over_queued;
+        dp->tiled = dp->tile_overflows = dp->tile_over_queued = 0;
     }
     uint64_t sites = 0, bytes = 0, held = 0, kept = 0;
     for (auto& r : e->recs) {
@@ -2177,6 +2209,7 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         st->h2d_bytes = h2d_bytes;
         st->chunks_tiled = tiled;
         st->tile_overflows = tile_over;
+        st->tile_overflows_queued = tile_oq;
     }
     timing_report(e, "ingest", wall() - t0);
     const uint64_t fe = e->first_err.load();

@@ -195,7 +195,7 @@ int sid_chunk_local_len(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
 int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_t c1, uint64_t n,
                         const char* conf_type, char* out, hipStream_t st);
 // -m local (sid_chunk_local_ok) in one pass over the text: the tile parse of
-// [c0, c1) with cap slots per tile (a multiple of 32, SID_TILE_CAP_MIN .. _MAX), the
+// [c0, c1) with cap slots per tile (a multiple of 16, SID_TILE_CAP_MIN .. _MAX), the
 // record lengths, the fix-up and the writer's offsets; sid_chunk_local_put
 // then writes the records into a buffer of sid_chunk_tile_bound.  No host
 // round trip inside.  Afterwards lb[1] bytes, lb[2] range flag, lb[3] sites,

@@ -1751,7 +1751,7 @@ __host__ __device__ constexpr uint32_t tp_cap_max(bool quad) { return quad ? SID
 __host__ __device__ constexpr uint32_t tp_tile(bool quad) { return (quad ? TP_ROWS_QUAD : TP_ROWS) * TILE; }
 
 struct TileOut {
-    uint32_t cap;               // slots per tile (a multiple of 32, SID_TILE_CAP_MIN .. _MAX)
+    uint32_t cap;               // slots per tile (a multiple of 16, powers of 2 included, SID_TILE_CAP_MIN .. _MAX)
     uint32_t* tcnt;             // per tile: its lines (above the cap: overflow; the writer takes the first cap)
     uint64_t* hdr;              // per slot: the header pair
     uint64_t* counts;           // per slot: counts of the fix-up's and the general routine's sites
@@ -3824,7 +3824,8 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
         const uint64_t nbs = (W->slots + FTB - 1) / FTB;
         if (nbs == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
                                  ? SID_OK : SID_EHIP;
-        const uint64_t magic = ~0ull / W->slot_cap + 1;   // ceil(2^64 / cap) (cap: a multiple of 32, not a power of 2)
+        if (W->slots >> 32) return SID_EINVAL;   // (a 4 GiB chunk has < 2^28 slots)
+        const uint64_t magic = ~0ull / W->slot_cap + 1;   // ceil(2^64 / cap): the slot's tile by a multiply-high, exact for slots < 2^32 (cap: a multiple of 16 up to 1024, powers of 2 included)
         sid_local_put_kernel<true><<<(unsigned)nbs, FTB, 0, st>>>(base, c1, nullptr, W->hdr, W->slots, W->tcnt,
                                                                  W->slot_cap, magic, W->counts, W->cls, ctx->ws.str1,
                                                                  ctx->ws.str2, W->code, W->hom, W->het, ct, W->boff,
@@ -3999,6 +4000,7 @@ int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64
 int sid_chunk_tile_compact(sid_chunk_ws* W, sid_off_t* starts, uint64_t* counts, uint64_t* hdr, hipStream_t st)
 {
     if (!W->slot_cap) return SID_ESTATE;
+    if (W->slots >> 32) return SID_EINVAL;   // (the magic's exact range; a 4 GiB chunk has < 2^28 slots)
     const uint64_t magic = ~0ull / W->slot_cap + 1;
     const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((W->slots + TB - 1) / TB, 1), 8192);
     sid_tile_compact_kernel<<<grid, TB, 0, st>>>(W->tcnt, W->toff, W->slots, W->slot_cap, magic, W->counts, W->hdr,

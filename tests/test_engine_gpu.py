@@ -636,7 +636,14 @@ def test_tile_parse_slot_caps(sid, oracle, tmp_path, extra):
     again through the two-pass path and the next ones get more slots), runs of 10-B lines
     (more lines than the most slots a tile has: the two-pass path), lines of
     3-5 KiB (past the tile's LDS halo: read from HBM), and 30x text between
-    them.  Every run's CSV is the oracle's."""
+    them.  Every run's CSV is the oracle's.
+
+    Over several chunks (--stats): tiles overflowed, at least once with the
+    device's next chunk already popped behind the overflowing one (the
+    run-ahead parse dropped and that chunk kept: round 5 lost such a chunk),
+    and the tile parse came back after the 10-B lines turned it off
+    (run.cpp Dev::tile_retry): the 30x and long-line text after them, three
+    quarters of the file, is tiled."""
     normal = sid.synth_text(61, 20_000, 30.0, sites_per_chrom=10 ** 6)
     zero = b"".join(b"chr2\t%d\tA\t0\t*\t*\n" % i for i in range(1, 20_000))
     tiny = b"".join(b"c\t%d\tA\t0\t*\n" % (i % 10) for i in range(1, 20_000))
@@ -653,3 +660,41 @@ def test_tile_parse_slot_caps(sid, oracle, tmp_path, extra):
     assert a.returncode == 0, a.stderr[-400:]
     assert a.stdout == b.stdout
     assert a.stderr == b.stderr
+    if not extra:
+        return
+    s = run(sid.CLI_PATH, ["--stats"] + extra + [str(p)])
+    assert s.returncode == 0 and s.stdout == b.stdout
+    st = json.loads(s.stderr.splitlines()[-1])
+    assert st["chunks"] > 8, st
+    assert st["tile_overflows"] > 0, st
+    assert st["tile_overflows_queued"] > 0, st
+    assert st["chunks_tiled"] >= 0.7 * st["chunks"], st
+
+
+def test_tile_parse_recovers_on_a_reused_engine(sid, oracle, tmp_path):
+    """A run of 10-B lines (more lines a tile than any slot list) turns the
+    tile parse off for the device (run.cpp Dev::tile_over); the engine's next
+    run starts with it on again (Dev::tile_reset) and tiles every chunk of 30x
+    text, and within one run a chunk of 30x text after the tiny lines turns it
+    back on (Dev::tile_retry).  Outputs are the oracle's throughout."""
+    tiny = b"".join(b"c\t%d\tA\t0\t*\n" % (i % 10) for i in range(1, 60_000))
+    normal = sid.synth_text(62, 30_000, 30.0, sites_per_chrom=10 ** 6)
+    eng = sid.Engine(chunk_bytes=200_000)
+    try:
+        for text, tag in ((tiny, "tiny"), (normal, "normal"), (tiny + normal, "both")):
+            p = tmp_path / f"{tag}.plp"
+            p.write_bytes(text)
+            ref = oracle.run_cli([str(p)])
+            assert ref.returncode == 0
+            eng.source_text(text)
+            out, st = eng.run()
+            assert out == ref.stdout, tag
+            if tag == "tiny":
+                assert st.tile_overflows >= 1 and st.chunks_tiled == 0, (st.chunks, st.chunks_tiled)
+            elif tag == "normal":
+                assert st.chunks > 8 and st.chunks_tiled >= st.chunks - 1, (st.chunks, st.chunks_tiled)
+            else:
+                tail = len(normal) // 200_000 - 2
+                assert st.chunks_tiled >= tail, (st.chunks, st.chunks_tiled, tail)
+    finally:
+        eng.close()

@@ -206,3 +206,25 @@ def test_quality_site_by_hand(oracle):
     p = chdtrc(1, float(2 * (lpt - lph)))
     assert abs(het[0] - p) < 1e-12 * p
     assert code[0] == (0 | (1 << 2) | 0x80) if p < 0.05 else code[0] == 0
+
+
+@pytest.mark.parametrize("method", ["quality", "local"])
+def test_oracle_range_equals_the_slice(sid, oracle, tmp_path, method):
+    """The CPU baseline's shard harness (ORACLE_RANGE=OFF:LEN, not a reference
+    option) reads only the line-aligned bytes [OFF, OFF+LEN) of the file, for
+    -m quality as for the other methods: its output equals the oracle over
+    that slice written as a file of its own (round 5's quality branch read to
+    EOF and took chrom/pos from byte 0)."""
+    import os
+    text = sid.synth_text(71, 6000, 30.0, sites_per_chrom=2500, mapq=True)
+    a = text.index(b"\n", len(text) // 3) + 1
+    b = text.index(b"\n", 2 * len(text) // 3) + 1
+    whole = tmp_path / "whole.plp"
+    whole.write_bytes(text)
+    part = tmp_path / "part.plp"
+    part.write_bytes(text[a:b])
+    ref = oracle.run_cli(["-m", method, str(part)])
+    got = oracle.run_cli(["-m", method, str(whole)], env=dict(os.environ, ORACLE_RANGE=f"{a}:{b - a}"))
+    assert ref.returncode == 0 and got.returncode == 0
+    assert got.stdout == ref.stdout and got.stderr == ref.stderr
+    assert got.stdout.count(b"\n") > 1000

@@ -6,7 +6,7 @@ per run, then the median wall per binary.
 
 usage: python3 tools/gpu/cli_ab.py OUT.jsonl build/sid build_dev/sid [...]
 env:   REPS (5), SITES (50000000), and per binary any KEY=VALUE given as
-       BIN:KEY=VALUE (e.g. build_dev/sid:SID_CLI_OVERLAP=0)
+       BIN:KEY=VALUE (e.g. build/sid:SID_UPLOAD_REGISTER=0)
 """
 import json
 import os
