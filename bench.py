@@ -31,6 +31,8 @@ Configs (--config):
       the profile histogram; N>1 all-gathers it over RCCL (device tensors,
       backend "nccl"), rank 0 runs the one Nelder-Mead estimate and broadcasts
       (pi, eps) over RCCL; then every rank formats its records
+  C3B -m bayes, seed 3, 50M sites per GPU (weak): the Lynch path's other
+      caller (call.cpp:145-211), as C3
   C4  -m local, seed 4, 3G sites in total = 24 chromosomes x 125M, quoted on
       8 GPUs: rank r takes the eighth [r*3G/8, (r+1)*3G/8) (375M sites, 30.4
       GB of text), so N = 8 runs the whole genome; the same step as C2 (host
@@ -73,6 +75,8 @@ CONFIGS = {
                desc="-m local, 50M-site 30x synthetic pileup per GPU"),
     "C3": dict(method="likelihood_ratio", R=True, seed=3, depth=30.0, per_gpu=50_000_000, total=None, spc=0,
                desc="-R -m likelihood_ratio, 50M-site 30x synthetic pileup per GPU"),
+    "C3B": dict(method="bayes", R=False, seed=3, depth=30.0, per_gpu=50_000_000, total=None, spc=0,
+                desc="-m bayes, 50M-site 30x synthetic pileup per GPU"),
     "C4": dict(method="local", R=False, seed=4, depth=30.0, per_gpu=None, total=3_000_000_000, spc=125_000_000,
                desc="-m local, 3G-site whole-genome 30x pileup (24 x 125M), site-range shards"),
     "C5": dict(method="local", R=False, seed=5, depth=200.0, per_gpu=None, total=500_000_000, spc=125_000_000,
@@ -86,8 +90,8 @@ def parse_args(argv=None):
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default=None, choices=sorted(CONFIGS))
-    p.add_argument("--method", default=None, choices=["local", "likelihood_ratio"],
-                   help="alias: local = C2, likelihood_ratio = C3")
+    p.add_argument("--method", default=None, choices=["local", "likelihood_ratio", "bayes"],
+                   help="alias: local = C2, likelihood_ratio = C3, bayes = C3B")
     p.add_argument("--sites", type=int, default=None, help="override: sites per GPU (C2/C3) or in total (C4/C5)")
     p.add_argument("--chunk-mib", type=int, default=0, help="engine chunk size (0 = the engine's default)")
     p.add_argument("--device-steps", type=int, default=0, help="device_path steps (0 = max(steps, 10))")
@@ -106,7 +110,7 @@ def parse_args(argv=None):
     p.add_argument("--no-node-cli", action="store_true", help="N > 1: skip the whole-node CLI leg")
     a = p.parse_args(argv)
     if a.config is None:
-        a.config = "C3" if a.method == "likelihood_ratio" else "C2"
+        a.config = {"likelihood_ratio": "C3", "bayes": "C3B"}.get(a.method, "C2")
     return a
 
 
@@ -169,10 +173,16 @@ def launch_ranks(a):
 def numa_bind(torch, gpu):
     """Run this rank on its GPU's NUMA node (the PCI device's local CPUs, within
     the CPUs this process may use), so pinned host buffers are allocated there
-    and the DMA does not cross sockets.  Returns the CPU list used, or None."""
+    and the DMA does not cross sockets.  Returns {pci, gpu_numa_node, cpus
+    (bound to; 0: not bound -- the GPU's local CPUs are none or all of this
+    job's)}, or None when the GPU's PCI function cannot be read."""
     try:
         pr = torch.cuda.get_device_properties(gpu)
         bdf = "%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id, pr.pci_device_id)
+        try:
+            node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+        except (OSError, ValueError):
+            node = None
         txt = open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read().strip()
         cpus = set()
         for part in txt.split(","):
@@ -180,9 +190,29 @@ def numa_bind(torch, gpu):
             cpus.update(range(int(lo), int(hi or lo) + 1))
         mine = cpus & os.sched_getaffinity(0)
         if not mine or mine == os.sched_getaffinity(0):
-            return None
+            return {"pci": bdf, "gpu_numa_node": node, "cpus": 0}
         os.sched_setaffinity(0, mine)
-        return {"pci": bdf, "cpus": len(mine)}
+        return {"pci": bdf, "gpu_numa_node": node, "cpus": len(mine)}
+    except Exception:
+        return None
+
+
+def numa_nodes_of(t):
+    """The NUMA nodes holding a pinned host tensor's pages (its first, middle
+    and last byte): get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR), x86-64 syscall
+    239 -- the node the kernel actually placed each page on."""
+    import ctypes
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        libc.syscall.restype = ctypes.c_long
+        out = []
+        n = t.numel()
+        for off in sorted({0, n // 2, max(0, n - 1)}):
+            node = ctypes.c_int(-1)
+            rc = libc.syscall(ctypes.c_long(239), ctypes.byref(node), ctypes.c_void_p(0), ctypes.c_ulong(0),
+                              ctypes.c_void_p(t.data_ptr() + off), ctypes.c_ulong(3))
+            out.append(node.value if rc == 0 else None)
+        return out
     except Exception:
         return None
 
@@ -284,6 +314,7 @@ class Rank:
         self.numa = numa_bind(torch, self.gpu)
         self.dist = None
         self.backend = None
+        self.last_table = None   # the Lynch paths' global unique-profile table (keys, counts) of the last step
         self.n_gpus, self.oversub = 1, False
         if self.world > 1:
             import torch.distributed as dist
@@ -340,6 +371,7 @@ class Rank:
         keys, cnts = eng.profile_table()
         keys, cnts = sdist.allgather_profile_table(keys, cnts, device=self.dev)
         eng.profile_load(keys, cnts)
+        self.last_table = (keys, cnts)
         torch = self.torch
         if self.rank == 0:
             est = eng.estimate()
@@ -354,14 +386,33 @@ class Rank:
             est = eng.estimate(given=g)
         return est
 
-    def run_step(self, eng, lynch):
+    def run_step(self, eng, lynch, capture=False):
+        """One step.  capture (untimed, one process): also keep the Lynch
+        paths' unique-profile table for the spot check (at N > 1 the exchange
+        keeps the gathered one)."""
         st = eng.ingest()
         if lynch and self.dist is not None:
             est = self.lynch_step_exchange(eng)
         else:
+            if lynch and capture:
+                self.last_table = eng.profile_table()
             est = eng.estimate()
         _, st2 = eng.emit()
         return st, st2, est
+
+    def gather(self, obj):
+        """Every rank's obj, in rank order (one process: [obj])."""
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def placement(self, host):
+        """This rank's host placement: its GPU, the GPU's PCI function and
+        NUMA node, the CPUs it was bound to, and the NUMA nodes of its pinned
+        text's pages (first, middle, last byte)."""
+        return dict({"rank": self.rank, "gpu": self.gpu}, **(self.numa or {}), text_numa_nodes=numa_nodes_of(host))
 
 
 def main():
@@ -400,10 +451,14 @@ def bench_weak(R, a, cfg):
     host = text[:ln].cpu().pin_memory()     # the rank's input, in host memory (its GPU's NUMA node)
     elapsed, st, st2, est, eng = pcie_leg(R, a, cfg, host, ln, n, lynch)
     sites_all = R.sum_over_ranks(st.sites)
-    # the first chunk's records from the host arena, for the cpu_baseline
-    # leg's spot check against the oracle (-m local: the records of a prefix
-    # of the text do not depend on the rest)
-    spot = eng.records_bytes(1) if not lynch else None
+    placement = R.gather(R.placement(host))
+    if lynch and R.dist is None:   # (one untimed step more: the profile table for the spot check)
+        R.run_step(eng, lynch, capture=True)
+    # the first chunk's records from the host arena, for every rank's spot
+    # check against the oracle (-m local: the records of a prefix of the text
+    # do not depend on the rest; the Lynch paths: given the global profile
+    # table, neither do they)
+    spot = eng.records_bytes(1)
     if a.dump_records:
         os.makedirs(a.dump_records, exist_ok=True)
         with open(os.path.join(a.dump_records, f"rank{R.rank}.csv"), "wb") as f:
@@ -419,6 +474,7 @@ def bench_weak(R, a, cfg):
     pcie = pcie_stats(a, ln, st, st2, elapsed, lynch)
     eng.close()
     del host
+    spot = spot_check_ranks(R, a, cfg, text, ln, spot, R.last_table if lynch else None)
 
     dp = device_path(R, a, cfg, text, ln, lynch)
     node_cli, node_cpu = None, None
@@ -451,8 +507,9 @@ def bench_weak(R, a, cfg):
                        if lynch and R.world > 1 else ""),
                    "ranks": R.world, "oversubscribed": R.oversub, "dist_backend": R.backend,
                    "rccl_world": R.world if R.dist is not None and R.backend == "nccl" else None,
-                   "numa": R.numa},
+                   "numa": placement},
         "pcie": pcie,
+        "spot_check": spot,
         "roofline": dp.pop("roofline"),
         "device_path": dp,
     }
@@ -467,7 +524,7 @@ def bench_weak(R, a, cfg):
         out["kernel_local"] = bench_kernel_local(torch, R.dev, cfg, n)
         out["cli"] = bench_cli(cfg, text, ln, n)
         if not a.no_cpu:
-            out["cpu_baseline"] = bench_cpu(cfg, text, ln, n, R.cpus0, spot=spot)
+            out["cpu_baseline"] = bench_cpu(cfg, text, ln, n, R.cpus0)
     return out, []
 
 
@@ -639,10 +696,12 @@ def bench_strong(R, a, cfg):
     torch.cuda.synchronize(R.dev)
     elapsed, st, st2, est, eng = pcie_leg(R, a, cfg, host, ln, n, lynch)
     sites_all = R.sum_over_ranks(st.sites)
-    spot = eng.records_bytes(1) if not lynch else None
+    placement = R.gather(R.placement(host))
+    spot = eng.records_bytes(1)
     pcie = pcie_stats(a, ln, st, st2, elapsed, lynch)
     eng.close()
     del host
+    spot = spot_check_ranks(R, a, cfg, text, ln, spot, None)
     if not a.chunk_mib:
         a.chunk_mib = STRONG_RESIDENT_CHUNK_MIB
     dp = device_path(R, a, cfg, text, ln, lynch)
@@ -667,8 +726,9 @@ def bench_strong(R, a, cfg):
                    "sites_per_gpu": per, "sites_all_ranks": sites_all, "first_site_rank0": 0,
                    "sites_per_chrom": cfg["spc"], "text_bytes_rank0": ln, "csv_bytes_rank0": st2.bytes_out,
                    "parallelism": f"site-range shards x{R.world}", "ranks": R.world,
-                   "oversubscribed": R.oversub, "numa": R.numa},
+                   "oversubscribed": R.oversub, "numa": placement},
         "pcie": pcie,
+        "spot_check": spot,
         "roofline": dp.pop("roofline"),
         "device_path": dp,
         "generator": {"ms": gen_ms, "inside_step": False,
@@ -676,7 +736,7 @@ def bench_strong(R, a, cfg):
                               "the timed region"},
     }
     if R.world == 1 and not a.no_extras and not a.no_cpu:
-        out["cpu_baseline"] = bench_cpu(cfg, text, ln, n, R.cpus0, spot=spot,
+        out["cpu_baseline"] = bench_cpu(cfg, text, ln, n, R.cpus0,
                                         sample_sites=50_000_000 if cfg["depth"] < 100 else 10_000_000)
     return out, []
 
@@ -988,6 +1048,18 @@ def bench_cli_node(R, cfg, holder, ln, n):
                            "sample": f"the node file ({sites:,} sites, every rank's shard, {total / 1e9:.2f} GB), "
                                      f"{P} line-aligned byte ranges, one oracle/_build/sid_oracle process each, "
                                      "CSV to /dev/null, wall"}
+                elif dt is not None:
+                    # the Lynch paths: one estimate over every site, so one
+                    # oracle process, on a bounded sample of the node file
+                    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                    import oracle
+                    m = min(sites, 4_000_000)
+                    dtc, rc = one_process([oracle.CLI] + method_flags(cfg), path, line_end(path, m))
+                    cpu = {"value": m / dtc if rc == 0 else None, "unit": "sites/s", "cores": 1, "kind": "port",
+                           "seconds": dtc, "cpu_model": cpu_model(), "cpu_share": cpu_share(R.cpus0)[1],
+                           "sample": f"the first {m:,} sites of the node file (rank 0's shard), one "
+                                     "oracle/_build/sid_oracle process (the Lynch estimate and BH are global: "
+                                     "call.cpp:62-143), CSV to /dev/null, wall"}
         finally:
             store.set("sid_node_cli_done", "1")
             try:
@@ -998,6 +1070,68 @@ def bench_cli_node(R, cfg, holder, ln, n):
         store.wait(["sid_node_cli_done"], timedelta(minutes=15))
     dist.barrier()
     return res, cpu
+
+
+def spot_check_ranks(R, a, cfg, text, ln, spot, table):
+    """Every rank checks its value leg's first chunk of records (from the
+    engine's pinned host arena, after the timed steps) byte for byte against
+    the oracle CLI over the same lines of its own text; for the Lynch paths
+    the oracle is given the global unique-profile table the rank used
+    (ORACLE_PROFILE_TABLE: the estimate and BH run over every rank's
+    profiles, call.cpp:62-143).  Gathered in rank order; a rank whose records
+    differ fails the bench on every rank (after the gather, so none hangs)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    res = {"rank": R.rank, "records": spot.count(b"\n"), "bytes": len(spot), "equal": None}
+    try:
+        if not os.path.exists(oracle.CLI):
+            oracle.build()
+        if spot:
+            # the text through the line of the chunk's last record (its chrom
+            # and position are unique in the rank's text; sites after it in
+            # the chunk, dropped by the Lynch paths' coverage filter, print
+            # nothing)
+            last = spot[:-1].rsplit(b"\n", 1)[-1]
+            chrom, pos = last.split(b",", 2)[:2]
+            key = chrom + b"\t" + pos + b"\t"
+            want = ((a.pcie_chunk_mib or 128) + 8) << 20
+            prefix = text[:min(ln, want)].cpu().numpy().tobytes()
+            at = 0 if prefix.startswith(key) else prefix.find(b"\n" + key) + 1
+            if at == 0 and not prefix.startswith(key):
+                res["equal"] = False
+                res["why"] = "the last record's line is not in the chunk's text"
+            else:
+                cut = prefix.index(b"\n", at) + 1
+                with tempfile.TemporaryDirectory() as td:
+                    path = os.path.join(td, "spot.plp")
+                    with open(path, "wb") as f:
+                        f.write(prefix[:cut])
+                    env = dict(os.environ)
+                    if table is not None:
+                        import numpy as np
+                        tp = os.path.join(td, "table.bin")
+                        np.stack([np.asarray(table[0], np.uint64), np.asarray(table[1], np.uint64)], 1).tofile(tp)
+                        env["ORACLE_PROFILE_TABLE"] = tp
+                        res["profile_table_rows"] = int(len(table[0]))
+                    r = subprocess.run([oracle.CLI] + method_flags(cfg) + [path], stdout=subprocess.PIPE,
+                                       stderr=subprocess.PIPE, env=env)
+                res["lines"] = prefix[:cut].count(b"\n")
+                res["equal"] = r.returncode == 0 and r.stdout == b"chrom,pos,label,gt,hom_conf,het_conf,conf_type\n" + spot
+                if r.returncode != 0:
+                    res["why"] = f"oracle rc {r.returncode}: {r.stderr.decode()[-200:]}"
+        else:
+            res["equal"] = ln == 0
+    except Exception as e:   # (reported, and fails the bench below)
+        res["equal"] = False
+        res["why"] = repr(e)[:300]
+    ranks = R.gather(res)
+    out = {"ranks_equal": all(x["equal"] for x in ranks), "ranks": ranks,
+           "what": "each rank's timed PCIe leg, its first chunk of records (engine host arena) vs the oracle CLI "
+                   "over the same lines of the rank's text" + (", given the global unique-profile table"
+                                                                  if table is not None else "")}
+    if not out["ranks_equal"]:
+        raise SystemExit(f"bench.py: a rank's records differ from the oracle's (spot check): {ranks}")
+    return out
 
 
 def write_text_file(text, ln, path):
@@ -1051,16 +1185,19 @@ def line_cuts(path, ln, P):
     return [(cuts[k], cuts[k + 1] - cuts[k]) for k in range(P) if cuts[k + 1] > cuts[k]]
 
 
-def oracle_shards(path, ln, P, flags, cpus):
-    """The oracle CLI in P processes over line-aligned byte ranges of one file
-    (ORACLE_RANGE: the harness's byte range), CSV to /dev/null: wall seconds,
-    or None when a process failed.  -m local only: its sites are independent
-    (the reference's whole-node shape, one sid per chromosome,
-    scripts/sid-pipeline/parallel-run-sid.sh:2, is the same split)."""
+def oracle_shards(path, ln, P, flags, cpus, cmd=None):
+    """The oracle CLI (or cmd, a command taking FILE last) in P processes over
+    line-aligned byte ranges of one file (ORACLE_RANGE: the harness's byte
+    range), CSV to /dev/null: wall seconds, or None when a process failed.
+    -m local only: its sites are independent (the reference's whole-node
+    shape, one sid per chromosome, scripts/sid-pipeline/parallel-run-sid.sh:2,
+    is the same split)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    if not os.path.exists(oracle.CLI):
-        oracle.build()
+    if cmd is None:
+        if not os.path.exists(oracle.CLI):
+            oracle.build()
+        cmd = [oracle.CLI] + flags
     ranges = line_cuts(path, ln, P)
     # the processes run on every CPU of the job (this thread's mask, which
     # they inherit, widened from the rank's NUMA binding for the forks)
@@ -1069,7 +1206,7 @@ def oracle_shards(path, ln, P, flags, cpus):
     try:
         with open(os.devnull, "wb") as dn:
             t0 = time.perf_counter()
-            procs = [subprocess.Popen([oracle.CLI] + flags + [path], stdout=dn, stderr=subprocess.DEVNULL,
+            procs = [subprocess.Popen(cmd + [path], stdout=dn, stderr=subprocess.DEVNULL,
                                       env=dict(os.environ, ORACLE_RANGE=f"{o}:{m}")) for o, m in ranges]
             rcs = [p.wait() for p in procs]
             dt = time.perf_counter() - t0
@@ -1078,18 +1215,48 @@ def oracle_shards(path, ln, P, flags, cpus):
     return None if any(rcs) else dt
 
 
-def method_flags(cfg):
-    return [] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) + ["-m", cfg["method"]]
+def one_process(cmd, path, c1):
+    """cmd over the first c1 bytes of path in one process, CSV to /dev/null:
+    (wall seconds, exit code)."""
+    with open(os.devnull, "wb") as dn:
+        t0 = time.perf_counter()
+        r = subprocess.run(cmd + [path], stdout=dn, stderr=subprocess.DEVNULL, env=dict(os.environ, ORACLE_RANGE=f"0:{c1}"))
+        return time.perf_counter() - t0, r.returncode
 
 
-def bench_cpu(cfg, text, ln, n, cpus, spot=None, sample_sites=None):
-    """The oracle CLI (reference sid.cpp/call.cpp/lynch/stats restated in C,
-    single-threaded) on the same text, bounded to sample_sites (default: all
-    n): one line-aligned shard process per CPU this job may use (-m local:
-    sites are independent), and one process on the first 4M sites.  spot:
-    the timed PCIe leg's first chunk of records (from the engine's host
-    arena), checked byte for byte against the oracle's CSV of the same lines
-    (untimed)."""
+def line_end(path, m):
+    """The byte offset after the file's first m lines."""
+    base = 0
+    with open(path, "rb") as f:
+        while m:
+            blk = f.read(1 << 24)
+            if not blk:
+                return base
+            k = blk.count(b"\n")
+            if k < m:
+                m -= k
+                base += len(blk)
+                continue
+            idx = -1
+            for _ in range(m):
+                idx = blk.find(b"\n", idx + 1)
+            return base + idx + 1
+    return base
+
+
+def bench_cpu(cfg, text, ln, n, cpus, sample_sites=None):
+    """The CPU path on the same text, bounded to sample_sites (default: all n),
+    on this job's CPUs:
+      value              the oracle CLI (reference sid.cpp/call.cpp/lynch/stats
+                         restated in C, single-threaded): one line-aligned
+                         shard process per CPU (-m local: sites are
+                         independent), and one process on the first 4M sites;
+                         the Lynch paths (a global estimate): one process
+      reference_sources  -m local: oracle/_ref/ref_pileup local, the
+                         reference's own pileup.cpp, countUniqueProfiles,
+                         profile map and call.hpp iostream output (each unique
+                         profile's GSL arithmetic from the oracle), timed
+                         the same two ways (timing only: it pins nothing)"""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     if not os.path.exists(oracle.CLI):
@@ -1118,45 +1285,47 @@ def bench_cpu(cfg, text, ln, n, cpus, spot=None, sample_sites=None):
                 cut += len(seg)
                 need -= k
         res = {"unit": "sites/s", "kind": "port", "cpu_model": cpu_model(), "cpu_share": share}
+        shard_desc = (f"{m_all:,} sites of the {cfg['desc']} text ({cut / 1e9:.2f} GB), {P} line-aligned byte ranges "
+                      f"of one file (one per CPU this job may use), one process each, CSV to /dev/null, wall")
         if cfg["method"] == "local":
             dt = oracle_shards(path, cut, P, flags, cpus)
             res.update({"value": m_all / dt if dt else None, "cores": P, "seconds": dt,
-                        "sample": f"{m_all:,} sites of the {cfg['desc']} text ({cut / 1e9:.2f} GB), {P} line-aligned "
-                                  f"byte ranges of one file (one per CPU this job may use), one "
-                                  f"oracle/_build/sid_oracle process each, CSV to /dev/null, wall"})
+                        "sample": shard_desc.replace("one process each", "one oracle/_build/sid_oracle process each")})
         # one core on the first 4M sites
         m = min(m_all, 4_000_000)
-        with open(path, "rb") as f:
-            head = f.read(min(cut, 1 << 31))
-        c1 = 0
-        for _ in range(m):
-            c1 = head.find(b"\n", c1) + 1
-        with open(os.devnull, "wb") as dn:
-            t0 = time.perf_counter()
-            r = subprocess.run([oracle.CLI] + flags + [path], stdout=dn, stderr=subprocess.DEVNULL,
-                               env=dict(os.environ, ORACLE_RANGE=f"0:{c1}"))
-            dt = time.perf_counter() - t0
-        single = {"value": m / dt if r.returncode == 0 else None, "cores": 1, "seconds": dt,
-                  "sample": f"the first {m:,} sites of the same text, one process"}
+        c1 = line_end(path, m)
+        dt, rc = one_process([oracle.CLI] + flags, path, c1)
+        single = {"value": m / dt if rc == 0 else None, "cores": 1, "seconds": dt,
+                  "sample": f"the first {m:,} sites of the same text, one process" + (
+                      " (the Lynch estimate is global: one process)" if cfg["method"] != "local" else "")}
         if "value" not in res:
             res.update(single)
             res["sample"] = single["sample"]
         else:
             res["single_core"] = single
-        if spot is not None:   # the checker: the value's own records against the oracle's
-            k = spot.count(b"\n")
-            c2 = 0
-            for _ in range(k):
-                c2 = head.find(b"\n", c2) + 1
-            r = subprocess.run([oracle.CLI] + flags + [path], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
-                               env=dict(os.environ, ORACLE_RANGE=f"0:{c2}"))
-            want = r.stdout
-            got = b"chrom,pos,label,gt,hom_conf,het_conf,conf_type\n" + spot
-            res["spot_check"] = {"sites": k, "bytes": len(spot), "equal": r.returncode == 0 and got == want,
-                                 "what": "the timed PCIe leg's first chunk of records (engine host arena) vs "
-                                         "the oracle CLI over the same lines"}
-            if not res["spot_check"]["equal"]:
-                raise SystemExit("bench.py: the value's records differ from the oracle's (spot check)")
+        if cfg["method"] == "local" and not cfg["R"] and oracle.ref_pileup_available():
+            cmd = [oracle.REF_PILEUP, "local"]
+            dts, rcs = one_process(cmd, path, c1)
+            dtp = oracle_shards(path, cut, P, flags, cpus, cmd=cmd)
+            ref_p = m_all / dtp if dtp else None
+            ref_1 = m / dts if rcs == 0 else None
+            res["reference_sources"] = {
+                "value": ref_p, "cores": P, "seconds": dtp, "sample": shard_desc,
+                "single_core": {"value": ref_1, "cores": 1, "seconds": dts,
+                                "sample": f"the first {m:,} sites, one process"},
+                # the same box, the same sample: how much faster the port is
+                "port_over_reference": {"cores": res["value"] / ref_p if ref_p and res.get("value") else None,
+                                        "single_core": single["value"] / ref_1 if ref_1 and single["value"]
+                                        else None},
+                "binary": "oracle/_ref/ref_pileup local (built by oracle/Makefile from the reference's pileup.cpp "
+                          "and call.hpp, unmodified, -O2 as its autotools default; -fopenmp dropped: readFile is "
+                          "serial)",
+                "what": "the reference's own -m local per-site work: ifstream + getline + parsePileupLine into "
+                        "std::vector<PileupLine> (call.cpp:11-20), countUniqueProfiles (pileup.cpp:169-196), "
+                        "std::map profile -> class (call.cpp:216-221, 274-285), records through call.hpp:29-38's "
+                        "operator<< on synced iostreams (sid.cpp:102-105); each unique profile's arithmetic "
+                        "(call.cpp:238-273, GSL) from the oracle, once per profile; timing only, output "
+                        "byte-equal to the oracle's (tests/test_oracle_kat.py)"}
     return res
 
 

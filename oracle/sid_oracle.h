@@ -129,6 +129,11 @@ int oracle_estimate(const oracle_profile* p, size_t u, const double dist[4],
 /* stats.cpp:58-80 */
 void oracle_bh(const double* p, size_t m, double* adj);
 
+/* Harness only: the whole input's unique-profile table (u pairs of u64 key
+ * A<<48|C<<32|G<<16|T and count), used by oracle_call_method in place of the
+ * table of its own sites until called again with NULL. */
+void oracle_given_profile_table(const uint64_t* key_count_pairs, size_t u);
+
 /* ---- whole-method drivers over per-site counts --------------------------
  * Outputs per site: code (bit6 = site dropped, i.e. its profile was filtered
  * out and the reference emits no record), hom_conf, het_conf.  For LR/bayes

@@ -140,6 +140,29 @@ int main(int argc, char** argv)
             range_off = off;
         }
     }
+    /* harness, not a reference option: ORACLE_PROFILE_TABLE=FILE (u64 key,
+       u64 count pairs) is the whole input's unique-profile table, for a
+       process that reads a part of it (bench.py's per-rank spot check of the
+       Lynch paths, whose estimate and BH are global: call.cpp:62-143) */
+    if (getenv("ORACLE_PROFILE_TABLE")) {
+        FILE* tf = fopen(getenv("ORACLE_PROFILE_TABLE"), "rb");
+        if (!tf) abort();
+        uint64_t* kc = NULL;
+        size_t u = 0, ucap = 0;
+        uint64_t pair[2];
+        while (fread(pair, sizeof pair, 1, tf) == 1) {
+            if (u == ucap) {
+                ucap = ucap ? 2 * ucap : 4096;
+                kc = (uint64_t*)realloc(kc, ucap * sizeof pair);
+            }
+            kc[2 * u] = pair[0];
+            kc[2 * u + 1] = pair[1];
+            ++u;
+        }
+        fclose(tf);
+        oracle_given_profile_table(kc, u);
+        free(kc);
+    }
     int method = -1;
     if (strcmp(o.method, "local") == 0) method = ORACLE_LOCAL;
     else if (strcmp(o.method, "bayes") == 0) method = ORACLE_BAYES;

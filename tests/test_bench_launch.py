@@ -57,6 +57,21 @@ def test_shared_gpu_rehearsal_reports_every_rank():
     assert d["n_gpus"] == 1
     assert d["config"]["sites_total"] == 2 * 200000
     assert d["value"] > 0
+    assert_self_checked(d, 2)
+
+
+def assert_self_checked(d, ranks):
+    """What every line carries at any N: each rank's spot
+    check of its first chunk of records against the oracle, and each rank's
+    placement with the NUMA node of its pinned text's pages."""
+    sc = d["spot_check"]
+    assert sc["ranks_equal"] is True and [r["rank"] for r in sc["ranks"]] == list(range(ranks))
+    assert all(r["equal"] is True and r["records"] > 0 for r in sc["ranks"])
+    numa = d["config"]["numa"]
+    assert [p["rank"] for p in numa] == list(range(ranks))
+    for p in numa:
+        assert p["text_numa_nodes"] and all(isinstance(x, int) and x >= 0 for x in p["text_numa_nodes"]), p
+        assert "gpu_numa_node" in p and p["pci"]
 
 
 @pytest.mark.gpu
@@ -100,18 +115,24 @@ def test_two_rank_lynch_exchange_equals_one_process(sid, oracle, gpu, tmp_path):
         assert (j["pi"], j["eps"], j["iterations"]) == (est.heterozygosity, est.error_rate, est.iterations)
         assert j["n_unique"] == u
     assert d["estimate"]["pi"] == est.heterozygosity and d["estimate"]["eps"] == est.error_rate
+    # each rank's first chunk checked by the bench itself, the oracle given the
+    # gathered profile table (u rows before the coverage filter)
+    assert_self_checked(d, 2)
+    assert all(r["profile_table_rows"] >= u for r in d["spot_check"]["ranks"])
 
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
-def test_shared_gpu_rehearsal_runs_the_node_cli():
+@pytest.mark.parametrize("config", ["C2", "C3"])
+def test_shared_gpu_rehearsal_runs_the_node_cli(config):
     """N > 1 (bench.py bench_cli_node): after the timed legs the ranks write
     their texts into one file and free their GPUs; rank 0 runs build/sid
-    --devices N over it (the whole node's drop-in) and the line carries it."""
+    --devices N over it (the whole node's drop-in) and the line carries it,
+    with the node's CPU baseline, every rank's spot check and placement."""
     if visible_gpus() != 1:
         pytest.skip("the rehearsal case: one visible GPU")
-    args = ["--gpus", "2", "--allow-shared-gpu", "--sites", "300000", "--steps", "1", "--warmup", "0",
-            "--device-steps", "1"]
+    args = ["--gpus", "2", "--allow-shared-gpu", "--config", config, "--sites", "300000", "--steps", "1",
+            "--warmup", "0", "--device-steps", "1"]
     r = run_bench(args, 500)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     d = json.loads([ln for ln in r.stdout.decode().splitlines() if ln.startswith('{"metric"')][0])
@@ -129,12 +150,17 @@ def test_shared_gpu_rehearsal_runs_the_node_cli():
     # the same run through the runtime's pageable path (SID_UPLOAD_REGISTER=0)
     assert cli["upload_pageable"]["cli_stats"]["chunks_registered"] == 0
     assert cli["cli_stats"]["chunks_registered"] > 0
-    # the whole node's CPU path beside it: the oracle over the same file, one
-    # shard process per CPU the job may use
+    assert_self_checked(d, 2)
+    # the whole node's CPU path beside it: -m local, the oracle over the same
+    # file, one shard process per CPU the job may use; the Lynch path (a
+    # global estimate), one oracle process on a stated sample
     import bench
     cpu = d["cpu_baseline"]
-    assert cpu["cores"] == bench.cpu_share(os.sched_getaffinity(0))[0]
-    assert cpu["value"] > 0 and cpu["kind"] == "port"
+    assert cpu["value"] > 0 and cpu["kind"] == "port" and cpu["sample"]
+    if config == "C2":
+        assert cpu["cores"] == bench.cpu_share(os.sched_getaffinity(0))[0]
+    else:
+        assert cpu["cores"] == 1 and "global" in cpu["sample"]
 
 
 @pytest.mark.gpu

@@ -108,21 +108,38 @@ def test_c2_pcie_path_equals_oracle(sid, c2):
     assert_same(sid.HEADER + got, ref, "C2 PCIe path (pinned host text, host arena)")
 
 
+# The C3 text (seed 3, 50M sites) through the Lynch path's three callers:
+# bench.py C3 (-R -m likelihood_ratio, call.cpp:62-143), C3B (-m bayes,
+# call.cpp:145-211) and -R -m local (call.cpp:213-289 with the estimate,
+# :223-234); the oracle runs each as one process (a global estimate), the
+# three at once.
+C3_METHODS = {"lr_R": (dict(method="likelihood_ratio", estimate_prior=True), ["-R", "-m", "likelihood_ratio"]),
+              "bayes": (dict(method="bayes"), ["-m", "bayes"]),
+              "local_R": (dict(method="local", estimate_prior=True), ["-R", "-m", "local"])}
+
+
 @pytest.fixture(scope="module")
 def c3(sid, gpu, oracle, tmp_path_factory):
     text, ln = gpu.synth_text_hbm(3, 30.0, 0, N)
     path = str(tmp_path_factory.mktemp("c3") / "c3.plp")
     write_text(text, ln, path)
-    r = subprocess.run([oracle.CLI, "-R", "-m", "likelihood_ratio", path], capture_output=True, timeout=1200)
-    assert r.returncode == 0, r.stderr
+
+    def one(flags):
+        r = subprocess.run([oracle.CLI] + flags + [path], capture_output=True, timeout=1500)
+        assert r.returncode == 0, r.stderr
+        return r
+    with cf.ThreadPoolExecutor(len(C3_METHODS)) as ex:
+        refs = dict(zip(C3_METHODS, ex.map(one, [f for _, f in C3_METHODS.values()])))
     os.unlink(path)
-    return text, ln, r
+    return text, ln, refs
 
 
-@pytest.mark.timeout(1200)
-def test_c3_device_path_equals_oracle(sid, c3, capfd):
-    text, ln, ref = c3
-    eng = sid.Engine(method="likelihood_ratio", estimate_prior=True, devices=1, lanes=1, verbose=True)
+@pytest.mark.timeout(1800)
+@pytest.mark.parametrize("kind", list(C3_METHODS))
+def test_c3_device_path_equals_oracle(sid, c3, capfd, kind):
+    text, ln, refs = c3
+    ref = refs[kind]
+    eng = sid.Engine(devices=1, lanes=1, verbose=True, **C3_METHODS[kind][0])
     eng.source_device_text(text.data_ptr(), ln, keep=text)
     capfd.readouterr()
     out, st = eng.run()
@@ -130,22 +147,28 @@ def test_c3_device_path_equals_oracle(sid, c3, capfd):
     eng.close()
     assert st.sites == N
     assert err == ref.stderr, (err, ref.stderr)   # unique profiles, pi-hat, eps-hat, iterations
-    assert_same(out, ref.stdout, "C3 device path (text in HBM, kept parse for pass 2)")
+    assert_same(out, ref.stdout, f"C3 text {kind}: device path (text in HBM, kept parse for pass 2)")
 
 
 @pytest.mark.timeout(900)
-def test_c3_pcie_path_equals_oracle(sid, c3):
-    text, ln, ref = c3
+@pytest.mark.parametrize("kind", list(C3_METHODS))
+def test_c3_pcie_path_equals_oracle(sid, c3, kind):
+    """bench.py pcie_engine's setup: 128 MiB host chunks, records into the
+    pinned host arena (pass 2)."""
+    import bench
+    text, ln, refs = c3
+    cfg = dict(bench.CONFIGS["C3"], method=C3_METHODS[kind][0]["method"],
+               R=C3_METHODS[kind][0].get("estimate_prior", False))
     host = text[:ln].cpu().pin_memory()
-    eng = sid.Engine(method="likelihood_ratio", estimate_prior=True, devices=1, device_sink=2,
-                     host_hold_bytes=int(ln * 0.6))
+    eng = bench.pcie_engine(cfg, 0, N, ln)
     eng.source_host_ptr(host.data_ptr(), ln, keep=host)
     st = eng.ingest()
     eng.estimate()
-    eng.emit()
+    _, st2 = eng.emit()
     got = eng.records_bytes(st.chunks)
     eng.close()
-    assert_same(sid.HEADER + got, ref.stdout, "C3 PCIe path (pinned host text, host arena in pass 2)")
+    assert st.chunks > 20 and st2.bytes_out == len(got)
+    assert_same(sid.HEADER + got, refs[kind].stdout, f"C3 text {kind}: PCIe path (pinned host text, host arena)")
 
 
 # ---- C4 / C5 (configs[3], configs[4]): the strong-scaling device path ----

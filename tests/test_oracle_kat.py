@@ -4,6 +4,7 @@ oracle/_ref is built, the reference's pileup.cpp itself.  CPU only."""
 import json
 import math
 import os
+import subprocess
 
 import numpy as np
 import pytest
@@ -228,3 +229,63 @@ def test_oracle_range_equals_the_slice(sid, oracle, tmp_path, method):
     assert ref.returncode == 0 and got.returncode == 0
     assert got.stdout == ref.stdout and got.stderr == ref.stderr
     assert got.stdout.count(b"\n") > 1000
+
+
+@pytest.mark.parametrize("src", ["golden", "synthetic", "edge"])
+def test_reference_sources_local_equals_oracle(sid, oracle, tmp_path, src):
+    """oracle/_ref/ref_pileup local -- the CPU baseline's "reference sources"
+    leg: the reference's pileup.cpp parse, countUniqueProfiles, a profile map
+    and call.hpp's operator<< over iostreams, each unique profile's arithmetic
+    from the oracle (GSL is absent) -- prints the oracle CLI's -m local CSV
+    byte for byte, whole file and over an ORACLE_RANGE byte range."""
+    import os
+    if not oracle.ref_pileup_available():
+        pytest.skip("oracle/_ref not built (no /root/reference)")
+    golden = os.path.join(os.path.dirname(__file__), "golden")
+    if src == "synthetic":
+        p = tmp_path / "s.plp"
+        p.write_bytes(sid.synth_text(73, 30_000, 30.0, sites_per_chrom=12_000))
+    else:
+        p = os.path.join(golden, "c1_10k.plp" if src == "golden" else "edge.plp")
+    text = open(p, "rb").read()
+    a = text.index(b"\n", len(text) // 4) + 1
+    b = text.index(b"\n", len(text) // 2) + 1
+    for env in ({}, {"ORACLE_RANGE": f"{a}:{b - a}"}):
+        e = dict(os.environ, **env)
+        want = oracle.run_cli([str(p)], env=e)
+        got = subprocess.run([oracle.REF_PILEUP, "local", str(p)], capture_output=True, env=e)
+        assert want.returncode == 0 and got.returncode == 0
+        assert got.stdout == want.stdout, (src, env)
+
+
+@pytest.mark.parametrize("flags", [["-R", "-m", "likelihood_ratio"], ["-m", "bayes"], ["-R", "-m", "local"]],
+                         ids=["lr_R", "bayes", "local_R"])
+def test_oracle_given_profile_table(sid, oracle, tmp_path, flags):
+    """The harness's ORACLE_PROFILE_TABLE (not a reference option): a process
+    that reads part of an input (ORACLE_RANGE) but is given the whole input's
+    unique-profile table prints exactly the whole run's records for its part
+    -- the Lynch estimate and BH are global (call.cpp:62-143) -- which is how
+    bench.py checks each rank's records at N ranks."""
+    import os
+    n = 40_000
+    text = sid.synth_text(74, n, 30.0, sites_per_chrom=10 ** 7)
+    counts = sid.synth_counts_host(74, n, 30.0)
+    keys, cnt = np.unique(sid.profile_key(counts), return_counts=True)
+    table = tmp_path / "table.bin"
+    np.stack([keys, cnt.astype(np.uint64)], 1).astype(np.uint64).tofile(table)
+    p = tmp_path / "all.plp"
+    p.write_bytes(text)
+    whole = oracle.run_cli(flags + [str(p)])
+    assert whole.returncode == 0
+    a = text.index(b"\n", len(text) // 2) + 1
+    pos0 = int(text[a:].split(b"\t", 2)[1])
+    env = dict(os.environ, ORACLE_RANGE=f"{a}:{len(text) - a}", ORACLE_PROFILE_TABLE=str(table))
+    part = oracle.run_cli(flags + [str(p)], env=env)
+    assert part.returncode == 0
+    rows = whole.stdout.split(b"\n")
+    tail = [r for r in rows[1:] if r and int(r.split(b",", 2)[1]) >= pos0]
+    assert part.stdout == b"\n".join([rows[0]] + tail) + b"\n"
+    assert part.stderr == whole.stderr   # (the same table: the same profile count and estimate)
+    # without the table the part's own estimate differs
+    own = oracle.run_cli(flags + [str(p)], env=dict(os.environ, ORACLE_RANGE=f"{a}:{len(text) - a}"))
+    assert own.stderr != whole.stderr
