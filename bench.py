@@ -1244,6 +1244,10 @@ def line_end(path, m):
     return base
 
 
+def method_flags(cfg):
+    return [] if cfg["method"] == "local" else (["-R"] if cfg["R"] else []) + ["-m", cfg["method"]]
+
+
 def bench_cpu(cfg, text, ln, n, cpus, sample_sites=None):
     """The CPU path on the same text, bounded to sample_sites (default: all n),
     on this job's CPUs:
