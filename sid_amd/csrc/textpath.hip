@@ -782,6 +782,16 @@ __device__ __forceinline__ uint32_t rb_entry(uint32_t c)
     }
 }
 
+// bits 0-3 of m as the bytes 0x00 / 0xFF of a word: each bit moved to its
+// byte's bit 0 by a 24-bit multiply, then times 0xFF.  (That multiply is a
+// v_mul_lo_u32, four a window; v_perm's constant selectors instead (12:
+// 0x00, 13: 0xFF) measured 2 % slower in the C2 parse stage:
+// profiles/ab_tile_r06.log.)
+__device__ __forceinline__ uint32_t nibble_bytes(uint32_t m)
+{
+    return (__umul24(m & 15u, 0x00204081u) & 0x01010101u) * 0xFFu;
+}
+
 // the four bytes of x through the table (byte b at LDS word b)
 __device__ __forceinline__ uint32_t rb_word(const uint32_t* lut, uint32_t x)
 {
@@ -819,10 +829,7 @@ __device__ __forceinline__ uint32_t rb_window16(const uint4 v, uint32_t valid, i
     const uint32_t cm = (vm | first) & ~skip;   // the bytes looked up
     uint32_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t bm = (__umul24((cm >> (4 * k)) & 15u, 0x00204081u) & 0x01010101u) * 0xFFu;
-        acc += rb_word(lut, ws[k] & bm);
-    }
+    for (int k = 0; k < 4; ++k) acc += rb_word(lut, ws[k] & nibble_bytes(cm >> (4 * k)));
     return acc;
 }
 
@@ -1967,35 +1974,48 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         // a tile inside the chunk (all but its first and last): no window needs
         // the chunk's bounds (block-uniform)
         const bool inner = g0 > c0 && g0 + TP_TILE <= c1;
-        // ---- load (windows at or past the chunk's end read as zeros).  Every
-        // load issued before the first is used, with no branch between them: a
-        // window past the chunk's end loads the tile's first window instead
-        // (g0 < c1, readable as every window before c1 is) and is zeroed.
-        // (Loads under a branch each, stored to LDS as they came, compiled to
-        // one round trip per row: a wait for each before the next was issued.)
+        // ---- load: the tile and its halo straight into LDS by LDS-DMA
+        // (global_load_lds_dwordx4: one wave-instruction fills 1 KiB at the
+        // wave's base, lane-linear; no VGPR holds the tile), then each lane's
+        // windows read back for the index.  A window at or past the chunk's
+        // end loads the tile's first window instead (g0 < c1, readable as
+        // every window before c1 is) and is zeroed once it has landed.
+        // (Against register loads stored to LDS: C2 parse 1.701-1.707 vs
+        // 1.714-1.726 ms per step, C5 10.19 vs 10.19-10.22: profiles/ab_tile_r06.log.)
         const uint64_t hat = g0 + TP_TILE + tid * 16;
         const bool hok = hat < c1;
-        uint4 hv = make_uint4(0, 0, 0, 0);
-        if (tid < TP_HALO / 16) hv = *(const uint4*)(text + (hok ? hat : g0));   // (whole waves)
         // the byte before the tile (one address for the block)
         const bool pok = g0 > c0 && g0 - 1 < c1;
         const uint32_t pbyte = (uint8_t)text[pok ? g0 - 1 : g0];
-        uint4 v[ROWS];
+        {
+            typedef __attribute__((address_space(3))) void lds_void;
+            const uint32_t wb = (tid & ~63u) * 16u;
 #pragma unroll
-        for (uint32_t k = 0; k < ROWS; ++k) {
-            const uint64_t at = g0 + k * TILE + tid * 16;
-            const bool ok = inner || at < c1;
-            const uint4 x = ld_nt(text + (ok ? at : g0));
-            v[k] = ok ? x : make_uint4(0, 0, 0, 0);
+            for (uint32_t k = 0; k < ROWS; ++k) {
+                const uint64_t at = g0 + k * TILE + tid * 16;
+                const bool ok = inner || at < c1;
+                __builtin_amdgcn_global_load_lds((const void*)(text + (ok ? at : g0)),
+                                                 (lds_void*)(tl + k * TILE + wb), 16, 0, 2 /* nt */);
+            }
+            if (tid < TP_HALO / 16)   // (whole waves)
+                __builtin_amdgcn_global_load_lds((const void*)(text + (hok ? hat : g0)), (lds_void*)(tl + TP_TILE + wb),
+                                                 16, 0, 0);
+            if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
+            __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): this wave's pieces have landed
+            if (!inner) {
+#pragma unroll
+                for (uint32_t k = 0; k < ROWS; ++k)
+                    if (g0 + k * TILE + tid * 16 >= c1) *(uint4*)(tl + k * TILE + tid * 16) = make_uint4(0, 0, 0, 0);
+            }
+            if (tid < TP_HALO / 16 && !hok) *(uint4*)(tl + TP_TILE + tid * 16) = make_uint4(0, 0, 0, 0);
         }
         if constexpr (QUAD) __builtin_amdgcn_s_setprio(2);
-#pragma unroll
-        for (uint32_t k = 0; k < ROWS; ++k) *(uint4*)(tl + k * TILE + tid * 16) = v[k];
-        if (tid < TP_HALO / 16) *(uint4*)(tl + TP_TILE + tid * 16) = hok ? hv : make_uint4(0, 0, 0, 0);
-        if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
         // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
         const uint32_t prev0 = tid ? 0u : pok ? (pbyte == '\n') : 1u;
         __syncthreads();
+        uint4 v[ROWS];
+#pragma unroll
+        for (uint32_t k = 0; k < ROWS; ++k) v[k] = *(const uint4*)(tl + k * TILE + tid * 16);
         TP_STAMP_AT(st1);
         // ---- line starts (bit j: byte j of the window starts a non-empty line in [c0, c1))
         // (the windows' newline masks computed before the barrier, while the
@@ -2071,10 +2091,14 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         __syncthreads();
         TP_STAMP_AT(st2);
         __builtin_amdgcn_s_setprio(0);
-        // a later tile's lines into L2: one 4-B load per 128-B line (the
-        // value kept to the kernel's end, so the loads stay in flight).
-        // (Issued at the block's start instead, before its own loads: C2
-        // parse 2.02-2.04 vs 1.95-1.96 ms per step.)
+        // a later tile's lines into L2: one 4-B load per 128-B line of tile
+        // t + pf_dist, its value consumed at the kernel's end by an empty asm
+        // (a compare of it there was hoisted here by the compiler, with a
+        // vmcnt(0) wait for the load before the parse: C2 parse 1.772-1.779
+        // -> 1.737-1.746 ms per step, C5 10.65 -> 10.26-10.32; issued right
+        // after the tile's loads instead: no gain; at the block's start,
+        // before them: C2 parse 2.02-2.04 vs 1.95-1.96; none at all: C2 parse
+        // +1 %, profiles/ab_tile_r06.log)
         uint32_t pf = 0;
         {
             const uint64_t u = t + pf_dist;
@@ -2135,8 +2159,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
                 if constexpr (LOCAL) bsum_add(j0 + (tid & ~63u), j, l);
             }
         }
-        // (the prefetch's value: kept live to here, never true)
-        if (pf == 0x5A5A5A5Au && c1 == 0) O.state[5] = pf;
+        asm volatile("; the prefetch's value, kept to here: %0" ::"v"(pf));
 #ifdef SID_TP_STAMP
         __syncthreads();
         if (tid == 0 && t < TP_STAMP_N) {
