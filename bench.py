@@ -763,8 +763,15 @@ def generate_resident(torch, sid_amd, dev, gpu, cfg, first, n):
     return text, ln
 
 
-VALU_ISSUE_PER_S = 256 * 4 / 2 * 2.4e9   # wave64 VALU instructions/s: 1024 SIMDs, one per 2 cycles, 2.4 GHz
-PMC_ROUND = os.environ.get("SID_PMC_ROUND", "r05")
+# wave64 VALU instructions/s the chip issues: 1024 SIMDs x one per 3.53
+# cycles at 2.33 GHz, measured (tools/debug/valu_rate_probe.hip,
+# profiles/valu_rate_probe_r06.jsonl: 32-bit integer VALU streams at 8 waves
+# a SIMD, the in-kernel clock).  A SIMD is 16 lanes wide: a wave64
+# instruction holds it for 4 cycles (157.3 TF f32 = 1024 x 16 lanes x 2 FMA x
+# 2 packed x 2.4 GHz).  (Round 5 priced one per 2 cycles at 2.4 GHz, 1.82x
+# this, and so read the tile parse as half busy.)
+VALU_ISSUE_PER_S = 1024 * 2.33e9 / 3.53
+PMC_ROUND = os.environ.get("SID_PMC_ROUND", "r06")
 
 
 def pcie_ceiling(text_bytes, csv_bytes, lynch, step_s):
