@@ -1920,10 +1920,10 @@ __device__ __forceinline__ int quad_tail(const char* __restrict__ text, uint64_t
 
 // LOCAL: -m local's class words and record lengths (sid_chunk_tile_local);
 // else every site's counts (the Lynch paths' first pass, sid_chunk_tile_counts).
-// One block per tile.  While a block parses its tile, one load per 128-B
-// line of tile blockIdx.x + pf_dist is in flight (pf_dist: the blocks
-// resident on the device, a multiple of the 8 XCDs; that tile's block then
-// runs about when this one ends, on the same XCD, and its loads hit L2).
+// One block per tile.  (Round 5 kept a later tile's lines in flight into L2
+// while a block parsed, one 4-B load per 128-B line: with the tile loaded by
+// LDS-DMA that prefetch fetched 101 B a site for 86 without it, and the
+// parse took 1.714-1.722 ms per C2 step for 1.698-1.702: profiles/ab_tile_r06.log.)
 #ifdef SID_TP_STAMP
 // (diagnostic builds: per-phase wall-clock stamps of the tile parse's and the
 // -m local writer's blocks, thread 0 of each)
@@ -1938,8 +1938,7 @@ __device__ uint32_t put_stamp[TP_STAMP_N][4];
 #endif
 template <bool QUAD, bool LOCAL>
 __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restrict__ text, uint64_t tile_base,
-                                                            uint64_t c0, uint64_t c1, uint64_t ntiles,
-                                                            uint32_t pf_dist, TileOut O, LocalLen LL)
+                                                            uint64_t c0, uint64_t c1, TileOut O, LocalLen LL)
 {
     constexpr uint32_t ROWS = QUAD ? TP_ROWS_QUAD : TP_ROWS, TP_TILE = ROWS * TILE;
     constexpr uint32_t LPR = QUAD ? TB / 4 : TB;   // lines per round of the block
@@ -2091,21 +2090,6 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         __syncthreads();
         TP_STAMP_AT(st2);
         __builtin_amdgcn_s_setprio(0);
-        // a later tile's lines into L2: one 4-B load per 128-B line of tile
-        // t + pf_dist, its value consumed at the kernel's end by an empty asm
-        // (a compare of it there was hoisted here by the compiler, with a
-        // vmcnt(0) wait for the load before the parse: C2 parse 1.772-1.779
-        // -> 1.737-1.746 ms per step, C5 10.65 -> 10.26-10.32; issued right
-        // after the tile's loads instead: no gain; at the block's start,
-        // before them: C2 parse 2.02-2.04 vs 1.95-1.96; none at all: C2 parse
-        // +1 %, profiles/ab_tile_r06.log)
-        uint32_t pf = 0;
-        {
-            const uint64_t u = t + pf_dist;
-            const uint32_t off = tid * 128u;
-            const uint64_t at = tile_base + u * TP_TILE + off;
-            if (u < ntiles && off < TP_TILE + TP_HALO && at < c1) pf = *(const uint32_t*)(text + at);
-        }
         // ---- parse, one lane (a quad of lanes) per line, from LDS; offsets
         // from the tile's first byte (32 bits: a chunk spans less than 4 GiB)
         const char* gtile = text + g0;
@@ -2159,7 +2143,6 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
                 if constexpr (LOCAL) bsum_add(j0 + (tid & ~63u), j, l);
             }
         }
-        asm volatile("; the prefetch's value, kept to here: %0" ::"v"(pf));
 #ifdef SID_TP_STAMP
         __syncthreads();
         if (tid == 0 && t < TP_STAMP_N) {
@@ -3892,31 +3875,15 @@ static uint64_t tile_count(uint64_t c0, uint64_t c1, bool quad)
     return c1 > c0 ? (c1 - t0 + tp_tile(quad) - 1) / tp_tile(quad) : 0;
 }
 
-// The tile parse's prefetch distance: the blocks resident on the device at
-// once (occupancy x CUs), a multiple of the 8 XCDs
-template <class K>
-static uint32_t resident_blocks(K kernel)
-{
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, TB, 0) != hipSuccess)
-        return 1536u;
-    return (uint32_t)std::max(8, (cus * std::max(per, 1)) & ~7);
-}
-
 template <bool LOCAL>
 static void launch_tile_parse(bool quad, const char* base, uint64_t c0, uint64_t c1, uint64_t ntp, const TileOut& O,
                               const LocalLen& LL, hipStream_t st)
 {
     const uint64_t tb = c0 & ~(uint64_t)15;
-    if (quad) {
-        static const uint32_t pf = resident_blocks(sid_tile_parse_kernel<true, LOCAL>);
-        sid_tile_parse_kernel<true, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp, pf, O, LL);
-    } else {
-        static const uint32_t pf = resident_blocks(sid_tile_parse_kernel<false, LOCAL>);
-        sid_tile_parse_kernel<false, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, ntp, pf, O, LL);
-    }
+    if (quad)
+        sid_tile_parse_kernel<true, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, O, LL);
+    else
+        sid_tile_parse_kernel<false, LOCAL><<<(unsigned)ntp, TB, 0, st>>>(base, tb, c0, c1, O, LL);
 #ifdef SID_TP_STAMP
     {
         const uint64_t m = std::min<uint64_t>(ntp, TP_STAMP_N);
