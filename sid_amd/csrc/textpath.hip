@@ -544,7 +544,7 @@ __device__ __forceinline__ bool is_c_space(uint32_t c) { return c == ' ' || (c >
 __device__ __forceinline__ bool is_digit(uint32_t c) { return c >= '0' && c <= '9'; }
 
 // parse.cpp ClassTable: 1..4 = A C G T (either case), 5 = '^', 6 = '+'/'-', 0 = other
-__device__ __forceinline__ uint32_t base_class(uint32_t c)
+__host__ __device__ constexpr uint32_t base_class(uint32_t c)
 {
     switch (c) {
     case 'A': case 'a': return 1;
@@ -768,7 +768,7 @@ __device__ __forceinline__ uint32_t not_digit(uint32_t x)
 // general routine then has strtok_r's view of it); every other byte 0.
 // Bytes not to count are zeroed before the lookup (NUL's entry is 0).
 constexpr uint32_t RB_M_SHIFT = 20, RB_BAD_SHIFT = 25;
-__device__ __forceinline__ uint32_t rb_entry(uint32_t c)
+__host__ __device__ constexpr uint32_t rb_entry(uint32_t c)
 {
     switch (c) {
     case 'A': case 'a': return 1u;
@@ -781,6 +781,26 @@ __device__ __forceinline__ uint32_t rb_entry(uint32_t c)
     default: return c < 0x21 ? 1u << 30 : 0;
     }
 }
+
+// The parse kernels' two LDS tables, built at compile time: each block copies
+// them in (a load a lane) instead of evaluating both switches per lane (the
+// branches of every case, serial in a wave, in every block: 13 % of the tile
+// parse's time, C2 parse 1.712 -> 1.51 ms, C5 10.13 -> 8.76 ms per step,
+// profiles/ab_tile_r06.log)
+struct TpTables {
+    uint32_t rb[256];
+    uint8_t cls[256];
+};
+constexpr TpTables make_tp_tables()
+{
+    TpTables t{};
+    for (uint32_t c = 0; c < 256; ++c) {
+        t.rb[c] = rb_entry(c);
+        t.cls[c] = (uint8_t)base_class(c);
+    }
+    return t;
+}
+__device__ constexpr TpTables k_tp_tables = make_tp_tables();
 
 // bits 0-3 of m as the bytes 0x00 / 0xFF of a word: each bit moved to its
 // byte's bit 0 by a 24-bit multiply, then times 0xFF.  (That multiply is a
@@ -1091,8 +1111,8 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
     __shared__ uint32_t rbl[256];
     __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
     if (threadIdx.x < 256) {
-        cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
-        rbl[threadIdx.x] = rb_entry(threadIdx.x);
+        cls[threadIdx.x] = k_tp_tables.cls[threadIdx.x];
+        rbl[threadIdx.x] = k_tp_tables.rb[threadIdx.x];
     }
     __syncthreads();
     const uint64_t lo = range[0], hi = range[1];
@@ -1128,8 +1148,8 @@ __global__ __launch_bounds__(TB) void sid_parse_quad_kernel(const char* __restri
     __shared__ uint32_t rbl[256];
     __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
     if (threadIdx.x < 256) {
-        cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
-        rbl[threadIdx.x] = rb_entry(threadIdx.x);
+        cls[threadIdx.x] = k_tp_tables.cls[threadIdx.x];
+        rbl[threadIdx.x] = k_tp_tables.rb[threadIdx.x];
     }
     __syncthreads();
     constexpr uint32_t LPB = TB / 4;   // lines per block step
@@ -1165,7 +1185,7 @@ __global__ __launch_bounds__(TB) void sid_parse_serial_kernel(const char* __rest
                                                               unsigned long long* nlate = nullptr)
 {
     __shared__ uint8_t cls[256];
-    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    if (threadIdx.x < 256) cls[threadIdx.x] = k_tp_tables.cls[threadIdx.x];
     __syncthreads();
     const uint64_t lo = range[0];
     const uint64_t m = fb ? *fbn : range[1] - lo;
@@ -1661,8 +1681,8 @@ __global__ __launch_bounds__(TB) void sid_parse_len_kernel(const char* __restric
     __shared__ uint32_t rbl[256];
     __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
     if (threadIdx.x < 256) {
-        cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
-        rbl[threadIdx.x] = rb_entry(threadIdx.x);
+        cls[threadIdx.x] = k_tp_tables.cls[threadIdx.x];
+        rbl[threadIdx.x] = k_tp_tables.rb[threadIdx.x];
     }
     __syncthreads();
     const uint64_t lo = range[0], hi = range[1];
@@ -1957,8 +1977,8 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     __shared__ uint32_t qmeta[QUAD ? tp_cap_max(true) : 1];   // the quad shape's headers (quad_head)
     __shared__ uint64_t qcnt[QUAD && LOCAL ? tp_cap_max(true) : 1];   // ... and counts (quad_bases)
     const uint32_t tid = threadIdx.x;
-    cls[tid] = (uint8_t)base_class(tid);
-    rbl[tid] = rb_entry(tid);
+    cls[tid] = k_tp_tables.cls[tid];
+    rbl[tid] = k_tp_tables.rb[tid];
     if (blockIdx.x == 0 && tid == 0) O.state[4] = ~0ull;   // no parse error yet
     const uint32_t cap = O.cap;
     {
@@ -2206,7 +2226,7 @@ __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restr
 {
     __shared__ uint8_t cls[256];
     __shared__ uint32_t red[2][TB / 64];
-    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    if (threadIdx.x < 256) cls[threadIdx.x] = k_tp_tables.cls[threadIdx.x];
     {
         // four tiles a 16-B load, four loads in flight a lane (one pass over
         // ~200k tiles at this grid; a load a tile, each waited for before the
@@ -2936,7 +2956,7 @@ __global__ __launch_bounds__(TB) void sid_quality_sum_kernel(const char* __restr
     __shared__ double T[4 * 256];
     __shared__ uint8_t cls[256];
     for (uint32_t i = threadIdx.x; i < 4 * 256; i += blockDim.x) T[i] = g_qtab[i];
-    if (threadIdx.x < 256) cls[threadIdx.x] = (uint8_t)base_class(threadIdx.x);
+    if (threadIdx.x < 256) cls[threadIdx.x] = k_tp_tables.cls[threadIdx.x];
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t w = counts[i];
