@@ -1977,8 +1977,6 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     __shared__ uint32_t qmeta[QUAD ? tp_cap_max(true) : 1];   // the quad shape's headers (quad_head)
     __shared__ uint64_t qcnt[QUAD && LOCAL ? tp_cap_max(true) : 1];   // ... and counts (quad_bases)
     const uint32_t tid = threadIdx.x;
-    cls[tid] = k_tp_tables.cls[tid];
-    rbl[tid] = k_tp_tables.rb[tid];
     if (blockIdx.x == 0 && tid == 0) O.state[4] = ~0ull;   // no parse error yet
     const uint32_t cap = O.cap;
     {
@@ -2020,6 +2018,11 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
                 __builtin_amdgcn_global_load_lds((const void*)(text + (hok ? hat : g0)), (lds_void*)(tl + TP_TILE + wb),
                                                  16, 0, 0);
             if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
+            // the LDS tables, loaded while the tile's pieces are in flight
+            // (copied in before them, their load's wait came before the
+            // tile's loads were issued)
+            cls[tid] = k_tp_tables.cls[tid];
+            rbl[tid] = k_tp_tables.rb[tid];
             __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): this wave's pieces have landed
             if (!inner) {
 #pragma unroll
