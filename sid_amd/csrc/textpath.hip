@@ -299,6 +299,22 @@ __device__ __forceinline__ uint32_t compress8(uint32_t a, uint32_t b)
     x |= x >> 14;                       // bits 2, 3, 6, 7 <- 16, 17, 20, 21
     return x & 0xFFu;
 }
+// bit 7 of each byte of four words -> 16 bits (word w's byte k at bit 4w+k):
+// the bytes (0x00 or 0x80) weighted by v_dot4 (1, 2, 4, 8 and 16 .. 128) and
+// summed, two words a dot product pair; 6 instructions for compress8's 16
+#ifndef SID_CMP_DOT
+#define SID_CMP_DOT 1
+#endif
+__device__ __forceinline__ uint32_t compress16(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+#if SID_CMP_DOT
+    const uint32_t lo = __builtin_amdgcn_udot4(b, 0x80402010u, __builtin_amdgcn_udot4(a, 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(d, 0x80402010u, __builtin_amdgcn_udot4(c, 0x08040201u, 0u, false), false);
+    return (lo >> 7) | (hi << 1);   // (hi: 128 x the high byte's bits)
+#else
+    return compress8(a, b) | (compress8(c, d) << 8);
+#endif
+}
 // a 16-B load marked non-temporal (streamed data read once: kept out of the
 // caches the data read again needs)
 // the intermediate arrays (line-start masks, line offsets, counts, header
@@ -324,8 +340,8 @@ __device__ __forceinline__ uint32_t line_start_mask(const char* __restrict__ tex
     const uint64_t at = tile0 + (uint64_t)threadIdx.x * 16;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (at < c1 && at + 16 > c0) v = *(const uint4*)(text + at);
-    uint32_t nl = compress8(eq_bytes(v.x, 0x0A0A0A0Au), eq_bytes(v.y, 0x0A0A0A0Au)) |
-                  (compress8(eq_bytes(v.z, 0x0A0A0A0Au), eq_bytes(v.w, 0x0A0A0A0Au)) << 8);
+    uint32_t nl = compress16(eq_bytes(v.x, 0x0A0A0A0Au), eq_bytes(v.y, 0x0A0A0A0Au), eq_bytes(v.z, 0x0A0A0A0Au),
+                             eq_bytes(v.w, 0x0A0A0A0Au));
     // is the byte before `at` a '\n': the neighbour lane's bit 15, or a load at a wave start
     uint32_t prev = (uint32_t)__shfl_up((int)(nl >> 15), 1, 64);
     if ((threadIdx.x & 63) == 0) prev = (at > c0 && at - 1 < c1) ? (text[at - 1] == '\n') : 1u;
@@ -400,8 +416,8 @@ __device__ __forceinline__ IxWin ix_load(const char* __restrict__ text, uint64_t
 __device__ __forceinline__ uint32_t ix_mask(const IxWin& w, uint64_t at, uint64_t c0, uint64_t c1)
 {
     const uint4 v = w.v;
-    uint32_t nl = compress8(eq_bytes(v.x, 0x0A0A0A0Au), eq_bytes(v.y, 0x0A0A0A0Au)) |
-                  (compress8(eq_bytes(v.z, 0x0A0A0A0Au), eq_bytes(v.w, 0x0A0A0A0Au)) << 8);
+    uint32_t nl = compress16(eq_bytes(v.x, 0x0A0A0A0Au), eq_bytes(v.y, 0x0A0A0A0Au), eq_bytes(v.z, 0x0A0A0A0Au),
+                             eq_bytes(v.w, 0x0A0A0A0Au));
     uint32_t prev = (uint32_t)__shfl_up((int)(nl >> 15), 1, 64);
     if ((threadIdx.x & 63) == 0) prev = w.prev;
     uint32_t m = ((nl << 1) | prev) & ~nl & 0xFFFFu;
@@ -833,10 +849,9 @@ __device__ __forceinline__ uint32_t rb_window16(const uint4 v, uint32_t valid, i
                                                 bool& done, uint32_t& carry, bool& bad)
 {
     const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-    const uint32_t L = compress8(low_bytes(ws[0]), low_bytes(ws[1])) |
-                       (compress8(low_bytes(ws[2]), low_bytes(ws[3])) << 8);
-    const uint32_t C = compress8(eq_bytes(ws[0], 0x5E5E5E5Eu), eq_bytes(ws[1], 0x5E5E5E5Eu)) |
-                       (compress8(eq_bytes(ws[2], 0x5E5E5E5Eu), eq_bytes(ws[3], 0x5E5E5E5Eu)) << 8);
+    const uint32_t L = compress16(low_bytes(ws[0]), low_bytes(ws[1]), low_bytes(ws[2]), low_bytes(ws[3]));
+    const uint32_t C = compress16(eq_bytes(ws[0], 0x5E5E5E5Eu), eq_bytes(ws[1], 0x5E5E5E5Eu),
+                                  eq_bytes(ws[2], 0x5E5E5E5Eu), eq_bytes(ws[3], 0x5E5E5E5Eu));
     uint32_t vm = done ? 0u : (MASKED ? valid : 0xFFFFu);
     const uint32_t lo = L & vm;
     const uint32_t first = lo & (0u - lo);      // the token's end, if in this window
@@ -995,9 +1010,9 @@ __device__ __forceinline__ int parse_header(const uint4 v0, const uint4 v1, cons
     uint32_t lowb[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) lowb[k] = low_bytes(w[k]);
-    const uint32_t l_lo = compress8(lowb[0], lowb[1]) | (compress8(lowb[2], lowb[3]) << 8) |
-                          (compress8(lowb[4], lowb[5]) << 16) | (compress8(lowb[6], lowb[7]) << 24);
-    const uint32_t l_hi = compress8(lowb[8], lowb[9]) | (compress8(lowb[10], lowb[11]) << 8);
+    const uint32_t l_lo = compress16(lowb[0], lowb[1], lowb[2], lowb[3]) |
+                          (compress16(lowb[4], lowb[5], lowb[6], lowb[7]) << 16);
+    const uint32_t l_hi = compress16(lowb[8], lowb[9], lowb[10], lowb[11]);
     // bit j = byte s0 + j, for the bytes inside the text and the 48 staged
     const uint32_t nb = (uint32_t)min((uint64_t)(HDR_BYTES - sh), avail);
     const uint64_t valid = (1ull << nb) - 1;   // (nb <= 48)
@@ -2055,8 +2070,8 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         for (uint32_t k = 0; k < ROWS; ++k) {
             const uint64_t at = g0 + k * TILE + tid * 16;
             const uint4 w = v[k];
-            const uint32_t nl = compress8(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au)) |
-                                (compress8(eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au)) << 8);
+            const uint32_t nl = compress16(eq_bytes(w.x, 0x0A0A0A0Au), eq_bytes(w.y, 0x0A0A0A0Au),
+                                           eq_bytes(w.z, 0x0A0A0A0Au), eq_bytes(w.w, 0x0A0A0A0Au));
             const uint32_t prev = (k == 0 && tid == 0) ? prev0 : (uint32_t)(pb[k] == '\n');
             uint32_t mk = ((nl << 1) | prev) & ~nl & 0xFFFFu;
             if (!inner) {
