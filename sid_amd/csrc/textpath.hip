@@ -2309,6 +2309,22 @@ __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restr
     }
 }
 
+// slot -> its tile (slot / cap) by one 32-bit multiply-high: t = mulhi(g, m)
+// >> s with s = floor(log2(cap - 1)), m = ceil(2^(32+s) / cap) < 2^32; the
+// error m cap - 2^(32+s) < cap <= 2^(s+1) keeps it exact for g < 2^28 (a
+// chunk of at most 4 GiB has fewer slots).  (A 64-bit multiply-high by
+// ceil(2^64 / cap) took a chain of quarter-rate multiplies a slot.)
+struct SlotDiv {
+    uint32_t m, s;
+};
+static SlotDiv slot_div(uint32_t cap)
+{
+    const uint32_t s = 31u - (uint32_t)__builtin_clz(cap - 1u);
+    return SlotDiv{(uint32_t)(((1ull << (32 + s)) + cap - 1) / cap), s};
+}
+__device__ __forceinline__ uint32_t slot_tile(uint32_t g, SlotDiv d) { return __umulhi(g, d.m) >> d.s; }
+constexpr uint64_t SID_SLOTS_MAX = 1ull << 28;
+
 // The tile parse's sites into file order (the Lynch paths' kept parse,
 // run.cpp use_pre: line offsets, counts, header pairs): slot g = tile * cap +
 // j goes to toff[tile] + j (toff: the tiles' exclusive prefix of their
@@ -2316,7 +2332,7 @@ __global__ __launch_bounds__(TB) void sid_tile_serial_kernel(const char* __restr
 // bytes, no valid pair), else 0 (unread)
 __global__ __launch_bounds__(TB) void sid_tile_compact_kernel(const uint32_t* __restrict__ tcnt,
                                                               const uint64_t* __restrict__ toff, uint64_t slots,
-                                                              uint32_t cap, uint64_t cap_magic,
+                                                              uint32_t cap, SlotDiv cdiv,
                                                               const uint64_t* __restrict__ counts,
                                                               const uint64_t* __restrict__ hdr,
                                                               sid_off_t* __restrict__ d_starts,
@@ -2324,8 +2340,8 @@ __global__ __launch_bounds__(TB) void sid_tile_compact_kernel(const uint32_t* __
                                                               uint64_t* __restrict__ d_hdr)
 {
     for (uint64_t g = (uint64_t)blockIdx.x * TB + threadIdx.x; g < slots; g += (uint64_t)gridDim.x * TB) {
-        const uint64_t t = __umul64hi(g, cap_magic);   // g / cap
-        const uint32_t j = (uint32_t)(g - t * cap);
+        const uint32_t t = slot_tile((uint32_t)g, cdiv);
+        const uint32_t j = (uint32_t)g - t * cap;
         if (j >= tcnt[t]) continue;
         const uint64_t i = toff[t] + j;
         const ulonglong2 hw = *(const ulonglong2*)(hdr + 2 * g);
@@ -2440,6 +2456,43 @@ __device__ __forceinline__ void lds_or_byte(unsigned long long* B, uint32_t q, u
 
 // "," + the decimal of 0 <= v < 10^10 + ",", left-aligned in 16 bytes (lo,
 // hi), zero after; nd = its digits
+// g < 10^4 as four ASCII digits, most significant first (byte 0): g / 100
+// and g % 100 in the two 16-bit halves of a word, both halves divided by 10
+// at once ((x 103) >> 10 is x / 10 below 179), full-rate 24-bit multiplies only
+__device__ __forceinline__ uint32_t four_digits(uint32_t g)
+{
+    const uint32_t hi2 = __umul24(g, 5243u) >> 19;   // g / 100 (exact below 43690)
+    const uint32_t p = hi2 | ((g - __umul24(hi2, 100u)) << 16);
+    const uint32_t t = (__umul24(p, 103u) >> 10) & 0x000F000Fu;
+    const uint32_t u = p - __umul24(t, 10u);
+    return 0x30303030u + (t | (u << 8));
+}
+#ifndef SID_POS_LOOP
+// v < 2^31 with nd digits -> ",digits," in lo (bytes 0-7) and hi: three
+// groups of four digits (two 32-bit divisions by 10^4), the twelve digits
+// with their leading zeros at bytes 1-12 and a ',' at 13, the zero digit at
+// byte 12 - nd made the leading ',', then shifted down by 12 - nd bytes.
+// (Eleven divisions by 10, each a quarter-rate multiply-high, before.)
+__device__ __forceinline__ void comma_num_comma(uint32_t v, int nd, uint64_t& lo, uint64_t& hi)
+{
+    const uint32_t q1 = v / 10000u, g0 = v - q1 * 10000u;
+    const uint32_t g2 = q1 / 10000u, g1 = q1 - g2 * 10000u;
+    const uint32_t w0 = four_digits(g0), w1 = four_digits(g1), w2 = four_digits(g2);
+    uint64_t L = ((uint64_t)w2 << 8) | ((uint64_t)w1 << 40);
+    uint64_t H = ((uint64_t)w1 >> 24) | ((uint64_t)w0 << 8) | ((uint64_t)',' << 40);
+    const uint32_t p = 12u - (uint32_t)nd;   // 2 .. 11
+    if (p < 8) L ^= 0x1Cull << (8 * p);      // '0' ^ ',' = 0x1C
+    else H ^= 0x1Cull << (8 * (p - 8));
+    const uint32_t sh = 8 * p;
+    if (sh >= 64) {
+        lo = H >> (sh - 64);
+        hi = 0;
+    } else {
+        lo = (L >> sh) | (H << (64 - sh));
+        hi = H >> sh;
+    }
+}
+#else
 __device__ __forceinline__ void comma_num_comma(uint32_t v, int nd, uint64_t& lo, uint64_t& hi)
 {
     // right-aligned first: byte 15 ',', byte 14 - j digit j (units first),
@@ -2463,6 +2516,7 @@ __device__ __forceinline__ void comma_num_comma(uint32_t v, int nd, uint64_t& lo
         hi = H >> sh;
     }
 }
+#endif
 
 // any record (the fix-up's sites, chroms the parse did not keep, positions
 // from the text) byte by byte into the OR buffer
@@ -2586,7 +2640,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
                                                            const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ hdr, uint64_t n,
                                                            const uint32_t* __restrict__ tcnt, uint32_t cap,
-                                                           uint64_t cap_magic,
+                                                           SlotDiv cdiv,
                                                            const uint64_t* __restrict__ counts,
                                                            const uint32_t* __restrict__ cwords,
                                                            const char* __restrict__ str1,
@@ -2622,8 +2676,8 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     if (tcnt && site) {   // slot i = tile * cap + j: a site when j is below the tile's count
         if (CLS) w0 = cwords[i];
         hw0 = *(const ulonglong2*)(hdr + 2 * i);
-        const uint64_t t = __umul64hi(i, cap_magic);   // i / cap (cap_magic = ceil(2^64 / cap), i < 2^32)
-        site = (uint32_t)(i - t * cap) < tcnt[t];
+        const uint32_t t = slot_tile((uint32_t)i, cdiv);   // (i < SID_SLOTS_MAX)
+        site = (uint32_t)i - t * cap < tcnt[t];
     }
     if (site) {
         uint32_t k;
@@ -3868,10 +3922,10 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
         const uint64_t nbs = (W->slots + FTB - 1) / FTB;
         if (nbs == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
                                  ? SID_OK : SID_EHIP;
-        if (W->slots >> 32) return SID_EINVAL;   // (a 4 GiB chunk has < 2^28 slots)
-        const uint64_t magic = ~0ull / W->slot_cap + 1;   // ceil(2^64 / cap): the slot's tile by a multiply-high, exact for slots < 2^32 (cap: a multiple of 16 up to 1024, powers of 2 included)
+        if (W->slots >= SID_SLOTS_MAX) return SID_EINVAL;   // (slot_tile's exact range: a 4 GiB chunk has fewer)
+        const SlotDiv cdiv = slot_div(W->slot_cap);
         sid_local_put_kernel<true><<<(unsigned)nbs, FTB, 0, st>>>(base, c1, nullptr, W->hdr, W->slots, W->tcnt,
-                                                                 W->slot_cap, magic, W->counts, W->cls, ctx->ws.str1,
+                                                                 W->slot_cap, cdiv, W->counts, W->cls, ctx->ws.str1,
                                                                  ctx->ws.str2, W->code, W->hom, W->het, ct, W->boff,
                                                                  W->state, W->lb, out);
         WCHECK(hipGetLastError());
@@ -3894,12 +3948,12 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
     if (nb == 0) return hipMemcpyAsync(W->lb + 4, W->state + 4, 8, hipMemcpyDeviceToDevice, st) == hipSuccess
                             ? SID_OK : SID_EHIP;
     if (W->cls_ready)
-        sid_local_put_kernel<true><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0, 0,
+        sid_local_put_kernel<true><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0, SlotDiv{0, 0},
                                                                 W->counts, W->cls,
                                                                 ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
                                                                 ct, W->boff, W->state, W->lb, out);
     else
-        sid_local_put_kernel<false><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0, 0,
+        sid_local_put_kernel<false><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0, SlotDiv{0, 0},
                                                                  W->counts, nullptr,
                                                                  ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
                                                                  ct, W->boff, W->state, W->lb, out);
@@ -4028,10 +4082,10 @@ int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64
 int sid_chunk_tile_compact(sid_chunk_ws* W, sid_off_t* starts, uint64_t* counts, uint64_t* hdr, hipStream_t st)
 {
     if (!W->slot_cap) return SID_ESTATE;
-    if (W->slots >> 32) return SID_EINVAL;   // (the magic's exact range; a 4 GiB chunk has < 2^28 slots)
-    const uint64_t magic = ~0ull / W->slot_cap + 1;
+    if (W->slots >= SID_SLOTS_MAX) return SID_EINVAL;   // (slot_tile's exact range: a 4 GiB chunk has fewer)
+    const SlotDiv cdiv = slot_div(W->slot_cap);
     const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((W->slots + TB - 1) / TB, 1), 8192);
-    sid_tile_compact_kernel<<<grid, TB, 0, st>>>(W->tcnt, W->toff, W->slots, W->slot_cap, magic, W->counts, W->hdr,
+    sid_tile_compact_kernel<<<grid, TB, 0, st>>>(W->tcnt, W->toff, W->slots, W->slot_cap, cdiv, W->counts, W->hdr,
                                                  starts, counts, hdr);
     W->slot_cap = 0;   // the dense layout again
     WCHECK(hipGetLastError());
