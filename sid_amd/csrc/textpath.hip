@@ -825,7 +825,7 @@ __device__ constexpr TpTables k_tp_tables = make_tp_tables();
 // profiles/ab_tile_r06.log.)
 __device__ __forceinline__ uint32_t nibble_bytes(uint32_t m)
 {
-    return (__umul24(m & 15u, 0x00204081u) & 0x01010101u) * 0xFFu;
+    return (__umul24(m & 15u, 0x00204081u) & 0x01010101u) * 0xFFu;   // ((b << 8) - b: the same time)
 }
 
 // the four bytes of x through the table (byte b at LDS word b)
@@ -891,13 +891,24 @@ __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t k
         const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
         return rb_window16<true>(v, valid, room, lut, done, carry, bad);
     };
+    // the windows' 5-bit fields summed in two words with 10 bits a field (A,
+    // G, '.' in one, C, T in the other: 4 instructions a window instead of
+    // 10), into the counters every 63 windows (a field gains at most 16 a
+    // window) and at the end (C2 parse 1.331-1.336 -> 1.320-1.323 ms)
+    uint32_t ev = 0, od = 0, nw = 0;
+    auto flush = [&]() {
+        nA += ev & 1023u;
+        nG += (ev >> 10) & 1023u;
+        nM += ev >> 20;
+        nC += (od >> 5) & 1023u;
+        nT += od >> 15;
+        ev = od = nw = 0;
+    };
     auto add = [&](uint32_t w) {
-        nA += w & 31u;
-        nC += (w >> 5) & 31u;
-        nG += (w >> 10) & 31u;
-        nT += (w >> 15) & 31u;
-        nM += (w >> RB_M_SHIFT) & 31u;
+        ev += w & 0x01F07C1Fu;
+        od += w & 0x000F83E0u;
         acc |= w;
+        if (++nw == 63) flush();
     };
     add(masked(*first, (uint32_t)(q & 15)));
     a += 16;
@@ -908,6 +919,7 @@ __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t k
         a += 16;
     }
     if (bad || (acc >> RB_BAD_SHIFT) != 0) return false;
+    flush();
     nA += kd == K_A ? nM : 0;
     nC += kd == K_C ? nM : 0;
     nG += kd == K_G ? nM : 0;
