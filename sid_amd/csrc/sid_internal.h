@@ -154,6 +154,8 @@ struct sid_chunk_ws {
                                   // major / minor bases, or SID_CLS_MISS); the counts are then written only for
                                   // the fix-up's sites
     bool cls_ready = false;       // cls holds this chunk's words (set by the parse, read by sid_chunk_local_put)
+    ulonglong2* twv = nullptr;    // the tile parse's wave entries (-m local, lane shape: chrom and position
+                                  // of the compact class words; site_cap / 32 + 1)
     uint8_t* code = nullptr;
     double* hom = nullptr;
     double* het = nullptr;
@@ -167,7 +169,7 @@ struct sid_chunk_ws {
                                   // [6] [7] fallback lines
     uint32_t slot_cap = 0;        // 0: sites in file order (index + parse); else the tile parse's layout: slots
     uint64_t slots = 0;           // of slot_cap per tile, `slots` of them (sid_chunk_tile_local)
-    bool tile_quad = false;       // (sid_chunk_tile_counts: the shape and tiles, for the compaction)
+    bool tile_quad = false;       // the tile parse's shape (the compaction; the -m local writer: wave entries or not)
     uint64_t tile_ntp = 0;
 };
 int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites);

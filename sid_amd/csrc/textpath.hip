@@ -1649,6 +1649,15 @@ __device__ __forceinline__ uint32_t local_word(uint32_t k, uint32_t f, uint32_t 
 {
     return k | (f << 28) | (s << 30);
 }
+// The tile parse's compact word (lane shape): SID_CLS_COMPACT set and the
+// position's offset (0..127) from its wave's reference line in bits 20-26;
+// the chrom (at most 8 bytes) and the reference position are the wave's
+// entry (tile_wave_store), so the site needs no header pair (the slot's 4 B
+// instead of 20 B, each way).  No compact word is SID_CLS_MISS: k < 0xFFFFF.
+constexpr uint32_t SID_CLS_COMPACT = 1u << 27;
+constexpr uint32_t SID_CLS_DPOS = 128;   // offsets 0 .. 127
+static_assert(SID_TAB_N + SID_TAB2_N < 0xFFFFFu, "a compact word never equals SID_CLS_MISS");
+__device__ __forceinline__ bool cls_compact(uint32_t w) { return (w & SID_CLS_COMPACT) && w != SID_CLS_MISS; }
 
 // The site's record length (0: a fix-up site, listed in LL.miss; a record
 // is never empty) and its class word into LL.cls[i]
@@ -1658,15 +1667,23 @@ __device__ __forceinline__ uint32_t local_word(uint32_t k, uint32_t f, uint32_t 
 // C5's parse 11.41 -> 11.28 ms per step, but cost more than it saved beside
 // quad_head: 11.19 with it, 11.03 without; for the lane shape, 2 KiB of the
 // ~30x profiles: C2 parse 1.79 -> 1.92 ms.)
-template <bool LIST = true>   // LIST: a fix-up site listed in LL.miss (else the caller fixes it up)
-__device__ __forceinline__ int local_site_tail(uint64_t c, uint64_t i, const uint8_t* L1, const LocalLen& LL)
+// the class word and tail length alone (-1 and SID_CLS_MISS: a fix-up site)
+__device__ __forceinline__ int local_site_word(uint64_t c, const uint8_t* L1, const LocalLen& LL, uint32_t* w)
 {
     uint32_t f, s, nf, ns, cov;
     sid_major(c, f, s, nf, ns, cov);
     const uint32_t k = local_entry(nf, ns, cov - nf - ns);
     const uint32_t L = k < SID_TAB_N ? L1[k] : k != UINT32_MAX ? LL.len2[k - SID_TAB_N] : 0xFFu;
-    const bool miss = L == 0xFFu;
-    LL.cls[i] = miss ? SID_CLS_MISS : local_word(k, f, s);   // (read back by the writer soon: through the caches)
+    *w = L == 0xFFu ? SID_CLS_MISS : local_word(k, f, s);
+    return L == 0xFFu ? -1 : (int)L;
+}
+template <bool LIST = true>   // LIST: a fix-up site listed in LL.miss (else the caller fixes it up)
+__device__ __forceinline__ int local_site_tail(uint64_t c, uint64_t i, const uint8_t* L1, const LocalLen& LL)
+{
+    uint32_t w;
+    const int L = local_site_word(c, L1, LL, &w);
+    const bool miss = L < 0;
+    LL.cls[i] = w;   // (read back by the writer soon: through the caches)
     if (miss) {
         if (LIST) LL.miss[atomicAdd(LL.nmiss, 1ull)] = (uint32_t)i;   // its bytes: the fix-up's
         return -1;
@@ -1814,6 +1831,8 @@ struct TileOut {
     unsigned long long* lb;     // [6] fallback count (zeroed before); [3] sites and [5] the most lines in a
                                 //   tile from tcnt (sid_tile_serial_kernel)
     uint64_t* state;            // [4] the chunk's parse error key: none yet
+    ulonglong2* twv;            // -m local, lane shape: per tile nwv wave entries (tile_wave_store), entry
+    uint32_t nwv;               //   j / 64 for the tile's slot j
 };
 
 // a slot's chrom and position from its header pair (the tile parse's layout)
@@ -1838,10 +1857,17 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
 // local's class word and record length, returned; the Lynch paths' counts),
 // or its slot and offset listed for the general routine.  (The quad shape:
 // quad_head, then quad_line.)
+// -m local's lines with a valid header pair, a chrom of at most 8 bytes and a
+// tabulated class leave their slot words to the wave (tile_wave_store): ws.
+struct LaneSlot {
+    uint64_t h0 = 0, h1 = 0;   // the header pair
+    uint32_t w = 0;            // the class word
+    bool elig = false;         // the words are the wave's to store
+};
 template <bool LOCAL, class Ld>
 __device__ __forceinline__ int tile_line(const char* __restrict__ text, const char* tl, Ld ld, uint64_t g0, uint32_t r0,
                                          uint64_t g, uint32_t len_t, uint64_t c1, const uint8_t* cls,
-                                         const uint32_t* rbl, const TileOut& O, const LocalLen& LL)
+                                         const uint32_t* rbl, const TileOut& O, const LocalLen& LL, LaneSlot& ws)
 {
     int l = 0;
     const uint64_t s0 = g0 + r0;
@@ -1860,14 +1886,25 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
         const bool hv = (h[0] >> 63) != 0;
         const uint32_t clen = (uint32_t)(h[0] >> 32) & 0xFFFu;
         if (!hv || clen > 8) h[1] = (uint32_t)s0;   // the writer reads the chrom, or tokenises, from the line
+        Head hd;
+        hd.clen = clen;
+        hd.pos = (int32_t)(uint32_t)h[0];
+        if (LOCAL && hv && clen <= 8) {
+            uint32_t w;
+            const int L = local_site_word(c, LL.len1, LL, &w);
+            if (L >= 0) {   // (a fix-up site: stored here, below)
+                ws.h0 = h[0];
+                ws.h1 = h[1];
+                ws.w = w;
+                ws.elig = true;
+                return local_rec_len(hd, (uint32_t)L);
+            }
+        }
         ST_MID(O.hdr + 2 * g, h[0]);
         ST_MID(O.hdr + 2 * g + 1, h[1]);
         if (!LOCAL) {
             ST_MID(O.counts + g, c);
         } else if (hv) {
-            Head hd;
-            hd.clen = clen;
-            hd.pos = (int32_t)(uint32_t)h[0];
             l = local_site_len(hd, c, g, LL.len1, LL);
         } else {   // position not a plain 1-9 digit run: the formatter's tokeniser
             l = local_site_len_text(text, c1, s0, c, g, LL);
@@ -1879,6 +1916,34 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
         O.fbo[k] = (uint32_t)s0;
     }
     return l;
+}
+
+// The wave's deferred slot words (converged lanes, slot g): the lowest lane
+// with words is the wave's reference, its chrom and position the wave's entry
+// (*e); a lane of the same chrom within SID_CLS_DPOS positions after it
+// stores only its compact class word, the others the class word and the
+// header pair
+__device__ __forceinline__ void tile_wave_store(const LaneSlot& ws, uint64_t g, ulonglong2* e, const TileOut& O,
+                                                const LocalLen& LL)
+{
+    const uint64_t em = __ballot(ws.elig);
+    if (em == 0) return;   // (wave-uniform)
+    const int r = __builtin_ctzll(em);
+    const uint32_t c8lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ws.h1, r);
+    const uint32_t c8hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ws.h1 >> 32), r);
+    const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ws.h0, r);
+    const uint32_t cl0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ws.h0 >> 32), r) & 0xFFFu;
+    const uint64_t c8 = c8lo | ((uint64_t)c8hi << 32);
+    const uint32_t dp = (uint32_t)ws.h0 - p0;
+    const bool cmp = ws.elig && ws.h1 == c8 && (((uint32_t)(ws.h0 >> 32) & 0xFFFu) == cl0) && dp < SID_CLS_DPOS;
+    if ((int)(threadIdx.x & 63u) == r) *e = make_ulonglong2(c8, (uint64_t)p0 | ((uint64_t)cl0 << 32));
+    if (cmp) {
+        LL.cls[g] = ws.w | SID_CLS_COMPACT | (dp << 20);
+    } else if (ws.elig) {
+        LL.cls[g] = ws.w;
+        ST_MID(O.hdr + 2 * g, ws.h0);
+        ST_MID(O.hdr + 2 * g + 1, ws.h1);
+    }
 }
 
 // The quad shape in two steps.  A line's header is the same work in each of
@@ -2155,7 +2220,13 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         // into the writer blocks' sums: a wave's slots (64, or 16 with quads,
         // from a multiple of 16) lie in one block or two
         auto bsum_add = [&](uint32_t wslot0, uint32_t j, int l) {
+            wslot0 = __builtin_amdgcn_readfirstlane(wslot0);
             const uint64_t gw = (g_tile + wslot0) / FTB;
+            if ((g_tile + wslot0 + 63) / FTB == gw) {   // (most waves: their slots in one block, one sum)
+                const uint32_t s = wave_sum((uint32_t)l);
+                if ((tid & 63u) == 0 && s) atomicAdd(LL.bsum + gw, s);
+                return;
+            }
             const uint32_t lo = (g_tile + j) / FTB == gw ? (uint32_t)l : 0u;
             const uint32_t slo = wave_sum(lo), shi = wave_sum((uint32_t)l - lo);
             if ((tid & 63u) == 0 && slo) atomicAdd(LL.bsum + gw, slo);
@@ -2189,8 +2260,12 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             for (uint32_t j0 = 0; j0 < cnt; j0 += LPR) {   // block-uniform trip count
                 const uint32_t j = j0 + tid;
                 int l = 0;
-                if (j < cnt) l = tile_line<LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, cls, rbl, O, LL);
-                if constexpr (LOCAL) bsum_add(j0 + (tid & ~63u), j, l);
+                LaneSlot ws;
+                if (j < cnt) l = tile_line<LOCAL>(text, tl, ld, g0, ls[j], g_tile + j, len_t, c1, cls, rbl, O, LL, ws);
+                if constexpr (LOCAL) {
+                    tile_wave_store(ws, g_tile + j, O.twv + t * O.nwv + ((j0 + (tid & ~63u)) >> 6), O, LL);
+                    bsum_add(j0 + (tid & ~63u), j, l);
+                }
             }
         }
 #ifdef SID_TP_STAMP
@@ -2335,6 +2410,10 @@ static SlotDiv slot_div(uint32_t cap)
     return SlotDiv{(uint32_t)(((1ull << (32 + s)) + cap - 1) / cap), s};
 }
 __device__ __forceinline__ uint32_t slot_tile(uint32_t g, SlotDiv d) { return __umulhi(g, d.m) >> d.s; }
+// the wave entries of a tile of cap slots (tile_wave_store): at most slots / 32
+// of them a chunk, as cap >= SID_TILE_CAP_MIN = 64 (sid_chunk_reserve)
+static uint32_t tile_nwv(uint32_t cap) { return (cap + 63) / 64; }
+static_assert(SID_TILE_CAP_MIN >= 64, "a tile's wave entries: at most two per 64 slots");
 constexpr uint64_t SID_SLOTS_MAX = 1ull << 28;
 
 // The tile parse's sites into file order (the Lynch paths' kept parse,
@@ -2647,13 +2726,15 @@ __device__ __noinline__ void miss_put(const char* text, uint64_t len, Head h, ui
 // their counts (the entry and the bases come with the word).  tcnt (the tile
 // parse's layout): n slots, slot i a site when i mod 2^cap_log2 is below its
 // tile's count, chrom and position by slot_head
-template <bool CLS>
+// WV: the slots' compact words and wave entries (the lane-shape tile parse,
+// tile_wave_store); else every slot's header pair
+template <bool CLS, bool WV = false>
 __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const char* __restrict__ text, uint64_t len,
                                                            const sid_off_t* __restrict__ starts,
                                                            const uint64_t* __restrict__ hdr, uint64_t n,
                                                            const uint32_t* __restrict__ tcnt, uint32_t cap,
-                                                           SlotDiv cdiv,
-                                                           const uint64_t* __restrict__ counts,
+                                                           SlotDiv cdiv, const ulonglong2* __restrict__ twv,
+                                                           uint32_t nwv, const uint64_t* __restrict__ counts,
                                                            const uint32_t* __restrict__ cwords,
                                                            const char* __restrict__ str1,
                                                            const char* __restrict__ str2,
@@ -2683,13 +2764,23 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     bool site = i < n;
     // the slot's class word and header pair loaded beside its tile's count
     // (a slot that holds no site: allocated, its words never used)
+    // (a compact word: no header pair, the chrom and the position from its
+    // wave's entry, loaded beside the word -- one address for most of a wave)
     uint32_t w0 = 0;
-    ulonglong2 hw0 = make_ulonglong2(0, 0);
+    ulonglong2 hw0 = make_ulonglong2(0, 0), te = hw0;
+    bool cw = false;
     if (tcnt && site) {   // slot i = tile * cap + j: a site when j is below the tile's count
+        // (without wave entries (the quad shape) every slot's header pair,
+        // loaded beside the word -- loaded after it, C5's writer took 1.16
+        // ms for 1.08)
         if (CLS) w0 = cwords[i];
-        hw0 = *(const ulonglong2*)(hdr + 2 * i);
+        if (!WV) hw0 = *(const ulonglong2*)(hdr + 2 * i);
         const uint32_t t = slot_tile((uint32_t)i, cdiv);   // (i < SID_SLOTS_MAX)
-        site = (uint32_t)i - t * cap < tcnt[t];
+        const uint32_t j = (uint32_t)i - t * cap;
+        if (WV) te = twv[(uint64_t)t * nwv + (j >> 6)];
+        site = j < tcnt[t];
+        cw = WV && cls_compact(w0);
+        if (WV && site && !cw) hw0 = *(const ulonglong2*)(hdr + 2 * i);
     }
     if (site) {
         uint32_t k;
@@ -2706,7 +2797,12 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         // (the record tail's load issued before the header pair's was
         // measured slower here: 0.88-0.89 vs 0.86-0.87 ms per C2 step; in
         // the Lynch writer, which looks the class up first, it pays)
-        {
+        if (cw) {
+            h.clen = (uint32_t)(te.y >> 32) & 0xFFFu;
+            h.pos = (int32_t)((uint32_t)te.y + ((w0 >> 20) & (SID_CLS_DPOS - 1)));
+            h.c8 = te.x;
+            h.cb = 0;
+        } else {
             Reader R{text, len};
             h = tcnt ? slot_head(R, hw0) : site_head(R, starts + i, hdr + 2 * i);
         }
@@ -3727,10 +3823,12 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
     if (sites > W->site_cap) {
         const uint64_t m = std::max<uint64_t>(sites, W->site_cap + W->site_cap / 2);
         for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
-                        (void*)W->bsum, (void*)W->boff, (void*)W->hdr, (void*)W->fb, (void*)W->lb, (void*)W->cls})
+                        (void*)W->bsum, (void*)W->boff, (void*)W->hdr, (void*)W->fb, (void*)W->lb, (void*)W->cls,
+                        (void*)W->twv})
             if (p) (void)hipFree(p);
         W->lb = nullptr;
         W->cls = nullptr;
+        W->twv = nullptr;
         W->starts = nullptr;
         W->counts = W->hdr = nullptr;
         W->fb = nullptr;
@@ -3744,6 +3842,7 @@ int sid_chunk_reserve(sid_chunk_ws* W, uint64_t bytes, uint64_t sites)
         WCHECK(hipMalloc(&W->counts, m * 8));
         WCHECK(hipMalloc(&W->cls, m * 4));
         WCHECK(hipMalloc(&W->hdr, m * 16));
+        WCHECK(hipMalloc(&W->twv, (m / 32 + 1) * 16));   // the tile parse's wave entries (tile_nwv)
         WCHECK(hipMalloc(&W->fb, m * 12));   // three site lists (sid_chunk_ws::fb)
         WCHECK(hipMalloc(&W->code, m));
         WCHECK(hipMalloc(&W->hom, m * 8));
@@ -3760,7 +3859,7 @@ void sid_chunk_release(sid_chunk_ws* W)
 {
     for (void* p : {(void*)W->starts, (void*)W->counts, (void*)W->code, (void*)W->hom, (void*)W->het,
                     (void*)W->bsum, (void*)W->boff, (void*)W->tcnt, (void*)W->toff, (void*)W->state,
-                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb, (void*)W->cls})
+                    (void*)W->hdr, (void*)W->fb, (void*)W->masks, (void*)W->lb, (void*)W->cls, (void*)W->twv})
         if (p) (void)hipFree(p);
     *W = sid_chunk_ws{};
 }
@@ -3936,10 +4035,10 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
                                  ? SID_OK : SID_EHIP;
         if (W->slots >= SID_SLOTS_MAX) return SID_EINVAL;   // (slot_tile's exact range: a 4 GiB chunk has fewer)
         const SlotDiv cdiv = slot_div(W->slot_cap);
-        sid_local_put_kernel<true><<<(unsigned)nbs, FTB, 0, st>>>(base, c1, nullptr, W->hdr, W->slots, W->tcnt,
-                                                                 W->slot_cap, cdiv, W->counts, W->cls, ctx->ws.str1,
-                                                                 ctx->ws.str2, W->code, W->hom, W->het, ct, W->boff,
-                                                                 W->state, W->lb, out);
+        auto put = W->tile_quad ? sid_local_put_kernel<true, false> : sid_local_put_kernel<true, true>;
+        put<<<(unsigned)nbs, FTB, 0, st>>>(base, c1, nullptr, W->hdr, W->slots, W->tcnt, W->slot_cap, cdiv, W->twv,
+                                           tile_nwv(W->slot_cap), W->counts, W->cls, ctx->ws.str1, ctx->ws.str2,
+                                           W->code, W->hom, W->het, ct, W->boff, W->state, W->lb, out);
         WCHECK(hipGetLastError());
 #ifdef SID_TP_STAMP
         {
@@ -3961,12 +4060,12 @@ int sid_chunk_local_put(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64_
                             ? SID_OK : SID_EHIP;
     if (W->cls_ready)
         sid_local_put_kernel<true><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0, SlotDiv{0, 0},
-                                                                W->counts, W->cls,
+                                                                nullptr, 0, W->counts, W->cls,
                                                                 ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
                                                                 ct, W->boff, W->state, W->lb, out);
     else
-        sid_local_put_kernel<false><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0, SlotDiv{0, 0},
-                                                                 W->counts, nullptr,
+        sid_local_put_kernel<false><<<(unsigned)nb, FTB, 0, st>>>(base, c1, W->starts, W->hdr, n, nullptr, 0,
+                                                                 SlotDiv{0, 0}, nullptr, 0, W->counts, nullptr,
                                                                  ctx->ws.str1, ctx->ws.str2, W->code, W->hom, W->het,
                                                                  ct, W->boff, W->state, W->lb, out);
     WCHECK(hipGetLastError());
@@ -4034,10 +4133,12 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
     const uint64_t ntp = tile_count(c0, c1, quad);
     const uint64_t slots = ntp * cap;
     if (slots > W->site_cap || ntp > W->tile_cap || slots >= (1ull << 32)) return SID_EINVAL;
+    if (ntp * tile_nwv(cap) > W->site_cap / 32 + 1) return SID_EINVAL;   // (never: cap >= 64)
     W->lens_ready = false;
     W->cls_ready = false;
     W->slot_cap = cap;
     W->slots = slots;
+    W->tile_quad = quad;   // (the quad shape stores no compact words: the writer reads every header pair)
     const uint64_t nb = (slots + FTB - 1) / FTB;
     WCHECK(hipMemsetAsync(W->lb, 0, 8 * 8, st));   // [0] fix-up sites [1] bytes [2] range [3] sites [5] max lines [6] [7]
     if (nb) WCHECK(hipMemsetAsync(W->bsum, 0, nb * 4, st));
@@ -4047,7 +4148,7 @@ int sid_chunk_tile_local(sid_ctx* ctx, sid_chunk_ws* W, const char* base, uint64
     }
     uint32_t* miss = W->fb + 2 * W->site_cap;
     const LocalLen LL{ctx->ws.len1, ctx->ws.len2, W->bsum, miss, W->lb, W->cls};
-    const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
+    const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state, W->twv, tile_nwv(cap)};
     launch_tile_parse<true>(quad, base, c0, c1, ntp, O, LL, st);
     const LocalFix F{LL, ctx->K, ctx->d_lnt, ct, W->code, W->hom, W->het};
     sid_tile_serial_kernel<true><<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp,
@@ -4079,7 +4180,7 @@ int sid_chunk_tile_counts(sid_chunk_ws* W, const char* base, uint64_t c0, uint64
         return SID_OK;
     }
     const LocalLen LL{};
-    const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state};
+    const TileOut O{cap, W->tcnt, W->hdr, W->counts, W->fb, W->starts, W->lb, W->state, nullptr, 0};
     launch_tile_parse<false>(quad, base, c0, c1, ntp, O, LL, st);
     sid_tile_serial_kernel<false><<<TILE_SERIAL_GRID, TB, 0, st>>>(base, c1, W->fb, W->starts, W->lb, W->tcnt, ntp,
                                                       cap, W->counts, W->hdr,

@@ -698,3 +698,41 @@ def test_tile_parse_recovers_on_a_reused_engine(sid, oracle, tmp_path):
                 assert st.chunks_tiled >= tail, (st.chunks, st.chunks_tiled, tail)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("extra", [[], ["--chunk-bytes", "150000", "--devices", "2"]], ids=["one-chunk", "150k-2dev"])
+def test_tile_compact_words_edges(sid, oracle, tmp_path, extra):
+    """The lane-shape tile parse's compact class words (textpath.hip
+    tile_wave_store: a site of its wave's reference chrom within 127
+    positions after the reference line stores 4 B, the chrom and position
+    coming from the wave's entry): position steps of 1, 126, 127, 128 and
+    10^5 inside a wave, positions going backwards, 10-digit positions (no
+    valid header pair), chroms changing every few lines with names of 1, 7, 8
+    and 9 bytes (8: the longest a header pair holds), and indel lines (the
+    general routine) as a wave's first lines, so its reference is a later
+    lane.  Every run's CSV is the oracle's."""
+    rng = np.random.default_rng(67)
+    alphabet = np.frombuffer(b"ACGTacgt.,", np.uint8)
+    names = [b"c", b"chr12ab", b"chrom_08", b"chrom_009", b"chr1"]
+    steps = [1, 1, 1, 126, 127, 128, 1, 1, 10 ** 5, -5, 1, -300, 2]
+    out, pos, chrom = [], 1, names[0]
+    for i in range(24_000):
+        if i % 37 == 0 or (i % 4096 < 128 and i % 11 == 0):
+            chrom = names[int(rng.integers(0, len(names)))]
+        pos = max(1, pos + steps[int(rng.integers(0, len(steps)))])
+        p = pos if i % 97 else 10 ** 9 + i   # (10 digits: the writer tokenises the line)
+        d = int(rng.integers(20, 40))
+        b = bytearray(rng.choice(alphabet, d).tobytes())
+        if i % 64 < 2 and i % 3 == 0:
+            b[d // 2:d // 2] = b"-1A"   # a wave's first lines through the general routine
+        out.append(b"%s\t%d\tA\t%d\t%s\t%s\n" % (chrom, p, d, bytes(b), b"I" * len(b)))
+    text = b"".join(out)
+    f = tmp_path / "compact.plp"
+    f.write_bytes(text)
+    b = oracle.run_cli([str(f)])
+    a = run(sid.CLI_PATH, ["--stats"] + extra + [str(f)])
+    assert b.returncode == 0
+    assert a.returncode == 0, a.stderr[-400:]
+    assert a.stdout == b.stdout
+    st = json.loads(a.stderr.splitlines()[-1])
+    assert st["chunks_tiled"] >= max(1, st["chunks"] - 1), st   # (through the tile parse)
