@@ -1061,7 +1061,11 @@ __device__ __forceinline__ int parse_header(const uint4 v0, const uint4 v1, cons
     const uint64_t nd = (uint64_t)not_digit(plo) | ((uint64_t)not_digit(phi) << 32);
     const uint64_t inl = L8 >= 8 ? ~0ull : ((1ull << (8 * L8)) - 1);
     const uint32_t d9 = (uint32_t)(uint8_t)stage[sh + t1 + 8] - '0';
-    const bool pos_ok = lp >= 1 && lp <= 9 && (nd & inl) == 0 && (lp < 9 || d9 < 10u);
+    // (a leading zero: the position's digits then differ from its printed
+    // ones -- the formatter's tokeniser takes it, so a valid pair's digit
+    // count is the printed position's, sid_i32_len)
+    const bool lz = lp > 1 && (plo & 0xFFu) == '0';
+    const bool pos_ok = !lz && lp >= 1 && lp <= 9 && (nd & inl) == 0 && (lp < 9 || d9 < 10u);
     // digit values (garbage above the digits only borrows upward, then shifts out)
     const uint64_t dv = ((uint64_t)(phi - 0x30303030u) << 32) | (plo - 0x30303030u);
     const uint64_t dz = L8 == 0 ? 0 : dv << ((8 * (8 - L8)) & 63);
@@ -1072,8 +1076,9 @@ __device__ __forceinline__ int parse_header(const uint4 v0, const uint4 v1, cons
                         __builtin_amdgcn_udot4(q1, 0x010A0000u, 0u, false);
     uint32_t pos = __umul24(h4, 10000u) + l4;
     if (lp == 9) pos = pos * 10u + d9;
-    // chrom (offset, length) and position for the formatter (bit 63: valid)
-    hdr[0] = pos_ok ? (1ull << 63) | ((uint64_t)t0 << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
+    // chrom (offset: bits 44-58, length: 32-43), position (0-31) and its
+    // digits (59-62) for the formatter (bit 63: valid)
+    hdr[0] = pos_ok ? (1ull << 63) | ((uint64_t)lp << 59) | ((uint64_t)t0 << 44) | ((uint64_t)l0 << 32) | pos : 0ull;
     // the chrom's first 8 bytes: the formatter then never reads the text for
     // names up to 8 bytes (reading them back fetched every line's cache lines)
     const uint64_t c8 = stage_u64(stage, sh + t0) & (l0 >= 8 ? ~0ull : ((1ull << (8 * l0)) - 1));
@@ -1303,7 +1308,7 @@ __device__ __forceinline__ Head site_head_hw(Reader& R, const Off* startp, const
         h.clen = (uint32_t)(hw.x >> 32) & 0xFFFu;
         h.pos = (int32_t)(uint32_t)hw.x;
         h.c8 = h.clen <= 8 ? hw.y : 0;
-        h.cb = (h.c8 || h.clen == 0) ? 0 : *startp + ((hw.x >> 44) & 0x7FFFFull);
+        h.cb = (h.c8 || h.clen == 0) ? 0 : *startp + ((hw.x >> 44) & 0x7FFFull);
         return h;
     }
     uint64_t q = *startp;
@@ -1843,7 +1848,7 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
         h.clen = (uint32_t)(hw.x >> 32) & 0xFFFu;
         h.pos = (int32_t)(uint32_t)hw.x;
         h.c8 = h.clen <= 8 ? hw.y : 0;
-        h.cb = h.clen <= 8 ? 0 : (uint64_t)(uint32_t)hw.y + ((hw.x >> 44) & 0x7FFFFull);
+        h.cb = h.clen <= 8 ? 0 : (uint64_t)(uint32_t)hw.y + ((hw.x >> 44) & 0x7FFFull);
         return h;
     }
     const uint64_t s0 = (uint32_t)hw.y;
@@ -1862,6 +1867,7 @@ __device__ __forceinline__ Head slot_head(Reader& R, const ulonglong2 hw)
 struct LaneSlot {
     uint64_t h0 = 0, h1 = 0;   // the header pair
     uint32_t w = 0;            // the class word
+    uint32_t pl = 0;           // the position's digits
     bool elig = false;         // the words are the wave's to store
 };
 template <bool LOCAL, class Ld>
@@ -1896,8 +1902,9 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
                 ws.h0 = h[0];
                 ws.h1 = h[1];
                 ws.w = w;
+                ws.pl = (uint32_t)(h[0] >> 59) & 15u;   // (parse_header: the printed digits)
                 ws.elig = true;
-                return local_rec_len(hd, (uint32_t)L);
+                return (int)(clen + ws.pl + 9 + (uint32_t)L);   // (local_rec_len)
             }
         }
         ST_MID(O.hdr + 2 * g, h[0]);
@@ -1922,7 +1929,14 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
 // with words is the wave's reference, its chrom and position the wave's entry
 // (*e); a lane of the same chrom within SID_CLS_DPOS positions after it
 // stores only its compact class word, the others the class word and the
-// header pair
+// header pair.  The entry: the chrom's 8 bytes; the position p0, the chrom's
+// length (bits 32-43), p0's digits n (44-47) and the offsets from p0 where
+// the digits grow, 10^n - p0 and 10^(n+1) - p0 (48-55, 56-63; 255: not below
+// SID_CLS_DPOS), so the writer counts a compact site's digits in 4
+// instructions (wave_pos_digits)
+__device__ constexpr uint64_t k_pow10[16] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull,
+                                              10000000ull, 100000000ull, 1000000000ull, 10000000000ull,
+                                              100000000000ull, 0, 0, 0, 0};
 __device__ __forceinline__ void tile_wave_store(const LaneSlot& ws, uint64_t g, ulonglong2* e, const TileOut& O,
                                                 const LocalLen& LL)
 {
@@ -1933,10 +1947,17 @@ __device__ __forceinline__ void tile_wave_store(const LaneSlot& ws, uint64_t g, 
     const uint32_t c8hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ws.h1 >> 32), r);
     const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ws.h0, r);
     const uint32_t cl0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ws.h0 >> 32), r) & 0xFFFu;
+    const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)ws.pl, r);
     const uint64_t c8 = c8lo | ((uint64_t)c8hi << 32);
     const uint32_t dp = (uint32_t)ws.h0 - p0;
     const bool cmp = ws.elig && ws.h1 == c8 && (((uint32_t)(ws.h0 >> 32) & 0xFFFu) == cl0) && dp < SID_CLS_DPOS;
-    if ((int)(threadIdx.x & 63u) == r) *e = make_ulonglong2(c8, (uint64_t)p0 | ((uint64_t)cl0 << 32));
+    if ((int)(threadIdx.x & 63u) == r) {
+        const uint64_t p10 = k_pow10[n0 & 15u];   // (n0 <= 9: a valid pair's position has at most 9 digits)
+        const uint64_t d1 = p10 - p0, d2 = 10u * p10 - p0;
+        const uint64_t y = (uint64_t)p0 | ((uint64_t)cl0 << 32) | ((uint64_t)n0 << 44) |
+                           ((d1 < SID_CLS_DPOS ? d1 : 255ull) << 48) | ((d2 < SID_CLS_DPOS ? d2 : 255ull) << 56);
+        *e = make_ulonglong2(c8, y);
+    }
     if (cmp) {
         LL.cls[g] = ws.w | SID_CLS_COMPACT | (dp << 20);
     } else if (ws.elig) {
@@ -2769,6 +2790,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
     uint32_t w0 = 0;
     ulonglong2 hw0 = make_ulonglong2(0, 0), te = hw0;
     bool cw = false;
+    int pl = 0;   // the position's digits (sid_i32_len)
     if (tcnt && site) {   // slot i = tile * cap + j: a site when j is below the tile's count
         // (without wave entries (the quad shape) every slot's header pair,
         // loaded beside the word -- loaded after it, C5's writer took 1.16
@@ -2797,14 +2819,17 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         // (the record tail's load issued before the header pair's was
         // measured slower here: 0.88-0.89 vs 0.86-0.87 ms per C2 step; in
         // the Lynch writer, which looks the class up first, it pays)
-        if (cw) {
-            h.clen = (uint32_t)(te.y >> 32) & 0xFFFu;
-            h.pos = (int32_t)((uint32_t)te.y + ((w0 >> 20) & (SID_CLS_DPOS - 1)));
+        if (cw) {   // (the entry: tile_wave_store)
+            const uint32_t dp = (w0 >> 20) & (SID_CLS_DPOS - 1), m = (uint32_t)(te.y >> 32);
+            h.clen = m & 0xFFFu;
+            h.pos = (int32_t)((uint32_t)te.y + dp);
             h.c8 = te.x;
             h.cb = 0;
+            pl = (int)(((m >> 12) & 15u) + (dp >= ((m >> 16) & 255u)) + (dp >= (m >> 24)));
         } else {
             Reader R{text, len};
             h = tcnt ? slot_head(R, hw0) : site_head(R, starts + i, hdr + 2 * i);
+            pl = tcnt && (hw0.x >> 63) ? (int)((hw0.x >> 59) & 15u) : sid_i32_len(h.pos);   // (parse_header's digits)
         }
         if (k != UINT32_MAX) {
             const uint4* e = (const uint4*)(k < SID_TAB_N ? str1 + (size_t)k * SID_STR_BYTES
@@ -2816,7 +2841,7 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         if (tab) {
             const bool het_l = (ea.x >> 8) & 1u;
             c = (uint8_t)(f | ((het_l ? s : f) << 2) | (het_l ? 0x80u : 0u));
-            l = local_rec_len(h, ea.x & 0xFFu);
+            l = (int)h.clen + pl + 9 + (int)(ea.x & 0xFFu);   // (local_rec_len)
         } else {   // the fix-up's site
             c = code[i];
             l = miss_len(h, c, hom[i], het[i], ct);
@@ -2839,7 +2864,6 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         // instead of 11, measured slower: writer 0.947 vs 0.930 ms per C2 step)
         const uint64_t c8[1] = {h.c8};
         lds_or_run<1>(B, my, c8);
-        const int pl = sid_i32_len(h.pos);
         uint64_t pv[2];
         comma_num_comma((uint32_t)h.pos, pl, pv[0], pv[1]);
         const uint32_t q1 = my + h.clen;

@@ -706,8 +706,8 @@ def test_tile_compact_words_edges(sid, oracle, tmp_path, extra):
     tile_wave_store: a site of its wave's reference chrom within 127
     positions after the reference line stores 4 B, the chrom and position
     coming from the wave's entry): position steps of 1, 126, 127, 128 and
-    10^5 inside a wave, positions going backwards, 10-digit positions (no
-    valid header pair), chroms changing every few lines with names of 1, 7, 8
+    10^5 inside a wave, positions going backwards, 10-digit positions and
+    zero-padded ones (no valid header pair: tokenised), chroms changing every few lines with names of 1, 7, 8
     and 9 bytes (8: the longest a header pair holds), and indel lines (the
     general routine) as a wave's first lines, so its reference is a later
     lane.  Every run's CSV is the oracle's."""
@@ -720,12 +720,14 @@ def test_tile_compact_words_edges(sid, oracle, tmp_path, extra):
         if i % 37 == 0 or (i % 4096 < 128 and i % 11 == 0):
             chrom = names[int(rng.integers(0, len(names)))]
         pos = max(1, pos + steps[int(rng.integers(0, len(steps)))])
-        p = pos if i % 97 else 10 ** 9 + i   # (10 digits: the writer tokenises the line)
+        p = b"%d" % (pos if i % 97 else 10 ** 9 + i)   # (10 digits: the writer tokenises the line)
+        if i % 53 == 0:
+            p = b"%07d" % pos   # (leading zeros: printed without them, tokenised too)
         d = int(rng.integers(20, 40))
         b = bytearray(rng.choice(alphabet, d).tobytes())
         if i % 64 < 2 and i % 3 == 0:
             b[d // 2:d // 2] = b"-1A"   # a wave's first lines through the general routine
-        out.append(b"%s\t%d\tA\t%d\t%s\t%s\n" % (chrom, p, d, bytes(b), b"I" * len(b)))
+        out.append(b"%s\t%s\tA\t%d\t%s\t%s\n" % (chrom, p, d, bytes(b), b"I" * len(b)))
     text = b"".join(out)
     f = tmp_path / "compact.plp"
     f.write_bytes(text)
