@@ -2083,7 +2083,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     constexpr uint32_t TP_HALO = tp_halo(QUAD);
     static_assert(TP_HALO % 1024 == 0 && TP_HALO / 16 <= TB, "the halo loaded by whole waves, a window a lane");
     __shared__ __attribute__((aligned(16))) char tl[TP_TILE + TP_HALO + 64];
-    __shared__ uint16_t ls[tp_cap_max(QUAD)];
+    __shared__ uint16_t ls[tp_cap_max(QUAD) + TB];   // (+ a dummy slot per thread: the index's absent starts)
     __shared__ uint8_t cls[256];
     __shared__ uint32_t rbl[256];
     __shared__ uint32_t wtot[TB / 64][NW];
@@ -2216,9 +2216,15 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             const uint32_t sh = 10 * (k % 3), w = k / 3;
             const uint32_t before = (((k % 3) == 1 ? bB[w] : bA[w]) >> sh) & 4095u;
             const uint32_t total = (((k % 3) == 1 ? tB[w] : tA[w]) >> sh) & 4095u;
-            uint32_t q = nlines + before + (((incl[w] - packed[w]) >> sh) & 1023u);
-            for (uint32_t mk = m[k]; mk; mk &= mk - 1, ++q)
-                if (q < cap) ls[q] = (uint16_t)(k * TILE + tid * 16 + (uint32_t)(__ffs(mk) - 1));
+            const uint32_t q = nlines + before + (((incl[w] - packed[w]) >> sh) & 1023u);
+            // the window's first start written unconditionally (to the
+            // thread's dummy slot when absent or past the cap), the rest --
+            // lines under 16 B -- one by one: no exec-masked loop per window
+            const uint32_t mk = m[k], off = k * TILE + tid * 16, dummy = tp_cap_max(QUAD) + tid;
+            ls[mk && q < cap ? q : dummy] = (uint16_t)(off + (uint32_t)__builtin_ctz(mk | 0x10000u));
+            uint32_t q2 = q + 1;
+            for (uint32_t r = mk & (mk - 1); r; r &= r - 1, ++q2)
+                if (q2 < cap) ls[q2] = (uint16_t)(off + (uint32_t)(__ffs(r) - 1));
             nlines += total;
         }
         const uint32_t cnt = min(nlines, cap);
