@@ -1498,41 +1498,48 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v)
 // the block's records, assembled at buf[0, tot), to dst (any alignment):
 // destination window k covers dst - phase + 16k; the inner windows read two
 // aligned LDS quads and shift them by the block-uniform (-phase) & 15 bytes
-template <bool SWZ = false>
-__device__ __forceinline__ void block_store(const char* buf, uint32_t tot, char* __restrict__ dst0)
+// (QW words and R bytes): one copy of the loop per QW, so no lane selects
+// the words (15 v_cndmask a window when QW was a variable)
+template <bool SWZ, uint32_t QW>
+__device__ __forceinline__ void block_store_q(const char* buf, uint32_t phase, uint32_t span, uint32_t r,
+                                              char* __restrict__ dst)
 {
     // SWZ: buf's quads are swizzled as swz_quad (the -m local writer's buffer)
     auto quad = [](uint32_t Q) { return SWZ ? (Q ^ ((Q >> 3) & 7u)) : Q; };
-    const uint32_t phase = (uint32_t)((uintptr_t)dst0 & 15u);
-    char* dst = dst0 - phase;   // 16-B aligned
-    const uint32_t span = phase + tot;
-    const uint32_t sh = (16u - phase) & 15u, q = sh >> 2, r = sh & 3u;
     const uint4* B = (const uint4*)buf;
     for (uint32_t k = threadIdx.x * 16; k < span; k += FTB * 16) {
         if (k >= phase && k + 16 <= span) {
             const uint32_t a16 = (k - phase) >> 4;   // quad holding byte k - phase
             const uint4 lo = B[quad(a16)], hi = B[quad(a16 + 1)];
-            const uint32_t x0 = q == 0 ? lo.x : q == 1 ? lo.y : q == 2 ? lo.z : lo.w;
-            const uint32_t x1 = q == 0 ? lo.y : q == 1 ? lo.z : q == 2 ? lo.w : hi.x;
-            const uint32_t x2 = q == 0 ? lo.z : q == 1 ? lo.w : q == 2 ? hi.x : hi.y;
-            const uint32_t x3 = q == 0 ? lo.w : q == 1 ? hi.x : q == 2 ? hi.y : hi.z;
-            const uint32_t x4 = q == 0 ? hi.x : q == 1 ? hi.y : q == 2 ? hi.z : hi.w;
-            uint4 v;
-            v.x = __builtin_amdgcn_alignbyte(x1, x0, r);
-            v.y = __builtin_amdgcn_alignbyte(x2, x1, r);
-            v.z = __builtin_amdgcn_alignbyte(x3, x2, r);
-            v.w = __builtin_amdgcn_alignbyte(x4, x3, r);
+            const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
             // streaming (non-temporal) stores: the records are not read again on
             // the device, and kept out of the caches they leave room for the next
             // chunk's text (writer 0.965 -> 0.934 ms and the index behind it
             // 0.975 -> 0.93 ms per C2 step, A/B of builds on one box)
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 nv = {v.x, v.y, v.z, v.w};
+            const u32x4 nv = {__builtin_amdgcn_alignbyte(w[QW + 1], w[QW], r),
+                              __builtin_amdgcn_alignbyte(w[QW + 2], w[QW + 1], r),
+                              __builtin_amdgcn_alignbyte(w[QW + 3], w[QW + 2], r),
+                              __builtin_amdgcn_alignbyte(w[QW + 4], w[QW + 3], r)};
             __builtin_nontemporal_store(nv, (u32x4*)(dst + k));
         } else {
             for (uint32_t j = k; j < k + 16 && j < span; ++j)
                 if (j >= phase) dst[j] = buf[quad((j - phase) >> 4) * 16 + ((j - phase) & 15u)];
         }
+    }
+}
+template <bool SWZ = false>
+__device__ __forceinline__ void block_store(const char* buf, uint32_t tot, char* __restrict__ dst0)
+{
+    const uint32_t phase = (uint32_t)((uintptr_t)dst0 & 15u);
+    char* dst = dst0 - phase;   // 16-B aligned
+    const uint32_t span = phase + tot;
+    const uint32_t sh = (16u - phase) & 15u, r = sh & 3u;
+    switch (sh >> 2) {   // (block-uniform)
+    case 0: block_store_q<SWZ, 0>(buf, phase, span, r, dst); break;
+    case 1: block_store_q<SWZ, 1>(buf, phase, span, r, dst); break;
+    case 2: block_store_q<SWZ, 2>(buf, phase, span, r, dst); break;
+    default: block_store_q<SWZ, 3>(buf, phase, span, r, dst); break;
     }
 }
 
