@@ -763,9 +763,9 @@ constexpr int HDR_BYTES = 48;   // bytes staged per lane for the header (3 align
 // lane's, or the block's padding -- garbage, masked by the caller)
 __device__ __forceinline__ uint64_t stage_u64(const char* stage, uint32_t off)
 {
-    const uint32_t a = off & ~7u, r = off & 7u;
+    const uint32_t a = off & ~7u, sh = 8u * (off & 7u);
     const uint64_t lo = *(const uint64_t*)(stage + a), hi = *(const uint64_t*)(stage + a + 8);
-    return r ? (lo >> (8 * r)) | (hi << (64 - 8 * r)) : lo;
+    return (lo >> sh) | ((hi << 1) << (63u - sh));   // (no lane branch around the second read)
 }
 // bit 7 of each byte of x that is not an ASCII digit
 __device__ __forceinline__ uint32_t not_digit(uint32_t x)
@@ -1041,26 +1041,28 @@ __device__ __forceinline__ int parse_header(const uint4 v0, const uint4 v1, cons
     // the low bytes before token 4 are then the four gaps, which must be ' '
     // or '\t' (a '\n', NUL or other control byte there ends or splits a
     // token differently)
-    bool ok = (N & 1) && t4 < (int)nb && t3 == t2 + 2;
-    ok = ok && __popcll(L & ((1ull << t4) - 1)) == 4;
-    if (!ok) return -1;
-    const uint32_t gaps = (uint32_t)(uint8_t)stage[sh + t1 - 1] | ((uint32_t)(uint8_t)stage[sh + t2 - 1] << 8) |
-                          ((uint32_t)(uint8_t)stage[sh + t2 + 1] << 16) | ((uint32_t)(uint8_t)stage[sh + t4 - 1] << 24);
-    if ((eq_bytes(gaps, 0x20202020u) | eq_bytes(gaps, 0x09090909u)) != 0x80808080u) return -1;
+    // (no early exits: every check folded into ok, the byte reads clamped to
+    // the 48 staged bytes -- each exit was an exec-masked branch and its
+    // own copy of the outputs' defaults)
+    bool ok = ((N & 1) != 0) & (t4 < (int)nb) & (t3 == t2 + 2);
+    ok &= __popcll(L & ((1ull << (t4 & 63)) - 1)) == 4;
+    auto at = [&](int t) { return (uint32_t)(uint8_t)stage[sh + (uint32_t)min(max(t, 0), 47)]; };
+    const uint32_t gaps = at(t1 - 1) | (at(t2 - 1) << 8) | (at(t2 + 1) << 16) | (at(t4 - 1) << 24);
+    ok &= (eq_bytes(gaps, 0x20202020u) | eq_bytes(gaps, 0x09090909u)) == 0x80808080u;
     const int t0 = 0;
     const int l0 = t1 - 1;
     const int lp = t2 - 1 - t1;
-    const uint32_t ref = (uint8_t)stage[sh + t2];
+    const uint32_t ref = at(t2);
     // the position: its first 8 bytes by two aligned 8-B LDS reads and a
     // funnel shift, digit-checked in SWAR, left-padded with zero digits and
     // summed by v_dot4 pairs (10, 1) and two 24-bit multiply-adds; a 9th digit
     // on top (at most 9: < 2^31, as the per-digit loop this replaces)
     const uint32_t L8 = min((uint32_t)lp, 8u);
-    const uint64_t p8 = stage_u64(stage, sh + t1);
+    const uint64_t p8 = stage_u64(stage, sh + (uint32_t)min(max(t1, 0), 47));
     const uint32_t plo = (uint32_t)p8, phi = (uint32_t)(p8 >> 32);
     const uint64_t nd = (uint64_t)not_digit(plo) | ((uint64_t)not_digit(phi) << 32);
     const uint64_t inl = L8 >= 8 ? ~0ull : ((1ull << (8 * L8)) - 1);
-    const uint32_t d9 = (uint32_t)(uint8_t)stage[sh + t1 + 8] - '0';
+    const uint32_t d9 = at(t1 + 8) - '0';   // (read within the staged bytes whenever lp == 9)
     // (a leading zero: the position's digits then differ from its printed
     // ones -- the formatter's tokeniser takes it, so a valid pair's digit
     // count is the printed position's, sid_i32_len)
@@ -1086,9 +1088,9 @@ __device__ __forceinline__ int parse_header(const uint4 v0, const uint4 v1, cons
     const uint32_t up = (ref >= 'a' && ref <= 'z') ? ref - 32 : ref;
     const uint32_t lw = (ref >= 'A' && ref <= 'Z') ? ref + 32 : ref;
     const uint32_t kd = cls[up], kc = cls[lw];
-    if (kd >= K_CARET || kc >= K_CARET || kd != kc) return -1;
+    ok &= (kd < K_CARET) & (kc < K_CARET) & (kd == kc);
     *kdp = kd;
-    return t4;
+    return ok ? t4 : -1;
 }
 
 // The fast path of one line (pileup.cpp:13-46 + :70-153 for the lines that
