@@ -50,6 +50,7 @@ pins its host buffers on its GPU's NUMA node (the PCI device's local CPUs).
 """
 import argparse
 import json
+import math
 import os
 import socket
 import statistics
@@ -252,10 +253,17 @@ def stage_bytes(stage, text_per_site, csv_per_site, fused):
         # written: textpath.hip sid_tile_compact_kernel)
         return text_per_site + 24 + 24 + 28
     if tile_parse(fused, text_per_site) and stage in ("parse", "fmt_write"):
-        # the tile parse reads the text once and writes each site's 4 B class
-        # word and 16 B header pair (textpath.hip sid_tile_parse_kernel); the
-        # writer reads those and writes the records
-        return {"parse": text_per_site + 4 + 16, "fmt_write": 4 + 16 + csv_per_site}[stage]
+        # the tile parse reads the text once and writes each site's slot
+        # words, which the writer reads before writing the records
+        # (textpath.hip sid_tile_parse_kernel, tile_wave_store): the lane
+        # shape a 4 B compact class word a site and a 16 B entry a wave of 64
+        # slots (a 20 KiB tile's lines, slots for 3 % more rounded up to 16:
+        # ~0.32 B a site); the quad shape the 4 B word and the 16 B header pair
+        slot = 4 + 16
+        if not parse_quad(text_per_site):
+            lines = 20480 / text_per_site
+            slot = 4 + 16 * math.ceil(math.ceil((lines * 1.03 + 2) / 16) * 16 / 64) / lines
+        return {"parse": text_per_site + slot, "fmt_write": slot + csv_per_site}[stage]
     return {
         "index": text_per_site + text_per_site / 8,    # text read once, line-start masks written
         # text read; line-start masks (1/8 of the text) read back, 4 B line
