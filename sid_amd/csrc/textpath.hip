@@ -803,8 +803,13 @@ __host__ __device__ constexpr uint32_t rb_entry(uint32_t c)
 // branches of every case, serial in a wave, in every block: 13 % of the tile
 // parse's time, C2 parse 1.712 -> 1.51 ms, C5 10.13 -> 8.76 ms per step,
 // profiles/ab_tile_r06.log)
+// rb[256 + m]: the 4-bit mask m as the bytes 0x00 / 0xFF of a word (the
+// read bases' kept bytes: one LDS read a word; round 6 first spread the bits
+// by a 24-bit multiply and multiplied by 0xFF -- v_perm's constant selectors,
+// or (b << 8) - b, were no faster)
+constexpr uint32_t RB_LUT_N = 256 + 16;
 struct TpTables {
-    uint32_t rb[256];
+    uint32_t rb[RB_LUT_N];
     uint8_t cls[256];
 };
 constexpr TpTables make_tp_tables()
@@ -814,19 +819,11 @@ constexpr TpTables make_tp_tables()
         t.rb[c] = rb_entry(c);
         t.cls[c] = (uint8_t)base_class(c);
     }
+    for (uint32_t m = 0; m < 16; ++m)
+        t.rb[256 + m] = (m & 1 ? 0xFFu : 0u) | (m & 2 ? 0xFF00u : 0u) | (m & 4 ? 0xFF0000u : 0u) | (m & 8 ? 0xFF000000u : 0u);
     return t;
 }
 __device__ constexpr TpTables k_tp_tables = make_tp_tables();
-
-// bits 0-3 of m as the bytes 0x00 / 0xFF of a word: each bit moved to its
-// byte's bit 0 by a 24-bit multiply, then times 0xFF.  (That multiply is a
-// v_mul_lo_u32, four a window; v_perm's constant selectors instead (12:
-// 0x00, 13: 0xFF) measured 2 % slower in the C2 parse stage:
-// profiles/ab_tile_r06.log.)
-__device__ __forceinline__ uint32_t nibble_bytes(uint32_t m)
-{
-    return (__umul24(m & 15u, 0x00204081u) & 0x01010101u) * 0xFFu;   // ((b << 8) - b: the same time)
-}
 
 // the four bytes of x through the table (byte b at LDS word b)
 __device__ __forceinline__ uint32_t rb_word(const uint32_t* lut, uint32_t x)
@@ -864,7 +861,7 @@ __device__ __forceinline__ uint32_t rb_window16(const uint4 v, uint32_t valid, i
     const uint32_t cm = (vm | first) & ~skip;   // the bytes looked up
     uint32_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) acc += rb_word(lut, ws[k] & nibble_bytes(cm >> (4 * k)));
+    for (int k = 0; k < 4; ++k) acc += rb_word(lut, ws[k] & lut[256 + ((cm >> (4 * k)) & 15u)]);
     return acc;
 }
 
@@ -1142,11 +1139,12 @@ __global__ __launch_bounds__(TB) void sid_parse_kernel(const char* __restrict__ 
                                                        uint32_t* __restrict__ fb, unsigned long long* fbn)
 {
     __shared__ uint8_t cls[256];
-    __shared__ uint32_t rbl[256];
+    __shared__ uint32_t rbl[RB_LUT_N];
     __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
     if (threadIdx.x < 256) {
         cls[threadIdx.x] = k_tp_tables.cls[threadIdx.x];
         rbl[threadIdx.x] = k_tp_tables.rb[threadIdx.x];
+        if (threadIdx.x < RB_LUT_N - 256) rbl[256 + threadIdx.x] = k_tp_tables.rb[256 + threadIdx.x];
     }
     __syncthreads();
     const uint64_t lo = range[0], hi = range[1];
@@ -1179,11 +1177,12 @@ __global__ __launch_bounds__(TB) void sid_parse_quad_kernel(const char* __restri
                                                             uint32_t* __restrict__ fb, unsigned long long* fbn)
 {
     __shared__ uint8_t cls[256];
-    __shared__ uint32_t rbl[256];
+    __shared__ uint32_t rbl[RB_LUT_N];
     __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
     if (threadIdx.x < 256) {
         cls[threadIdx.x] = k_tp_tables.cls[threadIdx.x];
         rbl[threadIdx.x] = k_tp_tables.rb[threadIdx.x];
+        if (threadIdx.x < RB_LUT_N - 256) rbl[256 + threadIdx.x] = k_tp_tables.rb[256 + threadIdx.x];
     }
     __syncthreads();
     constexpr uint32_t LPB = TB / 4;   // lines per block step
@@ -1736,11 +1735,12 @@ __global__ __launch_bounds__(TB) void sid_parse_len_kernel(const char* __restric
 {
     static_assert(FTB % 64 == 0 && TB % 64 == 0, "a wave's lines lie in one formatter block");
     __shared__ uint8_t cls[256];
-    __shared__ uint32_t rbl[256];
+    __shared__ uint32_t rbl[RB_LUT_N];
     __shared__ __attribute__((aligned(16))) char stage[TB * HDR_BYTES + 64];
     if (threadIdx.x < 256) {
         cls[threadIdx.x] = k_tp_tables.cls[threadIdx.x];
         rbl[threadIdx.x] = k_tp_tables.rb[threadIdx.x];
+        if (threadIdx.x < RB_LUT_N - 256) rbl[256 + threadIdx.x] = k_tp_tables.rb[256 + threadIdx.x];
     }
     __syncthreads();
     const uint64_t lo = range[0], hi = range[1];
@@ -2094,7 +2094,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
     __shared__ __attribute__((aligned(16))) char tl[TP_TILE + TP_HALO + 64];
     __shared__ uint16_t ls[tp_cap_max(QUAD) + TB];   // (+ a dummy slot per thread: the index's absent starts)
     __shared__ uint8_t cls[256];
-    __shared__ uint32_t rbl[256];
+    __shared__ uint32_t rbl[RB_LUT_N];
     __shared__ uint32_t wtot[TB / 64][NW];
     __shared__ uint32_t qmeta[QUAD ? tp_cap_max(true) : 1];   // the quad shape's headers (quad_head)
     __shared__ uint64_t qcnt[QUAD && LOCAL ? tp_cap_max(true) : 1];   // ... and counts (quad_bases)
@@ -2145,6 +2145,7 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             // tile's loads were issued)
             cls[tid] = k_tp_tables.cls[tid];
             rbl[tid] = k_tp_tables.rb[tid];
+            if (tid < RB_LUT_N - 256) rbl[256 + tid] = k_tp_tables.rb[256 + tid];
             __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): this wave's pieces have landed
             if (!inner) {
 #pragma unroll
