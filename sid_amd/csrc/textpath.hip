@@ -841,12 +841,16 @@ __device__ __forceinline__ uint32_t rb_word(const uint32_t* lut, uint32_t x)
 // start and before the text's end, room = bytes before the end) count; else
 // the whole window lies inside the text.  (A per-word form of the same logic
 // measured 1-2 % slower at 30x, 4 % at 200x.)
+// (Lpre: the window's low-byte mask when the caller has it -- the header
+// parse's mask of the line's first 48 bytes holds the first window's; ~0u:
+// computed here)
 template <bool MASKED>
 __device__ __forceinline__ uint32_t rb_window16(const uint4 v, uint32_t valid, int room, const uint32_t* lut,
-                                                bool& done, uint32_t& carry, bool& bad)
+                                                bool& done, uint32_t& carry, bool& bad, uint32_t Lpre = ~0u)
 {
     const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-    const uint32_t L = compress16(low_bytes(ws[0]), low_bytes(ws[1]), low_bytes(ws[2]), low_bytes(ws[3]));
+    const uint32_t L = Lpre != ~0u ? Lpre
+                                   : compress16(low_bytes(ws[0]), low_bytes(ws[1]), low_bytes(ws[2]), low_bytes(ws[3]));
     const uint32_t C = compress16(eq_bytes(ws[0], 0x5E5E5E5Eu), eq_bytes(ws[1], 0x5E5E5E5Eu),
                                   eq_bytes(ws[2], 0x5E5E5E5Eu), eq_bytes(ws[3], 0x5E5E5E5Eu));
     uint32_t vm = done ? 0u : (MASKED ? valid : 0xFFFFu);
@@ -875,7 +879,7 @@ __device__ __forceinline__ uint32_t rb_window16(const uint4 v, uint32_t valid, i
 // offsets' type (32-bit for the tile parse's offsets from its tile).
 template <class Ld, class Off = uint64_t>
 __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t kd, const uint32_t* lut,
-                                               const uint4* first, uint64_t* out)
+                                               const uint4* first, uint64_t* out, uint32_t Lfirst = ~0u)
 {
     uint32_t nA = 0, nC = 0, nG = 0, nT = 0, nM = 0;
     Off a = q & ~(Off)15;
@@ -883,10 +887,10 @@ __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t k
     bool done = false, bad = false;
     uint4 vn = ld(a + 16);   // the next window in flight while the first is counted
     uint32_t acc = 0;
-    auto masked = [&](const uint4& v, uint32_t lead) {
+    auto masked = [&](const uint4& v, uint32_t lead, uint32_t Lpre) {
         const int room = len > a ? (int)min(len - a, (Off)16) : 0;
         const uint32_t valid = ((room >= 16 ? 0xFFFFu : ((1u << room) - 1u)) >> lead) << lead;
-        return rb_window16<true>(v, valid, room, lut, done, carry, bad);
+        return rb_window16<true>(v, valid, room, lut, done, carry, bad, Lpre);
     };
     // the windows' 5-bit fields summed in two words with 10 bits a field (A,
     // G, '.' in one, C, T in the other: 4 instructions a window instead of
@@ -907,12 +911,12 @@ __device__ __forceinline__ bool read_bases_lut(Ld ld, Off len, Off q, uint32_t k
         acc |= w;
         if (++nw == 63) flush();
     };
-    add(masked(*first, (uint32_t)(q & 15)));
+    add(masked(*first, (uint32_t)(q & 15), Lfirst));
     a += 16;
     while (!done) {
         const uint4 v = vn;
         vn = ld(a + 16);
-        add(a + 16 <= len ? rb_window16<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u));
+        add(a + 16 <= len ? rb_window16<false>(v, 0u, 16, lut, done, carry, bad) : masked(v, 0u, ~0u));
         a += 16;
     }
     if (bad || (acc >> RB_BAD_SHIFT) != 0) return false;
@@ -1011,7 +1015,7 @@ __device__ __forceinline__ bool read_bases_quad(Ld ld, Off len, Off q, uint32_t 
 // stand for.
 __device__ __forceinline__ int parse_header(const uint4 v0, const uint4 v1, const uint4 v2, const char* stage,
                                             uint32_t sh, uint64_t avail, const uint8_t* cls, uint64_t* hdr,
-                                            uint32_t* kdp)
+                                            uint32_t* kdp, uint64_t* low48 = nullptr)
 {
     // low bytes (< 0x21: the separators, '\n', NUL, every other control byte)
     // of the 48 staged bytes as a 48-bit mask: 3 instructions a word
@@ -1022,6 +1026,7 @@ __device__ __forceinline__ int parse_header(const uint4 v0, const uint4 v1, cons
     const uint32_t l_lo = compress16(lowb[0], lowb[1], lowb[2], lowb[3]) |
                           (compress16(lowb[4], lowb[5], lowb[6], lowb[7]) << 16);
     const uint32_t l_hi = compress16(lowb[8], lowb[9], lowb[10], lowb[11]);
+    if (low48) *low48 = ((uint64_t)l_hi << 32) | l_lo;   // (the staged windows' low-byte masks, for the read bases)
     // bit j = byte s0 + j, for the bytes inside the text and the 48 staged
     const uint32_t nb = (uint32_t)min((uint64_t)(HDR_BYTES - sh), avail);
     const uint64_t valid = (1ull << nb) - 1;   // (nb <= 48)
@@ -1889,13 +1894,14 @@ __device__ __forceinline__ int tile_line(const char* __restrict__ text, const ch
     const char* stage = tl + (r0 & ~15u);
     const uint32_t sh = r0 & 15u;
     const uint4 v0 = *(const uint4*)stage, v1 = *(const uint4*)(stage + 16), v2 = *(const uint4*)(stage + 32);
-    uint64_t c = 0, h[2] = {0, 0};
+    uint64_t c = 0, h[2] = {0, 0}, low48 = 0;
     uint32_t kd = 0;
-    const int t4 = parse_header(v0, v1, v2, stage, sh, len_t - r0, cls, h, &kd);
+    const int t4 = parse_header(v0, v1, v2, stage, sh, len_t - r0, cls, h, &kd, &low48);
     bool ok = t4 >= 0;
     if (ok) {
-        const uint4* first = (const uint4*)(stage + ((sh + (uint32_t)t4) & 0x30u));
-        ok = read_bases_lut<Ld, uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, first, &c);
+        const uint32_t fw = (sh + (uint32_t)t4) & 0x30u;   // the read bases' first window (0, 16 or 32)
+        ok = read_bases_lut<Ld, uint32_t>(ld, len_t, r0 + (uint32_t)t4, kd, rbl, (const uint4*)(stage + fw), &c,
+                                          (uint32_t)(low48 >> fw) & 0xFFFFu);
     }
     if (ok) {
         const bool hv = (h[0] >> 63) != 0;
