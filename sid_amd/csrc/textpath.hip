@@ -2134,13 +2134,23 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
         const uint32_t pbyte = (uint8_t)text[pok ? g0 - 1 : g0];
         {
             typedef __attribute__((address_space(3))) void lds_void;
-            const uint32_t wb = (tid & ~63u) * 16u;
+            // (the wave's LDS base and the tile's text as scalars; an inner
+            // tile's rows at a 32-bit lane offset from it: no per-lane 64-bit
+            // bounds select a row)
+            const uint32_t wb = __builtin_amdgcn_readfirstlane((tid & ~63u) * 16u);
+            const char* const gt = text + g0;
+            if (inner) {
 #pragma unroll
-            for (uint32_t k = 0; k < ROWS; ++k) {
-                const uint64_t at = g0 + k * TILE + tid * 16;
-                const bool ok = inner || at < c1;
-                __builtin_amdgcn_global_load_lds((const void*)(text + (ok ? at : g0)),
-                                                 (lds_void*)(tl + k * TILE + wb), 16, 0, 2 /* nt */);
+                for (uint32_t k = 0; k < ROWS; ++k)
+                    __builtin_amdgcn_global_load_lds((const void*)(gt + (k * TILE + tid * 16)),
+                                                     (lds_void*)(tl + k * TILE + wb), 16, 0, 2 /* nt */);
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < ROWS; ++k) {
+                    const uint64_t at = g0 + k * TILE + tid * 16;
+                    __builtin_amdgcn_global_load_lds((const void*)(text + (at < c1 ? at : g0)),
+                                                     (lds_void*)(tl + k * TILE + wb), 16, 0, 2 /* nt */);
+                }
             }
             if (tid < TP_HALO / 16)   // (whole waves)
                 __builtin_amdgcn_global_load_lds((const void*)(text + (hok ? hat : g0)), (lds_void*)(tl + TP_TILE + wb),
