@@ -2155,13 +2155,16 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
             if (tid < TP_HALO / 16)   // (whole waves)
                 __builtin_amdgcn_global_load_lds((const void*)(text + (hok ? hat : g0)), (lds_void*)(tl + TP_TILE + wb),
                                                  16, 0, 0);
-            if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
             // the LDS tables, loaded while the tile's pieces are in flight
             // (copied in before them, their load's wait came before the
             // tile's loads were issued)
-            cls[tid] = k_tp_tables.cls[tid];
-            rbl[tid] = k_tp_tables.rb[tid];
-            if (tid < RB_LUT_N - 256) rbl[256 + tid] = k_tp_tables.rb[256 + tid];
+            // (all three loads issued before any LDS store: a store waits for
+            // every load ahead of it, the DMA's included)
+            const uint8_t cv = k_tp_tables.cls[tid];
+            const uint32_t rv = k_tp_tables.rb[tid], nv = k_tp_tables.rb[256 + (tid & (RB_LUT_N - 257))];
+            cls[tid] = cv;
+            rbl[tid] = rv;
+            rbl[256 + (tid & (RB_LUT_N - 257))] = nv;   // (every lane: the same values, no branch to sink the load into)
             __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): this wave's pieces have landed
             if (!inner) {
 #pragma unroll
@@ -2169,6 +2172,10 @@ __global__ __launch_bounds__(TB) void sid_tile_parse_kernel(const char* __restri
                     if (g0 + k * TILE + tid * 16 >= c1) *(uint4*)(tl + k * TILE + tid * 16) = make_uint4(0, 0, 0, 0);
             }
             if (tid < TP_HALO / 16 && !hok) *(uint4*)(tl + TP_TILE + tid * 16) = make_uint4(0, 0, 0, 0);
+            // (the padding after the halo zeroed once the wave's pieces have
+            // landed: an LDS store issued before the wait made the compiler
+            // wait for the wave's DMA first, ahead of the tables' loads)
+            if (tid < 4) *(uint32_t*)(tl + TP_TILE + TP_HALO + 4 * tid) = 0u;
         }
         if constexpr (QUAD) __builtin_amdgcn_s_setprio(2);
         // is the byte before the tile a '\n' (1 when there is none: the tile starts the chunk)
