@@ -2836,9 +2836,9 @@ __global__ __launch_bounds__(FTB, SID_PUT_WAVES) void sid_local_put_kernel(const
         // ms for 1.08)
         if (CLS) w0 = cwords[i];
         if (!WV) hw0 = *(const ulonglong2*)(hdr + 2 * i);
-        const uint32_t t = slot_tile((uint32_t)i, cdiv);   // (i < SID_SLOTS_MAX)
-        const uint32_t j = (uint32_t)i - t * cap;
-        if (WV) te = twv[(uint64_t)t * nwv + (j >> 6)];
+        const uint32_t t = slot_tile((uint32_t)i, cdiv);   // (i < SID_SLOTS_MAX: t < 2^22, 24-bit products)
+        const uint32_t j = (uint32_t)i - __umul24(t, cap);
+        if (WV) te = twv[__umul24(t, nwv) + (j >> 6)];
         site = j < tcnt[t];
         cw = WV && cls_compact(w0);
         if (WV && site && !cw) hw0 = *(const ulonglong2*)(hdr + 2 * i);
