@@ -226,9 +226,7 @@ __device__ __forceinline__ void sid_fallback_append(bool fb, uint64_t key, unsig
     if (off < cap) list[off] = key;
 }
 
-#ifndef SID_HIST_PAIRS
-#define SID_HIST_PAIRS 4
-#endif
+constexpr int SID_HIST_PAIRS = 4;   // site pairs a lane keeps in flight (16 B each)
 template <bool PAIRS>
 __global__ __launch_bounds__(1024) void sid_hist_dense_kernel(const uint64_t* __restrict__ counts, size_t n,
                                                               uint32_t* __restrict__ part,

@@ -290,30 +290,15 @@ __device__ __forceinline__ uint32_t low_bytes(uint32_t w)
     return ~(((w & 0x7F7F7F7Fu) + 0x5F5F5F5Fu) | w) & 0x80808080u;
 }
 
-// bit 7 of each byte of a and b -> 8 bits (a's in bits 0-3): the two words'
-// flags interleaved by nibble, then one shift-or ladder for both
-__device__ __forceinline__ uint32_t compress8(uint32_t a, uint32_t b)
-{
-    uint32_t x = (a >> 7) | (b >> 3);   // a: bits 0, 8, 16, 24; b: 4, 12, 20, 28
-    x |= x >> 7;                        // bits 1, 5 <- 8, 12
-    x |= x >> 14;                       // bits 2, 3, 6, 7 <- 16, 17, 20, 21
-    return x & 0xFFu;
-}
 // bit 7 of each byte of four words -> 16 bits (word w's byte k at bit 4w+k):
 // the bytes (0x00 or 0x80) weighted by v_dot4 (1, 2, 4, 8 and 16 .. 128) and
-// summed, two words a dot product pair; 6 instructions for compress8's 16
-#ifndef SID_CMP_DOT
-#define SID_CMP_DOT 1
-#endif
+// summed, two words a dot product pair: 6 instructions where a shift-or
+// ladder over nibble-interleaved flags took 16 (round 6, profiles/ab_tile_r06.log)
 __device__ __forceinline__ uint32_t compress16(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
 {
-#if SID_CMP_DOT
     const uint32_t lo = __builtin_amdgcn_udot4(b, 0x80402010u, __builtin_amdgcn_udot4(a, 0x08040201u, 0u, false), false);
     const uint32_t hi = __builtin_amdgcn_udot4(d, 0x80402010u, __builtin_amdgcn_udot4(c, 0x08040201u, 0u, false), false);
     return (lo >> 7) | (hi << 1);   // (hi: 128 x the high byte's bits)
-#else
-    return compress8(a, b) | (compress8(c, d) << 8);
-#endif
 }
 // a 16-B load marked non-temporal (streamed data read once: kept out of the
 // caches the data read again needs)
@@ -2618,7 +2603,6 @@ __device__ __forceinline__ uint32_t four_digits(uint32_t g)
     const uint32_t u = p - __umul24(t, 10u);
     return 0x30303030u + (t | (u << 8));
 }
-#ifndef SID_POS_LOOP
 // v < 2^31 with nd digits -> ",digits," in lo (bytes 0-7) and hi: three
 // groups of four digits (two 32-bit divisions by 10^4), the twelve digits
 // with their leading zeros at bytes 1-12 and a ',' at 13, the zero digit at
@@ -2643,31 +2627,6 @@ __device__ __forceinline__ void comma_num_comma(uint32_t v, int nd, uint64_t& lo
         hi = H >> sh;
     }
 }
-#else
-__device__ __forceinline__ void comma_num_comma(uint32_t v, int nd, uint64_t& lo, uint64_t& hi)
-{
-    // right-aligned first: byte 15 ',', byte 14 - j digit j (units first),
-    // byte 14 - nd the leading ','
-    uint64_t L = 0, H = (uint64_t)',' << 56;
-#pragma unroll
-    for (int j = 0; j <= 10; ++j) {
-        const uint32_t d = v % 10u;
-        v /= 10u;
-        const uint64_t byte = j < nd ? (uint64_t)('0' + d) : (j == nd ? (uint64_t)',' : 0ull);
-        const int p = 14 - j;
-        if (p >= 8) H |= byte << (8 * (p - 8));
-        else L |= byte << (8 * p);
-    }
-    const uint32_t sh = 8u * (uint32_t)(14 - nd);   // 32 .. 104 bits
-    if (sh >= 64) {
-        lo = H >> (sh - 64);
-        hi = 0;
-    } else {
-        lo = (L >> sh) | (H << (64 - sh));
-        hi = H >> sh;
-    }
-}
-#endif
 
 // any record (the fix-up's sites, chroms the parse did not keep, positions
 // from the text) byte by byte into the OR buffer
