@@ -117,11 +117,35 @@ class DevPool {
 public:
     int device = 0;
     ~DevPool() { release(); }
+    // A fitting buffer whose last use is done is taken first; while every
+    // fitting one is still in use (its event pending), up to two of them, a
+    // new one is allocated rather than waited for -- the records' buffer of
+    // a chunk is in use until its D2H completes, and the next chunk's writer
+    // waiting for that copy serialised writer and D2H chunk after chunk (the
+    // PCIe leg's last chunks then drained one D2H at a time after the last
+    // upload)
     char* get(uint64_t need, uint64_t* cap, hipStream_t st)
     {
         std::lock_guard<std::mutex> l(m_);
-        auto it = free_.lower_bound(need);
-        if (it != free_.end() && it->first <= 2 * need + (64u << 20)) {
+        const uint64_t top = 2 * need + (64u << 20);
+        const auto lo = free_.lower_bound(need);
+        auto it = free_.end();
+        int busy = 0;
+        for (auto jt = lo; jt != free_.end() && jt->first <= top; ++jt) {
+            if (!jt->second.ev || jt->second.st == st) {   // (returned on this stream: ordered, no wait)
+                it = jt;
+                break;
+            }
+            const hipError_t q = hipEventQuery(jt->second.ev);
+            if (q == hipSuccess) {
+                it = jt;
+                break;
+            }
+            (void)hipGetLastError();   // (hipErrorNotReady: not an error of this thread's work)
+            ++busy;
+        }
+        if (it == free_.end() && busy >= 2) it = lo;   // (growth bounded: wait for the first)
+        if (it != free_.end()) {
             Entry en = it->second;
             *cap = it->first;
             free_.erase(it);
@@ -151,7 +175,7 @@ public:
     {
         if (!p || !cap) return;   // cap 0: not a pooled buffer (the hold arena)
         std::lock_guard<std::mutex> l(m_);
-        Entry en{p, nullptr};
+        Entry en{p, nullptr, after};
         if (after) {
             if (evs_.empty()) {
                 hipEvent_t ev;
@@ -183,6 +207,7 @@ private:
     struct Entry {
         char* p;
         hipEvent_t ev;
+        hipStream_t st;   // the stream the event was recorded on
     };
     std::mutex m_;
     std::multimap<uint64_t, Entry> free_;
