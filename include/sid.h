@@ -334,9 +334,10 @@ typedef struct {
                                     source was pinned already)                     */
     double register_s;           /* host time in hipHostRegister / Unregister,
                                     summed over the uploaders                      */
-    double h2d_s;                /* device time of the host-to-device copies (HIP
-                                    events on the upload streams), summed over
-                                    the devices                                    */
+    double h2d_s;                /* device time of the host-to-device copies: the
+                                    span from each upload stream's first copy to
+                                    its last (HIP events), summed over the
+                                    devices                                        */
     uint64_t h2d_bytes;          /* bytes those copies moved                       */
     uint64_t chunks_tiled;       /* parsed by the tile parse (text read once)       */
     uint64_t tile_overflows;     /* chunks with a tile of more lines than its slots

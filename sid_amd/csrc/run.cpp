@@ -446,7 +446,8 @@ struct Dev {
         }
         return ev;
     }
-    // device time of the copies timed since the last call (the stream drained)
+    // device time of the uploads timed since the last call (the stream
+    // drained): each uploader's span, first copy's start to last copy's end
     double h2d_collect()
     {
         double s = 0;
@@ -1305,6 +1306,26 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
     bind_thread(d);
     if (hipSetDevice(d.device) != hipSuccess) return (void)fail(e, SID_EHIP);
     UploadReg reg(e, pass);
+    // the ingest's uploads timed as one span on the upload stream, from the
+    // first copy's start to the last one's end (the copies run back to back;
+    // a pair of events around every copy cost the step ~0.3 ms)
+    struct Span {
+        Dev& d;
+        hipEvent_t t0 = nullptr;
+        uint64_t bytes = 0;
+        ~Span()
+        {
+            if (!t0) return;
+            hipEvent_t t1 = d.h2d_event();
+            if (t1 && hipEventRecord(t1, d.s_up) == hipSuccess) {
+                d.h2d_pending.push_back({t0, t1});
+                d.h2d_bytes += bytes;
+            } else {
+                d.h2d_free.push_back(t0);
+                if (t1) d.h2d_free.push_back(t1);
+            }
+        }
+    } span{d};
     // the chunk this uploader copies after j from the host (UINT64_MAX: none)
     size_t at = 0;
     auto next_of = [&](uint64_t j) -> uint64_t {
@@ -1385,17 +1406,9 @@ void uploader(sid_engine* e, Dev& d, const std::vector<uint64_t>& list, int pass
         }
         uint64_t len = r.len;
         if (e->src == SRC_HOST || e->src == SRC_FILE) {
-            hipEvent_t h0 = pass == 1 && len ? d.h2d_event() : nullptr, h1 = h0 ? d.h2d_event() : nullptr;
-            if (h0 && h1) x = hipEventRecord(h0, d.s_up);
+            if (pass == 1 && len && !span.t0 && (span.t0 = d.h2d_event())) x = hipEventRecord(span.t0, d.s_up);
             if (len && x == hipSuccess) x = reg.copy(dst, j, d.s_up);
-            if (h0 && h1 && x == hipSuccess) {
-                x = hipEventRecord(h1, d.s_up);
-                d.h2d_pending.push_back({h0, h1});
-                d.h2d_bytes += len;
-            } else {
-                if (h0) d.h2d_free.push_back(h0);
-                if (h1) d.h2d_free.push_back(h1);
-            }
+            if (pass == 1 && span.t0 && x == hipSuccess) span.bytes += len;
             // the next chunk's pages pinned while this copy runs; the ones
             // whose copies are done released
             if (x == hipSuccess) reg.ahead(next_of(j));
