@@ -1522,6 +1522,13 @@ void compute(sid_engine* e, Dev& d, int pass)
         e->t_comp_sync += (uint64_t)((wall() - a) * 1e9);
         return r;
     };
+    // (an event instead of the stream: the work queued behind it is not waited for)
+    auto sync_ev = [&](hipEvent_t ev) {
+        const double a = wall();
+        const hipError_t r = hipEventSynchronize(ev);
+        e->t_comp_sync += (uint64_t)((wall() - a) * 1e9);
+        return r;
+    };
     // the next chunk, taken early so that its line index runs behind this
     // chunk's formatter (the GPU then does not idle over the host round trip
     // that reads the formatter's byte count); indexed: its site count is in hs[0]
@@ -1591,6 +1598,21 @@ void compute(sid_engine* e, Dev& d, int pass)
         bool sunk = false;       // pass 1, device sink: a scratch buffer, dropped
         hipEvent_t pe = nullptr;
         uint64_t n = 0;
+        // the tile path: this chunk's records and byte count done (recorded
+        // before the next chunk's tile parse is queued behind the writer: the
+        // host and the records' D2H wait for this, not for that parse, which
+        // waits for the next chunk's upload -- each chunk's D2H then runs
+        // behind its own writer instead of a chunk later)
+        struct Done {
+            Dev& d;
+            hipEvent_t ev = nullptr;
+            void drop()
+            {
+                if (ev) d.give_event(ev);
+                ev = nullptr;
+            }
+            ~Done() { drop(); }
+        } done{d};
         // -m local formatting in this pass, lines of up to 256 B on average (as
         // the device's last chunk had): the tile parse -- the text read once,
         // no host round trip before the writer (sid_chunk_tile_local).  A tile
@@ -1652,6 +1674,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                 if (rc != SID_OK) return (void)fail(e, rc);
                 // bytes, range flag, sites, parse error key, the most lines in a tile
                 x = hipMemcpyAsync(hs + 8, W.lb + 1, 5 * 8, hipMemcpyDeviceToHost, d.s_comp);
+                if (x == hipSuccess && (done.ev = d.take_event())) x = hipEventRecord(done.ev, d.s_comp);
                 // the next chunk's tile parse behind this writer (stream order:
                 // it rewrites the slots and W.lb after the writer and the copy
                 // have read them), so the GPU does not idle over the host round
@@ -1680,7 +1703,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                         next_quad = q2;
                     }
                 }
-                if (x == hipSuccess) x = sync();
+                if (x == hipSuccess) x = done.ev ? sync_ev(done.ev) : sync();
                 if (x != hipSuccess) return (void)hipfail(e, x);
                 const uint64_t maxl = hs[12];
                 if (maxl <= lg) {
@@ -1697,6 +1720,7 @@ void compute(sid_engine* e, Dev& d, int pass)
                     out = nullptr;
                     cap = 0;
                     via_host = sunk = false;
+                    done.drop();
                     ++d.tile_overflows;
                     d.tile_over_queued += have_next;
                     d.tile_over(maxl, quad);
@@ -1975,11 +1999,11 @@ void compute(sid_engine* e, Dev& d, int pass)
         if (pass == 1 && via_host) {
             char* hp = d.hh_take(bytes);
             if (hp) {   // D2H behind this chunk's formatter, while the next chunks upload
-                hipEvent_t ev = d.take_event();
-                if (!ev) return (void)fail(e, SID_EHIP);
-                x = hipEventRecord(ev, d.s_comp);
-                if (x == hipSuccess) x = hipStreamWaitEvent(d.s_d2h, ev, 0);
-                d.give_event(ev);
+                hipEvent_t ev = done.ev ? nullptr : d.take_event();
+                if (!done.ev && !ev) return (void)fail(e, SID_EHIP);
+                if (ev) x = hipEventRecord(ev, d.s_comp);
+                if (x == hipSuccess) x = hipStreamWaitEvent(d.s_d2h, ev ? ev : done.ev, 0);
+                if (ev) d.give_event(ev);
                 if (x == hipSuccess && bytes) x = hipMemcpyAsync(hp, out, bytes, hipMemcpyDeviceToHost, d.s_d2h);
                 if (x != hipSuccess) return (void)hipfail(e, x);
                 d.pool.put(out, cap, d.s_d2h);   // reusable once the copy is done
@@ -2020,9 +2044,12 @@ void compute(sid_engine* e, Dev& d, int pass)
         it.buf = out;
         it.cap = cap;
         it.len = bytes;
-        hipEvent_t ev = d.take_event();
-        if (!ev) return (void)fail(e, SID_EHIP);
-        (void)hipEventRecord(ev, d.s_comp);
+        hipEvent_t ev = done.ev;
+        done.ev = nullptr;
+        if (!ev) {
+            if (!(ev = d.take_event())) return (void)fail(e, SID_EHIP);
+            (void)hipEventRecord(ev, d.s_comp);
+        }
         it.ev = ev;
         if (!d.drain_q.push(it)) break;
     }
