@@ -771,10 +771,13 @@ void split_host_text(sid_engine* e, const char* t, uint64_t len)
     e->recs.clear();
     uint64_t at = 0;
     while (at < len) {
-        // the last chunk's work (compute, then its records' copy back) runs
-        // after the last upload: the tail is cut in halves down to 16 MiB
+        // the last chunks' work (compute, then their records' copies back)
+        // runs after the last upload: the last two chunks' worth of text is
+        // cut in halves down to 8-16 MiB, so each chunk's D2H (~0.6 of its
+        // upload's time) runs under the uploads still to come, and what is
+        // left after the last upload is one small chunk's
         const uint64_t rem = len - at;
-        const uint64_t want = (rem <= C && rem > (32ull << 20)) ? rem / 2 : C;
+        const uint64_t want = rem <= 2 * C && rem > (16ull << 20) ? std::min(C, rem / 2) : C;
         uint64_t end = next_line_start(t, len, std::max(at + 1, std::min(len, at + want)));
         if (end <= at) end = len;
         ChunkRec r;
@@ -2279,6 +2282,17 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
     start_queues(e);
     const double t_setup = wall();
     const int D = (int)e->devs.size();
+    // SID_ENGINE_TIMING: the first device's GPU timeline of the run -- its
+    // start, and after the join the ends of its compute and D2H streams,
+    // against its upload span (the head before the first copy, the tail
+    // after the last)
+    const bool timing = std::getenv("SID_ENGINE_TIMING") != nullptr;
+    hipEvent_t tz[3] = {nullptr, nullptr, nullptr};
+    if (timing) {
+        Dev& d0 = *e->devs[0];
+        for (auto& ev : tz) ev = d0.h2d_event();
+        if (tz[0]) (void)hipEventRecord(tz[0], d0.s_up);
+    }
     if (e->lynch)
         for (auto& dp : e->devs)
             if ((rc = sid_profile_reset(dp->ctx, dp->s_comp)) != SID_OK) return rc;
@@ -2306,9 +2320,27 @@ extern "C" int sid_engine_ingest(sid_engine* e, sid_run_stats* st)
         for (auto& dp : e->devs) (void)hipSetDevice(dp->device), (void)hipDeviceSynchronize();
         return e->rc.load();
     }
-    if (std::getenv("SID_ENGINE_TIMING"))
-        std::fprintf(stderr, "{\"ingest_setup_s\": %.6f, \"budgets_s\": %.6f, \"spawn_s\": %.6f, \"join_s\": %.6f}\n",
-                     t_setup - t0, t_budget - t0, t_spawn - t_setup, t_join - t_spawn);
+    if (timing) {
+        Dev& d0 = *e->devs[0];
+        if (tz[1]) (void)hipEventRecord(tz[1], d0.s_comp);
+        if (tz[2]) (void)hipEventRecord(tz[2], d0.s_d2h);
+        (void)hipSetDevice(d0.device);
+        float head = -1.f, tc = -1.f, td = -1.f;
+        if (hipStreamSynchronize(d0.s_comp) == hipSuccess && hipStreamSynchronize(d0.s_d2h) == hipSuccess &&
+            hipStreamSynchronize(d0.s_up) == hipSuccess && !d0.h2d_pending.empty() && tz[0] && tz[1] && tz[2]) {
+            (void)hipEventElapsedTime(&head, tz[0], d0.h2d_pending.front().first);
+            (void)hipEventElapsedTime(&tc, d0.h2d_pending.back().second, tz[1]);
+            (void)hipEventElapsedTime(&td, d0.h2d_pending.back().second, tz[2]);
+        }
+        (void)hipGetLastError();
+        for (auto ev : tz)
+            if (ev) d0.h2d_free.push_back(ev);
+        std::fprintf(stderr,
+                     "{\"ingest_setup_s\": %.6f, \"budgets_s\": %.6f, \"spawn_s\": %.6f, \"join_s\": %.6f, "
+                     "\"gpu_head_ms\": %.3f, \"gpu_tail_comp_ms\": %.3f, \"gpu_tail_d2h_ms\": %.3f, \"join_after_ms\": %.3f}\n",
+                     t_setup - t0, t_budget - t0, t_spawn - t_setup, t_join - t_spawn, head, tc, td,
+                     (wall() - t_join) * 1e3);
+    }
     double h2d_s = 0;
     uint64_t h2d_bytes = 0, tiled = 0, tile_over = 0, tile_oq = 0;
     for (auto& dp : e->devs) {
